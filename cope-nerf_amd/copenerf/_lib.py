@@ -1,0 +1,137 @@
+"""ctypes binding of libcopenerf.so (include/copenerf.h).
+
+This is the reference-side binding of the C ABI: the reference is pure Python,
+so the "FFI" it would grow for this path is a ctypes stub exactly like this one
+(see INTEGRATION.md).  The library is looked up next to this file; if it is
+missing, or cannot be loaded, every hot-path entry point raises -- there is no
+CPU fallback on the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_NAME = "libcopenerf.so"
+LIB_PATH = os.environ.get("COPENERF_LIB", os.path.join(_HERE, LIB_NAME))
+
+ABI_VERSION = 1
+
+c_f32p = ctypes.c_void_p  # device pointers are passed as integers
+c_i32 = ctypes.c_int32
+c_i64 = ctypes.c_int64
+c_f32 = ctypes.c_float
+c_ptr = ctypes.c_void_p
+
+# cn_epilogue
+EPI_STORE = 0
+EPI_SOFTPLUS = 1
+EPI_RELU = 2
+EPI_MUL = 3
+EPI_TANGENT = 4
+EPI_BWD_SOFTPLUS = 5
+EPI_BWD_RELU = 6
+
+
+class LinearDesc(ctypes.Structure):
+    _fields_ = [
+        ("A", c_ptr), ("A2", c_ptr), ("B", c_ptr), ("bias", c_ptr), ("rowv", c_ptr), ("colv", c_ptr),
+        ("aux0", c_ptr), ("aux1", c_ptr), ("out0", c_ptr), ("out1", c_ptr), ("out_split", c_ptr),
+        ("lda", c_i64), ("lda2", c_i64), ("ldb", c_i64), ("ld_aux0", c_i64), ("ld_aux1", c_i64),
+        ("ld_out0", c_i64), ("ld_out1", c_i64), ("ld_split", c_i64),
+        ("M", c_i32), ("N", c_i32), ("K", c_i32), ("K1", c_i32),
+        ("nzero", c_i32), ("nsplit", c_i32), ("epilogue", c_i32), ("tile", c_i32),
+        ("adiv", c_f32), ("odiv", c_f32), ("beta", c_f32), ("threshold", c_f32),
+    ]
+
+
+class WgradDesc(ctypes.Structure):
+    _fields_ = [
+        ("Y0", c_ptr), ("X0", c_ptr), ("Y1", c_ptr), ("X1", c_ptr),
+        ("workspace", c_ptr), ("dW", c_ptr), ("db", c_ptr),
+        ("ldy0", c_i64), ("ldx0", c_i64), ("ldy1", c_i64), ("ldx1", c_i64), ("ld_dw", c_i64),
+        ("workspace_bytes", c_i64),
+        ("M", c_i32), ("N", c_i32), ("K", c_i32), ("npairs", c_i32),
+        ("n_out", c_i32), ("k_out", c_i32), ("accumulate", c_i32), ("pad_", c_i32),
+    ]
+
+
+# name -> (restype, argtypes); mirrors include/copenerf.h one to one.
+SIGNATURES = {
+    "cn_abi_version": (c_i32, []),
+    "cn_last_error": (ctypes.c_char_p, []),
+    "cn_linear": (c_i32, [ctypes.POINTER(LinearDesc), c_ptr]),
+    "cn_wgrad_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32]),
+    "cn_wgrad": (c_i32, [ctypes.POINTER(WgradDesc), c_ptr]),
+    "cn_row_head": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i32, c_i32, c_ptr, c_i64,
+                            c_ptr, c_ptr]),
+    "cn_scale_cols": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr]),
+    "cn_sdf_embed": (c_i32, [c_i32, c_ptr, c_i64, c_i32, c_f32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_f32,
+                             c_ptr]),
+    "cn_sdf_grad_assemble": (c_i32, [c_i32, c_i32, c_f32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr,
+                                     c_i64, c_ptr]),
+    "cn_sdf_tangent_prep": (c_i32, [c_i32, c_i32, c_f32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64,
+                                    c_ptr, c_i64, c_f32, c_ptr]),
+    "cn_color_extras": (c_i32, [c_i32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_i32, c_i32, c_i32, c_ptr,
+                                c_i64, c_ptr]),
+    "cn_rgb_head_bwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32]),
+    "cn_rgb_head_bwd": (c_i32, [c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_ptr,
+                                c_ptr, c_i64, c_ptr]),
+    "cn_colsum_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32]),
+    "cn_colsum": (c_i32, [c_i32, c_i32, c_ptr, c_ptr, c_i64, c_f32, c_ptr, c_i32, c_ptr, c_i64, c_ptr]),
+    "cn_coarse_z": (c_i32, [c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr]),
+    "cn_points": (c_i32, [c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_i32, c_ptr, c_ptr, c_i32, c_ptr, c_ptr]),
+    "cn_up_sample_merge": (c_i32, [c_i32, c_i32, c_i32, c_f32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
+                                   c_ptr]),
+    "cn_composite_fwd": (c_i32, [c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
+                                 c_i32, c_f32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr]),
+    "cn_composite_bwd": (c_i32, [c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
+                                 c_i32, c_f32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
+                                 c_ptr]),
+}
+
+_lock = threading.Lock()
+_lib = None
+_load_error: str | None = None
+
+
+class LibraryMissing(RuntimeError):
+    pass
+
+
+def load(path: str | None = None):
+    """Load (once) and return the ctypes handle; raise LibraryMissing if absent."""
+    global _lib, _load_error
+    with _lock:
+        if _lib is not None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            _load_error = f"{p} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            raise LibraryMissing(_load_error)
+        try:
+            lib = ctypes.CDLL(p)
+        except OSError as e:  # pragma: no cover - depends on the loader
+            _load_error = f"cannot load {p}: {e}"
+            raise LibraryMissing(_load_error) from e
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        v = lib.cn_abi_version()
+        if v != ABI_VERSION:
+            raise LibraryMissing(f"{p}: ABI version {v}, expected {ABI_VERSION}")
+        _lib = lib
+        return lib
+
+
+def check(rc: int, name: str) -> None:
+    if rc != 0:
+        msg = load().cn_last_error()
+        raise RuntimeError(f"{name} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def call(name: str, *args) -> None:
+    lib = load()
+    check(getattr(lib, name)(*args), name)

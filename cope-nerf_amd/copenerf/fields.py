@@ -1,0 +1,618 @@
+"""SDF / colour / variance fields backed by the HIP kernels.
+
+API mirror of the reference modules (same constructor arguments, attribute
+names, parameter initialisation order and state-dict keys, so reference
+checkpoints and `pretrained_sdf/model.pt` load unchanged):
+
+  SDFNetwork            model/neus_fields.py:205-303
+  RenderingNetwork      model/neus_fields.py:307-374
+  SingleVarianceNetwork model/neus_fields.py:459-465
+  NeRF                  model/neus_fields.py:378-456  (constructed by train.py:39;
+                        the n_outside > 0 branch that calls it is out of scope)
+
+The forward passes do not run the torch layers: the effective (weight-normed)
+weights are packed once per call and the whole MLP -- encoding, 9 Linear +
+Softplus layers, the sdf head, the ∇ₓSDF pass and its create_graph double
+backward -- runs in cn_linear / cn_wgrad launches (see sdf_forward /
+sdf_backward below and DESIGN.md §3).
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+from typing import List, Optional
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+from .embedder import embed_dim
+from .ops import (EPI_BWD_RELU, EPI_BWD_SOFTPLUS, EPI_MUL, EPI_RELU, EPI_SOFTPLUS, EPI_STORE, EPI_TANGENT,
+                  SQRT2, rup)
+
+
+def effective_weight(lin: nn.Linear) -> torch.Tensor:
+    """W = g * v / ||v|| (torch.nn.utils.weight_norm, dim 0), or the plain weight."""
+    if hasattr(lin, "weight_v"):
+        return torch._weight_norm(lin.weight_v, lin.weight_g, 0)
+    return lin.weight
+
+
+def _empty(M, n, dev):
+    return torch.empty(M, n, device=dev, dtype=torch.float32)
+
+
+# ---------------------------------------------------------------------------
+# SDF network
+@dataclasses.dataclass
+class SDFLayout:
+    n_lin: int               # number of Linear layers (9)
+    in_dim: List[int]
+    out_dim: List[int]
+    E: int                   # encoding width (52)
+    KE: int                  # padded encoding width (64)
+    HL: int                  # leading dimension of hidden buffers (>= widths, multiple of 128)
+    skip: int                # index of the layer whose input is cat([x, emb]) / sqrt(2), or -1
+    multires: int
+    scale: float
+    beta: float = 100.0
+    threshold: float = 20.0
+
+    @property
+    def H_feat(self):
+        return self.out_dim[-1] - 1
+
+
+@dataclasses.dataclass
+class SDFPack:
+    Bf: list      # forward weights [Npad][Kpad], hidden layers
+    Bt: list      # transposed weights [in_pad][out_pad]
+    b: list       # hidden biases
+    w80: torch.Tensor   # [1, in8] sdf row / scale
+    b80: torch.Tensor   # [1] sdf bias / scale
+    w80p: torch.Tensor  # [HL] sdf row / scale, zero padded
+    Bf8: torch.Tensor   # feature rows of the last layer
+    Bt8: torch.Tensor
+    bf8: torch.Tensor
+
+
+def pack_sdf(lay: SDFLayout, Ws, bs) -> SDFPack:
+    with torch.no_grad():
+        Bf, Bt, b = [], [], []
+        for l in range(lay.n_lin - 1):
+            W = Ws[l].detach()
+            o, i = W.shape
+            kp = lay.KE if l == 0 else rup(i, 32)
+            Bf.append(F.pad(W, (0, kp - i, 0, rup(o, 128) - o)).contiguous())
+            tn = 64 if i <= 64 else 128
+            Bt.append(F.pad(W.t(), (0, rup(o, 32) - o, 0, rup(i, tn) - i)).contiguous())
+            b.append(bs[l].detach().contiguous())
+        W8, b8 = Ws[-1].detach(), bs[-1].detach()
+        s = float(lay.scale)
+        w80 = (W8[0] / s) if s != 1.0 else W8[0]
+        b80 = (b8[:1] / s) if s != 1.0 else b8[:1]
+        w80p = F.pad(w80, (0, lay.HL - w80.shape[0])).contiguous()
+        Wf = W8[1:]
+        o, i = Wf.shape
+        Bf8 = F.pad(Wf, (0, rup(i, 32) - i, 0, rup(o, 128) - o)).contiguous()
+        Bt8 = F.pad(Wf.t(), (0, rup(o, 32) - o, 0, rup(i, 128) - i)).contiguous()
+        return SDFPack(Bf, Bt, b, w80.contiguous()[None], b80.contiguous(), w80p, Bf8, Bt8, b8[1:].contiguous())
+
+
+def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool, want_grad: bool, keep: bool,
+                sdf_out: Optional[torch.Tensor] = None, dst: Optional[torch.Tensor] = None):
+    """Forward of SDFNetwork (neus_fields.py:268-283) and, with want_grad, the
+    ∇ₓSDF pass of SDFNetwork.gradient (neus_fields.py:291-303).
+
+    Returns a dict of device buffers; with keep=True everything the backward
+    needs (layer inputs U_l, softplus' σ_l, ∇ pass adjoints S_l) is retained.
+    """
+    M, dev = x.shape[0], x.device
+    nl, sk, HL, KE = lay.n_lin, lay.skip, lay.HL, lay.KE
+    keep_sig = keep or want_grad
+    U = [None] * nl
+    Sig = [None] * (nl - 1)
+    U[0] = _empty(M, KE, dev)
+    Usk, e_view = None, None
+    if sk >= 0:
+        Usk = _empty(M, HL, dev)
+        o = lay.out_dim[sk - 1]
+        e_view = Usk[:, o:o + lay.E]
+    ops.sdf_embed(x, lay.multires, lay.scale, U[0], e_view, SQRT2)
+    for l in range(nl - 1):
+        into = (l + 1) == sk
+        out = Usk if into else _empty(M, HL, dev)
+        sig = _empty(M, HL, dev) if keep_sig else None
+        K = KE if l == 0 else rup(lay.in_dim[l], 32)
+        ops.linear(U[l], pk.Bf[l], lay.out_dim[l], K, out, EPI_SOFTPLUS, bias=pk.b[l], out1=sig,
+                   nzero=lay.out_dim[l] if into else HL, odiv=SQRT2 if into else 1.0, beta=lay.beta,
+                   threshold=lay.threshold)
+        U[l + 1], Sig[l] = out, sig
+        if not keep_sig and l >= 1 and (l != sk):
+            U[l] = None  # free as we go on the no-grad sampler path
+    L8 = nl - 1
+    sdf = sdf_out if sdf_out is not None else _empty(M, 1, dev)
+    ops.row_head(U[L8], lay.in_dim[L8], pk.w80, pk.b80, 1, 0, sdf, dst_index=dst)
+    feat = None
+    if want_feat:
+        feat = _empty(M, rup(lay.H_feat, 128), dev)
+        ops.linear(U[L8], pk.Bf8, lay.H_feat, rup(lay.in_dim[L8], 32), feat, EPI_STORE, bias=pk.bf8,
+                   nzero=feat.shape[1])
+    G, S = None, None
+    if want_grad:
+        S = [None] * (nl - 1)
+        S[L8 - 1] = _empty(M, HL, dev)
+        ops.scale_cols(Sig[L8 - 1], HL, pk.w80p, S[L8 - 1])
+        QE = _empty(M, KE, dev) if sk >= 0 else None
+        for l in range(L8 - 1, 0, -1):
+            Kl = rup(lay.out_dim[l], 32)
+            S[l - 1] = _empty(M, HL, dev)
+            if l == sk:
+                ops.linear(S[l], pk.Bt[l], lay.in_dim[l], Kl, S[l - 1], EPI_MUL, aux0=Sig[l - 1],
+                           nsplit=lay.out_dim[l - 1], out_split=QE, nzero=HL, adiv=SQRT2)
+            else:
+                ops.linear(S[l], pk.Bt[l], lay.out_dim[l - 1], Kl, S[l - 1], EPI_MUL, aux0=Sig[l - 1], nzero=HL)
+        Q0 = _empty(M, KE, dev)
+        ops.linear(S[0], pk.Bt[0], lay.E, rup(lay.out_dim[0], 32), Q0, EPI_STORE, nzero=KE)
+        G = _empty(M, 4, dev)
+        ops.sdf_grad_assemble(lay.multires, lay.scale, U[0], Q0, QE, G)
+    return {"U": U, "Sig": Sig, "S": S, "sdf": sdf, "feat": feat, "G": G}
+
+
+def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG):
+    """Parameter gradients of SDFNetwork for upstream (dL/dsdf, dL/dfeature,
+    dL/d∇ₓSDF).  The ∇ₓSDF term (the create_graph double backward of
+    neus_fields.py:296) is computed forward-over-reverse:
+
+      tangent   u̇_0 = J_emb(x)·v,  ż_l = W_l u̇_l,  u̇_{l+1} = σ_l ⊙ ż_l
+      adjoint   Z_l = (W_{l+1}ᵀ Z_{l+1}) ⊙ σ_l + β s_l ⊙ (1-σ_l) ⊙ ż_l
+      weights   dW_l = Σ_m Z_l u_lᵀ + s_l u̇_lᵀ,   db_l = Σ_m Z_l
+
+    where s_l are the ∇ pass adjoints kept from the forward.  Six GEMMs per
+    layer instead of autograd's nine.
+    """
+    U, Sig, S = st["U"], st["Sig"], st["S"]
+    M, dev = U[0].shape[0], U[0].device
+    nl, sk, HL, KE = lay.n_lin, lay.skip, lay.HL, lay.KE
+    L8 = nl - 1
+    second = dG is not None
+    if second and S is None:
+        raise RuntimeError("SDF double backward needs the ∇ pass buffers (want_grad=True in forward)")
+    Ud, R = None, [None] * (nl - 1)
+    if second:
+        Ud = [None] * nl
+        Ud[0] = _empty(M, KE, dev)
+        Usk_d, e_view = None, None
+        if sk >= 0:
+            Usk_d = _empty(M, HL, dev)
+            o = lay.out_dim[sk - 1]
+            e_view = Usk_d[:, o:o + lay.E]
+        ops.sdf_tangent_prep(lay.multires, lay.scale, U[0], dG, Ud[0], e_view, SQRT2)
+        for l in range(nl - 1):
+            into = (l + 1) == sk
+            out = Usk_d if into else _empty(M, HL, dev)
+            R[l] = _empty(M, HL, dev)
+            K = KE if l == 0 else rup(lay.in_dim[l], 32)
+            ops.linear(Ud[l], pk.Bf[l], lay.out_dim[l], K, out, EPI_TANGENT, aux0=Sig[l], aux1=S[l], out1=R[l],
+                       nzero=lay.out_dim[l] if into else HL, odiv=SQRT2 if into else 1.0, beta=lay.beta)
+            Ud[l + 1] = out
+
+    i8, o8 = lay.in_dim[L8], lay.out_dim[L8]
+    dW8 = torch.empty(o8, i8, device=dev)
+    db8 = torch.empty(o8, device=dev)
+    if dfeat is not None:
+        ops.wgrad(dfeat, U[L8], lay.H_feat, i8, dW8[1:], db=db8[1:])
+    else:
+        dW8[1:].zero_()
+        db8[1:].zero_()
+    dsdf_flat = None
+    if dsdf is not None:
+        dsdf = dsdf.reshape(M, 1).contiguous()
+        dsdf_flat = dsdf
+        ops.colsum(U[L8], i8, dW8[0], w=dsdf, wdiv=lay.scale)
+        ops.colsum(dsdf, 1, db8[0:1], wdiv=lay.scale)
+    else:
+        dW8[0].zero_()
+        db8[0].zero_()
+    if second:
+        ops.colsum(Ud[L8], i8, dW8[0], wdiv=lay.scale, accumulate=True)
+
+    phi = dfeat if dfeat is not None else torch.zeros(M, lay.H_feat, device=dev)
+    Z = _empty(M, HL, dev)
+    ops.linear(phi, pk.Bt8, lay.out_dim[L8 - 1], rup(lay.H_feat, 32), Z, EPI_BWD_SOFTPLUS,
+               rowv=dsdf_flat, colv=pk.w80p if dsdf_flat is not None else None, aux0=Sig[L8 - 1],
+               aux1=R[L8 - 1], nzero=HL)
+    dWs, dbs = [None] * nl, [None] * nl
+    dWs[L8], dbs[L8] = dW8, db8
+    for l in range(L8 - 1, -1, -1):
+        Zl = Z
+        if l > 0:
+            Z = _empty(M, HL, dev)
+            ops.linear(Zl, pk.Bt[l], lay.out_dim[l - 1], rup(lay.out_dim[l], 32), Z, EPI_BWD_SOFTPLUS,
+                       aux0=Sig[l - 1], aux1=R[l - 1], nzero=HL, adiv=SQRT2 if l == sk else 1.0)
+        dW = torch.empty(lay.out_dim[l], lay.in_dim[l], device=dev)
+        db = torch.empty(lay.out_dim[l], device=dev)
+        ops.wgrad(Zl, U[l], lay.out_dim[l], lay.in_dim[l], dW, db=db,
+                  Y1=S[l] if second else None, X1=Ud[l] if second else None)
+        dWs[l], dbs[l] = dW, db
+        R[l] = None
+    return dWs, dbs
+
+
+class _SDFFieldFn(torch.autograd.Function):
+    """(x [M,4], weights...) -> (sdf [M,1], feature [M,H], ∇ₓSDF [M,4])."""
+
+    @staticmethod
+    def forward(ctx, x, lay, pk, want_feat, want_grad, *params):
+        ctx.set_materialize_grads(False)
+        keep = any(ctx.needs_input_grad[5:])
+        st = sdf_forward(lay, pk, x, want_feat=want_feat, want_grad=want_grad, keep=keep)
+        ctx.lay, ctx.pk, ctx.st = lay, pk, (st if keep else None)
+        ctx.nparams = len(params)
+        empty = x.new_empty(0)
+        feat = st["feat"][:, :lay.H_feat] if want_feat else empty
+        G = st["G"] if want_grad else x.new_empty(0)
+        if not want_feat:
+            ctx.mark_non_differentiable(feat)
+        if not want_grad:
+            ctx.mark_non_differentiable(G)
+        return st["sdf"], feat, G
+
+    @staticmethod
+    def backward(ctx, dsdf, dfeat, dG):
+        if ctx.needs_input_grad[0]:
+            raise NotImplementedError("copenerf: gradients w.r.t. SDF input points (ray / pose gradients, "
+                                      "eval.py:51-82) are not implemented yet")
+        none5 = (None,) * 5
+        if ctx.st is None:
+            return none5 + (None,) * ctx.nparams
+        if dfeat is not None and dfeat.stride(1) != 1:
+            dfeat = dfeat.contiguous()
+        if dG is not None:
+            dG = dG.contiguous()
+        dWs, dbs = sdf_backward(ctx.lay, ctx.pk, ctx.st, dsdf, dfeat, dG)
+        ctx.st = None
+        grads = []
+        for w, b in zip(dWs, dbs):
+            grads += [w, b]
+        return none5 + tuple(grads)
+
+
+def _init_geometric(lin: nn.Linear, l: int, dims, out_dim, skip_in, multires, n_lin, bias, inside_outside,
+                    d_pos: int):
+    """Geometric (sphere) initialisation of IDR / NeuS (neus_fields.py:241-259),
+    in the same RNG order as the reference so seeded builds give equal weights."""
+    if l == n_lin - 1:
+        mean = np.sqrt(np.pi) / np.sqrt(dims[l])
+        torch.nn.init.normal_(lin.weight, mean=-mean if inside_outside else mean, std=0.0001)
+        torch.nn.init.constant_(lin.bias, bias if inside_outside else -bias)
+    elif multires > 0 and l == 0:
+        torch.nn.init.constant_(lin.bias, 0.0)
+        torch.nn.init.constant_(lin.weight[:, d_pos:], 0.0)
+        torch.nn.init.normal_(lin.weight[:, :d_pos], 0.0, np.sqrt(2) / np.sqrt(out_dim))
+    elif multires > 0 and l in skip_in:
+        torch.nn.init.constant_(lin.bias, 0.0)
+        torch.nn.init.normal_(lin.weight, 0.0, np.sqrt(2) / np.sqrt(out_dim))
+        torch.nn.init.constant_(lin.weight[:, -(dims[0] - d_pos):], 0.0)
+    else:
+        torch.nn.init.constant_(lin.bias, 0.0)
+        torch.nn.init.normal_(lin.weight, 0.0, np.sqrt(2) / np.sqrt(out_dim))
+
+
+class SDFNetwork(nn.Module):
+    """Reference: model/neus_fields.py:205-303 (IDR SDF MLP, Softplus(beta=100))."""
+
+    def __init__(self, d_in, d_out, d_hidden, n_layers, skip_in=(4,), multires=0, bias=0.5, scale=1,
+                 geometric_init=True, weight_norm=True, inside_outside=False):
+        super().__init__()
+        dims = [d_in] + [d_hidden for _ in range(n_layers)] + [d_out]
+        if multires > 0:
+            dims[0] = embed_dim(multires, d_in)
+        self.d_in = d_in
+        self.multires = multires
+        self.num_layers = len(dims)
+        self.skip_in = list(skip_in)
+        self.scale = scale
+        self.dims = dims
+        n_lin = self.num_layers - 1
+        for l in range(n_lin):
+            out_dim = dims[l + 1] - dims[0] if (l + 1) in self.skip_in else dims[l + 1]
+            lin = nn.Linear(dims[l], out_dim)
+            if geometric_init:
+                _init_geometric(lin, l, dims, out_dim, self.skip_in, multires, n_lin, bias, inside_outside, 4)
+            if weight_norm:
+                lin = nn.utils.weight_norm(lin)
+            setattr(self, "lin" + str(l), lin)
+        self.activation = nn.Softplus(beta=100)
+        self._layout = None
+
+    # -- kernel plumbing ---------------------------------------------------
+    def layout(self) -> SDFLayout:
+        if self._layout is None:
+            if self.d_in != 4:
+                raise NotImplementedError("copenerf SDF kernels take (x, y, z, t) inputs (d_in = 4)")
+            if len(self.skip_in) > 1 or any(s <= 0 for s in self.skip_in):
+                raise NotImplementedError("copenerf SDF kernels support one skip connection")
+            n_lin = self.num_layers - 1
+            in_dim, out_dim = [], []
+            for l in range(n_lin):
+                lin = getattr(self, "lin" + str(l))
+                w = lin.weight_v if hasattr(lin, "weight_v") else lin.weight
+                out_dim.append(w.shape[0])
+                in_dim.append(w.shape[1])
+            E = self.dims[0]
+            hl = rup(max(max(in_dim), max(out_dim[:-1]), out_dim[-1] - 1), 128)
+            self._layout = SDFLayout(n_lin=n_lin, in_dim=in_dim, out_dim=out_dim, E=E, KE=rup(E, 64), HL=hl,
+                                     skip=self.skip_in[0] if self.skip_in else -1, multires=self.multires,
+                                     scale=float(self.scale), beta=float(self.activation.beta),
+                                     threshold=float(self.activation.threshold))
+        return self._layout
+
+    def params_and_pack(self):
+        """Effective weights (autograd-tracked) and their padded kernel images."""
+        lay = self.layout()
+        Ws, bs = [], []
+        for l in range(lay.n_lin):
+            lin = getattr(self, "lin" + str(l))
+            Ws.append(effective_weight(lin))
+            bs.append(lin.bias)
+        return Ws, bs, pack_sdf(lay, Ws, bs)
+
+    def field(self, x, *, want_feat=True, want_grad=True, packed=None):
+        """Fused (sdf, feature, ∇ₓsdf) of the points x [M, 4] in one launch sequence."""
+        Ws, bs, pk = packed if packed is not None else self.params_and_pack()
+        params = []
+        for w, b in zip(Ws, bs):
+            params += [w, b]
+        x = x.contiguous()
+        return _SDFFieldFn.apply(x, self.layout(), pk, want_feat, want_grad, *params)
+
+    # -- reference API -------------------------------------------------------
+    def forward(self, inputs):
+        sdf, feat, _ = self.field(inputs, want_feat=True, want_grad=False)
+        return torch.cat([sdf, feat], dim=-1)
+
+    def sdf(self, x):
+        sdf, _, _ = self.field(x, want_feat=False, want_grad=False)
+        return sdf
+
+    def sdf_hidden_appearance(self, x):
+        return self.forward(x)
+
+    def gradient(self, x):
+        _, _, g = self.field(x.detach(), want_feat=False, want_grad=True)
+        return g.unsqueeze(1)
+
+
+# ---------------------------------------------------------------------------
+# Colour network (mode 'idr')
+@dataclasses.dataclass
+class ColorLayout:
+    F: int          # feature width (256)
+    P: int          # point width (4: pts_time)
+    V: int          # encoded view-dir width (27)
+    Gd: int         # gradient width (4)
+    KX: int         # padded extras width (64)
+    HL: int
+    n_lin: int
+    in_dim: List[int]
+    out_dim: List[int]
+    multires_view: int
+
+
+@dataclasses.dataclass
+class ColorPack:
+    Bf: list
+    Bt: list
+    b: list
+    W3: torch.Tensor   # [3][H]
+    b3: torch.Tensor
+    Btf: torch.Tensor  # feature columns of lin0, transposed
+    Wg: torch.Tensor   # [4][H]: gradient columns of lin0, transposed
+
+
+def pack_color(lay: ColorLayout, Ws, bs) -> ColorPack:
+    with torch.no_grad():
+        P, V, Gd, Fd = lay.P, lay.V, lay.Gd, lay.F
+        W0 = Ws[0].detach()
+        o = W0.shape[0]
+        pts, emb, g, feat = (W0[:, 0:P], W0[:, P:P + V], W0[:, P + V:P + V + Gd], W0[:, P + V + Gd:])
+        ext = torch.cat([g, pts, emb], 1)
+        W0k = torch.cat([feat, F.pad(ext, (0, lay.KX - ext.shape[1]))], 1)
+        Bf = [F.pad(W0k, (0, 0, 0, rup(o, 128) - o)).contiguous()]
+        Bt = [None]
+        b = [bs[0].detach().contiguous()]
+        for l in range(1, lay.n_lin - 1):
+            W = Ws[l].detach()
+            oo, ii = W.shape
+            Bf.append(F.pad(W, (0, rup(ii, 32) - ii, 0, rup(oo, 128) - oo)).contiguous())
+            Bt.append(F.pad(W.t(), (0, rup(oo, 32) - oo, 0, rup(ii, 128) - ii)).contiguous())
+            b.append(bs[l].detach().contiguous())
+        Btf = F.pad(feat.t(), (0, rup(o, 32) - o, 0, rup(Fd, 128) - Fd)).contiguous()
+        Wg = g.t().contiguous()
+        return ColorPack(Bf, Bt, b, Ws[-1].detach().contiguous(), bs[-1].detach().contiguous(), Btf, Wg)
+
+
+class _ColorFieldFn(torch.autograd.Function):
+    """(pts_time [M,4], dirs, ∇ₓSDF [M,4], feature [M,F], weights...) -> rgb [M,3]."""
+
+    @staticmethod
+    def forward(ctx, pts, dirs, dir_div, G, feat, lay, pk, *params):
+        ctx.set_materialize_grads(False)
+        M, dev = pts.shape[0], pts.device
+        ext = _empty(M, lay.KX, dev)
+        ops.color_extras(G, pts, dirs, dir_div, lay.multires_view, ext)
+        H = []
+        A, A2, K1, K = feat, ext, lay.F, lay.F + lay.KX
+        for l in range(lay.n_lin - 1):
+            out = _empty(M, lay.HL, dev)
+            ops.linear(A, pk.Bf[l], lay.out_dim[l], K, out, EPI_RELU, bias=pk.b[l], A2=A2, K1=K1, nzero=lay.HL)
+            H.append(out)
+            A, A2, K1, K = out, None, None, rup(lay.out_dim[l], 32)
+        rgb = _empty(M, 3, dev)
+        ops.row_head(H[-1], lay.in_dim[-1], pk.W3, pk.b3, 3, 1, rgb)
+        ctx.lay, ctx.pk = lay, pk
+        ctx.bufs = (feat, ext, H, rgb)
+        return rgb
+
+    @staticmethod
+    def backward(ctx, drgb):
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            raise NotImplementedError("copenerf: colour-network gradients w.r.t. points / view directions "
+                                      "(ray / pose gradients) are not implemented yet")
+        lay, pk = ctx.lay, ctx.pk
+        feat, ext, H, rgb = ctx.bufs
+        ctx.bufs = None
+        nparams = 2 * lay.n_lin
+        if drgb is None:
+            return (None,) * (7 + nparams)
+        M, dev = rgb.shape[0], rgb.device
+        drgb = drgb.contiguous()
+        n = lay.n_lin
+        dWs, dbs = [None] * n, [None] * n
+        dWs[n - 1] = torch.empty(3, lay.in_dim[n - 1], device=dev)
+        dbs[n - 1] = torch.empty(3, device=dev)
+        dZ = _empty(M, lay.HL, dev)
+        ops.rgb_head_bwd(drgb, rgb, H[-1], lay.in_dim[n - 1], pk.W3, dZ, dWs[n - 1], dbs[n - 1])
+        for l in range(n - 2, 0, -1):
+            dW = torch.empty(lay.out_dim[l], lay.in_dim[l], device=dev)
+            db = torch.empty(lay.out_dim[l], device=dev)
+            ops.wgrad(dZ, H[l - 1], lay.out_dim[l], lay.in_dim[l], dW, db=db)
+            dWs[l], dbs[l] = dW, db
+            dZp = _empty(M, lay.HL, dev)
+            ops.linear(dZ, pk.Bt[l], lay.out_dim[l - 1], rup(lay.out_dim[l], 32), dZp, EPI_BWD_RELU, aux0=H[l - 1],
+                       nzero=lay.HL)
+            dZ = dZp
+        o0 = lay.out_dim[0]
+        dWf = torch.empty(o0, lay.F, device=dev)
+        db0 = torch.empty(o0, device=dev)
+        ops.wgrad(dZ, feat, o0, lay.F, dWf, db=db0)
+        dWx = torch.empty(o0, lay.KX, device=dev)
+        ops.wgrad(dZ, ext, o0, lay.KX, dWx)
+        P, V, Gd = lay.P, lay.V, lay.Gd
+        # back to the reference column order [pts | emb(dirs) | gradients | feature]
+        dWs[0] = torch.cat([dWx[:, Gd:Gd + P], dWx[:, Gd + P:Gd + P + V], dWx[:, 0:Gd], dWf], 1)
+        dbs[0] = db0
+        dfeat = None
+        if ctx.needs_input_grad[4]:
+            dfeat = _empty(M, lay.F, dev)
+            ops.linear(dZ, pk.Btf, lay.F, rup(o0, 32), dfeat, EPI_STORE, nzero=lay.F)
+        dG = None
+        if ctx.needs_input_grad[3]:
+            dG = _empty(M, Gd, dev)
+            ops.row_head(dZ, o0, pk.Wg, None, Gd, 0, dG)
+        grads = []
+        for w, b in zip(dWs, dbs):
+            grads += [w, b]
+        return (None, None, None, dG, dfeat, None, None) + tuple(grads)
+
+
+class RenderingNetwork(nn.Module):
+    """Reference: model/neus_fields.py:307-374."""
+
+    def __init__(self, d_feature, mode, d_in, d_out, d_hidden, n_layers, weight_norm=True, multires_view=0,
+                 squeeze_out=True, use_negative_ray_vector=False):
+        super().__init__()
+        self.mode = mode
+        self.squeeze_out = squeeze_out
+        self.use_negative_ray_vector = use_negative_ray_vector
+        dims = [d_in + d_feature] + [d_hidden for _ in range(n_layers)] + [d_out]
+        self.multires_view = multires_view
+        if multires_view > 0:
+            dims[0] += embed_dim(multires_view, 3) - 3
+        self.num_layers = len(dims)
+        self.d_feature = d_feature
+        self.d_in = d_in
+        for l in range(0, self.num_layers - 1):
+            lin = nn.Linear(dims[l], dims[l + 1])
+            if weight_norm:
+                lin = nn.utils.weight_norm(lin)
+            setattr(self, "lin" + str(l), lin)
+        self.relu = nn.ReLU()
+        self._layout = None
+
+    def layout(self) -> ColorLayout:
+        if self._layout is None:
+            if self.mode != "idr" or not self.squeeze_out or self.use_negative_ray_vector:
+                raise NotImplementedError("copenerf colour kernels implement mode='idr', squeeze_out=True, "
+                                          "use_negative_ray_vector=False (every shipped config)")
+            n = self.num_layers - 1
+            in_dim, out_dim = [], []
+            for l in range(n):
+                lin = getattr(self, "lin" + str(l))
+                w = lin.weight_v if hasattr(lin, "weight_v") else lin.weight
+                out_dim.append(w.shape[0])
+                in_dim.append(w.shape[1])
+            V = embed_dim(self.multires_view, 3)
+            P, Gd = 4, 4
+            if self.d_in != P + 3 + Gd or out_dim[-1] != 3 or self.d_feature % 32 != 0:
+                raise NotImplementedError("copenerf colour kernels expect d_in = 11 (pts_time, dirs, gradients), "
+                                          "d_out = 3, d_feature % 32 == 0")
+            hl = rup(max(out_dim[:-1]), 128)
+            self._layout = ColorLayout(F=self.d_feature, P=P, V=V, Gd=Gd, KX=rup(P + V + Gd, 64), HL=hl, n_lin=n,
+                                       in_dim=in_dim, out_dim=out_dim, multires_view=self.multires_view)
+        return self._layout
+
+    def params_and_pack(self):
+        lay = self.layout()
+        Ws, bs = [], []
+        for l in range(lay.n_lin):
+            lin = getattr(self, "lin" + str(l))
+            Ws.append(effective_weight(lin))
+            bs.append(lin.bias)
+        return Ws, bs, pack_color(lay, Ws, bs)
+
+    def color(self, points, normals, dirs, dir_div, feature_vectors, packed=None):
+        """rgb [M,3]; dirs is [M/dir_div, 3] (one row per ray when dir_div = S)."""
+        Ws, bs, pk = packed if packed is not None else self.params_and_pack()
+        params = []
+        for w, b in zip(Ws, bs):
+            params += [w, b]
+        if feature_vectors.stride(1) != 1:
+            feature_vectors = feature_vectors.contiguous()
+        return _ColorFieldFn.apply(points.contiguous(), dirs.contiguous(), int(dir_div), normals.contiguous(),
+                                   feature_vectors, self.layout(), pk, *params)
+
+    def forward(self, points, normals, view_dirs, feature_vectors):
+        return self.color(points, normals, view_dirs, 1, feature_vectors)
+
+
+class SingleVarianceNetwork(nn.Module):
+    """Reference: model/neus_fields.py:459-465."""
+
+    def __init__(self, init_val):
+        super().__init__()
+        self.register_parameter("variance", nn.Parameter(torch.tensor(init_val)))
+
+    def forward(self, x):
+        return torch.ones([len(x), 1], device=self.variance.device) * torch.exp(self.variance * 10.0)
+
+
+class NeRF(nn.Module):
+    """Reference: model/neus_fields.py:378-456.  Background (NeRF++) density MLP;
+    constructed by train.py:39 so checkpoints keep their keys, but rendered only
+    when n_outside > 0, which no shipped config sets -- out of scope here."""
+
+    def __init__(self, D=8, W=256, d_in=3, d_in_view=3, multires=0, multires_view=0, output_ch=4, skips=[4],
+                 use_viewdirs=False):
+        super().__init__()
+        self.D, self.W, self.d_in, self.d_in_view = D, W, d_in, d_in_view
+        self.input_ch = embed_dim(multires, d_in) if multires > 0 else 3
+        self.input_ch_view = embed_dim(multires_view, d_in_view) if multires_view > 0 else 3
+        self.skips = skips
+        self.use_viewdirs = use_viewdirs
+        self.pts_linears = nn.ModuleList(
+            [nn.Linear(self.input_ch, W)] +
+            [nn.Linear(W, W) if i not in self.skips else nn.Linear(W + self.input_ch, W) for i in range(D - 1)])
+        self.views_linears = nn.ModuleList([nn.Linear(self.input_ch_view + W, W // 2)])
+        if use_viewdirs:
+            self.feature_linear = nn.Linear(W, W)
+            self.alpha_linear = nn.Linear(W, 1)
+            self.rgb_linear = nn.Linear(W // 2, 3)
+        else:
+            self.output_linear = nn.Linear(W, output_ch)
+
+    def forward(self, input_pts, input_views):
+        raise NotImplementedError("NeRF++ background branch (n_outside > 0) is out of scope (SURVEY.md §2)")

@@ -1,0 +1,199 @@
+"""Tensor-level wrappers over the C ABI (one function per entry point).
+
+Every wrapper checks device, dtype and layout on the host, then launches on
+torch's current HIP stream.  Buffers are plain 2-D fp32 row-major tensors whose
+leading dimension (stride(0)) is passed explicitly, so column views such as
+``buf[:, :256]`` can be handed over without copies.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _lib
+from ._lib import (EPI_BWD_RELU, EPI_BWD_SOFTPLUS, EPI_MUL, EPI_RELU, EPI_SOFTPLUS, EPI_STORE,  # noqa: F401
+                   EPI_TANGENT)
+
+SQRT2 = float(math.sqrt(2.0))  # torch's x / np.sqrt(2) divides by the fp32 rounding of this
+
+
+def rup(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _need(t, name, *, ndim=2):
+    if t is None:
+        return
+    if not t.is_cuda:
+        raise RuntimeError(f"copenerf: {name} must be a CUDA/HIP tensor (got {t.device}); "
+                           "the HIP kernels have no CPU fallback")
+    if t.dtype != torch.float32 and t.dtype != torch.int32:
+        raise RuntimeError(f"copenerf: {name} must be float32 (got {t.dtype})")
+    if ndim == 2 and (t.dim() != 2 or t.stride(1) != 1):
+        raise RuntimeError(f"copenerf: {name} must be a row-major 2-D tensor (shape {tuple(t.shape)}, "
+                           f"strides {t.stride()})")
+
+
+def _ld(t):
+    return 0 if t is None else t.stride(0)
+
+
+def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None, colv=None, aux0=None,
+           aux1=None, out1=None, out_split=None, nsplit=None, nzero=None, adiv=1.0, odiv=1.0, beta=100.0,
+           threshold=20.0, tile=None, M=None):
+    """out = epilogue((A|A2) @ B[:N].T / adiv) -- cn_linear."""
+    for t, n in ((A, "A"), (A2, "A2"), (B, "B"), (out0, "out0"), (out1, "out1"), (aux0, "aux0"),
+                 (aux1, "aux1"), (out_split, "out_split")):
+        _need(t, n)
+    M = A.shape[0] if M is None else M
+    if tile is None:
+        tile = 1 if N <= 64 else 0
+    bn = 64 if tile == 1 else 128
+    if B.shape[0] < rup(N, bn) or B.shape[1] < K:
+        raise RuntimeError(f"cn_linear: B {tuple(B.shape)} too small for N={N}, K={K} (tile {tile})")
+    if out0.shape[0] < M:
+        raise RuntimeError("cn_linear: out0 has fewer rows than A")
+    d = _lib.LinearDesc()
+    d.A, d.A2, d.B, d.bias = _ptr(A), _ptr(A2), _ptr(B), _ptr(bias)
+    d.rowv, d.colv, d.aux0, d.aux1 = _ptr(rowv), _ptr(colv), _ptr(aux0), _ptr(aux1)
+    d.out0, d.out1, d.out_split = _ptr(out0), _ptr(out1), _ptr(out_split)
+    d.lda, d.lda2, d.ldb = _ld(A), _ld(A2), _ld(B)
+    d.ld_aux0, d.ld_aux1, d.ld_out0, d.ld_out1, d.ld_split = _ld(aux0), _ld(aux1), _ld(out0), _ld(out1), _ld(out_split)
+    d.M, d.N, d.K = M, N, K
+    d.K1 = K1 if K1 is not None else K
+    d.nzero = nzero if nzero is not None else N
+    d.nsplit = nsplit if nsplit is not None else N
+    d.epilogue, d.tile = epilogue, tile
+    d.adiv, d.odiv, d.beta, d.threshold = adiv, odiv, beta, threshold
+    _lib.check(_lib.load().cn_linear(d, _stream()), "cn_linear")
+    return out0
+
+
+def wgrad(Y0, X0, N, K, dW, *, db=None, Y1=None, X1=None, accumulate=False):
+    """dW[:n_out, :k_out] (+)= Y0ᵀX0 (+ Y1ᵀX1), db = colsum(Y0) -- cn_wgrad."""
+    for t, n in ((Y0, "Y0"), (X0, "X0"), (Y1, "Y1"), (X1, "X1"), (dW, "dW")):
+        _need(t, n)
+    M = Y0.shape[0]
+    lib = _lib.load()
+    nbytes = lib.cn_wgrad_workspace_bytes(M, N, K)
+    ws = torch.empty(nbytes // 4 + 1, device=Y0.device, dtype=torch.float32)
+    d = _lib.WgradDesc()
+    d.Y0, d.X0, d.Y1, d.X1 = _ptr(Y0), _ptr(X0), _ptr(Y1), _ptr(X1)
+    d.workspace, d.dW, d.db = _ptr(ws), _ptr(dW), _ptr(db)
+    d.ldy0, d.ldx0, d.ldy1, d.ldx1, d.ld_dw = _ld(Y0), _ld(X0), _ld(Y1), _ld(X1), _ld(dW)
+    d.workspace_bytes = ws.numel() * 4
+    d.M, d.N, d.K = M, N, rup(K, 64)
+    d.npairs = 2 if Y1 is not None else 1
+    d.n_out, d.k_out = dW.shape[0], dW.shape[1]
+    d.accumulate = 1 if accumulate else 0
+    _lib.check(lib.cn_wgrad(d, _stream()), "cn_wgrad")
+    return dW
+
+
+def row_head(A, K, W, b, C, act, out, dst_index=None, ld_out=None):
+    """out[dst(m)*ld_out + c] = act(A[m] . W[c] + b[c]); ld_out defaults to C (out [M, C])."""
+    _need(A, "A")
+    _need(W, "W")
+    if dst_index is not None and (dst_index.dtype != torch.int32 or not dst_index.is_contiguous()):
+        raise RuntimeError("row_head: dst_index must be contiguous int32")
+    if not out.is_contiguous():
+        raise RuntimeError("row_head: out must be contiguous")
+    _lib.call("cn_row_head", A.shape[0], K, _ptr(A), _ld(A), _ptr(W), _ld(W), _ptr(b), C, act, _ptr(out),
+              C if ld_out is None else ld_out, _ptr(dst_index), _stream())
+    return out
+
+
+def scale_cols(X, N, w, out):
+    _need(X, "X")
+    _need(out, "out")
+    _lib.call("cn_scale_cols", X.shape[0], N, _ptr(X), _ld(X), _ptr(w), _ptr(out), _ld(out), _stream())
+    return out
+
+
+def colsum(X, K, out, *, w=None, wdiv=1.0, accumulate=False):
+    _need(X, "X")
+    M = X.shape[0]
+    lib = _lib.load()
+    ws = torch.empty(lib.cn_colsum_workspace_bytes(M, K) // 4 + 1, device=X.device, dtype=torch.float32)
+    _lib.call("cn_colsum", M, K, _ptr(w), _ptr(X), _ld(X), wdiv, _ptr(out), 1 if accumulate else 0, _ptr(ws),
+              ws.numel() * 4, _stream())
+    return out
+
+
+def sdf_embed(x, multires, scale, U0, U4e=None, u4div=1.0):
+    _need(x, "x")
+    _need(U0, "U0")
+    _lib.call("cn_sdf_embed", x.shape[0], _ptr(x), _ld(x), multires, scale, U0.shape[1], _ptr(U0), _ld(U0),
+              _ptr(U4e), _ld(U4e), u4div, _stream())
+    return U0
+
+
+def sdf_grad_assemble(multires, scale, U0, Q0, QE, G):
+    _lib.call("cn_sdf_grad_assemble", U0.shape[0], multires, scale, _ptr(U0), _ld(U0), _ptr(Q0), _ld(Q0),
+              _ptr(QE), _ld(QE), _ptr(G), _ld(G), _stream())
+    return G
+
+
+def sdf_tangent_prep(multires, scale, U0, v, T0, T4e=None, t4div=1.0):
+    _need(v, "v")
+    _lib.call("cn_sdf_tangent_prep", U0.shape[0], multires, scale, T0.shape[1], _ptr(U0), _ld(U0), _ptr(v),
+              _ld(v), _ptr(T0), _ld(T0), _ptr(T4e), _ld(T4e), t4div, _stream())
+    return T0
+
+
+def color_extras(G, pts, dirs, dir_div, multires_view, ext):
+    for t, n in ((G, "G"), (pts, "pts"), (dirs, "dirs"), (ext, "ext")):
+        _need(t, n)
+    _lib.call("cn_color_extras", G.shape[0], _ptr(G), _ld(G), _ptr(pts), _ld(pts), _ptr(dirs), _ld(dirs),
+              dir_div, multires_view, ext.shape[1], _ptr(ext), _ld(ext), _stream())
+    return ext
+
+
+def rgb_head_bwd(drgb, rgb, H3, K, W3, dZ2, dW3, db3):
+    M = rgb.shape[0]
+    lib = _lib.load()
+    ws = torch.empty(lib.cn_rgb_head_bwd_workspace_bytes(M, K) // 4 + 1, device=rgb.device, dtype=torch.float32)
+    _lib.call("cn_rgb_head_bwd", M, K, _ptr(drgb), _ptr(rgb), _ptr(H3), _ld(H3), _ptr(W3), _ptr(dZ2), _ld(dZ2),
+              _ptr(dW3), _ptr(db3), _ptr(ws), ws.numel() * 4, _stream())
+
+
+def coarse_z(near, far, n, t_rand, z):
+    _lib.call("cn_coarse_z", z.shape[0], n, _ptr(near), _ptr(far), _ptr(t_rand), _ptr(z), _stream())
+    return z
+
+
+def points(rays_o, rays_d, z, t, pts, *, mid=False, near=None, far=None, n_coarse=0):
+    R, n = z.shape
+    _lib.call("cn_points", R, n, _ptr(rays_o), _ptr(rays_d), _ptr(z), _ptr(t), 1 if mid else 0, _ptr(near),
+              _ptr(far), n_coarse, _ptr(pts), _stream())
+    return pts
+
+
+def up_sample_merge(z, sdf, n_imp, inv_s, z_out, z_new, sdf_out=None, new_dst=None):
+    R, n = z.shape
+    _lib.call("cn_up_sample_merge", R, n, n_imp, float(inv_s), _ptr(z), _ptr(sdf), _ptr(z_out), _ptr(z_new),
+              _ptr(sdf_out), _ptr(new_dst), _stream())
+
+
+def composite_fwd(z, sdf, G, rgb, rays_d, inv_s, near, far, n_coarse, car, color, depth, weights, cdf):
+    R, S = z.shape
+    _lib.call("cn_composite_fwd", R, S, _ptr(z), _ptr(sdf), _ptr(G), G.stride(0), _ptr(rgb), _ptr(rays_d),
+              _ptr(inv_s), _ptr(near), _ptr(far), n_coarse, float(car), _ptr(color), _ptr(depth), _ptr(weights),
+              _ptr(cdf), _stream())
+
+
+def composite_bwd(z, sdf, G, rgb, rays_d, inv_s, near, far, n_coarse, car, dcolor, ddepth, dweights, dcdf,
+                  dsdf, dG, drgb, dinv_part):
+    R, S = z.shape
+    _lib.call("cn_composite_bwd", R, S, _ptr(z), _ptr(sdf), _ptr(G), G.stride(0), _ptr(rgb), _ptr(rays_d),
+              _ptr(inv_s), _ptr(near), _ptr(far), n_coarse, float(car), _ptr(dcolor), _ptr(ddepth),
+              _ptr(dweights), _ptr(dcdf), _ptr(dsdf), _ptr(dG), _ptr(drgb), _ptr(dinv_part), _stream())

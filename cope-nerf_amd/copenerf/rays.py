@@ -1,0 +1,127 @@
+"""Ray generation under SE(3) poses.
+
+Restates, on the device and without host syncs:
+  get_patch_indices                 model/training.py:413-436
+  arange_pixels (only the R needed) model/common.py:12-39
+  get_world_cameraOrigin_cameraRay  model/training.py:474-487 with
+  origin_to_world / image_points_to_world / transform_to_world  model/common.py:175-215
+  near_far_from_sphere, get_cos_anneal_ratio  model/training.py:101-124
+  vec2skew / Exp / make_c2w / convert3x4_4x4  model/common.py:255-308
+  PoseRetriever                     model/poses_retriever.py:6-32
+This is 4x4 matrix algebra plus O(R) elementwise work (microseconds), kept in
+torch device ops; the per-sample work starts at the sampler (cn_coarse_z).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+
+def get_patch_indices(h, w, patch_size, n_points, generator=None, device="cpu"):
+    """Flat pixel ids of n_points // patch_size**2 random patch_size x patch_size patches."""
+    n_patches = n_points // (patch_size ** 2)
+    h_adj, w_adj = h - patch_size + 1, w - patch_size + 1
+    n_patches = min(n_patches, h_adj * w_adj)
+    corners = torch.randperm(h_adj * w_adj, generator=generator, device=device)[:n_patches]
+    rows, cols = corners // w_adj, corners % w_adj
+    offs = torch.arange(patch_size, device=device).repeat(patch_size, 1)
+    offs = (offs + offs.t() * w).flatten()
+    return ((rows * w + cols).unsqueeze(1) + offs.view(-1)).flatten()
+
+
+def pixels_from_indices(idx, h, w):
+    """(pixel [R,2] long (x, y), normalised [R,2] float in [-1, 1]) of flat ids -- the
+    rows of arange_pixels((h, w)) the reference gathers, without building the grid."""
+    y, x = idx // w, idx % w
+    p = torch.stack([x, y], -1)
+    pn = p.float()
+    pn = torch.stack([2.0 * pn[:, 0] / (w - 1) - 1.0, 2.0 * pn[:, 1] / (h - 1) - 1.0], -1)
+    return p, pn
+
+
+def intrinsics_ndc(fx, fy, w, h, device="cpu"):
+    """K of the reference loaders (dataloading/dataset.py:108-111)."""
+    return torch.tensor([[2 * fx / w, 0, 0, 0], [0, -2 * fy / h, 0, 0], [0, 0, -1, 0], [0, 0, 0, 1]],
+                        dtype=torch.float32, device=device)
+
+
+def world_rays(pixels_norm, camera_mat, world_mat, scale_mat):
+    """rays_o [R,3], unit rays_d [R,3], |p - o| [R,1] (training.py:474-487)."""
+    inv = torch.inverse(scale_mat) @ torch.inverse(world_mat) @ torch.inverse(camera_mat)  # [4,4]
+    o = inv[:3, 3]
+    R = pixels_norm.shape[0]
+    ph = torch.cat([pixels_norm, torch.ones(R, 2, device=pixels_norm.device)], -1)  # [x, y, 1, 1]
+    pw = (ph @ inv.t())[:, :3]
+    v = pw - o
+    n = v.norm(2, -1)
+    return o.expand(R, 3).contiguous(), (v / n.unsqueeze(-1)).contiguous(), n.view(-1, 1)
+
+
+def near_far_from_sphere(rays_o, depth_range):
+    """The reference computes the sphere mid-point and then overwrites near/far
+    with the configured depth range (training.py:101-118)."""
+    R = rays_o.shape[0]
+    near = torch.full((R, 1), float(depth_range[0]), device=rays_o.device)
+    far = torch.full((R, 1), float(depth_range[1]), device=rays_o.device)
+    return near, far
+
+
+def get_cos_anneal_ratio(iter_step, anneal_end):
+    return 1.0 if anneal_end == 0.0 else float(np.min([1.0, iter_step / anneal_end]))
+
+
+def vec2skew(v):
+    z = torch.zeros(1, dtype=v.dtype, device=v.device)
+    return torch.stack([torch.cat([z, -v[2:3], v[1:2]]), torch.cat([v[2:3], z, -v[0:1]]),
+                        torch.cat([-v[1:2], v[0:1], z])], 0)
+
+
+def Exp(r):
+    """so(3) -> SO(3), Rodrigues with the reference's +1e-15 on |r|."""
+    K = vec2skew(r)
+    th = r.norm() + 1e-15
+    I = torch.eye(3, dtype=r.dtype, device=r.device)
+    return I + (torch.sin(th) / th) * K + ((1 - torch.cos(th)) / th ** 2) * (K @ K)
+
+
+def convert3x4_4x4(m):
+    if torch.is_tensor(m):
+        if m.dim() == 3:
+            out = torch.cat([m, torch.zeros_like(m[:, 0:1])], 1)
+            out[:, 3, 3] = 1.0
+            return out
+        return torch.cat([m, torch.tensor([[0, 0, 0, 1]], dtype=m.dtype, device=m.device)], 0)
+    if m.ndim == 3:
+        out = np.concatenate([m, np.zeros_like(m[:, 0:1])], 1)
+        out[:, 3, 3] = 1.0
+        return out
+    out = np.concatenate([m, np.array([[0, 0, 0, 1]], dtype=m.dtype)], 0)
+    out[3, 3] = 1.0
+    return out
+
+
+def make_c2w(r, t):
+    return convert3x4_4x4(torch.cat([Exp(r), t.unsqueeze(1)], 1))
+
+
+class PoseRetriever(nn.Module):
+    """Reference: model/poses_retriever.py:6-32 (learnable axis-angle + translation per camera)."""
+
+    def __init__(self, num_cams, learn_R=True, learn_t=True, init_c2w=None):
+        super().__init__()
+        self.num_cams = num_cams
+        if init_c2w is not None:
+            self.init_c2w = nn.Parameter(init_c2w, requires_grad=False)
+        else:
+            self.init_c2w = nn.Parameter(torch.eye(4).float().unsqueeze(0).repeat(num_cams, 1, 1),
+                                         requires_grad=False)
+        self.r = nn.Parameter(torch.zeros(num_cams, 3), requires_grad=learn_R)
+        self.t = nn.Parameter(torch.zeros(num_cams, 3), requires_grad=learn_t)
+
+    def forward(self, cam_id):
+        cam_id = int(cam_id)
+        c2w = make_c2w(self.r[cam_id], self.t[cam_id])
+        if self.init_c2w is not None:
+            c2w = c2w @ self.init_c2w[cam_id]
+        return c2w

@@ -1,0 +1,180 @@
+"""NeuSRenderer on the HIP kernels (reference: model/neus_renderer.py:107-591).
+
+forward() keeps the reference signature and output dict.  Inside:
+  coarse z + stratified jitter           cn_coarse_z            (neus_renderer.py:466-483)
+  4 x [NeuS up-sample + merge + SDF]     cn_up_sample_merge,    (neus_renderer.py:492-525)
+                                         SDF MLP on new points
+  render_core: SDF fwd + ∇ₓSDF + colour  _SDFFieldFn, _ColorFieldFn (neus_renderer.py:337-358)
+  alpha compositing                      _CompositeFn           (neus_renderer.py:360-420)
+Every step is a HIP launch on the current stream; the only host work is
+launch bookkeeping.  `t_rand` comes from torch's device RNG (the reference
+draws it on the CPU, neus_renderer.py:482); tests inject it via `t_rand=`.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .fields import _empty
+
+
+class _CompositeFn(torch.autograd.Function):
+    """(z, sdf, ∇ₓSDF, rgb, rays_d, inv_s) -> (colour, weighted z, weights, cdf)."""
+
+    @staticmethod
+    def forward(ctx, z, sdf, G, rgb, rays_d, inv_s, near, far, n_coarse, car):
+        ctx.set_materialize_grads(False)
+        R, S = z.shape
+        dev = z.device
+        color = _empty(R, 3, dev)
+        depth = _empty(R, 1, dev)
+        weights = _empty(R, S, dev)
+        cdf = _empty(R, S, dev)
+        ops.composite_fwd(z, sdf, G, rgb, rays_d, inv_s, near, far, n_coarse, car, color, depth, weights, cdf)
+        ctx.save_for_backward(z, sdf, G, rgb, rays_d, inv_s, near, far)
+        ctx.n_coarse, ctx.car = n_coarse, car
+        return color, depth, weights, cdf
+
+    @staticmethod
+    def backward(ctx, dcolor, ddepth, dweights, dcdf):
+        if ctx.needs_input_grad[4] or ctx.needs_input_grad[0]:
+            raise NotImplementedError("copenerf: compositing gradients w.r.t. rays / z (pose optimisation) "
+                                      "are not implemented yet")
+        z, sdf, G, rgb, rays_d, inv_s, near, far = ctx.saved_tensors
+        R, S = z.shape
+        M, dev = R * S, z.device
+        dsdf = _empty(M, 1, dev)
+        dG = _empty(M, 4, dev)
+        drgb = _empty(M, 3, dev)
+        dinv = torch.empty(R, device=dev)
+        c = lambda t: None if t is None else t.contiguous()  # noqa: E731
+        ops.composite_bwd(z, sdf, G, rgb, rays_d, inv_s, near, far, ctx.n_coarse, ctx.car, c(dcolor), c(ddepth),
+                          c(dweights), c(dcdf), dsdf, dG, drgb, dinv)
+        dinv_s = dinv.sum().reshape(inv_s.shape) if ctx.needs_input_grad[5] else None
+        return (None, dsdf if ctx.needs_input_grad[1] else None, dG if ctx.needs_input_grad[2] else None,
+                drgb if ctx.needs_input_grad[3] else None, None, dinv_s, None, None, None, None)
+
+
+class NeuSRenderer(nn.Module):
+    """Reference: model/neus_renderer.py:107-135 (constructor) and 453-584 (forward)."""
+
+    def __init__(self, nerf, sdf_network, deviation_network, color_network, motion_network, n_samples,
+                 n_importance, n_outside, up_sample_steps, perturb, n_max_network_queries,
+                 importance_sampling_start, naive_render):
+        super().__init__()
+        self.nerf = nerf
+        self.sdf_network = sdf_network
+        self.deviation_network = deviation_network
+        self.color_network = color_network
+        self.motion_network = motion_network
+        self.n_samples = n_samples
+        self.n_importance = n_importance
+        self.n_outside = n_outside
+        self.up_sample_steps = up_sample_steps
+        self.perturb = perturb
+        self.n_max_network_queries = n_max_network_queries
+        self.importance_sampling_start = importance_sampling_start
+        self.naive_render = naive_render
+        if n_outside > 0:
+            raise NotImplementedError("n_outside > 0 (NeRF++ background) is out of scope; every config uses 0")
+        if naive_render:
+            raise NotImplementedError("naive_render (logistic up-sampler) is out of scope; every config uses False")
+
+    # -- sampling ------------------------------------------------------------
+    @torch.no_grad()
+    def sample_z(self, rays_o, rays_d, time_step, near, far, n_samples, n_importance, t_rand, sdf_packed):
+        """Coarse + hierarchical z-values [R, n_samples + n_importance] (neus_renderer.py:466-525)."""
+        R, dev = rays_o.shape[0], rays_o.device
+        z = _empty(R, n_samples, dev)
+        ops.coarse_z(near, far, n_samples, t_rand, z)
+        if n_importance <= 0:
+            return z
+        sdfn = self.sdf_network
+        lay = sdfn.layout()
+        pk = sdf_packed[2]
+        from .fields import sdf_forward  # local: avoid a cycle at import
+        pts = torch.empty(R * n_samples, 4, device=dev)
+        ops.points(rays_o, rays_d, z, time_step, pts)
+        sdf = sdf_forward(lay, pk, pts, want_feat=False, want_grad=False, keep=False)["sdf"].view(R, n_samples)
+        k = n_importance // self.up_sample_steps
+        for i in range(self.up_sample_steps):
+            n = z.shape[1]
+            last = (i + 1) == self.up_sample_steps
+            z_out = _empty(R, n + k, dev)
+            z_new = _empty(R, k, dev)
+            sdf_out = None if last else _empty(R, n + k, dev)
+            new_dst = None if last else torch.empty(R * k, dtype=torch.int32, device=dev)
+            ops.up_sample_merge(z, sdf, k, 64 * 2 ** i, z_out, z_new, sdf_out, new_dst)
+            if not last:
+                pts = torch.empty(R * k, 4, device=dev)
+                ops.points(rays_o, rays_d, z_new, time_step, pts)
+                sdf_forward(lay, pk, pts, want_feat=False, want_grad=False, keep=False, sdf_out=sdf_out,
+                            dst=new_dst)
+            z, sdf = z_out, sdf_out
+        return z
+
+    # -- forward -------------------------------------------------------------
+    def forward(self, rays_o, rays_d, ray_d_norm, time_step, near, far, perturb_overwrite=-1, background_rgb=None,
+                cos_anneal_ratio=0.0, it=-1, eval=False, t_rand=None):
+        if rays_o.requires_grad or rays_d.requires_grad:
+            raise NotImplementedError("copenerf: ray gradients (eval.py pose optimisation) are not implemented yet")
+        R = len(rays_o)
+        dev = rays_o.device
+        if it >= self.importance_sampling_start:
+            n_samples, n_importance = self.n_samples, self.n_importance
+        else:
+            n_samples, n_importance = self.n_samples + self.n_importance, 0
+        rays_o = rays_o.contiguous().float()
+        rays_d = rays_d.contiguous().float()
+        near = near.contiguous().float()
+        far = far.contiguous().float()
+        time_step = time_step.reshape(-1)[:1].contiguous().float()
+        if not eval and t_rand is None:
+            t_rand = torch.rand([R, n_samples], device=dev)
+        if eval:
+            t_rand = None
+
+        sdf_packed = self.sdf_network.params_and_pack()
+        col_packed = self.color_network.params_and_pack()
+        z = self.sample_z(rays_o, rays_d, time_step, near, far, n_samples, n_importance, t_rand, sdf_packed)
+        S = z.shape[1]
+
+        # render_core (neus_renderer.py:307-450)
+        pts_time = torch.empty(R * S, 4, device=dev)
+        ops.points(rays_o, rays_d, z, time_step, pts_time, mid=True, near=near, far=far, n_coarse=n_samples)
+        sdf, feat, G = self.sdf_network.field(pts_time, want_feat=True, want_grad=True, packed=sdf_packed)
+        rgb = self.color_network.color(pts_time, G, rays_d, S, feat, packed=col_packed)
+        inv_s = self.deviation_network(torch.zeros([1, 3], device=dev))[:, :1].clip(1 / 1e3, 1 / 1e-3)
+        color, depth, weights, cdf = _CompositeFn.apply(z, sdf, G, rgb, rays_d, inv_s, near, far, n_samples,
+                                                        float(cos_anneal_ratio))
+        weighted_z_vals = depth.detach().clone()
+        depth_pred = depth / ray_d_norm if eval else depth
+        if background_rgb is not None:
+            color = color + background_rgb * (1.0 - weights.sum(dim=-1, keepdim=True))
+        normals = G[:, :3].reshape(R, S, 3)
+        sdf_flows = G[:, 3:].reshape(R, S, 1)
+        s_val = (1.0 / inv_s).expand(R * S, 1).reshape(R, S).mean(dim=-1, keepdim=True)
+        with torch.no_grad():
+            weight_inside = weights.sum(dim=-1).detach()
+            weight_outside = weights.new_zeros(R)
+        return {
+            "sdf": sdf,
+            "color_fine": color,
+            "depth_pred": depth_pred,
+            "weighted_z_vals": weighted_z_vals,
+            "s_val": s_val,
+            "cdf_fine": cdf,
+            "weight_sum": weights.sum(dim=-1, keepdim=True),
+            "weight_max": torch.max(weights, dim=-1, keepdim=True)[0],
+            "normals": normals,
+            "sdf_flows": sdf_flows,
+            "sampled_points": pts_time[:, :3].reshape(R, S, 3),
+            "weights": weights,
+            "inside_sphere": torch.ones_like(weights),
+            "weight_inside": weight_inside,
+            "weight_outside": weight_outside,
+        }
+
+    def extract_geometry(self, bound_min, bound_max, resolution, threshold=0.0):
+        raise NotImplementedError("mesh extraction (PyMCubes) is out of scope (SURVEY.md §2)")

@@ -1,0 +1,735 @@
+// cn_gemm.hip — fp32 MFMA GEMMs for the SDF / colour MLPs (gfx950).
+//
+// Every Linear of SDFNetwork (model/neus_fields.py:273-283, 9 layers, Softplus
+// beta=100) and RenderingNetwork (neus_fields.py:364-373, ReLU) is a GEMM over
+// M = R*S sample rows with K, N <= 320.  At fp32 these layers are MFMA-bound
+// (~67 FLOP per HBM byte at N=K=256 vs ~26 FLOP/B machine balance), so each
+// layer is one launch of `linear_kernel`, with the bias / activation /
+// derivative bookkeeping fused into the epilogue.
+//
+// Kernel shape (tile 0): 128x128 output tile per 256-thread workgroup, 2x2
+// waves, each wave 2x2 tiles of v_mfma_f32_32x32x2_f32 (64 fp32 accumulators).
+// K is streamed in 32-deep chunks through a double-buffered LDS image
+// [rows][32+4] (the +4 float pad makes the ds_read_b128 fragment reads
+// conflict-free).  Within a chunk, lane half h consumes k = 16h + s at MFMA
+// step s, so each lane reads 4 consecutive k with one ds_read_b128.
+// Tile 1 is 128x64 (4x1 waves of 1x2 tiles) for N or K = 64 shapes.
+//
+// `wgrad_kernel` computes dW = Σ_m Y[m]ᵀ X[m] (the reduction over the M sample
+// rows) with the same MFMA, splitting M over workgroups into fp32 slabs that
+// `wgrad_reduce` sums in a fixed order (bitwise reproducible, no atomics).
+#include "cn_common.h"
+
+#include <algorithm>
+
+namespace cn {
+
+struct LinearArgs {
+    const float* A;
+    const float* A2;
+    const float* B;
+    const float* bias;
+    const float* rowv;
+    const float* colv;
+    const float* aux0;
+    const float* aux1;
+    float* out0;
+    float* out1;
+    float* out_split;
+    int64_t lda, lda2, ldb, ld_aux0, ld_aux1, ld_out0, ld_out1, ld_split;
+    int M, N, K, K1, nzero, nsplit, n_tiles_m, n_tiles_n;
+    float adiv, odiv, beta, threshold;
+};
+
+template <int EPI>
+__device__ __forceinline__ void linear_epilogue(const LinearArgs& p, int row, int col, float v,
+                                                float bcol, float ccol) {
+    const int Nmain = (EPI == CN_EPI_MUL && p.nsplit < p.N) ? p.nsplit : p.N;
+    const int64_t r = row;
+    if (col < Nmain) {
+        if (p.adiv != 1.0f) v = v / p.adiv;
+        if (p.rowv) v = v + p.rowv[row] * ccol;
+        if constexpr (EPI == CN_EPI_STORE) {
+            p.out0[r * p.ld_out0 + col] = v + bcol;
+        } else if constexpr (EPI == CN_EPI_SOFTPLUS) {
+            const float z = v + bcol;
+            float a = softplus_ref(z, p.beta, p.threshold);
+            if (p.odiv != 1.0f) a = a / p.odiv;
+            p.out0[r * p.ld_out0 + col] = a;
+            if (p.out1) p.out1[r * p.ld_out1 + col] = softplus_grad_ref(z, p.beta, p.threshold);
+        } else if constexpr (EPI == CN_EPI_RELU) {
+            const float z = v + bcol;
+            p.out0[r * p.ld_out0 + col] = z > 0.0f ? z : 0.0f;
+        } else if constexpr (EPI == CN_EPI_MUL) {
+            p.out0[r * p.ld_out0 + col] = v * p.aux0[r * p.ld_aux0 + col];
+        } else if constexpr (EPI == CN_EPI_TANGENT) {
+            const float sg = p.aux0[r * p.ld_aux0 + col];
+            float a = v * sg;
+            if (p.odiv != 1.0f) a = a / p.odiv;
+            p.out0[r * p.ld_out0 + col] = a;
+            const float s = p.aux1[r * p.ld_aux1 + col];
+            p.out1[r * p.ld_out1 + col] = p.beta * s * (1.0f - sg) * v;
+        } else if constexpr (EPI == CN_EPI_BWD_SOFTPLUS) {
+            float o = v * p.aux0[r * p.ld_aux0 + col];
+            if (p.aux1) o = o + p.aux1[r * p.ld_aux1 + col];
+            p.out0[r * p.ld_out0 + col] = o;
+        } else if constexpr (EPI == CN_EPI_BWD_RELU) {
+            p.out0[r * p.ld_out0 + col] = p.aux0[r * p.ld_aux0 + col] > 0.0f ? v : 0.0f;
+        }
+    } else if (EPI == CN_EPI_MUL && col < p.N) {
+        if (p.adiv != 1.0f) v = v / p.adiv;
+        p.out_split[r * p.ld_split + (col - p.nsplit)] = v;
+        if (col < p.nzero) p.out0[r * p.ld_out0 + col] = 0.0f;
+    } else if (col < p.nzero) {
+        p.out0[r * p.ld_out0 + col] = 0.0f;
+        if ((EPI == CN_EPI_SOFTPLUS || EPI == CN_EPI_TANGENT) && p.out1)
+            p.out1[r * p.ld_out1 + col] = 0.0f;
+    }
+}
+
+template <int WM, int WN, int TM, int TN, int EPI>
+__global__ void __launch_bounds__(64 * WM * WN, 2) linear_kernel(LinearArgs p) {
+    constexpr int NT = 64 * WM * WN;
+    constexpr int BM = 32 * TM * WM;
+    constexpr int BN = 32 * TN * WN;
+    constexpr int BK = 32;
+    constexpr int LS = BK + 4;  // padded LDS row (floats)
+    constexpr int AF4 = BM * BK / 4;
+    constexpr int BF4 = BN * BK / 4;
+    static_assert(AF4 % NT == 0 && BF4 % NT == 0, "tile/thread mismatch");
+    constexpr int ALD = AF4 / NT;
+    constexpr int BLD = BF4 / NT;
+
+    __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LS];
+    float* sA = smem;
+    float* sB = smem + 2 * BM * LS;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave / WN;
+    const int wn = wave % WN;
+
+    // XCD-aware tile order: blocks b and b+8 are dispatched to the same XCD,
+    // so the N-tiles of one M-tile are placed 8 apart and share that XCD's L2
+    // copy of the A rows.  Grid is padded to a multiple of 8 M-tiles.
+    const int T = p.n_tiles_n;
+    const int bid = blockIdx.x;
+    const int grp = bid / (8 * T);
+    const int w = bid % (8 * T);
+    const int tm_idx = grp * 8 + (w & 7);
+    const int tn_idx = w >> 3;
+    const int m0 = tm_idx * BM;
+    if (m0 >= p.M) return;
+    const int n0 = tn_idx * BN;
+
+    floatx4 ra[ALD], rb[BLD];
+    const int nk = p.K / BK;
+
+    auto gload = [&](int kc) {
+        const int k0 = kc * BK;
+        const float* Ab;
+        int64_t la;
+        if (k0 < p.K1) {
+            Ab = p.A + k0;
+            la = p.lda;
+        } else {
+            Ab = p.A2 + (k0 - p.K1);
+            la = p.lda2;
+        }
+#pragma unroll
+        for (int q = 0; q < ALD; ++q) {
+            const int f = tid + q * NT;
+            const int row = f >> 3, c4 = f & 7;
+            const int gm = m0 + row;
+            if (gm < p.M)
+                ra[q] = *reinterpret_cast<const floatx4*>(Ab + (int64_t)gm * la + c4 * 4);
+            else
+                ra[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int q = 0; q < BLD; ++q) {
+            const int f = tid + q * NT;
+            const int row = f >> 3, c4 = f & 7;
+            rb[q] = *reinterpret_cast<const floatx4*>(p.B + (int64_t)(n0 + row) * p.ldb + k0 + c4 * 4);
+        }
+    };
+    auto lstore = [&](int buf) {
+        float* a = sA + buf * BM * LS;
+        float* b = sB + buf * BN * LS;
+#pragma unroll
+        for (int q = 0; q < ALD; ++q) {
+            const int f = tid + q * NT;
+            *reinterpret_cast<floatx4*>(a + (f >> 3) * LS + (f & 7) * 4) = ra[q];
+        }
+#pragma unroll
+        for (int q = 0; q < BLD; ++q) {
+            const int f = tid + q * NT;
+            *reinterpret_cast<floatx4*>(b + (f >> 3) * LS + (f & 7) * 4) = rb[q];
+        }
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+    gload(0);
+    lstore(0);
+    __syncthreads();
+
+    const int arow = wm * TM * 32 + (lane & 31);
+    const int brow = wn * TN * 32 + (lane & 31);
+    const int kofs = 16 * (lane >> 5);
+
+    for (int kc = 0; kc < nk; ++kc) {
+        const int cur = kc & 1;
+        if (kc + 1 < nk) gload(kc + 1);
+        const float* a_base = sA + cur * BM * LS + arow * LS + kofs;
+        const float* b_base = sB + cur * BN * LS + brow * LS + kofs;
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+            floatx4 af[TM], bf[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+                af[i] = *reinterpret_cast<const floatx4*>(a_base + i * 32 * LS + q4 * 4);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                bf[j] = *reinterpret_cast<const floatx4*>(b_base + j * 32 * LS + q4 * 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][e], bf[j][e], acc[i][j], 0, 0, 0);
+        }
+        if (kc + 1 < nk) lstore(cur ^ 1);
+        __syncthreads();
+    }
+
+    // Epilogue.  C/D layout of the 32x32 MFMA: col = lane&31,
+    // row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = n0 + wn * TN * 32 + j * 32 + (lane & 31);
+            const int rbase = m0 + wm * TM * 32 + i * 32 + 4 * (lane >> 5);
+            float bcol = 0.0f, ccol = 0.0f;
+            if (col < p.N) {
+                if (p.bias) bcol = p.bias[col];
+                if (p.colv) ccol = p.colv[col];
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = rbase + (r & 3) + 8 * (r >> 2);
+                if (row < p.M) linear_epilogue<EPI>(p, row, col, acc[i][j][r], bcol, ccol);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Weight gradient.
+struct WgradArgs {
+    const float* Y0;
+    const float* X0;
+    const float* Y1;
+    const float* X1;
+    float* part;   // [nslices][Npad][Kpad]
+    float* bpart;  // [nslices][Npad]
+    int64_t ldy0, ldx0, ldy1, ldx1;
+    int M, Npad, Kpad, npairs, rows_per_slice, n_tiles_k;
+};
+
+template <int WM, int WN, int TM, int TN>
+__global__ void __launch_bounds__(64 * WM * WN, 2) wgrad_kernel(WgradArgs p) {
+    constexpr int NT = 64 * WM * WN;
+    constexpr int BNo = 32 * TM * WM;  // output rows (n) per tile
+    constexpr int BKo = 32 * TN * WN;  // output cols (k) per tile
+    constexpr int MC = 32;             // sample rows per chunk
+    constexpr int YF4 = MC * BNo / 4;
+    constexpr int XF4 = MC * BKo / 4;
+    static_assert(YF4 % NT == 0 && XF4 % NT == 0, "tile/thread mismatch");
+    constexpr int YLD = YF4 / NT;
+    constexpr int XLD = XF4 / NT;
+
+    __shared__ __attribute__((aligned(16))) float smem[2 * MC * (BNo + BKo)];
+    float* sY = smem;
+    float* sX = smem + 2 * MC * BNo;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave / WN;
+    const int wn = wave % WN;
+
+    const int tile = blockIdx.x;
+    const int slice = blockIdx.y;
+    const int tn = tile / p.n_tiles_k;
+    const int tk = tile % p.n_tiles_k;
+    const int n0 = tn * BNo;
+    const int k0 = tk * BKo;
+    const int mbeg = slice * p.rows_per_slice;
+    const int mend = min(p.M, mbeg + p.rows_per_slice);
+    const int nch = mend > mbeg ? cdiv(mend - mbeg, MC) : 0;
+    const int total = nch * p.npairs;
+    const bool do_bias = (tk == 0) && (p.bpart != nullptr);
+
+    floatx4 ry[YLD], rx[XLD];
+    auto gload = [&](int c) {
+        const int pair = c / nch;
+        const int mrow = mbeg + (c - pair * nch) * MC;
+        const float* Y = pair ? p.Y1 : p.Y0;
+        const float* X = pair ? p.X1 : p.X0;
+        const int64_t ly = pair ? p.ldy1 : p.ldy0;
+        const int64_t lx = pair ? p.ldx1 : p.ldx0;
+#pragma unroll
+        for (int q = 0; q < YLD; ++q) {
+            const int f = tid + q * NT;
+            const int row = f / (BNo / 4), c4 = f % (BNo / 4);
+            const int gm = mrow + row;
+            ry[q] = gm < mend ? *reinterpret_cast<const floatx4*>(Y + (int64_t)gm * ly + n0 + c4 * 4)
+                              : floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int q = 0; q < XLD; ++q) {
+            const int f = tid + q * NT;
+            const int row = f / (BKo / 4), c4 = f % (BKo / 4);
+            const int gm = mrow + row;
+            rx[q] = gm < mend ? *reinterpret_cast<const floatx4*>(X + (int64_t)gm * lx + k0 + c4 * 4)
+                              : floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < YLD; ++q) {
+            const int f = tid + q * NT;
+            *reinterpret_cast<floatx4*>(sY + buf * MC * BNo + f * 4) = ry[q];
+        }
+#pragma unroll
+        for (int q = 0; q < XLD; ++q) {
+            const int f = tid + q * NT;
+            *reinterpret_cast<floatx4*>(sX + buf * MC * BKo + f * 4) = rx[q];
+        }
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+    float bacc = 0.0f;
+
+    if (total > 0) {
+        gload(0);
+        lstore(0);
+    }
+    __syncthreads();
+    const int h = lane >> 5;
+    const int ycol = wm * TM * 32 + (lane & 31);
+    const int xcol = wn * TN * 32 + (lane & 31);
+    for (int c = 0; c < total; ++c) {
+        const int cur = c & 1;
+        if (c + 1 < total) gload(c + 1);
+        const float* yb = sY + cur * MC * BNo;
+        const float* xb = sX + cur * MC * BKo;
+        if (do_bias && c < nch && tid < BNo) {
+#pragma unroll 8
+            for (int r = 0; r < MC; ++r) bacc += yb[r * BNo + tid];
+        }
+#pragma unroll
+        for (int s = 0; s < MC / 2; ++s) {
+            float af[TM], bf[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) af[i] = yb[(2 * s + h) * BNo + ycol + i * 32];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bf[j] = xb[(2 * s + h) * BKo + xcol + j * 32];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
+        if (c + 1 < total) lstore(cur ^ 1);
+        __syncthreads();
+    }
+
+    float* out = p.part + (int64_t)slice * p.Npad * p.Kpad;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = k0 + wn * TN * 32 + j * 32 + (lane & 31);
+            const int rbase = n0 + wm * TM * 32 + i * 32 + 4 * (lane >> 5);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = rbase + (r & 3) + 8 * (r >> 2);
+                out[(int64_t)row * p.Kpad + col] = acc[i][j][r];
+            }
+        }
+    }
+    if (do_bias && tid < BNo) p.bpart[(int64_t)slice * p.Npad + n0 + tid] = bacc;
+}
+
+__global__ void wgrad_reduce(const float* __restrict__ part, const float* __restrict__ bpart,
+                             int nslices, int Npad, int Kpad, float* dW, int64_t ld_dw, int n_out,
+                             int k_out, float* db, int accumulate) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t tot = (int64_t)n_out * k_out;
+    if (idx < tot) {
+        const int n = idx / k_out, k = idx % k_out;
+        double s = 0.0;  // fixed order over slices
+        const int64_t stride = (int64_t)Npad * Kpad;
+        const float* pp = part + (int64_t)n * Kpad + k;
+        for (int i = 0; i < nslices; ++i) s += pp[i * stride];
+        float v = (float)s;
+        if (accumulate) v += dW[(int64_t)n * ld_dw + k];
+        dW[(int64_t)n * ld_dw + k] = v;
+    }
+    if (db && idx < n_out) {
+        double s = 0.0;
+        for (int i = 0; i < nslices; ++i) s += bpart[(int64_t)i * Npad + idx];
+        float v = (float)s;
+        if (accumulate) v += db[idx];
+        db[idx] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Per-row heads: out[dst(m)][c] = act(sum_k A[m][k] W[c][k] + b[c]).  One
+// wavefront per row (K <= 256: one float4 per lane), shuffle reduction.
+__global__ void row_head_kernel(int M, int K, const float* __restrict__ A, int64_t lda,
+                                const float* __restrict__ W, int64_t ldw, const float* __restrict__ b,
+                                int C, int act, float* out, int64_t ld_out, const int* dst) {
+    const int lane = threadIdx.x & 63;
+    const int wpb = blockDim.x >> 6;
+    const int64_t wave0 = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6);
+    const int64_t nw = (int64_t)gridDim.x * wpb;
+    const int k = lane * 4;
+    floatx4 wv[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        wv[c] = (c < C && k < K) ? *reinterpret_cast<const floatx4*>(W + c * ldw + k)
+                                 : floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int64_t m = wave0; m < M; m += nw) {
+        const floatx4 a = k < K ? *reinterpret_cast<const floatx4*>(A + m * lda + k) : floatx4{0.f, 0.f, 0.f, 0.f};
+        float s[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) s[c] = a[0] * wv[c][0] + a[1] * wv[c][1] + a[2] * wv[c][2] + a[3] * wv[c][3];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) s[c] += __shfl_xor(s[c], off);
+        if (lane < C) {
+            float v = s[0];
+#pragma unroll
+            for (int c = 1; c < 4; ++c)
+                if (lane == c) v = s[c];
+            if (b) v = v + b[lane];
+            if (act == 1) v = sigmoidf_ref(v);
+            const int64_t o = dst ? (int64_t)dst[m] : m;
+            out[o * ld_out + lane] = v;
+        }
+    }
+}
+
+__global__ void scale_cols_kernel(int M, int N, const float* __restrict__ X, int64_t ldx,
+                                  const float* __restrict__ w, float* out, int64_t ldo) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t tot = (int64_t)M * N;
+    if (idx >= tot) return;
+    const int64_t m = idx / N;
+    const int n = idx % N;
+    out[m * ldo + n] = X[m * ldx + n] * w[n];
+}
+
+// ---------------------------------------------------------------------------
+// Colour head backward: sigmoid + Linear(256 -> 3) (neus_fields.py:367-373).
+// Block = 256 threads = one column each, over a slice of rows.
+constexpr int kHeadRowsPerBlock = 256;
+
+__global__ void rgb_head_bwd_kernel(int M, int K, const float* __restrict__ drgb, const float* __restrict__ rgb,
+                                    const float* __restrict__ H3, int64_t ld_h, const float* __restrict__ W3,
+                                    float* dZ2, int64_t ld_dz, float* part /*[nblk][4][K]*/) {
+    const int k = threadIdx.x;
+    const int m0 = blockIdx.x * kHeadRowsPerBlock;
+    const int m1 = min(M, m0 + kHeadRowsPerBlock);
+    const bool kv = k < K;
+    float w0 = 0.f, w1 = 0.f, w2 = 0.f;
+    if (kv) {
+        w0 = W3[k];
+        w1 = W3[K + k];
+        w2 = W3[2 * K + k];
+    }
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, ab = 0.f;
+    for (int m = m0; m < m1; ++m) {
+        const float g0 = drgb[3 * (int64_t)m], g1 = drgb[3 * (int64_t)m + 1], g2 = drgb[3 * (int64_t)m + 2];
+        const float y0 = rgb[3 * (int64_t)m], y1 = rgb[3 * (int64_t)m + 1], y2 = rgb[3 * (int64_t)m + 2];
+        // torch sigmoid_backward: grad * (1 - y) * y
+        const float d0 = g0 * (1.0f - y0) * y0;
+        const float d1 = g1 * (1.0f - y1) * y1;
+        const float d2 = g2 * (1.0f - y2) * y2;
+        if (kv) {
+            const float hv = H3[(int64_t)m * ld_h + k];
+            const float dh = d0 * w0 + d1 * w1 + d2 * w2;
+            dZ2[(int64_t)m * ld_dz + k] = hv > 0.0f ? dh : 0.0f;
+            a0 += d0 * hv;
+            a1 += d1 * hv;
+            a2 += d2 * hv;
+        }
+        if (k < 3) ab += (k == 0 ? d0 : (k == 1 ? d1 : d2));
+    }
+    float* pb = part + (int64_t)blockIdx.x * 4 * K;
+    if (kv) {
+        pb[k] = a0;
+        pb[K + k] = a1;
+        pb[2 * K + k] = a2;
+    }
+    if (k < 3) pb[3 * K + k] = ab;
+}
+
+__global__ void rgb_head_reduce(const float* __restrict__ part, int nblk, int K, float* dW3, float* db3) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx < 3 * K) {
+        double s = 0.0;
+        for (int i = 0; i < nblk; ++i) s += part[(int64_t)i * 4 * K + idx];
+        dW3[idx] = (float)s;
+    } else if (idx < 3 * K + 3) {
+        const int c = idx - 3 * K;
+        double s = 0.0;
+        for (int i = 0; i < nblk; ++i) s += part[(int64_t)i * 4 * K + 3 * K + c];
+        db3[c] = (float)s;
+    }
+}
+
+// Column sums over row slices (thread = column), then a fixed-order reduce.
+constexpr int kColsumRows = 1024;
+
+__global__ void colsum_kernel(int M, int K, const float* __restrict__ w, const float* __restrict__ X, int64_t ldx,
+                              float* part) {
+    const int k = blockIdx.y * blockDim.x + threadIdx.x;
+    const int m0 = blockIdx.x * kColsumRows;
+    const int m1 = min(M, m0 + kColsumRows);
+    if (k >= K) return;
+    float a = 0.0f;
+    for (int m = m0; m < m1; ++m) {
+        const float x = X[(int64_t)m * ldx + k];
+        a += w ? w[m] * x : x;
+    }
+    part[(int64_t)blockIdx.x * K + k] = a;
+}
+
+__global__ void colsum_reduce(const float* __restrict__ part, int nblk, int K, float wdiv, float* out,
+                              int accumulate) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= K) return;
+    double s = 0.0;
+    for (int i = 0; i < nblk; ++i) s += part[(int64_t)i * K + k];
+    float v = (float)s;
+    if (wdiv != 1.0f) v = v / wdiv;
+    if (accumulate) v += out[k];
+    out[k] = v;
+}
+
+// ---------------------------------------------------------------------------
+static void wgrad_geometry(int M, int N, int K, int* tile, int* Npad, int* Kpad, int* nslices,
+                           int* rows_per_slice) {
+    const int t = (K % 128 == 0) ? 0 : 1;
+    const int BNo = 128, BKo = t == 0 ? 128 : 64;
+    *tile = t;
+    *Npad = cdiv(N, BNo) * BNo;
+    *Kpad = cdiv(K, BKo) * BKo;
+    const int tiles = (*Npad / BNo) * (*Kpad / BKo);
+    int ns = std::max(1, 1024 / tiles);
+    ns = std::min(ns, std::max(1, cdiv(M, 512)));
+    int rps = cdiv(cdiv(M, ns), 32) * 32;
+    ns = std::max(1, cdiv(M, rps));
+    *nslices = ns;
+    *rows_per_slice = rps;
+}
+
+}  // namespace cn
+
+using namespace cn;
+
+template <int WM, int WN, int TM, int TN>
+static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_t s) {
+    constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
+    a.n_tiles_m = cdiv(d->M, BM);
+    a.n_tiles_n = cdiv(d->N, BN);
+    const int grid = cdiv(a.n_tiles_m, 8) * 8 * a.n_tiles_n;
+    dim3 block(64 * WM * WN);
+    switch (d->epilogue) {
+        case CN_EPI_STORE: linear_kernel<WM, WN, TM, TN, CN_EPI_STORE><<<grid, block, 0, s>>>(a); break;
+        case CN_EPI_SOFTPLUS: linear_kernel<WM, WN, TM, TN, CN_EPI_SOFTPLUS><<<grid, block, 0, s>>>(a); break;
+        case CN_EPI_RELU: linear_kernel<WM, WN, TM, TN, CN_EPI_RELU><<<grid, block, 0, s>>>(a); break;
+        case CN_EPI_MUL: linear_kernel<WM, WN, TM, TN, CN_EPI_MUL><<<grid, block, 0, s>>>(a); break;
+        case CN_EPI_TANGENT: linear_kernel<WM, WN, TM, TN, CN_EPI_TANGENT><<<grid, block, 0, s>>>(a); break;
+        case CN_EPI_BWD_SOFTPLUS: linear_kernel<WM, WN, TM, TN, CN_EPI_BWD_SOFTPLUS><<<grid, block, 0, s>>>(a); break;
+        case CN_EPI_BWD_RELU: linear_kernel<WM, WN, TM, TN, CN_EPI_BWD_RELU><<<grid, block, 0, s>>>(a); break;
+        default: set_error("cn_linear: bad epilogue %d", d->epilogue); return CN_ERR_ARG;
+    }
+    return check_launch("cn_linear");
+}
+
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
+    CN_REQUIRE(d, CN_ERR_ARG, "cn_linear: null desc");
+    CN_REQUIRE(d->A && d->B && d->out0, CN_ERR_ARG, "cn_linear: A, B and out0 are required");
+    CN_REQUIRE(d->M >= 0 && d->N > 0 && d->K > 0, CN_ERR_SHAPE, "cn_linear: bad M/N/K %d/%d/%d", d->M, d->N, d->K);
+    CN_REQUIRE(d->K % 32 == 0, CN_ERR_SHAPE, "cn_linear: K=%d must be a multiple of 32", d->K);
+    CN_REQUIRE(d->tile == 0 || d->tile == 1, CN_ERR_ARG, "cn_linear: bad tile %d", d->tile);
+    const int K1 = d->A2 ? d->K1 : d->K;
+    CN_REQUIRE(K1 > 0 && K1 <= d->K && K1 % 32 == 0, CN_ERR_SHAPE, "cn_linear: bad K1=%d", K1);
+    CN_REQUIRE(d->lda >= K1 && d->lda % 4 == 0 && al16(d->A), CN_ERR_ALIGN, "cn_linear: A must be 16B aligned with lda>=K1, lda%%4==0");
+    if (d->A2) CN_REQUIRE(d->lda2 >= d->K - K1 && d->lda2 % 4 == 0 && al16(d->A2), CN_ERR_ALIGN, "cn_linear: bad A2/lda2");
+    CN_REQUIRE(d->ldb >= d->K && d->ldb % 4 == 0 && al16(d->B), CN_ERR_ALIGN, "cn_linear: bad B/ldb");
+    const int nzero = std::max(d->nzero, d->N);
+    CN_REQUIRE(d->ld_out0 >= nzero, CN_ERR_SHAPE, "cn_linear: ld_out0=%lld < nzero=%d", (long long)d->ld_out0, nzero);
+    const int e = d->epilogue;
+    if (e == CN_EPI_MUL || e == CN_EPI_TANGENT || e == CN_EPI_BWD_SOFTPLUS || e == CN_EPI_BWD_RELU)
+        CN_REQUIRE(d->aux0 && d->ld_aux0 >= d->N, CN_ERR_ARG, "cn_linear: epilogue %d needs aux0", e);
+    if (e == CN_EPI_TANGENT)
+        CN_REQUIRE(d->aux1 && d->out1 && d->ld_aux1 >= d->N && d->ld_out1 >= nzero, CN_ERR_ARG,
+                   "cn_linear: tangent epilogue needs aux1/out1");
+    if (e == CN_EPI_SOFTPLUS && d->out1) CN_REQUIRE(d->ld_out1 >= nzero, CN_ERR_SHAPE, "cn_linear: ld_out1");
+    if (e == CN_EPI_MUL && d->nsplit < d->N)
+        CN_REQUIRE(d->out_split && d->nsplit >= 0 && d->ld_split >= d->N - d->nsplit, CN_ERR_ARG,
+                   "cn_linear: split output required");
+    CN_REQUIRE((d->rowv == nullptr) == (d->colv == nullptr), CN_ERR_ARG, "cn_linear: rowv/colv go together");
+    if (d->M == 0) return CN_OK;
+
+    LinearArgs a;
+    a.A = d->A; a.A2 = d->A2; a.B = d->B; a.bias = d->bias; a.rowv = d->rowv; a.colv = d->colv;
+    a.aux0 = d->aux0; a.aux1 = d->aux1; a.out0 = d->out0; a.out1 = d->out1; a.out_split = d->out_split;
+    a.lda = d->lda; a.lda2 = d->lda2; a.ldb = d->ldb; a.ld_aux0 = d->ld_aux0; a.ld_aux1 = d->ld_aux1;
+    a.ld_out0 = d->ld_out0; a.ld_out1 = d->ld_out1; a.ld_split = d->ld_split;
+    a.M = d->M; a.N = d->N; a.K = d->K; a.K1 = K1; a.nzero = nzero;
+    a.nsplit = (e == CN_EPI_MUL && d->out_split) ? d->nsplit : d->N;
+    a.adiv = d->adiv == 0.0f ? 1.0f : d->adiv;
+    a.odiv = d->odiv == 0.0f ? 1.0f : d->odiv;
+    a.beta = d->beta;
+    a.threshold = d->threshold;
+    hipStream_t s = (hipStream_t)stream;
+    if (d->tile == 0) return launch_linear_tile<2, 2, 2, 2>(d, a, s);
+    return launch_linear_tile<4, 1, 1, 2>(d, a, s);
+}
+
+extern "C" size_t cn_wgrad_workspace_bytes(int32_t M, int32_t N, int32_t K) {
+    int tile, Npad, Kpad, ns, rps;
+    wgrad_geometry(std::max(M, 1), N, K, &tile, &Npad, &Kpad, &ns, &rps);
+    return sizeof(float) * ((size_t)ns * Npad * Kpad + (size_t)ns * Npad);
+}
+
+extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
+    CN_REQUIRE(d, CN_ERR_ARG, "cn_wgrad: null desc");
+    CN_REQUIRE(d->Y0 && d->X0 && d->dW && d->workspace, CN_ERR_ARG, "cn_wgrad: Y0, X0, dW, workspace required");
+    CN_REQUIRE(d->npairs == 1 || (d->npairs == 2 && d->Y1 && d->X1), CN_ERR_ARG, "cn_wgrad: bad npairs");
+    CN_REQUIRE(d->M >= 0 && d->N > 0 && d->K > 0 && d->K % 64 == 0, CN_ERR_SHAPE,
+               "cn_wgrad: bad shape M=%d N=%d K=%d (K must be a multiple of 64)", d->M, d->N, d->K);
+    int tile, Npad, Kpad, ns, rps;
+    wgrad_geometry(std::max(d->M, 1), d->N, d->K, &tile, &Npad, &Kpad, &ns, &rps);
+    CN_REQUIRE(d->n_out <= Npad && d->k_out <= Kpad && d->n_out > 0 && d->k_out > 0, CN_ERR_SHAPE, "cn_wgrad: bad n_out/k_out");
+    CN_REQUIRE(d->ldy0 >= Npad && d->ldx0 >= Kpad && d->ldy0 % 4 == 0 && d->ldx0 % 4 == 0 && al16(d->Y0) && al16(d->X0),
+               CN_ERR_ALIGN, "cn_wgrad: Y0/X0 must be 16B aligned with ld >= padded tile (%d, %d)", Npad, Kpad);
+    if (d->npairs == 2)
+        CN_REQUIRE(d->ldy1 >= Npad && d->ldx1 >= Kpad && d->ldy1 % 4 == 0 && d->ldx1 % 4 == 0 && al16(d->Y1) && al16(d->X1),
+                   CN_ERR_ALIGN, "cn_wgrad: Y1/X1 alignment");
+    const size_t need = cn_wgrad_workspace_bytes(d->M, d->N, d->K);
+    CN_REQUIRE((size_t)d->workspace_bytes >= need, CN_ERR_SHAPE, "cn_wgrad: workspace %lld < %zu", (long long)d->workspace_bytes, need);
+    hipStream_t s = (hipStream_t)stream;
+    WgradArgs a;
+    a.Y0 = d->Y0; a.X0 = d->X0; a.Y1 = d->Y1; a.X1 = d->X1;
+    a.part = d->workspace;
+    a.bpart = d->db ? d->workspace + (size_t)ns * Npad * Kpad : nullptr;
+    a.ldy0 = d->ldy0; a.ldx0 = d->ldx0; a.ldy1 = d->ldy1; a.ldx1 = d->ldx1;
+    a.M = d->M; a.Npad = Npad; a.Kpad = Kpad; a.npairs = d->npairs; a.rows_per_slice = rps;
+    const int BKo = tile == 0 ? 128 : 64;
+    a.n_tiles_k = Kpad / BKo;
+    dim3 grid((Npad / 128) * a.n_tiles_k, ns);
+    if (tile == 0)
+        wgrad_kernel<2, 2, 2, 2><<<grid, 256, 0, s>>>(a);
+    else
+        wgrad_kernel<2, 2, 2, 1><<<grid, 256, 0, s>>>(a);
+    int rc = check_launch("cn_wgrad");
+    if (rc) return rc;
+    const int64_t tot = std::max<int64_t>((int64_t)d->n_out * d->k_out, d->n_out);
+    wgrad_reduce<<<cdiv((int)tot, 256), 256, 0, s>>>(a.part, a.bpart, ns, Npad, Kpad, d->dW, d->ld_dw, d->n_out,
+                                                    d->k_out, d->db, d->accumulate);
+    return check_launch("cn_wgrad(reduce)");
+}
+
+extern "C" int cn_row_head(int32_t M, int32_t K, const float* A, int64_t lda, const float* W, int64_t ldw,
+                           const float* b, int32_t C, int32_t act, float* out, int64_t ld_out,
+                           const int32_t* dst_index, cn_stream_t stream) {
+    CN_REQUIRE(A && W && out, CN_ERR_ARG, "cn_row_head: null pointer");
+    CN_REQUIRE(K > 0 && K <= 256 && K % 4 == 0 && C >= 1 && C <= 4, CN_ERR_UNSUPPORTED, "cn_row_head: K=%d C=%d", K, C);
+    CN_REQUIRE(lda % 4 == 0 && ldw % 4 == 0 && al16(A) && al16(W), CN_ERR_ALIGN, "cn_row_head: alignment");
+    CN_REQUIRE(act == 0 || act == 1, CN_ERR_ARG, "cn_row_head: act");
+    if (M == 0) return CN_OK;
+    const int blocks = std::min(cdiv(M, 4), 4096);
+    row_head_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(M, K, A, lda, W, ldw, b, C, act, out, ld_out, dst_index);
+    return check_launch("cn_row_head");
+}
+
+extern "C" int cn_scale_cols(int32_t M, int32_t N, const float* X, int64_t ldx, const float* w, float* out,
+                             int64_t ld_out, cn_stream_t stream) {
+    CN_REQUIRE(X && w && out, CN_ERR_ARG, "cn_scale_cols: null pointer");
+    if ((int64_t)M * N == 0) return CN_OK;
+    const int64_t tot = (int64_t)M * N;
+    scale_cols_kernel<<<(int)((tot + 255) / 256), 256, 0, (hipStream_t)stream>>>(M, N, X, ldx, w, out, ld_out);
+    return check_launch("cn_scale_cols");
+}
+
+extern "C" size_t cn_rgb_head_bwd_workspace_bytes(int32_t M, int32_t K) {
+    return sizeof(float) * (size_t)std::max(1, cdiv(M, kHeadRowsPerBlock)) * 4 * K;
+}
+
+extern "C" int cn_rgb_head_bwd(int32_t M, int32_t K, const float* drgb, const float* rgb, const float* H3,
+                               int64_t ld_h, const float* W3, float* dZ2, int64_t ld_dz, float* dW3, float* db3,
+                               float* workspace, int64_t workspace_bytes, cn_stream_t stream) {
+    CN_REQUIRE(drgb && rgb && H3 && W3 && dZ2 && dW3 && db3 && workspace, CN_ERR_ARG, "cn_rgb_head_bwd: null pointer");
+    CN_REQUIRE(K > 0 && K <= 256, CN_ERR_UNSUPPORTED, "cn_rgb_head_bwd: K=%d", K);
+    CN_REQUIRE((size_t)workspace_bytes >= cn_rgb_head_bwd_workspace_bytes(M, K), CN_ERR_SHAPE, "cn_rgb_head_bwd: workspace");
+    const int nblk = std::max(1, cdiv(M, kHeadRowsPerBlock));
+    hipStream_t s = (hipStream_t)stream;
+    rgb_head_bwd_kernel<<<nblk, 256, 0, s>>>(M, K, drgb, rgb, H3, ld_h, W3, dZ2, ld_dz, workspace);
+    int rc = check_launch("cn_rgb_head_bwd");
+    if (rc) return rc;
+    rgb_head_reduce<<<cdiv(3 * K + 3, 256), 256, 0, s>>>(workspace, nblk, K, dW3, db3);
+    return check_launch("cn_rgb_head_bwd(reduce)");
+}
+
+extern "C" size_t cn_colsum_workspace_bytes(int32_t M, int32_t K) {
+    return sizeof(float) * (size_t)std::max(1, cdiv(M, kColsumRows)) * K;
+}
+
+extern "C" int cn_colsum(int32_t M, int32_t K, const float* w, const float* X, int64_t ldx, float wdiv, float* out,
+                         int32_t accumulate, float* workspace, int64_t workspace_bytes, cn_stream_t stream) {
+    CN_REQUIRE(X && out && workspace, CN_ERR_ARG, "cn_colsum: null pointer");
+    CN_REQUIRE(K > 0 && ldx >= K, CN_ERR_SHAPE, "cn_colsum: K=%d ldx=%lld", K, (long long)ldx);
+    CN_REQUIRE((size_t)workspace_bytes >= cn_colsum_workspace_bytes(M, K), CN_ERR_SHAPE, "cn_colsum: workspace");
+    const int nblk = std::max(1, cdiv(M, kColsumRows));
+    hipStream_t s = (hipStream_t)stream;
+    dim3 grid(nblk, cdiv(K, 256));
+    if (M > 0) {
+        colsum_kernel<<<grid, 256, 0, s>>>(M, K, w, X, ldx, workspace);
+        int rc = check_launch("cn_colsum");
+        if (rc) return rc;
+    } else {
+        if (hipMemsetAsync(workspace, 0, sizeof(float) * K, s) != hipSuccess) {
+            set_error("cn_colsum: hipMemsetAsync failed");
+            return CN_ERR_LAUNCH;
+        }
+    }
+    colsum_reduce<<<cdiv(K, 256), 256, 0, s>>>(workspace, nblk, K, wdiv == 0.f ? 1.f : wdiv, out, accumulate);
+    return check_launch("cn_colsum(reduce)");
+}

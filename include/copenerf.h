@@ -1,0 +1,228 @@
+/* copenerf.h — C ABI of libcopenerf.so, the MI355X (gfx950) kernels behind the
+ * cope-nerf NeuS volumetric-rendering hot path.
+ *
+ * The reference (HoangChuongNguyen/cope-nerf) is pure PyTorch: it has no FFI.
+ * Each entry point below replaces one group of aten calls on the hot path and
+ * cites the reference lines it restates (paths relative to the reference root).
+ * The host side that binds these symbols is cope-nerf_amd/copenerf/_lib.py
+ * (ctypes); INTEGRATION.md shows the binding a maintainer would add.
+ *
+ * Conventions
+ *  - All pointers are device pointers (fp32 unless typed otherwise), row-major,
+ *    with explicit leading dimensions in ELEMENTS.  The caller owns all memory.
+ *  - `stream` is a hipStream_t (passed as void* so that this header needs no HIP
+ *    headers).  Nothing here allocates, synchronises, or uses the null stream:
+ *    any sequence of calls is hipGraph-capturable and re-entrant across devices
+ *    (torch.nn.DataParallel runs one host thread per GPU, train.py:54).
+ *  - Return 0 on success, a negative cn_status on a bad argument or a failed
+ *    launch; cn_last_error() holds the message (thread-local).  Asynchronous
+ *    device faults surface at the caller's next synchronisation.
+ */
+#ifndef COPENERF_H_
+#define COPENERF_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CN_ABI_VERSION 1
+
+typedef void* cn_stream_t; /* hipStream_t */
+
+typedef enum cn_status {
+    CN_OK = 0,
+    CN_ERR_ARG = -1,         /* null pointer / bad enum */
+    CN_ERR_SHAPE = -2,       /* inconsistent sizes or leading dimensions */
+    CN_ERR_ALIGN = -3,       /* pointer / leading dimension not 16-byte aligned */
+    CN_ERR_LAUNCH = -4,      /* hipLaunchKernel failed */
+    CN_ERR_UNSUPPORTED = -5  /* configuration outside what the kernels implement */
+} cn_status;
+
+int cn_abi_version(void);
+const char* cn_last_error(void);
+
+/* ------------------------------------------------------------------------ *
+ * Fully-connected layers: out = epilogue((A · Bᵀ) / adiv [+ rowv ⊗ colv])
+ * Replaces every nn.Linear of SDFNetwork (model/neus_fields.py:273-283) and
+ * RenderingNetwork (model/neus_fields.py:364-370), the first-order backward of
+ * those layers (autograd of the same lines), the ∇ₓSDF pass of
+ * SDFNetwork.gradient (neus_fields.py:291-303) and its create_graph double
+ * backward.  Computed with v_mfma_f32_32x32x2_f32 (exact fp32 products).
+ *
+ *   A   : [M][>=K] (lda), optionally a virtual concat: columns k < K1 come from
+ *         A, columns k >= K1 from A2 (column k-K1).  K, K1 multiples of 32.
+ *   B   : [Npad][K] (ldb), Npad = N rounded up to the tile width (128, or 64
+ *         when tile == 1); rows >= N must be readable (zero-padded weights).
+ *   Columns [0, N) of out0 get the epilogue value, columns [N, nzero) get 0.
+ * ------------------------------------------------------------------------ */
+typedef enum cn_epilogue {
+    CN_EPI_STORE = 0,        /* out0 = v + bias                                      */
+    CN_EPI_SOFTPLUS = 1,     /* z = v + bias; out0 = softplus_beta(z)/odiv; out1 = softplus'(z) */
+    CN_EPI_RELU = 2,         /* out0 = relu(v + bias)                                */
+    CN_EPI_MUL = 3,          /* out0 = v * aux0 (cols < nsplit); out_split = v (cols >= nsplit) */
+    CN_EPI_TANGENT = 4,      /* out0 = v*aux0/odiv (aux0 = sp'); out1 = beta*aux1*(1-aux0)*v (aux1 = s) */
+    CN_EPI_BWD_SOFTPLUS = 5, /* out0 = v*aux0 + aux1 (aux1 nullable)                 */
+    CN_EPI_BWD_RELU = 6      /* out0 = aux0 > 0 ? v : 0                              */
+} cn_epilogue;
+
+typedef struct cn_linear_desc {
+    const float* A;
+    const float* A2;
+    const float* B;
+    const float* bias;   /* [N] or NULL */
+    const float* rowv;   /* [M] or NULL : rank-1 term rowv[m]*colv[n] added to v */
+    const float* colv;   /* [N] or NULL */
+    const float* aux0;
+    const float* aux1;
+    float* out0;
+    float* out1;
+    float* out_split;
+    int64_t lda, lda2, ldb, ld_aux0, ld_aux1, ld_out0, ld_out1, ld_split;
+    int32_t M, N, K, K1;
+    int32_t nzero, nsplit;
+    int32_t epilogue;    /* cn_epilogue */
+    int32_t tile;        /* 0: 128x128 block tile, 1: 128x64 */
+    float adiv, odiv;    /* divisors applied to A·Bᵀ and to the activation (0 means 1);
+                            divisions, not reciprocals, to round like torch's x / sqrt(2) */
+    float beta, threshold; /* Softplus(beta, threshold) of neus_fields.py:266 */
+} cn_linear_desc;
+
+int cn_linear(const cn_linear_desc* d, cn_stream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * Weight gradient: dW[n][k] = sum_m ( Y0[m][n]*X0[m][k] + Y1[m][n]*X1[m][k] ),
+ * db[n] = sum_m Y0[m][n].  Reduction over the M = R*S sample rows is split
+ * over workgroups into fp32 slabs (workspace) and summed in a fixed order, so
+ * the result is bitwise reproducible.  Replaces the dW/db of the autograd of
+ * every Linear above, including the create_graph term of neus_fields.py:296.
+ * ------------------------------------------------------------------------ */
+typedef struct cn_wgrad_desc {
+    const float* Y0;
+    const float* X0;
+    const float* Y1;     /* NULL when npairs == 1 */
+    const float* X1;
+    float* workspace;    /* cn_wgrad_workspace_bytes() */
+    float* dW;           /* [n_out][k_out] (ld_dw) */
+    float* db;           /* [n_out] or NULL */
+    int64_t ldy0, ldx0, ldy1, ldx1, ld_dw;
+    int64_t workspace_bytes;
+    int32_t M, N, K;     /* N, K: valid columns of Y and X (Y/X readable up to the padded tile) */
+    int32_t npairs;
+    int32_t n_out, k_out;
+    int32_t accumulate;  /* 1: dW += result (db too), 0: dW = result */
+    int32_t pad_;
+} cn_wgrad_desc;
+
+size_t cn_wgrad_workspace_bytes(int32_t M, int32_t N, int32_t K);
+int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * Per-row heads (neus_fields.py:279-283 last Linear row 0 = sdf;
+ * neus_fields.py:367-373 last colour Linear + sigmoid):
+ *   out[dst(m)][c] = act( sum_k A[m][k]*W[c][k] + b[c] ),  c < C (C <= 4)
+ * act: 0 none, 1 sigmoid.  dst(m) = dst_index ? dst_index[m] : m.
+ * ------------------------------------------------------------------------ */
+int cn_row_head(int32_t M, int32_t K, const float* A, int64_t lda, const float* W, int64_t ldw,
+                const float* b, int32_t C, int32_t act, float* out, int64_t ld_out,
+                const int32_t* dst_index, cn_stream_t stream);
+
+/* out[k] (+)= (sum_m (w ? w[m] : 1) * X[m][k]) / wdiv, k < K: the sdf row of the
+ * last SDF Linear's weight gradient (neus_fields.py:283, row 0 of lin8) and its
+ * create_graph term; fixed-order slab reduction. */
+size_t cn_colsum_workspace_bytes(int32_t M, int32_t K);
+int cn_colsum(int32_t M, int32_t K, const float* w, const float* X, int64_t ldx, float wdiv, float* out,
+              int32_t accumulate, float* workspace, int64_t workspace_bytes, cn_stream_t stream);
+
+/* out[m][n] = X[m][n] * w[n] for n < N (seed of the ∇ₓSDF pass, neus_fields.py:295-302) */
+int cn_scale_cols(int32_t M, int32_t N, const float* X, int64_t ldx, const float* w, float* out,
+                  int64_t ld_out, cn_stream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * Positional encoding of the SDF input (neus_embedder.py:6-51 with
+ * include_input, log-sampled bands 2^0..2^(multires-1), [sin, cos]; applied at
+ * neus_fields.py:269-271 to x*scale):
+ *   U0[m][0..4+8*multires) = embed(scale * x[m][0..4)),  zeros up to kpad.
+ *   If U4e != NULL also U4e[m][j] = u4_scale * U0[m][j] (the skip-connection
+ *   copy of neus_fields.py:276-277).
+ * ------------------------------------------------------------------------ */
+int cn_sdf_embed(int32_t M, const float* x, int64_t ldx, int32_t multires, float scale, int32_t kpad,
+                 float* U0, int64_t ld_u0, float* U4e, int64_t ld_u4, float u4_scale, cn_stream_t stream);
+
+/* ∇ₓSDF from the embedding adjoint: G[m][i] = scale * J_embed(x)ᵀ (Q0[m] + QE[m])
+ * (neus_fields.py:291-303; the chain rule through neus_embedder.py:20-22). */
+int cn_sdf_grad_assemble(int32_t M, int32_t multires, float scale, const float* U0, int64_t ld_u0,
+                         const float* Q0, int64_t ld_q0, const float* QE, int64_t ld_qe,
+                         float* G, int64_t ld_g, cn_stream_t stream);
+
+/* Tangent of the embedding along v = dL/d(∇ₓSDF) (forward-over-reverse form
+ * of the double backward of neus_fields.py:296):
+ *   T0[m] = scale * J_embed(x) v[m] (zeros up to kpad);  T4e[m] = t4_scale * T0[m]. */
+int cn_sdf_tangent_prep(int32_t M, int32_t multires, float scale, int32_t kpad, const float* U0,
+                        int64_t ld_u0, const float* v, int64_t ld_v, float* T0, int64_t ld_t0,
+                        float* T4e, int64_t ld_t4, float t4_scale, cn_stream_t stream);
+
+/* Colour-network input extras (neus_fields.py:346-356, mode 'idr'):
+ *   ext[m] = [ G[m][0..4), pts[m][0..4), embed_view(dirs[m / dir_div]) (3+6*multires_view), 0... ]
+ * The 256 feature columns are read in place by cn_linear through A/A2. */
+int cn_color_extras(int32_t M, const float* G, int64_t ld_g, const float* pts, int64_t ld_p,
+                    const float* dirs, int64_t ld_d, int32_t dir_div, int32_t multires_view,
+                    int32_t kpad, float* ext, int64_t ld_ext, cn_stream_t stream);
+
+/* Backward of the colour head (sigmoid(Linear 256->3), neus_fields.py:367-373):
+ *   dz3 = drgb*rgb*(1-rgb);  dZ2[m][k] = (H3[m][k] > 0) * sum_c dz3[m][c]*W3[c][k];
+ *   dW3 = sum_m dz3ᵀ H3, db3 = sum_m dz3 (fixed-order slab reduction). */
+size_t cn_rgb_head_bwd_workspace_bytes(int32_t M, int32_t K);
+int cn_rgb_head_bwd(int32_t M, int32_t K, const float* drgb, const float* rgb, const float* H3,
+                    int64_t ld_h, const float* W3, float* dZ2, int64_t ld_dz, float* dW3, float* db3,
+                    float* workspace, int64_t workspace_bytes, cn_stream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * Sampling along rays (neus_renderer.py:453-525).
+ * ------------------------------------------------------------------------ */
+/* z[r][i] = near*(1-lin_i) + far*lin_i, lin = linspace(0,1,n); stratified
+ * jitter with t_rand [R][n] when t_rand != NULL (neus_renderer.py:466-483). */
+int cn_coarse_z(int32_t R, int32_t n, const float* near, const float* far, const float* t_rand,
+                float* z, cn_stream_t stream);
+
+/* pts_time[r*n+i] = [o_r + d_r * zz_i, t]: zz = z (mid == 0) or the section
+ * midpoints z + dists/2 with the last dist = (far[0]-near[0])/n_coarse
+ * (neus_renderer.py:337-350, 495-498, 286-291). */
+int cn_points(int32_t R, int32_t n, const float* rays_o, const float* rays_d, const float* z,
+              const float* t, int32_t mid, const float* near, const float* far, int32_t n_coarse,
+              float* pts_time, cn_stream_t stream);
+
+/* One NeuS up-sampling round + merge (neus_renderer.py:178-224 up_sample,
+ * 39-70 sample_pdf det=True, 282-298 cat_z_vals).  One wavefront per ray.
+ *   z_out = sorted merge of z and the n_imp new samples;
+ *   z_new = the new samples [R][n_imp];
+ *   if sdf_out: sdf_out[r][pos(old i)] = sdf[r][i] and new_dst[r*n_imp+j] =
+ *   r*(n+n_imp) + pos(new j) (cn_row_head scatters the new SDF there). */
+int cn_up_sample_merge(int32_t R, int32_t n, int32_t n_imp, float inv_s, const float* z,
+                       const float* sdf, float* z_out, float* z_new, float* sdf_out, int32_t* new_dst,
+                       cn_stream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * Alpha compositing (neus_renderer.py:337-420, render_core).  One wavefront
+ * per ray; transmittance as an exclusive product scan across the wave.
+ * G holds ∇ₓSDF rows (normals = G[m][0..3)), sdf/G/rgb are indexed m = r*S+i.
+ * ------------------------------------------------------------------------ */
+int cn_composite_fwd(int32_t R, int32_t S, const float* z, const float* sdf, const float* G,
+                     int64_t ld_g, const float* rgb, const float* rays_d, const float* inv_s,
+                     const float* near, const float* far, int32_t n_coarse, float cos_anneal_ratio,
+                     float* color, float* depth, float* weights, float* cdf, cn_stream_t stream);
+
+int cn_composite_bwd(int32_t R, int32_t S, const float* z, const float* sdf, const float* G,
+                     int64_t ld_g, const float* rgb, const float* rays_d, const float* inv_s,
+                     const float* near, const float* far, int32_t n_coarse, float cos_anneal_ratio,
+                     const float* dcolor, const float* ddepth, const float* dweights,
+                     const float* dcdf, float* dsdf, float* dG, float* drgb, float* dinv_s_part,
+                     cn_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* COPENERF_H_ */

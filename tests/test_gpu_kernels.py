@@ -1,0 +1,260 @@
+"""HIP kernels against plain torch fp32 (GEMM family) and against the CPU oracle
+(fields, compositing, sampler).  All calls go through the C ABI."""
+import math
+
+import pytest
+import torch
+
+from helpers import build_modules, fixture, oracle_params
+from oracle import neus_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rnd(*s, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return ((torch.rand(*s, generator=g) * 2 - 1) * scale).to(DEV)
+
+
+def _ops():
+    from copenerf import ops
+    return ops
+
+
+# ----------------------------------------------------------------------------- GEMM family
+@pytest.mark.parametrize("M,N,K,tile", [(1000, 256, 256, 0), (130, 204, 224, 0), (777, 52, 256, 1),
+                                        (64, 256, 64, 0), (4096, 128, 96, 0)])
+def test_linear_store_matches_torch(M, N, K, tile):
+    ops = _ops()
+    A = _rnd(M, K, seed=1)
+    bn = 64 if tile else 128
+    Np = ops.rup(N, bn)
+    B = torch.zeros(Np, K, device=DEV)
+    B[:N] = _rnd(N, K, seed=2, scale=0.1)
+    bias = _rnd(N, seed=3)
+    ld = ops.rup(N, 128)
+    out = torch.full((M, ld), float("nan"), device=DEV)
+    ops.linear(A, B, N, K, out, ops.EPI_STORE, bias=bias, nzero=ld, tile=tile)
+    ref = (A.double() @ B[:N].double().t() + bias.double()).float()
+    torch.testing.assert_close(out[:, :N], ref, rtol=1e-5, atol=1e-5)
+    assert torch.all(out[:, N:] == 0)
+
+
+def test_linear_virtual_concat_rank1_and_divisor():
+    ops = _ops()
+    M, K1, K2, N = 333, 256, 64, 256
+    A, A2 = _rnd(M, K1, seed=4), _rnd(M, K2, seed=5)
+    B = _rnd(N, K1 + K2, seed=6, scale=0.1)
+    rowv, colv = _rnd(M, seed=7), _rnd(N, seed=8)
+    out = torch.empty(M, N, device=DEV)
+    ops.linear(A, B, N, K1 + K2, out, ops.EPI_STORE, A2=A2, K1=K1, rowv=rowv, colv=colv, adiv=ops.SQRT2)
+    ref = torch.cat([A, A2], 1).double() @ B.double().t() / ops.SQRT2 + rowv.double()[:, None] * colv.double()
+    torch.testing.assert_close(out, ref.float(), rtol=1e-5, atol=1e-5)
+
+
+def test_linear_softplus_and_derivative():
+    ops = _ops()
+    M, N, K = 517, 256, 256
+    A = _rnd(M, K, seed=9, scale=0.3)
+    B = _rnd(N, K, seed=10, scale=0.05)
+    bias = _rnd(N, seed=11, scale=0.3)
+    a, s = torch.empty(M, N, device=DEV), torch.empty(M, N, device=DEV)
+    ops.linear(A, B, N, K, a, ops.EPI_SOFTPLUS, bias=bias, out1=s, beta=100.0, threshold=20.0)
+    z = torch.nn.functional.linear(A, B, bias)
+    torch.testing.assert_close(a, torch.nn.functional.softplus(z, beta=100), rtol=1e-5, atol=2e-5)
+    torch.testing.assert_close(s, torch.where(z * 100 > 20, torch.ones_like(z), torch.sigmoid(100 * z)),
+                               rtol=1e-4, atol=1e-5)
+
+
+def test_linear_mul_split_tangent_bwd_relu():
+    ops = _ops()
+    M, N, K = 300, 256, 224
+    A = _rnd(M, K, seed=12)
+    B = _rnd(N, K, seed=13, scale=0.1)
+    aux0 = torch.rand(M, N, device=DEV)
+    aux1 = _rnd(M, N, seed=14)
+    v = (A.double() @ B.double().t()).float()
+    out, split = torch.empty(M, 256, device=DEV), torch.empty(M, 64, device=DEV)
+    ops.linear(A, B, N, K, out, ops.EPI_MUL, aux0=aux0, nsplit=204, out_split=split, nzero=256, adiv=ops.SQRT2)
+    torch.testing.assert_close(out[:, :204], (v / ops.SQRT2 * aux0)[:, :204], rtol=1e-5, atol=1e-5)
+    assert torch.all(out[:, 204:] == 0)
+    torch.testing.assert_close(split[:, :52], (v / ops.SQRT2)[:, 204:], rtol=1e-5, atol=1e-5)
+    o0, o1 = torch.empty(M, N, device=DEV), torch.empty(M, N, device=DEV)
+    ops.linear(A, B, N, K, o0, ops.EPI_TANGENT, aux0=aux0, aux1=aux1, out1=o1, beta=100.0)
+    torch.testing.assert_close(o0, v * aux0, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(o1, 100.0 * aux1 * (1 - aux0) * v, rtol=1e-4, atol=1e-4)
+    o2 = torch.empty(M, N, device=DEV)
+    ops.linear(A, B, N, K, o2, ops.EPI_BWD_SOFTPLUS, aux0=aux0, aux1=aux1)
+    torch.testing.assert_close(o2, v * aux0 + aux1, rtol=1e-5, atol=1e-5)
+    o3 = torch.empty(M, N, device=DEV)
+    ops.linear(A, B, N, K, o3, ops.EPI_BWD_RELU, aux0=aux1)
+    torch.testing.assert_close(o3, torch.where(aux1 > 0, v, torch.zeros_like(v)), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("M,N,K,pairs", [(70000, 256, 256, 2), (1000, 204, 64, 1), (5, 256, 256, 1),
+                                         (4097, 256, 320, 1)])
+def test_wgrad_matches_torch(M, N, K, pairs):
+    ops = _ops()
+    ldn, ldk = ops.rup(N, 128), ops.rup(K, 128 if K % 128 == 0 else 64)
+    Y0, X0 = _rnd(M, ldn, seed=15), _rnd(M, ldk, seed=16)
+    Y1, X1 = (_rnd(M, ldn, seed=17), _rnd(M, ldk, seed=18)) if pairs == 2 else (None, None)
+    dW = torch.empty(N, K, device=DEV)
+    db = torch.empty(N, device=DEV)
+    ops.wgrad(Y0, X0, N, K, dW, db=db, Y1=Y1, X1=X1)
+    ref = Y0[:, :N].double().t() @ X0[:, :K].double()
+    if pairs == 2:
+        ref = ref + Y1[:, :N].double().t() @ X1[:, :K].double()
+    tol = 1e-6 * math.sqrt(M) + 1e-5
+    torch.testing.assert_close(dW, ref.float(), rtol=1e-4, atol=tol)
+    torch.testing.assert_close(db, Y0[:, :N].double().sum(0).float(), rtol=1e-4, atol=tol)
+    # determinism: the slab reduction has a fixed order
+    dW2 = torch.empty_like(dW)
+    ops.wgrad(Y0, X0, N, K, dW2, Y1=Y1, X1=X1)
+    assert torch.equal(dW, dW2)
+
+
+def test_row_head_colsum_scale_cols():
+    ops = _ops()
+    M, K = 5000, 256
+    A = _rnd(M, K, seed=19)
+    W = _rnd(3, K, seed=20, scale=0.1)
+    b = _rnd(3, seed=21)
+    out = torch.empty(M, 3, device=DEV)
+    ops.row_head(A, K, W, b, 3, 1, out)
+    torch.testing.assert_close(out, torch.sigmoid(A @ W.t() + b), rtol=1e-5, atol=1e-6)
+    w = _rnd(M, seed=22)
+    cs = torch.empty(K, device=DEV)
+    ops.colsum(A, K, cs, w=w, wdiv=2.0)
+    torch.testing.assert_close(cs, ((w.double()[:, None] * A.double()).sum(0) / 2).float(), rtol=1e-5, atol=1e-4)
+    sc = torch.empty(M, K, device=DEV)
+    ops.scale_cols(A, K, W[0].contiguous(), sc)
+    torch.testing.assert_close(sc, A * W[0], rtol=0, atol=0)
+
+
+def test_c_abi_rejects_bad_arguments():
+    ops = _ops()
+    A = torch.zeros(10, 30, device=DEV)
+    B = torch.zeros(128, 30, device=DEV)
+    with pytest.raises(RuntimeError, match="multiple of 32"):
+        ops.linear(A, B, 16, 30, torch.empty(10, 16, device=DEV), ops.EPI_STORE)
+    with pytest.raises(RuntimeError, match="CUDA/HIP tensor"):
+        ops.linear(A.cpu(), B, 16, 32, torch.empty(10, 16, device=DEV), ops.EPI_STORE)
+
+
+# ----------------------------------------------------------------------------- fields vs oracle
+def _sdf_points(M, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.cat([(torch.rand(M, 3, generator=g) - 0.5) * 1.6, torch.full((M, 1), 0.25)], -1)
+
+
+@pytest.mark.parametrize("dh", [256, 64])
+def test_sdf_field_forward_gradient_and_double_backward(dh):
+    sdf, col, dev = build_modules(31, dh, dh)
+    P, Pc, var, leaves = oracle_params(sdf, col, dev)
+    M = 3000
+    x = _sdf_points(M, 5)
+    g = torch.Generator().manual_seed(6)
+    a, Bm, C = torch.randn(M, 1, generator=g), torch.randn(M, 256, generator=g) * 0.01, torch.randn(M, 4, generator=g)
+    # oracle
+    out = O.sdf_mlp(P, x)
+    gr = O.sdf_gradient(P, x)
+    L = (a * out[:, :1]).sum() + (Bm * out[:, 1:]).sum() + (C * gr).sum()
+    names = [n for n in leaves if n.startswith("sdf.")]
+    ref_grads = torch.autograd.grad(L, [leaves[n] for n in names])
+    # HIP
+    sdf_g = sdf.to(DEV)
+    s, f, G = sdf_g.field(x.to(DEV), want_feat=True, want_grad=True)
+    torch.testing.assert_close(s.cpu(), out[:, :1].detach(), rtol=1e-4, atol=2e-5)
+    torch.testing.assert_close(f.cpu(), out[:, 1:].detach(), rtol=1e-4, atol=2e-5)
+    torch.testing.assert_close(G.cpu(), gr.detach(), rtol=1e-3, atol=1e-4)
+    Lg = (a.to(DEV) * s).sum() + (Bm.to(DEV) * f).sum() + (C.to(DEV) * G).sum()
+    params = dict(sdf_g.named_parameters())
+    got = torch.autograd.grad(Lg, [params[n[4:]] for n in names])
+    for n, r, gg in zip(names, ref_grads, got):
+        scale = r.abs().max().item() + 1e-6
+        torch.testing.assert_close(gg.cpu(), r, rtol=2e-3, atol=2e-4 * scale, msg=lambda m: f"{n}: {m}")
+
+
+def test_color_field_forward_backward():
+    sdf, col, dev = build_modules(32)
+    P, Pc, var, leaves = oracle_params(sdf, col, dev)
+    fx = fixture("seams")
+    R, S = 16, 16
+    M = R * S
+    pts = fx["col_pts"][:M]
+    dirs_r = fx["col_dirs"][:R]
+    dirs = dirs_r[:, None, :].expand(R, S, 3).reshape(M, 3)
+    feat = fx["col_feat"][:M].clone().requires_grad_(True)
+    gg = fx["col_g"][:M].clone().requires_grad_(True)
+    D = fx["col_D"][:M]
+    rgb = O.color_mlp(Pc, pts, gg, dirs, feat)
+    names = [n for n in leaves if n.startswith("col.")]
+    ref = torch.autograd.grad((D * rgb).sum(), [leaves[n] for n in names] + [feat, gg])
+    colg = col.to(DEV)
+    featg = feat.detach().to(DEV).requires_grad_(True)
+    ggg = gg.detach().to(DEV).requires_grad_(True)
+    rgbg = colg.color(pts.to(DEV), ggg, dirs_r.to(DEV), S, featg)
+    torch.testing.assert_close(rgbg.cpu(), rgb.detach(), rtol=1e-4, atol=1e-5)
+    params = dict(colg.named_parameters())
+    got = torch.autograd.grad((D.to(DEV) * rgbg).sum(), [params[n[4:]] for n in names] + [featg, ggg])
+    for n, r, g in zip(names + ["feat", "g"], ref, got):
+        torch.testing.assert_close(g.cpu(), r, rtol=1e-3, atol=1e-5 * (r.abs().max().item() + 1e-3),
+                                   msg=lambda m: f"{n}: {m}")
+
+
+def test_composite_forward_backward():
+    from copenerf.renderer import _CompositeFn
+    g = torch.Generator().manual_seed(40)
+    R, S = 37, 128
+    z = torch.sort(torch.rand(R, S, generator=g) * 2.5 + 0.1, -1)[0]
+    sdf = (0.9 - z.reshape(-1, 1)) + 0.05 * torch.randn(R * S, 1, generator=g)
+    Gm = torch.randn(R * S, 4, generator=g)
+    rgb = torch.rand(R * S, 3, generator=g)
+    rays_d = torch.nn.functional.normalize(torch.randn(R, 3, generator=g), dim=-1)
+    near, far = torch.full((R, 1), 0.1), torch.full((R, 1), 2.6)
+    inv_s = torch.tensor([[30.0]])
+    car = 0.3
+    dcol, ddep, dw = torch.randn(R, 3, generator=g), torch.randn(R, 1, generator=g), torch.randn(R, S, generator=g)
+    # oracle
+    leaves = [t.clone().requires_grad_(True) for t in (sdf, Gm, rgb, inv_s)]
+    sd = (far[0, 0] - near[0, 0]) / 64
+    dists = torch.cat([z[:, 1:] - z[:, :-1], sd.expand(R, 1)], -1)
+    dirs = rays_d[:, None, :].expand(R, S, 3).reshape(-1, 3)
+    c, d, w, pc = O.composite(z, dists, leaves[0], leaves[1][:, :3], leaves[2].reshape(R, S, 3), dirs, leaves[3], car)
+    Lr = (dcol * c).sum() + (ddep * d).sum() + (dw * w).sum()
+    ref = torch.autograd.grad(Lr, leaves)
+    # HIP
+    gl = [t.to(DEV).requires_grad_(True) for t in (sdf, Gm, rgb, inv_s)]
+    cg, dg, wg, pcg = _CompositeFn.apply(z.to(DEV), gl[0], gl[1], gl[2], rays_d.to(DEV), gl[3], near.to(DEV),
+                                         far.to(DEV), 64, car)
+    torch.testing.assert_close(cg.cpu(), c, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(dg.cpu(), d, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(wg.cpu(), w, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(pcg.cpu(), pc.reshape(R, S), rtol=1e-5, atol=1e-6)
+    Lg = (dcol.to(DEV) * cg).sum() + (ddep.to(DEV) * dg).sum() + (dw.to(DEV) * wg).sum()
+    got = torch.autograd.grad(Lg, gl)
+    for n, r, gg in zip(("sdf", "G", "rgb", "inv_s"), ref, got):
+        torch.testing.assert_close(gg.cpu(), r, rtol=1e-4, atol=1e-5 * (r.abs().max().item() + 1e-3),
+                                   msg=lambda m: f"{n}: {m}")
+
+
+@pytest.mark.parametrize("n", [64, 80, 96, 112])
+def test_up_sample_merge_matches_reference_seams(n):
+    ops = _ops()
+    fx = fixture("seams")
+    z, sd = fx[f"up{n}_z"], fx[f"up{n}_sdf"]
+    R = z.shape[0]
+    z_out, z_new = torch.empty(R, n + 16, device=DEV), torch.empty(R, 16, device=DEV)
+    sdf_out = torch.empty(R, n + 16, device=DEV)
+    dst = torch.empty(R * 16, dtype=torch.int32, device=DEV)
+    ops.up_sample_merge(z.to(DEV), sd.to(DEV), 16, float(fx[f"up{n}_invs"]), z_out, z_new, sdf_out, dst)
+    torch.testing.assert_close(z_new.cpu(), fx[f"up{n}_new"], rtol=0, atol=2e-6)
+    torch.testing.assert_close(z_out.cpu(), fx[f"up{n}_cat"], rtol=0, atol=2e-6)
+    # the scatter map puts every new sample where its z landed and old sdf at the old z positions
+    flat = z_out.reshape(-1)
+    assert torch.equal(flat[dst.long()], z_new.reshape(-1))
+    pos_old = sdf_out.clone().reshape(-1)
+    pos_old[dst.long()] = float("nan")
+    kept = pos_old[~torch.isnan(pos_old)].reshape(R, n)
+    torch.testing.assert_close(kept.cpu(), sd, rtol=0, atol=0)
