@@ -86,8 +86,7 @@ def pack_sdf(lay: SDFLayout, Ws, bs) -> SDFPack:
             o, i = W.shape
             kp = lay.KE if l == 0 else rup(i, 32)
             Bf.append(F.pad(W, (0, kp - i, 0, rup(o, 128) - o)).contiguous())
-            tn = 64 if i <= 64 else 128
-            Bt.append(F.pad(W.t(), (0, rup(o, 32) - o, 0, rup(i, tn) - i)).contiguous())
+            Bt.append(F.pad(W.t(), (0, rup(o, 32) - o, 0, rup(i, 128) - i)).contiguous())
             b.append(bs[l].detach().contiguous())
         W8, b8 = Ws[-1].detach(), bs[-1].detach()
         s = float(lay.scale)
@@ -343,7 +342,7 @@ class SDFNetwork(nn.Module):
                 out_dim.append(w.shape[0])
                 in_dim.append(w.shape[1])
             E = self.dims[0]
-            hl = rup(max(max(in_dim), max(out_dim[:-1]), out_dim[-1] - 1), 128)
+            hl = rup(max(max(in_dim[1:]), max(out_dim[:-1])), 128)  # hidden buffers (feature has its own)
             self._layout = SDFLayout(n_lin=n_lin, in_dim=in_dim, out_dim=out_dim, E=E, KE=rup(E, 64), HL=hl,
                                      skip=self.skip_in[0] if self.skip_in else -1, multires=self.multires,
                                      scale=float(self.scale), beta=float(self.activation.beta),

@@ -56,7 +56,7 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
         _need(t, n)
     M = A.shape[0] if M is None else M
     if tile is None:
-        tile = 1 if N <= 64 else 0
+        tile = 1 if max(N, nzero or 0) <= 64 else 0
     bn = 64 if tile == 1 else 128
     if B.shape[0] < rup(N, bn) or B.shape[1] < K:
         raise RuntimeError(f"cn_linear: B {tuple(B.shape)} too small for N={N}, K={K} (tile {tile})")

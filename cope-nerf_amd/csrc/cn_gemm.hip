@@ -593,6 +593,9 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     if (d->A2) CN_REQUIRE(d->lda2 >= d->K - K1 && d->lda2 % 4 == 0 && al16(d->A2), CN_ERR_ALIGN, "cn_linear: bad A2/lda2");
     CN_REQUIRE(d->ldb >= d->K && d->ldb % 4 == 0 && al16(d->B), CN_ERR_ALIGN, "cn_linear: bad B/ldb");
     const int nzero = std::max(d->nzero, d->N);
+    const int bn = d->tile == 0 ? 128 : 64;
+    CN_REQUIRE(nzero <= cdiv(d->N, bn) * bn, CN_ERR_SHAPE,
+               "cn_linear: nzero=%d beyond the column tiles covering N=%d (tile width %d)", nzero, d->N, bn);
     CN_REQUIRE(d->ld_out0 >= nzero, CN_ERR_SHAPE, "cn_linear: ld_out0=%lld < nzero=%d", (long long)d->ld_out0, nzero);
     const int e = d->epilogue;
     if (e == CN_EPI_MUL || e == CN_EPI_TANGENT || e == CN_EPI_BWD_SOFTPLUS || e == CN_EPI_BWD_RELU)

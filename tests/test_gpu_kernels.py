@@ -33,7 +33,7 @@ def test_linear_store_matches_torch(M, N, K, tile):
     B = torch.zeros(Np, K, device=DEV)
     B[:N] = _rnd(N, K, seed=2, scale=0.1)
     bias = _rnd(N, seed=3)
-    ld = ops.rup(N, 128)
+    ld = ops.rup(N, bn)
     out = torch.full((M, ld), float("nan"), device=DEV)
     ops.linear(A, B, N, K, out, ops.EPI_STORE, bias=bias, nzero=ld, tile=tile)
     ref = (A.double() @ B[:N].double().t() + bias.double()).float()
