@@ -1,0 +1,190 @@
+"""bench.py — train-step throughput of the MI355X NeuS hot path.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Metric (BASELINE.json): rays/sec of a full training step incl. backward at
+4096 rays x 128 samples per GPU (64 coarse + 4x16 importance, fp32, fixed
+poses, synthetic data): patch sampling + ray generation, the HIP renderer
+forward, L1 rgb + 0.1 eikonal + edge-aware / plain depth smoothness, the HIP
+backward (incl. the ∇ₓSDF double backward), the gradient all-reduce (N > 1)
+and Adam.  Weak scaling: every rank renders its own 4096 rays.
+
+The JSON line also carries
+  roofline      the dominant kernel's algorithmic FLOPs / its average launch
+                time, measured with HIP events on the launching stream over the
+                timed steps, against the gfx950 fp32 MFMA peak; `traffic` is
+                the rocprofv3 PMC (FETCH_SIZE + WRITE_SIZE) per launch read from
+                profiles/ when a counter pass for this kernel is committed;
+  cpu_baseline  the CPU oracle (oracle/neus_oracle.py, a torch port of the
+                reference path) timed on this box's host cores on a bounded
+                sample (rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "cope-nerf_amd"), ROOT]
+
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, = fp32 vector peak
+RAYS = 4096
+SAMPLES = 128
+GFLOP_PER_RAY_REF = 1.4809  # reference GEMM FLOPs per ray per train step (64+4x16)
+
+
+def kernel_symbol(key):
+    if key[0] == "linear":
+        tiles = {0: "2, 2, 2, 2", 1: "4, 1, 1, 2"}
+        epi = {"store": 0, "softplus": 1, "relu": 2, "mul": 3, "tangent": 4, "bwd_softplus": 5, "bwd_relu": 6}
+        return f"void cn::linear_kernel<{tiles[key[1]]}, {epi[key[2]]}>(cn::LinearArgs)"
+    return "cn::wgrad_kernel (+ wgrad_reduce)"
+
+
+def pmc_traffic(symbol):
+    """Per-launch HBM bytes of `symbol` from the newest committed counter pass."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+    for f in reversed(files):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        k = d.get("kernels", {}).get(symbol)
+        if k and k.get("hbm_bytes_per_launch"):
+            return float(k["hbm_bytes_per_launch"]), os.path.relpath(f, ROOT)
+    return None, None
+
+
+def cpu_baseline(rays=256, steps=2):
+    """Time the CPU oracle (torch restatement of the reference path) on the host."""
+    from tests.helpers import build_modules, oracle_params
+    from oracle import neus_oracle as O
+    threads = int(os.environ.get("COPENERF_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    torch.set_num_threads(threads)
+    mods = build_modules(678)
+    g = torch.Generator().manual_seed(0)
+
+    def one(R):
+        P, Pc, var, leaves = oracle_params(*mods)
+        o = torch.zeros(R, 3)
+        d = torch.cat([(torch.rand(R, 2, generator=g) - 0.5), -torch.ones(R, 1)], -1)
+        nrm = d.norm(dim=-1, keepdim=True)
+        out = O.render(P, Pc, var, o, d / nrm, nrm, torch.zeros(1), torch.full((R, 1), 0.01), torch.full((R, 1), 5.0),
+                       car=0.5, t_rand=torch.rand(R, 64, generator=g))
+        loss = O.train_loss(out, torch.rand(R, 3, generator=g))
+        torch.autograd.grad(loss, list(leaves.values()))
+
+    one(16)  # warm the allocator / MKL
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one(rays)
+    dt = time.perf_counter() - t0
+    return {"value": round(rays * steps / dt, 3), "unit": "rays/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/neus_oracle.py train step (fwd + L1/eikonal/smoothness loss + backward, no optimiser), "
+                      f"{steps} steps x {rays} rays x 128 samples (64+4x16), full-width nets, fp32, "
+                      f"torch {torch.__version__} CPU, {threads} threads, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rays", type=int, default=RAYS)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    torch.cuda.set_device(local)
+    if distributed:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from copenerf import ops
+    from copenerf.train_step import SyntheticTrainer
+    tr = SyntheticTrainer(f"cuda:{local}", rays=args.rays, distributed=distributed)
+
+    for _ in range(args.warmup):
+        tr.step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+
+    timer = ops.KernelTimer()
+    ops.set_kernel_timer(timer)
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = tr.step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ops.set_kernel_timer(None)
+    if distributed:
+        t = torch.tensor([elapsed], device=f"cuda:{local}", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    if not torch.isfinite(loss).item():
+        raise RuntimeError("non-finite loss in the timed steps")
+
+    agg = timer.summary()
+    dom_key = max(agg, key=lambda k: agg[k]["ms"])
+    dom = agg[dom_key]
+    avg_ms = dom["ms"] / dom["launches"]
+    achieved = dom["flops"] / dom["launches"] / (avg_ms * 1e-3) / 1e12
+    symbol = kernel_symbol(dom_key)
+    traffic, traffic_src = pmc_traffic(symbol)
+    kernels_ms = sum(a["ms"] for a in agg.values()) / args.steps
+    rays_total = args.rays * world * args.steps
+    result = {
+        "metric": "rays/sec (train step incl. backward) at 4096 rays × 128 samples",
+        "value": round(rays_total / elapsed, 1),
+        "unit": "rays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (random 540x960 image, 4x4 patches, fixed identity pose, geometric-init SDF, seed 678)",
+        "config": {"workload": "C2: synthetic scene, 4096 rays x 128 samples (64 coarse + 4x16 importance) per GPU, "
+                               "fp32, fixed poses, full train step (fwd + losses + bwd + Adam)",
+                   "rays_per_gpu": args.rays, "samples_per_ray": SAMPLES, "global_rays": args.rays * world,
+                   "parallelism": f"dp{world}" if world > 1 else "single"},
+        "roofline": {"bound": "mfma", "kernel": symbol, "achieved": round(achieved, 2),
+                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "launches_per_step": dom["launches"] / args.steps, "avg_launch_ms": round(avg_ms, 4),
+                     "algorithmic_gflop_per_launch": round(dom["flops"] / dom["launches"] / 1e9, 3)},
+        "effective_ref_tflops": round(rays_total / elapsed * GFLOP_PER_RAY_REF / 1e3, 2),
+        "gemm_ms_per_step": round(kernels_ms, 3),
+        "kernel_breakdown_ms_per_step": {"/".join(map(str, k)): round(v["ms"] / args.steps, 3) for k, v in
+                                         sorted(agg.items(), key=lambda kv: -kv[1]["ms"])},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -127,7 +127,7 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
         K = KE if l == 0 else rup(lay.in_dim[l], 32)
         ops.linear(U[l], pk.Bf[l], lay.out_dim[l], K, out, EPI_SOFTPLUS, bias=pk.b[l], out1=sig,
                    nzero=lay.out_dim[l] if into else HL, odiv=SQRT2 if into else 1.0, beta=lay.beta,
-                   threshold=lay.threshold)
+                   threshold=lay.threshold, kalg=lay.in_dim[l])
         U[l + 1], Sig[l] = out, sig
         if not keep_sig and l >= 1 and (l != sk):
             U[l] = None  # free as we go on the no-grad sampler path
@@ -150,11 +150,12 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
             S[l - 1] = _empty(M, HL, dev)
             if l == sk:
                 ops.linear(S[l], pk.Bt[l], lay.in_dim[l], Kl, S[l - 1], EPI_MUL, aux0=Sig[l - 1],
-                           nsplit=lay.out_dim[l - 1], out_split=QE, nzero=HL, adiv=SQRT2)
+                           nsplit=lay.out_dim[l - 1], out_split=QE, nzero=HL, adiv=SQRT2, kalg=lay.out_dim[l])
             else:
-                ops.linear(S[l], pk.Bt[l], lay.out_dim[l - 1], Kl, S[l - 1], EPI_MUL, aux0=Sig[l - 1], nzero=HL)
+                ops.linear(S[l], pk.Bt[l], lay.out_dim[l - 1], Kl, S[l - 1], EPI_MUL, aux0=Sig[l - 1], nzero=HL,
+                           kalg=lay.out_dim[l])
         Q0 = _empty(M, KE, dev)
-        ops.linear(S[0], pk.Bt[0], lay.E, rup(lay.out_dim[0], 32), Q0, EPI_STORE, nzero=KE)
+        ops.linear(S[0], pk.Bt[0], lay.E, rup(lay.out_dim[0], 32), Q0, EPI_STORE, nzero=KE, kalg=lay.out_dim[0])
         G = _empty(M, 4, dev)
         ops.sdf_grad_assemble(lay.multires, lay.scale, U[0], Q0, QE, G)
     return {"U": U, "Sig": Sig, "S": S, "sdf": sdf, "feat": feat, "G": G}
@@ -195,7 +196,8 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG):
             R[l] = _empty(M, HL, dev)
             K = KE if l == 0 else rup(lay.in_dim[l], 32)
             ops.linear(Ud[l], pk.Bf[l], lay.out_dim[l], K, out, EPI_TANGENT, aux0=Sig[l], aux1=S[l], out1=R[l],
-                       nzero=lay.out_dim[l] if into else HL, odiv=SQRT2 if into else 1.0, beta=lay.beta)
+                       nzero=lay.out_dim[l] if into else HL, odiv=SQRT2 if into else 1.0, beta=lay.beta,
+                       kalg=lay.in_dim[l])
             Ud[l + 1] = out
 
     i8, o8 = lay.in_dim[L8], lay.out_dim[L8]
@@ -230,7 +232,7 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG):
         if l > 0:
             Z = _empty(M, HL, dev)
             ops.linear(Zl, pk.Bt[l], lay.out_dim[l - 1], rup(lay.out_dim[l], 32), Z, EPI_BWD_SOFTPLUS,
-                       aux0=Sig[l - 1], aux1=R[l - 1], nzero=HL, adiv=SQRT2 if l == sk else 1.0)
+                       aux0=Sig[l - 1], aux1=R[l - 1], nzero=HL, adiv=SQRT2 if l == sk else 1.0, kalg=lay.out_dim[l])
         dW = torch.empty(lay.out_dim[l], lay.in_dim[l], device=dev)
         db = torch.empty(lay.out_dim[l], device=dev)
         ops.wgrad(Zl, U[l], lay.out_dim[l], lay.in_dim[l], dW, db=db,
@@ -447,7 +449,8 @@ class _ColorFieldFn(torch.autograd.Function):
         A, A2, K1, K = feat, ext, lay.F, lay.F + lay.KX
         for l in range(lay.n_lin - 1):
             out = _empty(M, lay.HL, dev)
-            ops.linear(A, pk.Bf[l], lay.out_dim[l], K, out, EPI_RELU, bias=pk.b[l], A2=A2, K1=K1, nzero=lay.HL)
+            ops.linear(A, pk.Bf[l], lay.out_dim[l], K, out, EPI_RELU, bias=pk.b[l], A2=A2, K1=K1, nzero=lay.HL,
+                       kalg=lay.in_dim[l])
             H.append(out)
             A, A2, K1, K = out, None, None, rup(lay.out_dim[l], 32)
         rgb = _empty(M, 3, dev)

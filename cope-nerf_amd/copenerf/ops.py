@@ -18,6 +18,43 @@ from ._lib import (EPI_BWD_RELU, EPI_BWD_SOFTPLUS, EPI_MUL, EPI_RELU, EPI_SOFTPL
 SQRT2 = float(math.sqrt(2.0))  # torch's x / np.sqrt(2) divides by the fp32 rounding of this
 
 
+class KernelTimer:
+    """Brackets cn_linear / cn_wgrad launches with HIP events on the launching
+    stream (torch's current stream) and keeps (key, events, algorithmic FLOPs)."""
+
+    def __init__(self):
+        self.records = []
+
+    def start(self):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def stop(self, key, e0, flops):
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        self.records.append((key, e0, e1, flops))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        agg = {}
+        for key, e0, e1, fl in self.records:
+            a = agg.setdefault(key, {"launches": 0, "ms": 0.0, "flops": 0.0})
+            a["launches"] += 1
+            a["ms"] += e0.elapsed_time(e1)
+            a["flops"] += fl
+        return agg
+
+
+_timer = None
+EPI_NAMES = {0: "store", 1: "softplus", 2: "relu", 3: "mul", 4: "tangent", 5: "bwd_softplus", 6: "bwd_relu"}
+
+
+def set_kernel_timer(t):
+    global _timer
+    _timer = t
+
+
 def rup(x: int, m: int) -> int:
     return (x + m - 1) // m * m
 
@@ -49,8 +86,9 @@ def _ld(t):
 
 def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None, colv=None, aux0=None,
            aux1=None, out1=None, out_split=None, nsplit=None, nzero=None, adiv=1.0, odiv=1.0, beta=100.0,
-           threshold=20.0, tile=None, M=None):
-    """out = epilogue((A|A2) @ B[:N].T / adiv) -- cn_linear."""
+           threshold=20.0, tile=None, M=None, kalg=None):
+    """out = epilogue((A|A2) @ B[:N].T / adiv) -- cn_linear.  kalg: the unpadded
+    inner dimension (for the FLOP count of the kernel timer only)."""
     for t, n in ((A, "A"), (A2, "A2"), (B, "B"), (out0, "out0"), (out1, "out1"), (aux0, "aux0"),
                  (aux1, "aux1"), (out_split, "out_split")):
         _need(t, n)
@@ -74,7 +112,12 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     d.nsplit = nsplit if nsplit is not None else N
     d.epilogue, d.tile = epilogue, tile
     d.adiv, d.odiv, d.beta, d.threshold = adiv, odiv, beta, threshold
-    _lib.check(_lib.load().cn_linear(d, _stream()), "cn_linear")
+    if _timer is not None:
+        e0 = _timer.start()
+        _lib.check(_lib.load().cn_linear(d, _stream()), "cn_linear")
+        _timer.stop(("linear", tile, EPI_NAMES[epilogue]), e0, 2.0 * M * N * (kalg or K))
+    else:
+        _lib.check(_lib.load().cn_linear(d, _stream()), "cn_linear")
     return out0
 
 
@@ -95,7 +138,12 @@ def wgrad(Y0, X0, N, K, dW, *, db=None, Y1=None, X1=None, accumulate=False):
     d.npairs = 2 if Y1 is not None else 1
     d.n_out, d.k_out = dW.shape[0], dW.shape[1]
     d.accumulate = 1 if accumulate else 0
-    _lib.check(lib.cn_wgrad(d, _stream()), "cn_wgrad")
+    if _timer is not None:
+        e0 = _timer.start()
+        _lib.check(lib.cn_wgrad(d, _stream()), "cn_wgrad")
+        _timer.stop(("wgrad", d.npairs), e0, 2.0 * M * d.n_out * d.k_out * d.npairs)
+    else:
+        _lib.check(lib.cn_wgrad(d, _stream()), "cn_wgrad")
     return dW
 
 

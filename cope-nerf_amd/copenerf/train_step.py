@@ -1,0 +1,105 @@
+"""One cope-nerf training iteration on synthetic data (the per-iteration
+sequence of train.py:407-532 restricted to the rendering hot path):
+
+  patch sampling + ray generation   training.py:413-487      (rays.py, device)
+  NeuSRenderer forward               train.py:441-444         (HIP)
+  losses: L1 rgb, eikonal, edge-aware + plain depth smoothness on 4x4 patches
+                                     training.py:506-533, train.py:519-526
+  backward + Adam                    training.py:552-558      (HIP backward, torch Adam)
+
+Data-parallel over ranks: each rank renders its own R rays;
+gradients of SDF + colour + variance are summed with ONE all-reduce of a flat
+fp32 bucket (RCCL over xGMI when the process group is nccl) and divided by the
+world size, which equals the gradient of the mean loss over all ranks' rays.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from .fields import RenderingNetwork, SDFNetwork, SingleVarianceNetwork
+from .losses import EdgePreservingSmoothnessLoss, SmoothnessLoss, eikonal_loss, rgb_l1
+from .rays import get_patch_indices, intrinsics_ndc, near_far_from_sphere, pixels_from_indices, world_rays
+from .renderer import NeuSRenderer
+
+SDF_CFG = dict(d_in=4, d_out=257, d_hidden=256, n_layers=8, skip_in=[4], multires=6, bias=0.5, scale=1.0,
+               geometric_init=True, weight_norm=True)
+COL_CFG = dict(d_feature=256, mode="idr", d_in=11, d_out=3, d_hidden=256, n_layers=4, weight_norm=True,
+               multires_view=4, squeeze_out=True, use_negative_ray_vector=False)
+REN_CFG = dict(n_samples=64, n_importance=64, n_outside=0, up_sample_steps=4, perturb=1.0,
+               n_max_network_queries=64000, importance_sampling_start=0, naive_render=False)
+
+
+def flat_allreduce_mean(params, group=None):
+    """Sum every gradient across ranks in one flat bucket, then divide by world size."""
+    grads = [p.grad for p in params if p.grad is not None]
+    if not grads:
+        return
+    world = dist.get_world_size(group)
+    flat = torch.cat([g.reshape(-1) for g in grads])
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+    flat.div_(world)
+    off = 0
+    for g in grads:
+        n = g.numel()
+        g.copy_(flat[off:off + n].view_as(g))
+        off += n
+
+
+class SyntheticTrainer:
+    def __init__(self, device, rays=4096, H=540, W=960, patch=4, seed=678, depth_range=(0.01, 5.0),
+                 cos_anneal_ratio=0.5, lr=1e-3, weights=dict(rgb=1.0, eikonal=0.1, edge=1.0, smooth=1e-4),
+                 distributed=False, sdf_cfg=None, col_cfg=None, ren_cfg=None):
+        self.device = torch.device(device)
+        self.R, self.H, self.W, self.patch = rays, H, W, patch
+        self.depth_range = depth_range
+        self.car = cos_anneal_ratio
+        self.w = weights
+        self.distributed = distributed
+        torch.manual_seed(seed)
+        self.sdf = SDFNetwork(**(sdf_cfg or SDF_CFG)).to(self.device)
+        self.col = RenderingNetwork(**(col_cfg or COL_CFG)).to(self.device)
+        self.var = SingleVarianceNetwork(0.3).to(self.device)
+        self.renderer = NeuSRenderer(None, self.sdf, self.var, self.col, None, **(ren_cfg or REN_CFG)).to(self.device)
+        self.params = list(self.sdf.parameters()) + list(self.var.parameters()) + list(self.col.parameters())
+        self.opt = torch.optim.Adam(self.params, lr=lr)
+        gen = torch.Generator(device=self.device).manual_seed(seed + (dist.get_rank() if distributed else 0))
+        self.gen = gen
+        self.image = torch.rand(3, H, W, device=self.device, generator=gen)
+        f = 0.9 * W
+        self.K = intrinsics_ndc(f, f, W, H, device=self.device)
+        self.I = torch.eye(4, device=self.device)
+        self.time_step = torch.zeros(1, device=self.device)
+        self.edge = EdgePreservingSmoothnessLoss(patch)
+        self.smooth = SmoothnessLoss(patch)
+        self.it = 0
+
+    def make_batch(self):
+        idx = get_patch_indices(self.H, self.W, self.patch, self.R, generator=self.gen, device=self.device)
+        pix, pixn = pixels_from_indices(idx, self.H, self.W)
+        rays_o, rays_d, norm = world_rays(pixn, self.K, self.I, self.I)
+        rgb_gt = self.image[:, pix[:, 1], pix[:, 0]].t().contiguous()
+        return rays_o, rays_d, norm, rgb_gt
+
+    def loss(self, out, rgb_gt):
+        w = self.w
+        loss = w["rgb"] * rgb_l1(out["color_fine"], rgb_gt) + w["eikonal"] * eikonal_loss(out["normals"])
+        if self.patch > 1:
+            d = out["depth_pred"].view(-1, self.patch, self.patch, 1)
+            g = rgb_gt.view(-1, self.patch, self.patch, 3)
+            loss = loss + w["edge"] * self.edge(d, g) + w["smooth"] * self.smooth(d)
+        return loss
+
+    def step(self):
+        rays_o, rays_d, norm, rgb_gt = self.make_batch()
+        near, far = near_far_from_sphere(rays_o, self.depth_range)
+        out = self.renderer(rays_o, rays_d, norm, self.time_step, near, far, cos_anneal_ratio=self.car,
+                            it=self.it, eval=False)
+        loss = self.loss(out, rgb_gt)
+        self.opt.zero_grad(set_to_none=True)
+        loss.backward()
+        if self.distributed:
+            flat_allreduce_mean(self.params)
+        self.opt.step()
+        self.it += 1
+        return loss
