@@ -1,0 +1,73 @@
+"""The C ABI library loads, exports exactly what include/copenerf.h declares,
+and rejects bad arguments before touching the GPU (no device needed)."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "copenerf.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(cn_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_and_binding_agree():
+    from copenerf import _lib
+    assert set(_declared()) == set(_lib.SIGNATURES), set(_declared()) ^ set(_lib.SIGNATURES)
+
+
+def test_library_exports_every_declared_symbol():
+    from copenerf import _lib
+    lib = _lib.load()
+    for name in _declared():
+        assert hasattr(lib, name), name
+    m = re.search(r"#define CN_ABI_VERSION (\d+)", open(HEADER).read())
+    assert lib.cn_abi_version() == int(m.group(1)) == _lib.ABI_VERSION
+
+
+def test_struct_layouts_match_header_order():
+    from copenerf import _lib
+    src = open(HEADER).read()
+    for cname, py in (("cn_linear_desc", _lib.LinearDesc), ("cn_wgrad_desc", _lib.WgradDesc)):
+        body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (cname, cname), src, re.S).group(1)
+        body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+        names = []
+        for decl in body.split(";"):
+            decl = decl.strip()
+            if not decl:
+                continue
+            decl = re.sub(r"^(const\s+)?\w+\s*\**", "", decl)
+            names += [n.strip(" *") for n in decl.split(",")]
+        assert names == [f[0] for f in py._fields_], (cname, names)
+    assert ctypes.sizeof(_lib.LinearDesc) % 8 == 0
+
+
+def test_argument_validation_without_gpu():
+    from copenerf import _lib
+    lib = _lib.load()
+    assert lib.cn_linear(None, None) == -1
+    assert b"null desc" in lib.cn_last_error()
+    d = _lib.LinearDesc()
+    d.A, d.B, d.out0 = 16, 16, 16
+    d.M, d.N, d.K = 8, 8, 30  # K not a multiple of 32
+    assert lib.cn_linear(ctypes.byref(d), None) == -2
+    assert b"multiple of 32" in lib.cn_last_error()
+    assert lib.cn_row_head(1, 300, 16, 4, 16, 4, None, 1, 0, 16, 1, None, None) == -5
+    assert lib.cn_up_sample_merge(1, 300, 16, 1.0, 16, 16, 16, 16, None, None, None) == -5
+    w = _lib.WgradDesc()
+    assert lib.cn_wgrad(ctypes.byref(w), None) == -1
+    assert lib.cn_wgrad_workspace_bytes(524288, 256, 256) >= 4 * 256 * 256
+
+
+def test_product_path_refuses_cpu_tensors():
+    from copenerf import SDFNetwork
+    torch.manual_seed(0)
+    net = SDFNetwork(d_in=4, d_out=257, d_hidden=64, n_layers=8, skip_in=[4], multires=6)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        net.sdf(torch.zeros(8, 4))

@@ -1,0 +1,77 @@
+"""Data-parallel gradient exchange (train_step.flat_allreduce_mean) on 2 gloo
+ranks: each rank differentiates the oracle on its half of the rays; after the
+flat all-reduce every rank holds the single-process gradient of the full batch."""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from helpers import REN_CFG
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _batch(R, seed):
+    g = torch.Generator().manual_seed(seed)
+    o = torch.tensor([0.05, -0.03, 1.6]).expand(R, 3).contiguous()
+    d = torch.cat([(torch.rand(R, 2, generator=g) - 0.5) * 0.5, -torch.ones(R, 1)], -1)
+    n = d.norm(dim=-1, keepdim=True)
+    return o, d / n, n, torch.rand(R, 64, generator=g), torch.rand(R, 3, generator=g)
+
+
+def _grads(rows):
+    from helpers import build_modules, oracle_params
+    from oracle import neus_oracle as O
+    P, Pc, var, leaves = oracle_params(*build_modules(9, 64, 64))
+    o, d, n, tr, gt = rows
+    R = o.shape[0]
+    out = O.render(P, Pc, var, o, d, n, torch.tensor([0.1]), torch.full((R, 1), 0.01), torch.full((R, 1), 3.0),
+                   car=0.5, t_rand=tr, n_samples=REN_CFG["n_samples"], n_importance=REN_CFG["n_importance"])
+    loss = O.train_loss(out, gt)
+    names = list(leaves)
+    gr = torch.autograd.grad(loss, [leaves[k] for k in names])
+    return names, gr
+
+
+def _worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "cope-nerf_amd"), root, os.path.join(root, "tests")]
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    from copenerf.train_step import flat_allreduce_mean
+    full = _batch(32, 0)
+    half = tuple(t[rank * 16:(rank + 1) * 16] for t in full)  # whole 4x4 patches per rank
+    names, gr = _grads(half)
+    params = [torch.nn.Parameter(torch.zeros_like(g)) for g in gr]
+    for p, g in zip(params, gr):
+        p.grad = g.clone()
+    flat_allreduce_mean(params)
+    q.put((rank, {n: p.grad.numpy().copy() for n, p in zip(names, params)}))  # by value, not shared memory
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_allreduce_equals_full_batch():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    names, ref = _grads(_batch(32, 0))
+    for n, r in zip(names, ref):
+        for rank in range(world):
+            torch.testing.assert_close(torch.from_numpy(res[rank][n]), r, rtol=1e-4, atol=1e-6, msg=lambda m: f"{n} rank {rank}: {m}")
