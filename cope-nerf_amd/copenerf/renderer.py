@@ -116,7 +116,10 @@ class NeuSRenderer(nn.Module):
 
     # -- forward -------------------------------------------------------------
     def forward(self, rays_o, rays_d, ray_d_norm, time_step, near, far, perturb_overwrite=-1, background_rgb=None,
-                cos_anneal_ratio=0.0, it=-1, eval=False, t_rand=None):
+                cos_anneal_ratio=0.0, it=-1, eval=False, t_rand=None, z_vals=None):
+        """Reference signature (neus_renderer.py:453) plus two test hooks: `t_rand`
+        injects the stratified jitter, `z_vals` [R, S] skips the sampler and renders
+        at the given sample positions (the render_core seam)."""
         if rays_o.requires_grad or rays_d.requires_grad:
             raise NotImplementedError("copenerf: ray gradients (eval.py pose optimisation) are not implemented yet")
         R = len(rays_o)
@@ -137,7 +140,10 @@ class NeuSRenderer(nn.Module):
 
         sdf_packed = self.sdf_network.params_and_pack()
         col_packed = self.color_network.params_and_pack()
-        z = self.sample_z(rays_o, rays_d, time_step, near, far, n_samples, n_importance, t_rand, sdf_packed)
+        if z_vals is None:
+            z = self.sample_z(rays_o, rays_d, time_step, near, far, n_samples, n_importance, t_rand, sdf_packed)
+        else:
+            z = z_vals.contiguous().float()
         S = z.shape[1]
 
         # render_core (neus_renderer.py:307-450)

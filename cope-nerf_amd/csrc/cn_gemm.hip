@@ -41,49 +41,83 @@ struct LinearArgs {
     float adiv, odiv, beta, threshold;
 };
 
+// Softplus and softplus' sharing one exp: a = log1p(e)/beta, sg = e/(1 + e),
+// e = exp(beta z); linear branch above the threshold exactly as
+// torch.nn.Softplus(beta, threshold).  log1p(e) = log(t) * e / (t - 1) with
+// t = 1 + e rounded (Goldberg) keeps full relative accuracy for small e with one
+// accurate logf instead of log1pf; reciprocals are v_rcp_f32 (1 ulp).
+__device__ __forceinline__ void softplus_fast(float z, float beta, float inv_beta, float thr, float& a, float& sg) {
+    const float bx = z * beta;
+    if (bx > thr) {
+        a = z;
+        sg = 1.0f;
+    } else {
+        const float e = expf(bx);
+        const float t = 1.0f + e;
+        const float tm1 = t - 1.0f;
+        const float l = tm1 == 0.0f ? e : logf(t) * (e * __frcp_rn(tm1));
+        a = l * inv_beta;
+        sg = e * __frcp_rn(t);
+    }
+}
+
+struct EpiCols {
+    floatx4 bias, colv;
+    int col;     // first of the 4 columns
+    int region;  // 0 main, 1 split, 2 zero-fill, 3 nothing
+};
+
+// One float4 (4 consecutive columns of one row) of the epilogue.
 template <int EPI>
-__device__ __forceinline__ void linear_epilogue(const LinearArgs& p, int row, int col, float v,
-                                                float bcol, float ccol) {
-    const int Nmain = (EPI == CN_EPI_MUL && p.nsplit < p.N) ? p.nsplit : p.N;
-    const int64_t r = row;
-    if (col < Nmain) {
-        if (p.adiv != 1.0f) v = v / p.adiv;
-        if (p.rowv) v = v + p.rowv[row] * ccol;
-        if constexpr (EPI == CN_EPI_STORE) {
-            p.out0[r * p.ld_out0 + col] = v + bcol;
-        } else if constexpr (EPI == CN_EPI_SOFTPLUS) {
-            const float z = v + bcol;
-            float a = softplus_ref(z, p.beta, p.threshold);
-            if (p.odiv != 1.0f) a = a / p.odiv;
-            p.out0[r * p.ld_out0 + col] = a;
-            if (p.out1) p.out1[r * p.ld_out1 + col] = softplus_grad_ref(z, p.beta, p.threshold);
-        } else if constexpr (EPI == CN_EPI_RELU) {
-            const float z = v + bcol;
-            p.out0[r * p.ld_out0 + col] = z > 0.0f ? z : 0.0f;
-        } else if constexpr (EPI == CN_EPI_MUL) {
-            p.out0[r * p.ld_out0 + col] = v * p.aux0[r * p.ld_aux0 + col];
-        } else if constexpr (EPI == CN_EPI_TANGENT) {
-            const float sg = p.aux0[r * p.ld_aux0 + col];
-            float a = v * sg;
-            if (p.odiv != 1.0f) a = a / p.odiv;
-            p.out0[r * p.ld_out0 + col] = a;
-            const float s = p.aux1[r * p.ld_aux1 + col];
-            p.out1[r * p.ld_out1 + col] = p.beta * s * (1.0f - sg) * v;
-        } else if constexpr (EPI == CN_EPI_BWD_SOFTPLUS) {
-            float o = v * p.aux0[r * p.ld_aux0 + col];
-            if (p.aux1) o = o + p.aux1[r * p.ld_aux1 + col];
-            p.out0[r * p.ld_out0 + col] = o;
-        } else if constexpr (EPI == CN_EPI_BWD_RELU) {
-            p.out0[r * p.ld_out0 + col] = p.aux0[r * p.ld_aux0 + col] > 0.0f ? v : 0.0f;
+__device__ __forceinline__ void epi_vec(const LinearArgs& p, const EpiCols& c, int64_t row, floatx4 v, floatx4 x0,
+                                        floatx4 x1, float rv) {
+    floatx4 o0, o1;
+    const int col = c.col;
+    if (c.region == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float u = v[q];
+            if (p.adiv != 1.0f) u = u / p.adiv;
+            if (p.rowv) u = u + rv * c.colv[q];
+            if constexpr (EPI == CN_EPI_STORE) {
+                o0[q] = u + c.bias[q];
+            } else if constexpr (EPI == CN_EPI_SOFTPLUS) {
+                float a, sg;
+                softplus_fast(u + c.bias[q], p.beta, 1.0f / p.beta, p.threshold, a, sg);
+                if (p.odiv != 1.0f) a = a / p.odiv;
+                o0[q] = a;
+                o1[q] = sg;
+            } else if constexpr (EPI == CN_EPI_RELU) {
+                const float z = u + c.bias[q];
+                o0[q] = z > 0.0f ? z : 0.0f;
+            } else if constexpr (EPI == CN_EPI_MUL) {
+                o0[q] = u * x0[q];
+            } else if constexpr (EPI == CN_EPI_TANGENT) {
+                float a = u * x0[q];
+                if (p.odiv != 1.0f) a = a / p.odiv;
+                o0[q] = a;
+                o1[q] = p.beta * x1[q] * (1.0f - x0[q]) * u;
+            } else if constexpr (EPI == CN_EPI_BWD_SOFTPLUS) {
+                float o = u * x0[q];
+                if (p.aux1) o = o + x1[q];
+                o0[q] = o;
+            } else if constexpr (EPI == CN_EPI_BWD_RELU) {
+                o0[q] = x0[q] > 0.0f ? u : 0.0f;
+            }
         }
-    } else if (EPI == CN_EPI_MUL && col < p.N) {
-        if (p.adiv != 1.0f) v = v / p.adiv;
-        p.out_split[r * p.ld_split + (col - p.nsplit)] = v;
-        if (col < p.nzero) p.out0[r * p.ld_out0 + col] = 0.0f;
-    } else if (col < p.nzero) {
-        p.out0[r * p.ld_out0 + col] = 0.0f;
+        *reinterpret_cast<floatx4*>(p.out0 + row * p.ld_out0 + col) = o0;
+        if ((EPI == CN_EPI_SOFTPLUS && p.out1) || EPI == CN_EPI_TANGENT)
+            *reinterpret_cast<floatx4*>(p.out1 + row * p.ld_out1 + col) = o1;
+    } else if (c.region == 1) {  // EPI_MUL split columns: raw (A·Bᵀ)/adiv
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o0[q] = p.adiv != 1.0f ? v[q] / p.adiv : v[q];
+        *reinterpret_cast<floatx4*>(p.out_split + row * p.ld_split + (col - p.nsplit)) = o0;
+        if (col < p.nzero)
+            *reinterpret_cast<floatx4*>(p.out0 + row * p.ld_out0 + col) = floatx4{0.f, 0.f, 0.f, 0.f};
+    } else if (c.region == 2) {
+        *reinterpret_cast<floatx4*>(p.out0 + row * p.ld_out0 + col) = floatx4{0.f, 0.f, 0.f, 0.f};
         if ((EPI == CN_EPI_SOFTPLUS || EPI == CN_EPI_TANGENT) && p.out1)
-            p.out1[r * p.ld_out1 + col] = 0.0f;
+            *reinterpret_cast<floatx4*>(p.out1 + row * p.ld_out1 + col) = floatx4{0.f, 0.f, 0.f, 0.f};
     }
 }
 
@@ -211,25 +245,64 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) linear_kernel(LinearArgs p) {
         __syncthreads();
     }
 
-    // Epilogue.  C/D layout of the 32x32 MFMA: col = lane&31,
-    // row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+    // Epilogue, phase 1: the loop ended on a barrier, so the staging LDS is free;
+    // park the accumulator tile there.  C/D layout of the 32x32 MFMA:
+    // col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+    constexpr int CS = BN + 4;
+    static_assert(BM * CS <= 2 * (BM + BN) * LS, "C tile must fit in the staging LDS");
+    float* sC = smem;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int col = n0 + wn * TN * 32 + j * 32 + (lane & 31);
-            const int rbase = m0 + wm * TM * 32 + i * 32 + 4 * (lane >> 5);
-            float bcol = 0.0f, ccol = 0.0f;
-            if (col < p.N) {
-                if (p.bias) bcol = p.bias[col];
-                if (p.colv) ccol = p.colv[col];
-            }
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int row = rbase + (r & 3) + 8 * (r >> 2);
-                if (row < p.M) linear_epilogue<EPI>(p, row, col, acc[i][j][r], bcol, ccol);
+                const int row = wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                sC[row * CS + wn * TN * 32 + j * 32 + (lane & 31)] = acc[i][j][r];
             }
+    __syncthreads();
+
+    // Phase 2: row-wise, 4 columns per thread, 16-byte coalesced loads / stores;
+    // every aux load of a group of passes is issued before its math.
+    constexpr int C4 = BN / 4;
+    constexpr int RPP = NT / C4;
+    constexpr int PASSES = BM / RPP;
+    constexpr int GROUP = PASSES < 4 ? PASSES : 4;
+    const int c4 = tid % C4;
+    const int rr = tid / C4;
+    EpiCols c;
+    c.col = n0 + 4 * c4;
+    const int Nmain = (EPI == CN_EPI_MUL && p.nsplit < p.N) ? p.nsplit : p.N;
+    c.region = c.col < Nmain ? 0 : (c.col < p.N ? 1 : (c.col < p.nzero ? 2 : 3));
+    if (c.region == 3) return;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        c.bias[q] = (p.bias && c.region == 0) ? p.bias[c.col + q] : 0.0f;
+        c.colv[q] = (p.colv && c.region == 0) ? p.colv[c.col + q] : 0.0f;
+    }
+    constexpr bool kAux0 = EPI == CN_EPI_MUL || EPI == CN_EPI_TANGENT || EPI == CN_EPI_BWD_SOFTPLUS ||
+                           EPI == CN_EPI_BWD_RELU;
+    constexpr bool kAux1 = EPI == CN_EPI_TANGENT || EPI == CN_EPI_BWD_SOFTPLUS;
+#pragma unroll
+    for (int pb = 0; pb < PASSES; pb += GROUP) {
+        floatx4 v[GROUP], x0[GROUP], x1[GROUP];
+        float rv[GROUP];
+        int64_t grow[GROUP];
+#pragma unroll
+        for (int q = 0; q < GROUP; ++q) {
+            const int row = rr + (pb + q) * RPP;
+            grow[q] = m0 + row;
+            v[q] = *reinterpret_cast<const floatx4*>(sC + row * CS + 4 * c4);
+            const bool ok = grow[q] < p.M && c.region == 0;
+            x0[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+            x1[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+            if (kAux0 && ok) x0[q] = *reinterpret_cast<const floatx4*>(p.aux0 + grow[q] * p.ld_aux0 + c.col);
+            if (kAux1 && ok && p.aux1) x1[q] = *reinterpret_cast<const floatx4*>(p.aux1 + grow[q] * p.ld_aux1 + c.col);
+            rv[q] = (p.rowv && ok) ? p.rowv[grow[q]] : 0.0f;
         }
+#pragma unroll
+        for (int q = 0; q < GROUP; ++q)
+            if (grow[q] < p.M) epi_vec<EPI>(p, c, grow[q], v[q], x0[q], x1[q], rv[q]);
     }
 }
 
@@ -608,6 +681,14 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
         CN_REQUIRE(d->out_split && d->nsplit >= 0 && d->ld_split >= d->N - d->nsplit, CN_ERR_ARG,
                    "cn_linear: split output required");
     CN_REQUIRE((d->rowv == nullptr) == (d->colv == nullptr), CN_ERR_ARG, "cn_linear: rowv/colv go together");
+    // the epilogue moves 4 columns per 16-byte access
+    CN_REQUIRE(d->N % 4 == 0 && nzero % 4 == 0 && (e != CN_EPI_MUL || d->nsplit % 4 == 0), CN_ERR_SHAPE,
+               "cn_linear: N, nzero and nsplit must be multiples of 4");
+    CN_REQUIRE(al16(d->out0) && d->ld_out0 % 4 == 0 && (!d->out1 || (al16(d->out1) && d->ld_out1 % 4 == 0)) &&
+                   (!d->aux0 || (al16(d->aux0) && d->ld_aux0 % 4 == 0)) &&
+                   (!d->aux1 || (al16(d->aux1) && d->ld_aux1 % 4 == 0)) &&
+                   (!d->out_split || (al16(d->out_split) && d->ld_split % 4 == 0)),
+               CN_ERR_ALIGN, "cn_linear: outputs / aux must be 16-byte aligned with leading dims % 4 == 0");
     if (d->M == 0) return CN_OK;
 
     LinearArgs a;

@@ -1,0 +1,59 @@
+"""Microbenchmark of cn_linear / cn_wgrad at the C2 layer shape against
+torch.matmul (hipBLASLt fp32) on the same device: TFLOP/s per variant."""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "cope-nerf_amd"), ROOT]
+from copenerf import ops  # noqa: E402
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def main():
+    M = int(os.environ.get("M", 524288))
+    N = K = 256
+    dev = "cuda"
+    A = torch.randn(M, K, device=dev) * 0.1
+    B = torch.randn(N, K, device=dev) * 0.05
+    bias = torch.randn(N, device=dev) * 0.1
+    aux0 = torch.rand(M, N, device=dev)
+    aux1 = torch.randn(M, N, device=dev)
+    o0 = torch.empty(M, N, device=dev)
+    o1 = torch.empty(M, N, device=dev)
+    fl = 2.0 * M * N * K
+    res = {}
+    res["torch.matmul (hipBLASLt)"] = timeit(lambda: torch.matmul(A, B.t(), out=o0))
+    res["torch addmm+softplus"] = timeit(lambda: torch.nn.functional.softplus(torch.addmm(bias, A, B.t()), beta=100))
+    for name, epi, kw in (("store", ops.EPI_STORE, dict(bias=bias)),
+                          ("softplus", ops.EPI_SOFTPLUS, dict(bias=bias, out1=o1)),
+                          ("softplus(no sig)", ops.EPI_SOFTPLUS, dict(bias=bias)),
+                          ("mul", ops.EPI_MUL, dict(aux0=aux0)),
+                          ("tangent", ops.EPI_TANGENT, dict(aux0=aux0, aux1=aux1, out1=o1)),
+                          ("bwd_softplus", ops.EPI_BWD_SOFTPLUS, dict(aux0=aux0, aux1=aux1)),
+                          ("relu", ops.EPI_RELU, dict(bias=bias))):
+        res["cn_linear " + name] = timeit(lambda: ops.linear(A, B, N, K, o0, epi, **kw))
+    dW = torch.empty(N, K, device=dev)
+    db = torch.empty(N, device=dev)
+    res["cn_wgrad 1 pair"] = timeit(lambda: ops.wgrad(A, A, N, K, dW, db=db))
+    res["cn_wgrad 2 pairs"] = timeit(lambda: ops.wgrad(A, A, N, K, dW, db=db, Y1=aux1, X1=aux0)) / 2
+    res["torch A^T A"] = timeit(lambda: torch.matmul(A.t(), A, out=dW))
+    for k, ms in res.items():
+        print(f"{k:32s} {ms*1e3:9.1f} us  {fl / ms / 1e9:8.1f} TFLOP/s")
+
+
+if __name__ == "__main__":
+    main()
