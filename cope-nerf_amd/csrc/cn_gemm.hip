@@ -21,6 +21,7 @@
 #include "cn_common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace cn {
 
@@ -121,20 +122,40 @@ __device__ __forceinline__ void epi_vec(const LinearArgs& p, const EpiCols& c, i
     }
 }
 
-template <int WM, int WN, int TM, int TN, int EPI>
-__global__ void __launch_bounds__(64 * WM * WN, 2) linear_kernel(LinearArgs p) {
+// Virtual tile vt -> (tm, tn).  XCD-aware: blocks b and b+8 are dispatched to
+// the same XCD, so the T N-tiles of one M-tile are placed 8 apart and share that
+// XCD's L2 copy of the A rows.  Tiles are padded to a multiple of 8 M-tiles.
+__device__ __forceinline__ void tile_coords(int vt, int T, int& tm, int& tn) {
+    const int grp = vt / (8 * T);
+    const int w = vt % (8 * T);
+    tm = grp * 8 + (w & 7);
+    tn = w >> 3;
+}
+
+// Persistent over output tiles: gridDim.x workgroups (2 per CU) walk the
+// virtual tiles; the first K-chunk of the next tile is fetched into registers
+// while the current tile's epilogue runs, so only the first tile of a
+// workgroup pays the cold-start latency.
+template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int EPI>
+__global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel(LinearArgs p) {
     constexpr int NT = 64 * WM * WN;
     constexpr int BM = 32 * TM * WM;
     constexpr int BN = 32 * TN * WN;
-    constexpr int BK = 32;
-    constexpr int LS = BK + 4;  // padded LDS row (floats)
+    constexpr int LS = BK + 4;  // padded LDS row (floats): conflict-free ds_read_b128 for BK = 16, 32
+    constexpr int KC4 = BK / 4; // float4 per staged row
     constexpr int AF4 = BM * BK / 4;
     constexpr int BF4 = BN * BK / 4;
     static_assert(AF4 % NT == 0 && BF4 % NT == 0, "tile/thread mismatch");
     constexpr int ALD = AF4 / NT;
     constexpr int BLD = BF4 / NT;
+    constexpr int CS = BN + 4;
+    constexpr int LDS_FLOATS = 2 * (BM + BN) * LS;
+    // the epilogue parks the C tile in the staging LDS, in NPART row slabs if it does not fit
+    constexpr int NPART = (BM * CS <= LDS_FLOATS) ? 1 : ((BM / 2) * CS <= LDS_FLOATS ? 2 : 4);
+    static_assert((BM / NPART) * CS <= LDS_FLOATS, "C tile slab must fit in the staging LDS");
+    constexpr int PROWS = BM / NPART;
 
-    __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LS];
+    __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
     float* sA = smem;
     float* sB = smem + 2 * BM * LS;
 
@@ -143,24 +164,13 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) linear_kernel(LinearArgs p) {
     const int wave = tid >> 6;
     const int wm = wave / WN;
     const int wn = wave % WN;
-
-    // XCD-aware tile order: blocks b and b+8 are dispatched to the same XCD,
-    // so the N-tiles of one M-tile are placed 8 apart and share that XCD's L2
-    // copy of the A rows.  Grid is padded to a multiple of 8 M-tiles.
     const int T = p.n_tiles_n;
-    const int bid = blockIdx.x;
-    const int grp = bid / (8 * T);
-    const int w = bid % (8 * T);
-    const int tm_idx = grp * 8 + (w & 7);
-    const int tn_idx = w >> 3;
-    const int m0 = tm_idx * BM;
-    if (m0 >= p.M) return;
-    const int n0 = tn_idx * BN;
-
-    floatx4 ra[ALD], rb[BLD];
+    const int ntiles = ((p.n_tiles_m + 7) / 8) * 8 * T;
     const int nk = p.K / BK;
 
-    auto gload = [&](int kc) {
+    // DEPTH register sets stage the next DEPTH K-chunks (global -> registers -> LDS).
+    floatx4 ra[DEPTH][ALD], rb[DEPTH][BLD];
+    auto gload = [&](int set, int kc, int m0, int n0) {
         const int k0 = kc * BK;
         const float* Ab;
         int64_t la;
@@ -174,135 +184,189 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) linear_kernel(LinearArgs p) {
 #pragma unroll
         for (int q = 0; q < ALD; ++q) {
             const int f = tid + q * NT;
-            const int row = f >> 3, c4 = f & 7;
+            const int row = f / KC4, c4 = f % KC4;
             const int gm = m0 + row;
             if (gm < p.M)
-                ra[q] = *reinterpret_cast<const floatx4*>(Ab + (int64_t)gm * la + c4 * 4);
+                ra[set][q] = *reinterpret_cast<const floatx4*>(Ab + (int64_t)gm * la + c4 * 4);
             else
-                ra[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+                ra[set][q] = floatx4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
         for (int q = 0; q < BLD; ++q) {
             const int f = tid + q * NT;
-            const int row = f >> 3, c4 = f & 7;
-            rb[q] = *reinterpret_cast<const floatx4*>(p.B + (int64_t)(n0 + row) * p.ldb + k0 + c4 * 4);
+            const int row = f / KC4, c4 = f % KC4;
+            rb[set][q] = *reinterpret_cast<const floatx4*>(p.B + (int64_t)(n0 + row) * p.ldb + k0 + c4 * 4);
         }
     };
-    auto lstore = [&](int buf) {
+    auto lstore = [&](int set, int buf) {
         float* a = sA + buf * BM * LS;
         float* b = sB + buf * BN * LS;
 #pragma unroll
         for (int q = 0; q < ALD; ++q) {
             const int f = tid + q * NT;
-            *reinterpret_cast<floatx4*>(a + (f >> 3) * LS + (f & 7) * 4) = ra[q];
+            *reinterpret_cast<floatx4*>(a + (f / KC4) * LS + (f % KC4) * 4) = ra[set][q];
         }
 #pragma unroll
         for (int q = 0; q < BLD; ++q) {
             const int f = tid + q * NT;
-            *reinterpret_cast<floatx4*>(b + (f >> 3) * LS + (f & 7) * 4) = rb[q];
+            *reinterpret_cast<floatx4*>(b + (f / KC4) * LS + (f % KC4) * 4) = rb[set][q];
         }
     };
-
-    floatx16 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-
-    gload(0);
-    lstore(0);
-    __syncthreads();
+    auto next_valid = [&](int vt) {
+        for (; vt < ntiles; vt += gridDim.x) {
+            int tm, tn;
+            tile_coords(vt, T, tm, tn);
+            if (tm * BM < p.M) return vt;
+        }
+        return ntiles;
+    };
 
     const int arow = wm * TM * 32 + (lane & 31);
     const int brow = wn * TN * 32 + (lane & 31);
-    const int kofs = 16 * (lane >> 5);
-
-    for (int kc = 0; kc < nk; ++kc) {
-        const int cur = kc & 1;
-        if (kc + 1 < nk) gload(kc + 1);
-        const float* a_base = sA + cur * BM * LS + arow * LS + kofs;
-        const float* b_base = sB + cur * BN * LS + brow * LS + kofs;
-#pragma unroll
-        for (int q4 = 0; q4 < 4; ++q4) {
-            floatx4 af[TM], bf[TN];
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-                af[i] = *reinterpret_cast<const floatx4*>(a_base + i * 32 * LS + q4 * 4);
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-                bf[j] = *reinterpret_cast<const floatx4*>(b_base + j * 32 * LS + q4 * 4);
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][e], bf[j][e], acc[i][j], 0, 0, 0);
-        }
-        if (kc + 1 < nk) lstore(cur ^ 1);
-        __syncthreads();
-    }
-
-    // Epilogue, phase 1: the loop ended on a barrier, so the staging LDS is free;
-    // park the accumulator tile there.  C/D layout of the 32x32 MFMA:
-    // col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
-    constexpr int CS = BN + 4;
-    static_assert(BM * CS <= 2 * (BM + BN) * LS, "C tile must fit in the staging LDS");
-    float* sC = smem;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                sC[row * CS + wn * TN * 32 + j * 32 + (lane & 31)] = acc[i][j][r];
-            }
-    __syncthreads();
-
-    // Phase 2: row-wise, 4 columns per thread, 16-byte coalesced loads / stores;
-    // every aux load of a group of passes is issued before its math.
+    const int kofs = (BK / 2) * (lane >> 5);
+    const int Nmain = (EPI == CN_EPI_MUL && p.nsplit < p.N) ? p.nsplit : p.N;
     constexpr int C4 = BN / 4;
     constexpr int RPP = NT / C4;
-    constexpr int PASSES = BM / RPP;
-    constexpr int GROUP = PASSES < 4 ? PASSES : 4;
-    const int c4 = tid % C4;
-    const int rr = tid / C4;
-    EpiCols c;
-    c.col = n0 + 4 * c4;
-    const int Nmain = (EPI == CN_EPI_MUL && p.nsplit < p.N) ? p.nsplit : p.N;
-    c.region = c.col < Nmain ? 0 : (c.col < p.N ? 1 : (c.col < p.nzero ? 2 : 3));
-    if (c.region == 3) return;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        c.bias[q] = (p.bias && c.region == 0) ? p.bias[c.col + q] : 0.0f;
-        c.colv[q] = (p.colv && c.region == 0) ? p.colv[c.col + q] : 0.0f;
-    }
+    constexpr int GMAX = OCC >= 4 ? 2 : 4;  // rows of aux loads in flight per thread (VGPR budget)
+    constexpr int GROUP = (PROWS / RPP) < GMAX ? (PROWS / RPP) : GMAX;
+    static_assert((PROWS / RPP) % GROUP == 0, "epilogue passes");
     constexpr bool kAux0 = EPI == CN_EPI_MUL || EPI == CN_EPI_TANGENT || EPI == CN_EPI_BWD_SOFTPLUS ||
                            EPI == CN_EPI_BWD_RELU;
     constexpr bool kAux1 = EPI == CN_EPI_TANGENT || EPI == CN_EPI_BWD_SOFTPLUS;
+
+    int vt = next_valid(blockIdx.x);
+    if (vt >= ntiles) return;
+    int tm, tn;
+    tile_coords(vt, T, tm, tn);
+    gload(0, 0, tm * BM, tn * BN);
+
+    while (vt < ntiles) {
+        const int m0 = tm * BM, n0 = tn * BN;
+        const int vt_next = next_valid(vt + gridDim.x);
+        int tm_next = 0, tn_next = 0;
+        if (vt_next < ntiles) tile_coords(vt_next, T, tm_next, tn_next);
+
+        lstore(0, 0);
+        __syncthreads();
+        if (DEPTH == 2) gload(1, 1, m0, n0);  // nk is even for DEPTH 2
+
+        floatx16 acc[TM][TN];
 #pragma unroll
-    for (int pb = 0; pb < PASSES; pb += GROUP) {
-        floatx4 v[GROUP], x0[GROUP], x1[GROUP];
-        float rv[GROUP];
-        int64_t grow[GROUP];
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int q = 0; q < GROUP; ++q) {
-            const int row = rr + (pb + q) * RPP;
-            grow[q] = m0 + row;
-            v[q] = *reinterpret_cast<const floatx4*>(sC + row * CS + 4 * c4);
-            const bool ok = grow[q] < p.M && c.region == 0;
-            x0[q] = floatx4{0.f, 0.f, 0.f, 0.f};
-            x1[q] = floatx4{0.f, 0.f, 0.f, 0.f};
-            if (kAux0 && ok) x0[q] = *reinterpret_cast<const floatx4*>(p.aux0 + grow[q] * p.ld_aux0 + c.col);
-            if (kAux1 && ok && p.aux1) x1[q] = *reinterpret_cast<const floatx4*>(p.aux1 + grow[q] * p.ld_aux1 + c.col);
-            rv[q] = (p.rowv && ok) ? p.rowv[grow[q]] : 0.0f;
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+        auto compute = [&](int cur) {
+            const float* a_base = sA + cur * BM * LS + arow * LS + kofs;
+            const float* b_base = sB + cur * BN * LS + brow * LS + kofs;
+#pragma unroll
+            for (int q4 = 0; q4 < BK / 8; ++q4) {
+                floatx4 af[TM], bf[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+                    af[i] = *reinterpret_cast<const floatx4*>(a_base + i * 32 * LS + q4 * 4);
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    bf[j] = *reinterpret_cast<const floatx4*>(b_base + j * 32 * LS + q4 * 4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][e], bf[j][e], acc[i][j], 0, 0, 0);
+            }
+        };
+
+        if constexpr (DEPTH == 1) {
+            for (int kc = 0; kc < nk; ++kc) {
+                const int cur = kc & 1;
+                if (kc + 1 < nk)
+                    gload(0, kc + 1, m0, n0);
+                else if (vt_next < ntiles)
+                    gload(0, 0, tm_next * BM, tn_next * BN);  // next tile's first chunk, consumed after the epilogue
+                compute(cur);
+                if (kc + 1 < nk) lstore(0, cur ^ 1);
+                __syncthreads();
+            }
+        } else {
+            // chunk k+1 is in flight in set (k+1)&1 while chunk k is computed from LDS buffer k&1
+            for (int kc = 0; kc < nk; kc += 2) {
+                if (kc + 2 < nk)
+                    gload(0, kc + 2, m0, n0);
+                else if (vt_next < ntiles)
+                    gload(0, 0, tm_next * BM, tn_next * BN);
+                compute(0);
+                lstore(1, 1);
+                __syncthreads();
+                if (kc + 3 < nk) gload(1, kc + 3, m0, n0);
+                compute(1);
+                if (kc + 2 < nk) lstore(0, 0);
+                __syncthreads();
+            }
+        }
+
+        // Epilogue: park the accumulator tile (or a slab of PROWS rows of it) in the
+        // now free staging LDS, then process it row-wise with 16-byte coalesced
+        // loads / stores; every aux load of a group of passes is issued before its math.
+        // C/D layout of the 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+        float* sC = smem;
+        const int c4 = tid % C4;
+        const int rr = tid / C4;
+        EpiCols c;
+        c.col = n0 + 4 * c4;
+        c.region = c.col < Nmain ? 0 : (c.col < p.N ? 1 : (c.col < p.nzero ? 2 : 3));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            c.bias[q] = (p.bias && c.region == 0) ? p.bias[c.col + q] : 0.0f;
+            c.colv[q] = (p.colv && c.region == 0) ? p.colv[c.col + q] : 0.0f;
         }
 #pragma unroll
-        for (int q = 0; q < GROUP; ++q)
-            if (grow[q] < p.M) epi_vec<EPI>(p, c, grow[q], v[q], x0[q], x1[q], rv[q]);
+        for (int part = 0; part < NPART; ++part) {
+            if (part > 0) __syncthreads();  // previous slab consumed
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int row = wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                        if (NPART == 1 || row / PROWS == part)
+                            sC[(row - part * PROWS) * CS + wn * TN * 32 + j * 32 + (lane & 31)] = acc[i][j][r];
+                    }
+            __syncthreads();
+            if (c.region != 3) {
+#pragma unroll
+                for (int pb = 0; pb < PROWS / RPP; pb += GROUP) {
+                    floatx4 v[GROUP], x0[GROUP], x1[GROUP];
+                    float rv[GROUP];
+                    int64_t grow[GROUP];
+#pragma unroll
+                    for (int q = 0; q < GROUP; ++q) {
+                        const int row = rr + (pb + q) * RPP;
+                        grow[q] = m0 + part * PROWS + row;
+                        v[q] = *reinterpret_cast<const floatx4*>(sC + row * CS + 4 * c4);
+                        const bool ok = grow[q] < p.M && c.region == 0;
+                        x0[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+                        x1[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+                        if (kAux0 && ok)
+                            x0[q] = *reinterpret_cast<const floatx4*>(p.aux0 + grow[q] * p.ld_aux0 + c.col);
+                        if (kAux1 && ok && p.aux1)
+                            x1[q] = *reinterpret_cast<const floatx4*>(p.aux1 + grow[q] * p.ld_aux1 + c.col);
+                        rv[q] = (p.rowv && ok) ? p.rowv[grow[q]] : 0.0f;
+                    }
+#pragma unroll
+                    for (int q = 0; q < GROUP; ++q)
+                        if (grow[q] < p.M) epi_vec<EPI>(p, c, grow[q], v[q], x0[q], x1[q], rv[q]);
+                }
+            }
+        }
+        __syncthreads();  // sC is the next tile's staging buffer
+        vt = vt_next;
+        tm = tm_next;
+        tn = tn_next;
     }
 }
 
@@ -632,27 +696,43 @@ static void wgrad_geometry(int M, int N, int K, int* tile, int* Npad, int* Kpad,
 
 using namespace cn;
 
-template <int WM, int WN, int TM, int TN>
+template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH>
 static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_t s) {
     constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
     a.n_tiles_m = cdiv(d->M, BM);
     a.n_tiles_n = cdiv(d->N, BN);
-    const int grid = cdiv(a.n_tiles_m, 8) * 8 * a.n_tiles_n;
+    const int ntiles = cdiv(a.n_tiles_m, 8) * 8 * a.n_tiles_n;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) cus = v;
+    }
+    const int grid = std::min(ntiles, OCC * cus);  // OCC resident workgroups per CU
     dim3 block(64 * WM * WN);
     switch (d->epilogue) {
-        case CN_EPI_STORE: linear_kernel<WM, WN, TM, TN, CN_EPI_STORE><<<grid, block, 0, s>>>(a); break;
-        case CN_EPI_SOFTPLUS: linear_kernel<WM, WN, TM, TN, CN_EPI_SOFTPLUS><<<grid, block, 0, s>>>(a); break;
-        case CN_EPI_RELU: linear_kernel<WM, WN, TM, TN, CN_EPI_RELU><<<grid, block, 0, s>>>(a); break;
-        case CN_EPI_MUL: linear_kernel<WM, WN, TM, TN, CN_EPI_MUL><<<grid, block, 0, s>>>(a); break;
-        case CN_EPI_TANGENT: linear_kernel<WM, WN, TM, TN, CN_EPI_TANGENT><<<grid, block, 0, s>>>(a); break;
-        case CN_EPI_BWD_SOFTPLUS: linear_kernel<WM, WN, TM, TN, CN_EPI_BWD_SOFTPLUS><<<grid, block, 0, s>>>(a); break;
-        case CN_EPI_BWD_RELU: linear_kernel<WM, WN, TM, TN, CN_EPI_BWD_RELU><<<grid, block, 0, s>>>(a); break;
+#define CN_EPI_CASE(E) \
+        case E: linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, E><<<grid, block, 0, s>>>(a); break;
+        CN_EPI_CASE(CN_EPI_STORE)
+        CN_EPI_CASE(CN_EPI_SOFTPLUS)
+        CN_EPI_CASE(CN_EPI_RELU)
+        CN_EPI_CASE(CN_EPI_MUL)
+        CN_EPI_CASE(CN_EPI_TANGENT)
+        CN_EPI_CASE(CN_EPI_BWD_SOFTPLUS)
+        CN_EPI_CASE(CN_EPI_BWD_RELU)
+#undef CN_EPI_CASE
         default: set_error("cn_linear: bad epilogue %d", d->epilogue); return CN_ERR_ARG;
     }
     return check_launch("cn_linear");
 }
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// Main-loop variant of the 128x128 tile (benchmarking aid, process-wide):
+// 0 = 2-deep register prefetch (default when K % 64 == 0), 1 = 1-deep.
+static int g_linear_variant = [] {
+    const char* e = getenv("COPENERF_LINEAR_VARIANT");
+    return e ? atoi(e) : 0;
+}();
 
 extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     CN_REQUIRE(d, CN_ERR_ARG, "cn_linear: null desc");
@@ -703,8 +783,13 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     a.beta = d->beta;
     a.threshold = d->threshold;
     hipStream_t s = (hipStream_t)stream;
-    if (d->tile == 0) return launch_linear_tile<2, 2, 2, 2>(d, a, s);
-    return launch_linear_tile<4, 1, 1, 2>(d, a, s);
+    const bool even = (d->K % 64) == 0;  // DEPTH-2 prefetch consumes K in pairs of 32-chunks
+    if (d->tile == 0) {
+        if (g_linear_variant == 1 || !even) return launch_linear_tile<2, 2, 2, 2, 32, 2, 1>(d, a, s);
+        return launch_linear_tile<2, 2, 2, 2, 32, 2, 2>(d, a, s);
+    }
+    if (even) return launch_linear_tile<4, 1, 1, 2, 32, 2, 2>(d, a, s);
+    return launch_linear_tile<4, 1, 1, 2, 32, 2, 1>(d, a, s);
 }
 
 extern "C" size_t cn_wgrad_workspace_bytes(int32_t M, int32_t N, int32_t K) {
