@@ -515,29 +515,70 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) wgrad_kernel(WgradArgs p) {
     if (do_bias && tid < BNo) p.bpart[(int64_t)slice * p.Npad + n0 + tid] = bacc;
 }
 
-__global__ void wgrad_reduce(const float* __restrict__ part, const float* __restrict__ bpart,
-                             int nslices, int Npad, int Kpad, float* dW, int64_t ld_dw, int n_out,
-                             int k_out, float* db, int accumulate) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t tot = (int64_t)n_out * k_out;
-    if (idx < tot) {
-        const int n = idx / k_out, k = idx % k_out;
-        double s = 0.0;  // fixed order over slices
-        const int64_t stride = (int64_t)Npad * Kpad;
-        const float* pp = part + (int64_t)n * Kpad + k;
-        for (int i = 0; i < nslices; ++i) s += pp[i * stride];
-        float v = (float)s;
-        if (accumulate) v += dW[(int64_t)n * ld_dw + k];
-        dW[(int64_t)n * ld_dw + k] = v;
+// Sum of nslab fp32 slabs: out[r*ldo + c] (+)= (sum_s part[s*stride + r*ldp + c]) / div
+// for r < rows, c < cols.  A workgroup owns 64 float4 column groups x 4 slab
+// groups; each thread sums its slab group in double with 4 loads in flight, the 4
+// groups combine through LDS in a fixed order (bitwise reproducible).
+__global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ part, int nslab, int64_t stride,
+                                                          int rows, int cols, int64_t ldp, float* out, int64_t ldo,
+                                                          float div, int accumulate) {
+    __shared__ double red[4][64][4];
+    const int c4n = cdiv(cols, 4);
+    const int64_t g = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);  // float4 group over rows x c4n
+    const int sg = threadIdx.x >> 6;
+    const bool valid = g < (int64_t)rows * c4n;
+    const int r = valid ? (int)(g / c4n) : 0;
+    const int c = valid ? (int)(g % c4n) * 4 : 0;
+    const bool vec = valid && (c + 3 < cols) && (ldp % 4 == 0) && (stride % 4 == 0);
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    if (valid) {
+        const float* base = part + (int64_t)r * ldp + c;
+        int sl = sg;
+        for (; sl + 12 < nslab; sl += 16) {
+            floatx4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const float* q = base + (int64_t)(sl + 4 * u) * stride;
+                if (vec) {
+                    v[u] = *reinterpret_cast<const floatx4*>(q);
+                } else {
+                    for (int e = 0; e < 4; ++e) v[u][e] = (c + e < cols) ? q[e] : 0.0f;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) a[e] += (double)v[u][e];
+        }
+        for (; sl < nslab; sl += 4) {
+            const float* q = base + (int64_t)sl * stride;
+            for (int e = 0; e < 4; ++e) a[e] += (c + e < cols) ? (double)q[e] : 0.0;
+        }
     }
-    if (db && idx < n_out) {
-        double s = 0.0;
-        for (int i = 0; i < nslices; ++i) s += bpart[(int64_t)i * Npad + idx];
-        float v = (float)s;
-        if (accumulate) v += db[idx];
-        db[idx] = v;
+    for (int e = 0; e < 4; ++e) red[sg][threadIdx.x & 63][e] = a[e];
+    __syncthreads();
+    if (sg == 0 && valid) {
+        const int t = threadIdx.x & 63;
+        for (int e = 0; e < 4 && c + e < cols; ++e) {
+            const double tot = ((red[0][t][e] + red[1][t][e]) + red[2][t][e]) + red[3][t][e];
+            float v = (float)tot;
+            if (div != 1.0f) v = v / div;
+            float* o = out + (int64_t)r * ldo + c + e;
+            if (accumulate) v += *o;
+            *o = v;
+        }
     }
 }
+
+static int launch_slab_reduce(const float* part, int nslab, int64_t stride, int rows, int cols, int64_t ldp, float* out,
+                              int64_t ldo, float div, int accumulate, hipStream_t s) {
+    const int64_t groups = (int64_t)rows * cdiv(cols, 4);
+    if (groups == 0) return CN_OK;
+    slab_reduce_kernel<<<(int)((groups + 63) / 64), 256, 0, s>>>(part, nslab, stride, rows, cols, ldp, out, ldo, div,
+                                                                 accumulate);
+    return check_launch("slab_reduce");
+}
+
 
 // ---------------------------------------------------------------------------
 // Per-row heads: out[dst(m)][c] = act(sum_k A[m][k] W[c][k] + b[c]).  One
@@ -632,47 +673,40 @@ __global__ void rgb_head_bwd_kernel(int M, int K, const float* __restrict__ drgb
     if (k < 3) pb[3 * K + k] = ab;
 }
 
-__global__ void rgb_head_reduce(const float* __restrict__ part, int nblk, int K, float* dW3, float* db3) {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx < 3 * K) {
-        double s = 0.0;
-        for (int i = 0; i < nblk; ++i) s += part[(int64_t)i * 4 * K + idx];
-        dW3[idx] = (float)s;
-    } else if (idx < 3 * K + 3) {
-        const int c = idx - 3 * K;
-        double s = 0.0;
-        for (int i = 0; i < nblk; ++i) s += part[(int64_t)i * 4 * K + 3 * K + c];
-        db3[c] = (float)s;
-    }
-}
 
-// Column sums over row slices (thread = column), then a fixed-order reduce.
+// Column sums over row slices: a workgroup = 64 float4 column groups x 4 row
+// groups, LDS combine; slabs then summed by slab_reduce in a fixed order.
 constexpr int kColsumRows = 1024;
 
-__global__ void colsum_kernel(int M, int K, const float* __restrict__ w, const float* __restrict__ X, int64_t ldx,
-                              float* part) {
-    const int k = blockIdx.y * blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(256) colsum_kernel(int M, int K, const float* __restrict__ w,
+                                                     const float* __restrict__ X, int64_t ldx, float* part) {
+    __shared__ float red[4][256];
+    const int c = (blockIdx.y * 64 + (threadIdx.x & 63)) * 4;
+    const int rg = threadIdx.x >> 6;
     const int m0 = blockIdx.x * kColsumRows;
     const int m1 = min(M, m0 + kColsumRows);
-    if (k >= K) return;
-    float a = 0.0f;
-    for (int m = m0; m < m1; ++m) {
-        const float x = X[(int64_t)m * ldx + k];
-        a += w ? w[m] * x : x;
+    floatx4 a = {0.f, 0.f, 0.f, 0.f};
+    const bool vec = (c + 3 < K) && (ldx % 4 == 0);
+    if (c < K) {
+        for (int m = m0 + rg; m < m1; m += 4) {
+            floatx4 x;
+            if (vec) {
+                x = *reinterpret_cast<const floatx4*>(X + (int64_t)m * ldx + c);
+            } else {
+                for (int e = 0; e < 4; ++e) x[e] = (c + e < K) ? X[(int64_t)m * ldx + c + e] : 0.0f;
+            }
+            const float wm = w ? w[m] : 1.0f;
+            for (int e = 0; e < 4; ++e) a[e] += w ? wm * x[e] : x[e];
+        }
     }
-    part[(int64_t)blockIdx.x * K + k] = a;
-}
-
-__global__ void colsum_reduce(const float* __restrict__ part, int nblk, int K, float wdiv, float* out,
-                              int accumulate) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= K) return;
-    double s = 0.0;
-    for (int i = 0; i < nblk; ++i) s += part[(int64_t)i * K + k];
-    float v = (float)s;
-    if (wdiv != 1.0f) v = v / wdiv;
-    if (accumulate) v += out[k];
-    out[k] = v;
+    for (int e = 0; e < 4; ++e) red[rg][(threadIdx.x & 63) * 4 + e] = a[e];
+    __syncthreads();
+    if (rg == 0 && c < K) {
+        for (int e = 0; e < 4 && c + e < K; ++e) {
+            const int t = (threadIdx.x & 63) * 4 + e;
+            part[(int64_t)blockIdx.x * K + c + e] = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -830,10 +864,14 @@ extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
         wgrad_kernel<2, 2, 2, 1><<<grid, 256, 0, s>>>(a);
     int rc = check_launch("cn_wgrad");
     if (rc) return rc;
-    const int64_t tot = std::max<int64_t>((int64_t)d->n_out * d->k_out, d->n_out);
-    wgrad_reduce<<<cdiv((int)tot, 256), 256, 0, s>>>(a.part, a.bpart, ns, Npad, Kpad, d->dW, d->ld_dw, d->n_out,
-                                                    d->k_out, d->db, d->accumulate);
-    return check_launch("cn_wgrad(reduce)");
+    rc = launch_slab_reduce(a.part, ns, (int64_t)Npad * Kpad, d->n_out, d->k_out, Kpad, d->dW, d->ld_dw, 1.0f,
+                            d->accumulate, s);
+    if (rc) return rc;
+    if (d->db) {
+        rc = launch_slab_reduce(a.bpart, ns, Npad, 1, d->n_out, Npad, d->db, d->n_out, 1.0f, d->accumulate, s);
+        if (rc) return rc;
+    }
+    return CN_OK;
 }
 
 extern "C" int cn_row_head(int32_t M, int32_t K, const float* A, int64_t lda, const float* W, int64_t ldw,
@@ -873,8 +911,9 @@ extern "C" int cn_rgb_head_bwd(int32_t M, int32_t K, const float* drgb, const fl
     rgb_head_bwd_kernel<<<nblk, 256, 0, s>>>(M, K, drgb, rgb, H3, ld_h, W3, dZ2, ld_dz, workspace);
     int rc = check_launch("cn_rgb_head_bwd");
     if (rc) return rc;
-    rgb_head_reduce<<<cdiv(3 * K + 3, 256), 256, 0, s>>>(workspace, nblk, K, dW3, db3);
-    return check_launch("cn_rgb_head_bwd(reduce)");
+    rc = launch_slab_reduce(workspace, nblk, 4 * K, 3, K, K, dW3, K, 1.0f, 0, s);
+    if (rc) return rc;
+    return launch_slab_reduce(workspace + 3 * K, nblk, 4 * K, 1, 3, 3, db3, 3, 1.0f, 0, s);
 }
 
 extern "C" size_t cn_colsum_workspace_bytes(int32_t M, int32_t K) {
@@ -899,6 +938,5 @@ extern "C" int cn_colsum(int32_t M, int32_t K, const float* w, const float* X, i
             return CN_ERR_LAUNCH;
         }
     }
-    colsum_reduce<<<cdiv(K, 256), 256, 0, s>>>(workspace, nblk, K, wdiv == 0.f ? 1.f : wdiv, out, accumulate);
-    return check_launch("cn_colsum(reduce)");
+    return launch_slab_reduce(workspace, nblk, K, 1, K, K, out, K, wdiv == 0.f ? 1.f : wdiv, accumulate, s);
 }
