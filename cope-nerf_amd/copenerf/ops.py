@@ -47,7 +47,8 @@ class KernelTimer:
 
 
 _timer = None
-EPI_NAMES = {0: "store", 1: "softplus", 2: "relu", 3: "mul", 4: "tangent", 5: "bwd_softplus", 6: "bwd_relu"}
+EPI_NAMES = {0: "store", 1: "softplus", 2: "relu", 3: "mul", 4: "tangent", 5: "bwd_softplus", 6: "bwd_relu",
+             7: "bench_mainloop"}
 
 
 def set_kernel_timer(t):
@@ -93,6 +94,9 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
                  (aux1, "aux1"), (out_split, "out_split")):
         _need(t, n)
     M = A.shape[0] if M is None else M
+    # the epilogue reads bias / colv as float4
+    bias = bias if bias is None or bias.data_ptr() % 16 == 0 else bias.clone()
+    colv = colv if colv is None or colv.data_ptr() % 16 == 0 else colv.clone()
     if tile is None:
         tile = 1 if max(N, nzero or 0) <= 64 else 0
     bn = 64 if tile == 1 else 128

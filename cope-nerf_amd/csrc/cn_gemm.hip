@@ -37,89 +37,59 @@ struct LinearArgs {
     float* out0;
     float* out1;
     float* out_split;
-    int64_t lda, lda2, ldb, ld_aux0, ld_aux1, ld_out0, ld_out1, ld_split;
+    int lda, lda2, ldb, ld_aux0, ld_aux1, ld_out0, ld_out1, ld_split;
     int M, N, K, K1, nzero, nsplit, n_tiles_m, n_tiles_n;
-    float adiv, odiv, beta, threshold;
+    float inv_adiv, inv_odiv, beta, threshold;
 };
 
-// Softplus and softplus' sharing one exp: a = log1p(e)/beta, sg = e/(1 + e),
-// e = exp(beta z); linear branch above the threshold exactly as
-// torch.nn.Softplus(beta, threshold).  log1p(e) = log(t) * e / (t - 1) with
-// t = 1 + e rounded (Goldberg) keeps full relative accuracy for small e with one
-// accurate logf instead of log1pf; reciprocals are v_rcp_f32 (1 ulp).
-__device__ __forceinline__ void softplus_fast(float z, float beta, float inv_beta, float thr, float& a, float& sg) {
-    const float bx = z * beta;
-    if (bx > thr) {
-        a = z;
-        sg = 1.0f;
-    } else {
-        const float e = expf(bx);
-        const float t = 1.0f + e;
-        const float tm1 = t - 1.0f;
-        const float l = tm1 == 0.0f ? e : logf(t) * (e * __frcp_rn(tm1));
-        a = l * inv_beta;
-        sg = e * __frcp_rn(t);
-    }
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+// Buffer views: every global access of the GEMM goes through a buffer resource
+// whose base is a tile row and whose record count ends at the last valid row,
+// so (a) per-access addressing is a per-lane 32-bit voffset fixed for the whole
+// kernel plus a wave-uniform soffset (column offset) and SALU-built descriptors,
+// no 64-bit VALU address math, and (b) rows >= M read as zero and their stores
+// are dropped by the range check, with no per-row compare.  The range check
+// covers voffset only (not soffset), so the row part of every offset is either
+// in voffset or in the descriptor base.  On gfx950 the f32 MFMA and VALU instructions of the
+// waves of one SIMD issue strictly one after the other (tools/probes), so every
+// VALU instruction removed here is matrix-pipe time won back.
+// bytes: a tile's extent, < 2^31 by the host's leading-dimension limit; <= 0 = empty view
+__device__ __forceinline__ rsrc_t make_view(const float* base, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, bytes < 0 ? 0 : bytes, 0x00020000);
+}
+// A tile's rows of one tensor: base = its first row, bytes = extent up to the last valid row.
+struct TileView {
+    const float* base;
+    int ld;
+    int bytes;
+};
+__device__ __forceinline__ rsrc_t view_at(const TileView& t, int lrow) {
+    return make_view(t.base + (int64_t)lrow * t.ld, t.bytes - lrow * t.ld * 4);
+}
+__device__ __forceinline__ floatx4 bload4(rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+__device__ __forceinline__ float bload1(rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+__device__ __forceinline__ void bstore4(rsrc_t r, int voff, int soff, floatx4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, soff, 0);
 }
 
-struct EpiCols {
-    floatx4 bias, colv;
-    int col;     // first of the 4 columns
-    int region;  // 0 main, 1 split, 2 zero-fill, 3 nothing
-};
-
-// One float4 (4 consecutive columns of one row) of the epilogue.
-template <int EPI>
-__device__ __forceinline__ void epi_vec(const LinearArgs& p, const EpiCols& c, int64_t row, floatx4 v, floatx4 x0,
-                                        floatx4 x1, float rv) {
-    floatx4 o0, o1;
-    const int col = c.col;
-    if (c.region == 0) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            float u = v[q];
-            if (p.adiv != 1.0f) u = u / p.adiv;
-            if (p.rowv) u = u + rv * c.colv[q];
-            if constexpr (EPI == CN_EPI_STORE) {
-                o0[q] = u + c.bias[q];
-            } else if constexpr (EPI == CN_EPI_SOFTPLUS) {
-                float a, sg;
-                softplus_fast(u + c.bias[q], p.beta, 1.0f / p.beta, p.threshold, a, sg);
-                if (p.odiv != 1.0f) a = a / p.odiv;
-                o0[q] = a;
-                o1[q] = sg;
-            } else if constexpr (EPI == CN_EPI_RELU) {
-                const float z = u + c.bias[q];
-                o0[q] = z > 0.0f ? z : 0.0f;
-            } else if constexpr (EPI == CN_EPI_MUL) {
-                o0[q] = u * x0[q];
-            } else if constexpr (EPI == CN_EPI_TANGENT) {
-                float a = u * x0[q];
-                if (p.odiv != 1.0f) a = a / p.odiv;
-                o0[q] = a;
-                o1[q] = p.beta * x1[q] * (1.0f - x0[q]) * u;
-            } else if constexpr (EPI == CN_EPI_BWD_SOFTPLUS) {
-                float o = u * x0[q];
-                if (p.aux1) o = o + x1[q];
-                o0[q] = o;
-            } else if constexpr (EPI == CN_EPI_BWD_RELU) {
-                o0[q] = x0[q] > 0.0f ? u : 0.0f;
-            }
-        }
-        *reinterpret_cast<floatx4*>(p.out0 + row * p.ld_out0 + col) = o0;
-        if ((EPI == CN_EPI_SOFTPLUS && p.out1) || EPI == CN_EPI_TANGENT)
-            *reinterpret_cast<floatx4*>(p.out1 + row * p.ld_out1 + col) = o1;
-    } else if (c.region == 1) {  // EPI_MUL split columns: raw (A·Bᵀ)/adiv
-#pragma unroll
-        for (int q = 0; q < 4; ++q) o0[q] = p.adiv != 1.0f ? v[q] / p.adiv : v[q];
-        *reinterpret_cast<floatx4*>(p.out_split + row * p.ld_split + (col - p.nsplit)) = o0;
-        if (col < p.nzero)
-            *reinterpret_cast<floatx4*>(p.out0 + row * p.ld_out0 + col) = floatx4{0.f, 0.f, 0.f, 0.f};
-    } else if (c.region == 2) {
-        *reinterpret_cast<floatx4*>(p.out0 + row * p.ld_out0 + col) = floatx4{0.f, 0.f, 0.f, 0.f};
-        if ((EPI == CN_EPI_SOFTPLUS || EPI == CN_EPI_TANGENT) && p.out1)
-            *reinterpret_cast<floatx4*>(p.out1 + row * p.ld_out1 + col) = floatx4{0.f, 0.f, 0.f, 0.f};
-    }
+// torch.nn.Softplus(beta, threshold) and its derivative from one exponential,
+// on the hardware transcendentals: e = 2^(z beta log2 e), a = log2(1 + e) ln2 / beta,
+// sg = e / (1 + e); the linear branch (beta z > threshold) exactly as torch.
+// Absolute error of a is ~1e-9 (log2 of the rounded 1 + e; v_exp/v_log/v_rcp are
+// 1 ulp), far below the fp32 GEMM rounding of the layer that produced z.
+__device__ __forceinline__ void softplus_hw(float z, float c_exp, float c_thr, float c_log, float& a, float& sg) {
+    const float y = z * c_exp;  // beta z log2(e)
+    const float e = __builtin_amdgcn_exp2f(y);
+    const float t = 1.0f + e;
+    const bool lin = y > c_thr;  // beta z > threshold (boundary moved by <= 1 ulp; the branches agree to 1e-10 there)
+    a = lin ? z : __builtin_amdgcn_logf(t) * c_log;
+    sg = lin ? 1.0f : e * __builtin_amdgcn_rcpf(t);
 }
 
 // Virtual tile vt -> (tm, tn).  XCD-aware: blocks b and b+8 are dispatched to
@@ -132,22 +102,22 @@ __device__ __forceinline__ void tile_coords(int vt, int T, int& tm, int& tn) {
     tn = w >> 3;
 }
 
-// Persistent over output tiles: gridDim.x workgroups (2 per CU) walk the
+// Persistent over output tiles: gridDim.x workgroups (OCC per CU) walk the
 // virtual tiles; the first K-chunk of the next tile is fetched into registers
 // while the current tile's epilogue runs, so only the first tile of a
 // workgroup pays the cold-start latency.
-template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int EPI>
+template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int EPI, bool ROWV>
 __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel(LinearArgs p) {
     constexpr int NT = 64 * WM * WN;
     constexpr int BM = 32 * TM * WM;
     constexpr int BN = 32 * TN * WN;
     constexpr int LS = BK + 4;  // padded LDS row (floats): conflict-free ds_read_b128 for BK = 16, 32
     constexpr int KC4 = BK / 4; // float4 per staged row
-    constexpr int AF4 = BM * BK / 4;
-    constexpr int BF4 = BN * BK / 4;
-    static_assert(AF4 % NT == 0 && BF4 % NT == 0, "tile/thread mismatch");
-    constexpr int ALD = AF4 / NT;
-    constexpr int BLD = BF4 / NT;
+    static_assert(NT % KC4 == 0, "staging rows");
+    constexpr int RSTEP = NT / KC4;  // staged rows per load instruction
+    static_assert(BM % RSTEP == 0 && BN % RSTEP == 0, "tile/thread mismatch");
+    constexpr int ALD = BM / RSTEP;
+    constexpr int BLD = BN / RSTEP;
     constexpr int CS = BN + 4;
     constexpr int LDS_FLOATS = 2 * (BM + BN) * LS;
     // the epilogue parks the C tile in the staging LDS, in NPART row slabs if it does not fit
@@ -168,49 +138,42 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     const int ntiles = ((p.n_tiles_m + 7) / 8) * 8 * T;
     const int nk = p.K / BK;
 
-    // DEPTH register sets stage the next DEPTH K-chunks (global -> registers -> LDS).
+    // staging: thread tid loads rows tid/KC4 + q*RSTEP, float4 column tid%KC4
+    const int srow = tid / KC4, sc4 = tid % KC4;
+    int voA[ALD], voA2[ALD], voB[BLD];  // byte offsets of the staged rows (range-checked)
+#pragma unroll
+    for (int q = 0; q < ALD; ++q) {
+        voA[q] = ((srow + q * RSTEP) * p.lda + sc4 * 4) * 4;
+        voA2[q] = ((srow + q * RSTEP) * p.lda2 + sc4 * 4) * 4;
+    }
+#pragma unroll
+    for (int q = 0; q < BLD; ++q) voB[q] = ((srow + q * RSTEP) * p.ldb + sc4 * 4) * 4;
+    const int lds_st = srow * LS + sc4 * 4;
+
     floatx4 ra[DEPTH][ALD], rb[DEPTH][BLD];
     auto gload = [&](int set, int kc, int m0, int n0) {
         const int k0 = kc * BK;
-        const float* Ab;
-        int64_t la;
+        const int rows = min(BM, p.M - m0);
         if (k0 < p.K1) {
-            Ab = p.A + k0;
-            la = p.lda;
+            const rsrc_t rA = make_view(p.A + (int64_t)m0 * p.lda, rows * p.lda * 4);
+#pragma unroll
+            for (int q = 0; q < ALD; ++q) ra[set][q] = bload4(rA, voA[q], k0 * 4);
         } else {
-            Ab = p.A2 + (k0 - p.K1);
-            la = p.lda2;
-        }
+            const rsrc_t rA = make_view(p.A2 + (int64_t)m0 * p.lda2, rows * p.lda2 * 4);
 #pragma unroll
-        for (int q = 0; q < ALD; ++q) {
-            const int f = tid + q * NT;
-            const int row = f / KC4, c4 = f % KC4;
-            const int gm = m0 + row;
-            if (gm < p.M)
-                ra[set][q] = *reinterpret_cast<const floatx4*>(Ab + (int64_t)gm * la + c4 * 4);
-            else
-                ra[set][q] = floatx4{0.f, 0.f, 0.f, 0.f};
+            for (int q = 0; q < ALD; ++q) ra[set][q] = bload4(rA, voA2[q], (k0 - p.K1) * 4);
         }
+        const rsrc_t rB = make_view(p.B + (int64_t)n0 * p.ldb, BN * p.ldb * 4);
 #pragma unroll
-        for (int q = 0; q < BLD; ++q) {
-            const int f = tid + q * NT;
-            const int row = f / KC4, c4 = f % KC4;
-            rb[set][q] = *reinterpret_cast<const floatx4*>(p.B + (int64_t)(n0 + row) * p.ldb + k0 + c4 * 4);
-        }
+        for (int q = 0; q < BLD; ++q) rb[set][q] = bload4(rB, voB[q], k0 * 4);
     };
     auto lstore = [&](int set, int buf) {
-        float* a = sA + buf * BM * LS;
-        float* b = sB + buf * BN * LS;
+        float* a = sA + buf * BM * LS + lds_st;
+        float* b = sB + buf * BN * LS + lds_st;
 #pragma unroll
-        for (int q = 0; q < ALD; ++q) {
-            const int f = tid + q * NT;
-            *reinterpret_cast<floatx4*>(a + (f / KC4) * LS + (f % KC4) * 4) = ra[set][q];
-        }
+        for (int q = 0; q < ALD; ++q) *reinterpret_cast<floatx4*>(a + q * RSTEP * LS) = ra[set][q];
 #pragma unroll
-        for (int q = 0; q < BLD; ++q) {
-            const int f = tid + q * NT;
-            *reinterpret_cast<floatx4*>(b + (f / KC4) * LS + (f % KC4) * 4) = rb[set][q];
-        }
+        for (int q = 0; q < BLD; ++q) *reinterpret_cast<floatx4*>(b + q * RSTEP * LS) = rb[set][q];
     };
     auto next_valid = [&](int vt) {
         for (; vt < ntiles; vt += gridDim.x) {
@@ -227,12 +190,25 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     const int Nmain = (EPI == CN_EPI_MUL && p.nsplit < p.N) ? p.nsplit : p.N;
     constexpr int C4 = BN / 4;
     constexpr int RPP = NT / C4;
-    constexpr int GMAX = OCC >= 4 ? 2 : 4;  // rows of aux loads in flight per thread (VGPR budget)
+    constexpr int GMAX = OCC >= 3 ? 2 : 4;  // rows of aux loads in flight per thread (VGPR budget)
     constexpr int GROUP = (PROWS / RPP) < GMAX ? (PROWS / RPP) : GMAX;
     static_assert((PROWS / RPP) % GROUP == 0, "epilogue passes");
     constexpr bool kAux0 = EPI == CN_EPI_MUL || EPI == CN_EPI_TANGENT || EPI == CN_EPI_BWD_SOFTPLUS ||
                            EPI == CN_EPI_BWD_RELU;
     constexpr bool kAux1 = EPI == CN_EPI_TANGENT || EPI == CN_EPI_BWD_SOFTPLUS;
+    constexpr bool kOut1 = EPI == CN_EPI_SOFTPLUS || EPI == CN_EPI_TANGENT;
+
+    // epilogue thread geometry: row rr + k*RPP of the slab, columns 4*c4 .. 4*c4+3
+    const int c4 = tid % C4;
+    const int rr = tid / C4;
+    const int voO0 = (rr * p.ld_out0 + 4 * c4) * 4;
+    const int voO1 = (rr * p.ld_out1 + 4 * c4) * 4;
+    const int voX0 = (rr * p.ld_aux0 + 4 * c4) * 4;
+    const int voX1 = (rr * p.ld_aux1 + 4 * c4) * 4;
+    const int voS = (rr * p.ld_split + 4 * c4) * 4;
+    const float c_exp = p.beta * 1.44269504088896341f;        // beta log2(e)
+    const float c_thr = p.threshold * 1.44269504088896341f;   // threshold in the log2 domain
+    const float c_log = 0.693147180559945309f / p.beta;       // ln(2) / beta
 
     int vt = next_valid(blockIdx.x);
     if (vt >= ntiles) return;
@@ -308,21 +284,45 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             }
         }
 
+        if constexpr (EPI == 7) {  // benchmark only: main loop alone, keep every accumulator live
+            float sum = 0.0f;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) sum += acc[i][j][r];
+            p.out0[(int64_t)(m0 + (tid & 127)) * p.ld_out0 + n0 + (tid >> 7)] = sum;
+            vt = vt_next;
+            tm = tm_next;
+            tn = tn_next;
+            continue;
+        }
         // Epilogue: park the accumulator tile (or a slab of PROWS rows of it) in the
         // now free staging LDS, then process it row-wise with 16-byte coalesced
-        // loads / stores; every aux load of a group of passes is issued before its math.
-        // C/D layout of the 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
-        float* sC = smem;
-        const int c4 = tid % C4;
-        const int rr = tid / C4;
-        EpiCols c;
-        c.col = n0 + 4 * c4;
-        c.region = c.col < Nmain ? 0 : (c.col < p.N ? 1 : (c.col < p.nzero ? 2 : 3));
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            c.bias[q] = (p.bias && c.region == 0) ? p.bias[c.col + q] : 0.0f;
-            c.colv[q] = (p.colv && c.region == 0) ? p.colv[c.col + q] : 0.0f;
+        // buffer loads / stores; every aux load of a group of passes is issued
+        // before its math.  C/D layout of the 32x32 MFMA: col = lane&31,
+        // row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+        const int rows = min(BM, p.M - m0);
+        // per-tile views, re-based on the pass's first row by SALU arithmetic (view_at)
+        const TileView tO0 = {p.out0 + (int64_t)m0 * p.ld_out0 + n0, p.ld_out0, (rows * p.ld_out0 - n0) * 4};
+        const TileView tO1 = {p.out1 + (int64_t)m0 * p.ld_out1 + n0, p.ld_out1, p.out1 ? (rows * p.ld_out1 - n0) * 4 : 0};
+        const TileView tX0 = {p.aux0 + (int64_t)m0 * p.ld_aux0 + n0, p.ld_aux0, p.aux0 ? (rows * p.ld_aux0 - n0) * 4 : 0};
+        const TileView tX1 = {p.aux1 + (int64_t)m0 * p.ld_aux1 + n0, p.ld_aux1, p.aux1 ? (rows * p.ld_aux1 - n0) * 4 : 0};
+        const TileView tR = {p.rowv + m0, 1, ROWV ? rows * 4 : 0};
+        const int sh = n0 - p.nsplit;  // out_split column of this tile's first column
+        const TileView tS = {p.out_split + (int64_t)m0 * p.ld_split + sh, p.ld_split,
+                             p.out_split ? (rows * p.ld_split - sh) * 4 : 0};
+
+        const bool tile_main = n0 + BN <= Nmain;
+        const int col = n0 + 4 * c4;
+        const int region = col < Nmain ? 0 : (col < p.N ? 1 : (col < p.nzero ? 2 : 3));
+        floatx4 bias = {0.f, 0.f, 0.f, 0.f}, colv = {0.f, 0.f, 0.f, 0.f};
+        if (region == 0) {
+            if (p.bias) bias = *reinterpret_cast<const floatx4*>(p.bias + col);
+            if (ROWV) colv = *reinterpret_cast<const floatx4*>(p.colv + col);
         }
+        float* sC = smem;
 #pragma unroll
         for (int part = 0; part < NPART; ++part) {
             if (part > 0) __syncthreads();  // previous slab consumed
@@ -337,29 +337,79 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                             sC[(row - part * PROWS) * CS + wn * TN * 32 + j * 32 + (lane & 31)] = acc[i][j][r];
                     }
             __syncthreads();
-            if (c.region != 3) {
+            if (region == 3) continue;
 #pragma unroll
-                for (int pb = 0; pb < PROWS / RPP; pb += GROUP) {
-                    floatx4 v[GROUP], x0[GROUP], x1[GROUP];
-                    float rv[GROUP];
-                    int64_t grow[GROUP];
+            for (int pb = 0; pb < PROWS / RPP; pb += GROUP) {
+                floatx4 v[GROUP], x0[GROUP], x1[GROUP];
+                float rv[GROUP];
+#pragma unroll
+                for (int q = 0; q < GROUP; ++q) {
+                    const int lrow = part * PROWS + (pb + q) * RPP;  // slab row offset of this pass (wave-uniform)
+                    v[q] = *reinterpret_cast<const floatx4*>(sC + (rr + (pb + q) * RPP) * CS + 4 * c4);
+                    // unconditional: the views make reads past a row (columns >= N) or
+                    // past the last row harmless, and only region-0 lanes use the values
+                    if (kAux0) x0[q] = bload4(view_at(tX0, lrow), voX0, 0);
+                    if (kAux1) x1[q] = bload4(view_at(tX1, lrow), voX1, 0);
+                    if (ROWV) rv[q] = bload1(view_at(tR, lrow), rr * 4, 0);
+                }
+                // main-region values of pass q (the EPI's math on 4 columns)
+                auto main_vals = [&](int q, floatx4& o0, floatx4& o1) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        // scaling by 1/adiv, 1/odiv is a multiply by exactly 1.0 when absent:
+                        // no per-element select for a uniform flag
+                        float u = v[q][e] * p.inv_adiv;
+                        if (ROWV) u = u + rv[q] * colv[e];
+                        if constexpr (EPI == CN_EPI_STORE) {
+                            o0[e] = u + bias[e];
+                        } else if constexpr (EPI == CN_EPI_SOFTPLUS) {
+                            float a, sg;
+                            softplus_hw(u + bias[e], c_exp, c_thr, c_log, a, sg);
+                            o0[e] = a * p.inv_odiv;
+                            o1[e] = sg;
+                        } else if constexpr (EPI == CN_EPI_RELU) {
+                            const float z = u + bias[e];
+                            o0[e] = z > 0.0f ? z : 0.0f;
+                        } else if constexpr (EPI == CN_EPI_MUL) {
+                            o0[e] = u * x0[q][e];
+                        } else if constexpr (EPI == CN_EPI_TANGENT) {
+                            o0[e] = u * x0[q][e] * p.inv_odiv;
+                            o1[e] = p.beta * x1[q][e] * (1.0f - x0[q][e]) * u;
+                        } else if constexpr (EPI == CN_EPI_BWD_SOFTPLUS) {
+                            o0[e] = u * x0[q][e] + x1[q][e];  // aux1 absent: a zero-record view reads 0
+                        } else if constexpr (EPI == CN_EPI_BWD_RELU) {
+                            o0[e] = x0[q][e] > 0.0f ? u : 0.0f;
+                        }
+                    }
+                };
+                if (tile_main) {  // wave-uniform: every column of the tile is in the main region
 #pragma unroll
                     for (int q = 0; q < GROUP; ++q) {
-                        const int row = rr + (pb + q) * RPP;
-                        grow[q] = m0 + part * PROWS + row;
-                        v[q] = *reinterpret_cast<const floatx4*>(sC + row * CS + 4 * c4);
-                        const bool ok = grow[q] < p.M && c.region == 0;
-                        x0[q] = floatx4{0.f, 0.f, 0.f, 0.f};
-                        x1[q] = floatx4{0.f, 0.f, 0.f, 0.f};
-                        if (kAux0 && ok)
-                            x0[q] = *reinterpret_cast<const floatx4*>(p.aux0 + grow[q] * p.ld_aux0 + c.col);
-                        if (kAux1 && ok && p.aux1)
-                            x1[q] = *reinterpret_cast<const floatx4*>(p.aux1 + grow[q] * p.ld_aux1 + c.col);
-                        rv[q] = (p.rowv && ok) ? p.rowv[grow[q]] : 0.0f;
+                        const int lrow = part * PROWS + (pb + q) * RPP;
+                        floatx4 o0, o1;
+                        main_vals(q, o0, o1);
+                        bstore4(view_at(tO0, lrow), voO0, 0, o0);
+                        if (kOut1) bstore4(view_at(tO1, lrow), voO1, 0, o1);  // absent out1: empty view
                     }
+                } else {
 #pragma unroll
-                    for (int q = 0; q < GROUP; ++q)
-                        if (grow[q] < p.M) epi_vec<EPI>(p, c, grow[q], v[q], x0[q], x1[q], rv[q]);
+                    for (int q = 0; q < GROUP; ++q) {
+                        const int lrow = part * PROWS + (pb + q) * RPP;
+                        floatx4 o0, o1;
+                        if (region == 0) {
+                            main_vals(q, o0, o1);
+                            bstore4(view_at(tO0, lrow), voO0, 0, o0);
+                            if (kOut1) bstore4(view_at(tO1, lrow), voO1, 0, o1);
+                        } else if (region == 1) {  // EPI_MUL split columns: raw (A·Bᵀ)/adiv
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) o0[e] = v[q][e] * p.inv_adiv;
+                            bstore4(view_at(tS, lrow), voS, 0, o0);
+                            if (col < p.nzero) bstore4(view_at(tO0, lrow), voO0, 0, floatx4{0.f, 0.f, 0.f, 0.f});
+                        } else {  // region 2: zero fill
+                            bstore4(view_at(tO0, lrow), voO0, 0, floatx4{0.f, 0.f, 0.f, 0.f});
+                            if (kOut1) bstore4(view_at(tO1, lrow), voO1, 0, floatx4{0.f, 0.f, 0.f, 0.f});
+                        }
+                    }
                 }
             }
         }
@@ -730,6 +780,13 @@ static void wgrad_geometry(int M, int N, int K, int* tile, int* Npad, int* Kpad,
 
 using namespace cn;
 
+// Kernel variant (benchmarking aid, process-wide): 0 = 2-deep register prefetch
+// when K % 64 == 0 (else 1-deep), 1 = always 1-deep, 2 = BK 16 at 3 workgroups/CU.
+static int g_linear_variant = [] {
+    const char* e = getenv("COPENERF_LINEAR_VARIANT");
+    return e ? atoi(e) : 0;
+}();
+
 template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH>
 static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_t s) {
     constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
@@ -744,8 +801,11 @@ static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_
     const int grid = std::min(ntiles, OCC * cus);  // OCC resident workgroups per CU
     dim3 block(64 * WM * WN);
     switch (d->epilogue) {
-#define CN_EPI_CASE(E) \
-        case E: linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, E><<<grid, block, 0, s>>>(a); break;
+#define CN_EPI_CASE(E)                                                                     \
+        case E:                                                                            \
+            if (d->rowv) linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, E, true><<<grid, block, 0, s>>>(a); \
+            else linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, E, false><<<grid, block, 0, s>>>(a);        \
+            break;
         CN_EPI_CASE(CN_EPI_STORE)
         CN_EPI_CASE(CN_EPI_SOFTPLUS)
         CN_EPI_CASE(CN_EPI_RELU)
@@ -754,19 +814,13 @@ static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_
         CN_EPI_CASE(CN_EPI_BWD_SOFTPLUS)
         CN_EPI_CASE(CN_EPI_BWD_RELU)
 #undef CN_EPI_CASE
+        case 7: linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, 7, false><<<grid, block, 0, s>>>(a); break;
         default: set_error("cn_linear: bad epilogue %d", d->epilogue); return CN_ERR_ARG;
     }
     return check_launch("cn_linear");
 }
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
-
-// Main-loop variant of the 128x128 tile (benchmarking aid, process-wide):
-// 0 = 2-deep register prefetch (default when K % 64 == 0), 1 = 1-deep.
-static int g_linear_variant = [] {
-    const char* e = getenv("COPENERF_LINEAR_VARIANT");
-    return e ? atoi(e) : 0;
-}();
 
 extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     CN_REQUIRE(d, CN_ERR_ARG, "cn_linear: null desc");
@@ -795,6 +849,7 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
         CN_REQUIRE(d->out_split && d->nsplit >= 0 && d->ld_split >= d->N - d->nsplit, CN_ERR_ARG,
                    "cn_linear: split output required");
     CN_REQUIRE((d->rowv == nullptr) == (d->colv == nullptr), CN_ERR_ARG, "cn_linear: rowv/colv go together");
+    CN_REQUIRE(al16(d->bias) && al16(d->colv), CN_ERR_ALIGN, "cn_linear: bias / colv must be 16-byte aligned");
     // the epilogue moves 4 columns per 16-byte access
     CN_REQUIRE(d->N % 4 == 0 && nzero % 4 == 0 && (e != CN_EPI_MUL || d->nsplit % 4 == 0), CN_ERR_SHAPE,
                "cn_linear: N, nzero and nsplit must be multiples of 4");
@@ -803,26 +858,35 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
                    (!d->aux1 || (al16(d->aux1) && d->ld_aux1 % 4 == 0)) &&
                    (!d->out_split || (al16(d->out_split) && d->ld_split % 4 == 0)),
                CN_ERR_ALIGN, "cn_linear: outputs / aux must be 16-byte aligned with leading dims % 4 == 0");
+    // buffer views address a 128-row tile with 32-bit byte offsets
+    constexpr int64_t kMaxLd = 1 << 20;
+    CN_REQUIRE(d->lda < kMaxLd && d->lda2 < kMaxLd && d->ldb < kMaxLd && d->ld_aux0 < kMaxLd && d->ld_aux1 < kMaxLd &&
+                   d->ld_out0 < kMaxLd && d->ld_out1 < kMaxLd && d->ld_split < kMaxLd,
+               CN_ERR_SHAPE, "cn_linear: leading dimensions must be < 2^20");
     if (d->M == 0) return CN_OK;
 
     LinearArgs a;
     a.A = d->A; a.A2 = d->A2; a.B = d->B; a.bias = d->bias; a.rowv = d->rowv; a.colv = d->colv;
     a.aux0 = d->aux0; a.aux1 = d->aux1; a.out0 = d->out0; a.out1 = d->out1; a.out_split = d->out_split;
-    a.lda = d->lda; a.lda2 = d->lda2; a.ldb = d->ldb; a.ld_aux0 = d->ld_aux0; a.ld_aux1 = d->ld_aux1;
-    a.ld_out0 = d->ld_out0; a.ld_out1 = d->ld_out1; a.ld_split = d->ld_split;
+    a.lda = (int)d->lda; a.lda2 = (int)d->lda2; a.ldb = (int)d->ldb;
+    a.ld_aux0 = (int)d->ld_aux0; a.ld_aux1 = (int)d->ld_aux1;
+    a.ld_out0 = (int)d->ld_out0; a.ld_out1 = (int)d->ld_out1; a.ld_split = (int)d->ld_split;
     a.M = d->M; a.N = d->N; a.K = d->K; a.K1 = K1; a.nzero = nzero;
     a.nsplit = (e == CN_EPI_MUL && d->out_split) ? d->nsplit : d->N;
-    a.adiv = d->adiv == 0.0f ? 1.0f : d->adiv;
-    a.odiv = d->odiv == 0.0f ? 1.0f : d->odiv;
+    const float adiv = d->adiv == 0.0f ? 1.0f : d->adiv;
+    const float odiv = d->odiv == 0.0f ? 1.0f : d->odiv;
+    a.inv_adiv = 1.0f / adiv;
+    a.inv_odiv = 1.0f / odiv;
     a.beta = d->beta;
     a.threshold = d->threshold;
     hipStream_t s = (hipStream_t)stream;
     const bool even = (d->K % 64) == 0;  // DEPTH-2 prefetch consumes K in pairs of 32-chunks
     if (d->tile == 0) {
-        if (g_linear_variant == 1 || !even) return launch_linear_tile<2, 2, 2, 2, 32, 2, 1>(d, a, s);
-        return launch_linear_tile<2, 2, 2, 2, 32, 2, 2>(d, a, s);
+        if (g_linear_variant == 2) return launch_linear_tile<2, 2, 2, 2, 16, 3, 2>(d, a, s);
+        if (even && g_linear_variant == 0) return launch_linear_tile<2, 2, 2, 2, 32, 2, 2>(d, a, s);
+        return launch_linear_tile<2, 2, 2, 2, 32, 2, 1>(d, a, s);
     }
-    if (even) return launch_linear_tile<4, 1, 1, 2, 32, 2, 2>(d, a, s);
+    if (even && g_linear_variant == 0) return launch_linear_tile<4, 1, 1, 2, 32, 2, 2>(d, a, s);
     return launch_linear_tile<4, 1, 1, 2, 32, 2, 1>(d, a, s);
 }
 

@@ -44,7 +44,8 @@ def main():
                           ("mul", ops.EPI_MUL, dict(aux0=aux0)),
                           ("tangent", ops.EPI_TANGENT, dict(aux0=aux0, aux1=aux1, out1=o1)),
                           ("bwd_softplus", ops.EPI_BWD_SOFTPLUS, dict(aux0=aux0, aux1=aux1)),
-                          ("relu", ops.EPI_RELU, dict(bias=bias))):
+                          ("relu", ops.EPI_RELU, dict(bias=bias)),
+                          ("main loop only (bench)", 7, {})):
         res["cn_linear " + name] = timeit(lambda: ops.linear(A, B, N, K, o0, epi, **kw))
     dW = torch.empty(N, K, device=dev)
     db = torch.empty(N, device=dev)

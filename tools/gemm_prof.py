@@ -1,0 +1,32 @@
+"""Launch each cn_linear epilogue a few times at the C2 layer shape (for
+rocprofv3 --pmc / --kernel-trace runs; the per-kernel names carry the EPI)."""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "cope-nerf_amd"), ROOT]
+from copenerf import ops  # noqa: E402
+
+
+def main():
+    M = int(os.environ.get("M", 524288))
+    N = K = 256
+    dev = "cuda"
+    A = torch.randn(M, K, device=dev) * 0.1
+    B = torch.randn(N, K, device=dev) * 0.05
+    bias = torch.randn(N, device=dev) * 0.1
+    aux0 = torch.rand(M, N, device=dev)
+    aux1 = torch.randn(M, N, device=dev)
+    o0 = torch.empty(M, N, device=dev)
+    o1 = torch.empty(M, N, device=dev)
+    for epi, kw in ((ops.EPI_STORE, dict(bias=bias)), (ops.EPI_SOFTPLUS, dict(bias=bias, out1=o1)),
+                    (ops.EPI_TANGENT, dict(aux0=aux0, aux1=aux1, out1=o1)), (7, {})):
+        for _ in range(int(os.environ.get("REPS", 5))):
+            ops.linear(A, B, N, K, o0, epi, **kw)
+    torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    main()
