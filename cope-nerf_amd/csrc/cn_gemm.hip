@@ -74,6 +74,12 @@ __device__ __forceinline__ floatx4 bload4(rsrc_t r, int voff, int soff) {
 __device__ __forceinline__ float bload1(rsrc_t r, int voff, int soff) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
 }
+// the value goes through a by-value parameter: __builtin_bit_cast applied directly
+// to a vector element (acc[i][j][r]) miscompiles in ROCm 7.2 clang (every store
+// of an unrolled loop gets element 0)
+__device__ __forceinline__ void bstore1(rsrc_t r, int voff, int soff, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, soff, 0);
+}
 __device__ __forceinline__ void bstore4(rsrc_t r, int voff, int soff, floatx4 v) {
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, soff, 0);
 }
@@ -429,7 +435,7 @@ struct WgradArgs {
     const float* X1;
     float* part;   // [nslices][Npad][Kpad]
     float* bpart;  // [nslices][Npad]
-    int64_t ldy0, ldx0, ldy1, ldx1;
+    int ldy0, ldx0, ldy1, ldx1;
     int M, Npad, Kpad, npairs, rows_per_slice, n_tiles_k;
 };
 
@@ -467,30 +473,27 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) wgrad_kernel(WgradArgs p) {
     const int total = nch * p.npairs;
     const bool do_bias = (tk == 0) && (p.bpart != nullptr);
 
+    // buffer views (see linear_kernel): the chunk's first row is the descriptor
+    // base (SALU), rows past mend read as zero through the range check
+    constexpr int YRS = NT / (BNo / 4);  // staged rows per Y load instruction
+    constexpr int XRS = NT / (BKo / 4);
+    const int yrow = tid / (BNo / 4), yc4 = tid % (BNo / 4);
+    const int xrow = tid / (BKo / 4), xc4 = tid % (BKo / 4);
     floatx4 ry[YLD], rx[XLD];
     auto gload = [&](int c) {
-        const int pair = c / nch;
+        const int pair = c >= nch;
         const int mrow = mbeg + (c - pair * nch) * MC;
         const float* Y = pair ? p.Y1 : p.Y0;
         const float* X = pair ? p.X1 : p.X0;
-        const int64_t ly = pair ? p.ldy1 : p.ldy0;
-        const int64_t lx = pair ? p.ldx1 : p.ldx0;
+        const int ly = pair ? p.ldy1 : p.ldy0;
+        const int lx = pair ? p.ldx1 : p.ldx0;
+        const int nrows = min(MC, mend - mrow);
+        const rsrc_t vY = make_view(Y + (int64_t)mrow * ly + n0, (nrows * ly - n0) * 4);
+        const rsrc_t vX = make_view(X + (int64_t)mrow * lx + k0, (nrows * lx - k0) * 4);
 #pragma unroll
-        for (int q = 0; q < YLD; ++q) {
-            const int f = tid + q * NT;
-            const int row = f / (BNo / 4), c4 = f % (BNo / 4);
-            const int gm = mrow + row;
-            ry[q] = gm < mend ? *reinterpret_cast<const floatx4*>(Y + (int64_t)gm * ly + n0 + c4 * 4)
-                              : floatx4{0.f, 0.f, 0.f, 0.f};
-        }
+        for (int q = 0; q < YLD; ++q) ry[q] = bload4(vY, ((yrow + q * YRS) * ly + yc4 * 4) * 4, 0);
 #pragma unroll
-        for (int q = 0; q < XLD; ++q) {
-            const int f = tid + q * NT;
-            const int row = f / (BKo / 4), c4 = f % (BKo / 4);
-            const int gm = mrow + row;
-            rx[q] = gm < mend ? *reinterpret_cast<const floatx4*>(X + (int64_t)gm * lx + k0 + c4 * 4)
-                              : floatx4{0.f, 0.f, 0.f, 0.f};
-        }
+        for (int q = 0; q < XLD; ++q) rx[q] = bload4(vX, ((xrow + q * XRS) * lx + xc4 * 4) * 4, 0);
     };
     auto lstore = [&](int buf) {
 #pragma unroll
@@ -548,18 +551,18 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) wgrad_kernel(WgradArgs p) {
         __syncthreads();
     }
 
-    float* out = p.part + (int64_t)slice * p.Npad * p.Kpad;
+    // slab stores: lane offset in voffset, the accumulator row step in soffset
+    const rsrc_t vP = make_view(p.part + (int64_t)slice * p.Npad * p.Kpad, p.Npad * p.Kpad * 4);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             const int col = k0 + wn * TN * 32 + j * 32 + (lane & 31);
             const int rbase = n0 + wm * TM * 32 + i * 32 + 4 * (lane >> 5);
+            const int vo = (rbase * p.Kpad + col) * 4;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = rbase + (r & 3) + 8 * (r >> 2);
-                out[(int64_t)row * p.Kpad + col] = acc[i][j][r];
-            }
+            for (int r = 0; r < 16; ++r)
+                bstore1(vP, vo, ((r & 3) + 8 * (r >> 2)) * p.Kpad * 4, acc[i][j][r]);
         }
     }
     if (do_bias && tid < BNo) p.bpart[(int64_t)slice * p.Npad + n0 + tid] = bacc;
@@ -910,6 +913,8 @@ extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
     if (d->npairs == 2)
         CN_REQUIRE(d->ldy1 >= Npad && d->ldx1 >= Kpad && d->ldy1 % 4 == 0 && d->ldx1 % 4 == 0 && al16(d->Y1) && al16(d->X1),
                    CN_ERR_ALIGN, "cn_wgrad: Y1/X1 alignment");
+    CN_REQUIRE(d->ldy0 < (1 << 20) && d->ldx0 < (1 << 20) && d->ldy1 < (1 << 20) && d->ldx1 < (1 << 20), CN_ERR_SHAPE,
+               "cn_wgrad: leading dimensions must be < 2^20");
     const size_t need = cn_wgrad_workspace_bytes(d->M, d->N, d->K);
     CN_REQUIRE((size_t)d->workspace_bytes >= need, CN_ERR_SHAPE, "cn_wgrad: workspace %lld < %zu", (long long)d->workspace_bytes, need);
     hipStream_t s = (hipStream_t)stream;
@@ -917,7 +922,7 @@ extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
     a.Y0 = d->Y0; a.X0 = d->X0; a.Y1 = d->Y1; a.X1 = d->X1;
     a.part = d->workspace;
     a.bpart = d->db ? d->workspace + (size_t)ns * Npad * Kpad : nullptr;
-    a.ldy0 = d->ldy0; a.ldx0 = d->ldx0; a.ldy1 = d->ldy1; a.ldx1 = d->ldx1;
+    a.ldy0 = (int)d->ldy0; a.ldx0 = (int)d->ldx0; a.ldy1 = (int)d->ldy1; a.ldx1 = (int)d->ldx1;
     a.M = d->M; a.Npad = Npad; a.Kpad = Kpad; a.npairs = d->npairs; a.rows_per_slice = rps;
     const int BKo = tile == 0 ? 128 : 64;
     a.n_tiles_k = Kpad / BKo;
