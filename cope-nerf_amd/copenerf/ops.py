@@ -22,8 +22,9 @@ class KernelTimer:
     """Brackets cn_linear / cn_wgrad launches with HIP events on the launching
     stream (torch's current stream) and keeps (key, events, algorithmic FLOPs)."""
 
-    def __init__(self):
+    def __init__(self, detail=False):
         self.records = []
+        self.detail = detail  # key launches by shape as well
 
     def start(self):
         e = torch.cuda.Event(enable_timing=True)
@@ -119,7 +120,8 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     if _timer is not None:
         e0 = _timer.start()
         _lib.check(_lib.load().cn_linear(d, _stream()), "cn_linear")
-        _timer.stop(("linear", tile, EPI_NAMES[epilogue]), e0, 2.0 * M * N * (kalg or K))
+        key = ("linear", tile, EPI_NAMES[epilogue])
+        _timer.stop(key + ((M, N, K),) if _timer.detail else key, e0, 2.0 * M * N * (kalg or K))
     else:
         _lib.check(_lib.load().cn_linear(d, _stream()), "cn_linear")
     return out0
@@ -145,7 +147,9 @@ def wgrad(Y0, X0, N, K, dW, *, db=None, Y1=None, X1=None, accumulate=False):
     if _timer is not None:
         e0 = _timer.start()
         _lib.check(lib.cn_wgrad(d, _stream()), "cn_wgrad")
-        _timer.stop(("wgrad", d.npairs), e0, 2.0 * M * d.n_out * d.k_out * d.npairs)
+        key = ("wgrad", d.npairs)
+        _timer.stop(key + ((M, d.n_out, d.k_out),) if _timer.detail else key, e0,
+                    2.0 * M * d.n_out * d.k_out * d.npairs)
     else:
         _lib.check(lib.cn_wgrad(d, _stream()), "cn_wgrad")
     return dW

@@ -436,7 +436,7 @@ struct WgradArgs {
     float* part;   // [nslices][Npad][Kpad]
     float* bpart;  // [nslices][Npad]
     int ldy0, ldx0, ldy1, ldx1;
-    int M, Npad, Kpad, npairs, rows_per_slice, n_tiles_k;
+    int M, Npad, Kpad, npairs, rows_per_slice, n_tiles_n, n_tiles_k, nslices;
 };
 
 template <int WM, int WN, int TM, int TN>
@@ -461,8 +461,13 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) wgrad_kernel(WgradArgs p) {
     const int wm = wave / WN;
     const int wn = wave % WN;
 
-    const int tile = blockIdx.x;
-    const int slice = blockIdx.y;
+    // XCD-aware: blocks b and b+8 share an XCD (and its L2), so the T output tiles
+    // of one M-slice, which read the same Y / X rows, are placed 8 blocks apart
+    const int T = p.n_tiles_n * p.n_tiles_k;
+    const int b = blockIdx.x;
+    const int tile = (b >> 3) % T;
+    const int slice = (b & 7) + 8 * ((b >> 3) / T);
+    if (slice >= p.nslices) return;
     const int tn = tile / p.n_tiles_k;
     const int tk = tile % p.n_tiles_k;
     const int n0 = tn * BNo;
@@ -926,7 +931,9 @@ extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
     a.M = d->M; a.Npad = Npad; a.Kpad = Kpad; a.npairs = d->npairs; a.rows_per_slice = rps;
     const int BKo = tile == 0 ? 128 : 64;
     a.n_tiles_k = Kpad / BKo;
-    dim3 grid((Npad / 128) * a.n_tiles_k, ns);
+    a.n_tiles_n = Npad / 128;
+    a.nslices = ns;
+    dim3 grid(cdiv(ns, 8) * 8 * a.n_tiles_n * a.n_tiles_k);
     if (tile == 0)
         wgrad_kernel<2, 2, 2, 2><<<grid, 256, 0, s>>>(a);
     else
