@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libcopenerf.so"
 LIB_PATH = os.environ.get("COPENERF_LIB", os.path.join(_HERE, LIB_NAME))
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 c_f32p = ctypes.c_void_p  # device pointers are passed as integers
 c_i32 = ctypes.c_int32
@@ -88,7 +88,10 @@ SIGNATURES = {
                                  c_i32, c_f32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr]),
     "cn_composite_bwd": (c_i32, [c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
                                  c_i32, c_f32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
-                                 c_ptr]),
+                                 c_ptr, c_ptr]),
+    "cn_points_bwd": (c_i32, [c_i32, c_i32, c_ptr, c_i32, c_ptr, c_ptr, c_i32, c_ptr, c_i64, c_ptr, c_ptr,
+                              c_ptr]),
+    "cn_color_extras_bwd": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_i32, c_ptr, c_i32, c_ptr]),
 }
 
 _lock = threading.Lock()

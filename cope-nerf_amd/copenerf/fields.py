@@ -161,6 +161,41 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
     return {"U": U, "Sig": Sig, "S": S, "sdf": sdf, "feat": feat, "G": G}
 
 
+def sdf_input_grad(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat):
+    """dL/dx of the sdf / feature outputs (the non-detached SDF forward of
+    neus_renderer.py:352; the ∇ₓSDF pass runs on detached points,
+    neus_renderer.py:356, so it contributes nothing here).  Primal adjoint chain
+    P_{l-1} = (W_lᵀ P_l) ⊙ σ_{l-1} from P_7 = (W_8fᵀ dfeat + dsdf w80) ⊙ σ_7, then
+    dx = scale · J_emb(x)ᵀ (W_0ᵀ P_0 + skip-embedding part)."""
+    U, Sig = st["U"], st["Sig"]
+    M, dev = U[0].shape[0], U[0].device
+    nl, sk, HL, KE = lay.n_lin, lay.skip, lay.HL, lay.KE
+    L8 = nl - 1
+    dx = _empty(M, 4, dev)
+    if dsdf is None and dfeat is None:
+        return dx.zero_()
+    dsdf_flat = None if dsdf is None else dsdf.reshape(M, 1).contiguous()
+    phi = dfeat if dfeat is not None else torch.zeros(M, lay.H_feat, device=dev)
+    P = _empty(M, HL, dev)
+    ops.linear(phi, pk.Bt8, lay.out_dim[L8 - 1], rup(lay.H_feat, 32), P, EPI_BWD_SOFTPLUS,
+               rowv=dsdf_flat, colv=pk.w80p if dsdf_flat is not None else None, aux0=Sig[L8 - 1], nzero=HL)
+    PE = _empty(M, KE, dev) if sk >= 0 else None
+    for l in range(L8 - 1, 0, -1):
+        Kl = rup(lay.out_dim[l], 32)
+        Pn = _empty(M, HL, dev)
+        if l == sk:
+            ops.linear(P, pk.Bt[l], lay.in_dim[l], Kl, Pn, EPI_MUL, aux0=Sig[l - 1], nsplit=lay.out_dim[l - 1],
+                       out_split=PE, nzero=HL, adiv=SQRT2, kalg=lay.out_dim[l])
+        else:
+            ops.linear(P, pk.Bt[l], lay.out_dim[l - 1], Kl, Pn, EPI_MUL, aux0=Sig[l - 1], nzero=HL,
+                       kalg=lay.out_dim[l])
+        P = Pn
+    P0 = _empty(M, KE, dev)
+    ops.linear(P, pk.Bt[0], lay.E, rup(lay.out_dim[0], 32), P0, EPI_STORE, nzero=KE, kalg=lay.out_dim[0])
+    ops.sdf_grad_assemble(lay.multires, lay.scale, U[0], P0, PE, dx)
+    return dx
+
+
 def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG):
     """Parameter gradients of SDFNetwork for upstream (dL/dsdf, dL/dfeature,
     dL/d∇ₓSDF).  The ∇ₓSDF term (the create_graph double backward of
@@ -248,7 +283,7 @@ class _SDFFieldFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, lay, pk, want_feat, want_grad, *params):
         ctx.set_materialize_grads(False)
-        keep = any(ctx.needs_input_grad[5:])
+        keep = any(ctx.needs_input_grad[5:]) or ctx.needs_input_grad[0]
         st = sdf_forward(lay, pk, x, want_feat=want_feat, want_grad=want_grad, keep=keep)
         ctx.lay, ctx.pk, ctx.st = lay, pk, (st if keep else None)
         ctx.nparams = len(params)
@@ -263,22 +298,22 @@ class _SDFFieldFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dsdf, dfeat, dG):
-        if ctx.needs_input_grad[0]:
-            raise NotImplementedError("copenerf: gradients w.r.t. SDF input points (ray / pose gradients, "
-                                      "eval.py:51-82) are not implemented yet")
-        none5 = (None,) * 5
+        none4 = (None,) * 4
         if ctx.st is None:
-            return none5 + (None,) * ctx.nparams
+            return (None,) + none4 + (None,) * ctx.nparams
         if dfeat is not None and dfeat.stride(1) != 1:
             dfeat = dfeat.contiguous()
         if dG is not None:
             dG = dG.contiguous()
-        dWs, dbs = sdf_backward(ctx.lay, ctx.pk, ctx.st, dsdf, dfeat, dG)
+        dx = sdf_input_grad(ctx.lay, ctx.pk, ctx.st, dsdf, dfeat) if ctx.needs_input_grad[0] else None
+        grads = [None] * ctx.nparams
+        if any(ctx.needs_input_grad[5:]):
+            dWs, dbs = sdf_backward(ctx.lay, ctx.pk, ctx.st, dsdf, dfeat, dG)
+            grads = []
+            for w, b in zip(dWs, dbs):
+                grads += [w, b]
         ctx.st = None
-        grads = []
-        for w, b in zip(dWs, dbs):
-            grads += [w, b]
-        return none5 + tuple(grads)
+        return (dx,) + none4 + tuple(grads)
 
 
 def _init_geometric(lin: nn.Linear, l: int, dims, out_dim, skip_in, multires, n_lin, bias, inside_outside,
@@ -412,6 +447,7 @@ class ColorPack:
     b3: torch.Tensor
     Btf: torch.Tensor  # feature columns of lin0, transposed
     Wg: torch.Tensor   # [4][H]: gradient columns of lin0, transposed
+    Bxt: torch.Tensor  # [64][Hpad]: extras columns [g | pts | emb(dirs)] of lin0, transposed (ray gradients)
 
 
 def pack_color(lay: ColorLayout, Ws, bs) -> ColorPack:
@@ -433,7 +469,8 @@ def pack_color(lay: ColorLayout, Ws, bs) -> ColorPack:
             b.append(bs[l].detach().contiguous())
         Btf = F.pad(feat.t(), (0, rup(o, 32) - o, 0, rup(Fd, 128) - Fd)).contiguous()
         Wg = g.t().contiguous()
-        return ColorPack(Bf, Bt, b, Ws[-1].detach().contiguous(), bs[-1].detach().contiguous(), Btf, Wg)
+        Bxt = F.pad(ext.t(), (0, rup(o, 32) - o, 0, 64 - ext.shape[1])).contiguous()
+        return ColorPack(Bf, Bt, b, Ws[-1].detach().contiguous(), bs[-1].detach().contiguous(), Btf, Wg, Bxt)
 
 
 class _ColorFieldFn(torch.autograd.Function):
@@ -457,13 +494,11 @@ class _ColorFieldFn(torch.autograd.Function):
         ops.row_head(H[-1], lay.in_dim[-1], pk.W3, pk.b3, 3, 1, rgb)
         ctx.lay, ctx.pk = lay, pk
         ctx.bufs = (feat, ext, H, rgb)
+        ctx.dirs, ctx.dir_div = (dirs, dir_div) if ctx.needs_input_grad[1] else (None, 1)
         return rgb
 
     @staticmethod
     def backward(ctx, drgb):
-        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
-            raise NotImplementedError("copenerf: colour-network gradients w.r.t. points / view directions "
-                                      "(ray / pose gradients) are not implemented yet")
         lay, pk = ctx.lay, ctx.pk
         feat, ext, H, rgb = ctx.bufs
         ctx.bufs = None
@@ -501,14 +536,26 @@ class _ColorFieldFn(torch.autograd.Function):
         if ctx.needs_input_grad[4]:
             dfeat = _empty(M, lay.F, dev)
             ops.linear(dZ, pk.Btf, lay.F, rup(o0, 32), dfeat, EPI_STORE, nzero=lay.F)
-        dG = None
-        if ctx.needs_input_grad[3]:
+        dG = dpts = ddirs = None
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            # ray / pose gradients: d ext = dZ0 W0[:, ext] in one GEMM, ext = [g | pts | emb(dirs)]
+            d_ext = _empty(M, 64, dev)
+            ops.linear(dZ, pk.Bxt, rup(Gd + P + V, 4), rup(o0, 32), d_ext, EPI_STORE, nzero=64, kalg=o0)
+            if ctx.needs_input_grad[3]:
+                dG = d_ext[:, 0:Gd]
+            if ctx.needs_input_grad[0]:
+                dpts = d_ext[:, Gd:Gd + P]
+            if ctx.needs_input_grad[1]:
+                dirs = ctx.dirs
+                ddirs = torch.empty(dirs.shape[0], 3, device=dev)
+                ops.color_extras_bwd(d_ext, dirs, ctx.dir_div, lay.multires_view, ddirs)
+        elif ctx.needs_input_grad[3]:
             dG = _empty(M, Gd, dev)
             ops.row_head(dZ, o0, pk.Wg, None, Gd, 0, dG)
         grads = []
         for w, b in zip(dWs, dbs):
             grads += [w, b]
-        return (None, None, None, dG, dfeat, None, None) + tuple(grads)
+        return (dpts, ddirs, None, dG, dfeat, None, None) + tuple(grads)
 
 
 class RenderingNetwork(nn.Module):

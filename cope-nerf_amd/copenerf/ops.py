@@ -248,8 +248,26 @@ def composite_fwd(z, sdf, G, rgb, rays_d, inv_s, near, far, n_coarse, car, color
 
 
 def composite_bwd(z, sdf, G, rgb, rays_d, inv_s, near, far, n_coarse, car, dcolor, ddepth, dweights, dcdf,
-                  dsdf, dG, drgb, dinv_part):
+                  dsdf, dG, drgb, dinv_part, drays_d=None):
     R, S = z.shape
     _lib.call("cn_composite_bwd", R, S, _ptr(z), _ptr(sdf), _ptr(G), G.stride(0), _ptr(rgb), _ptr(rays_d),
               _ptr(inv_s), _ptr(near), _ptr(far), n_coarse, float(car), _ptr(dcolor), _ptr(ddepth),
-              _ptr(dweights), _ptr(dcdf), _ptr(dsdf), _ptr(dG), _ptr(drgb), _ptr(dinv_part), _stream())
+              _ptr(dweights), _ptr(dcdf), _ptr(dsdf), _ptr(dG), _ptr(drgb), _ptr(dinv_part), _ptr(drays_d),
+              _stream())
+
+
+def points_bwd(z, dP, drays_o, drays_d, *, mid=False, near=None, far=None, n_coarse=0):
+    """drays_o = sum_i dP_i, drays_d = sum_i dP_i * zz_i per ray -- cn_points_bwd."""
+    _need(dP, "dP")
+    R, n = z.shape
+    _lib.call("cn_points_bwd", R, n, _ptr(z), 1 if mid else 0, _ptr(near), _ptr(far), n_coarse, _ptr(dP), _ld(dP),
+              _ptr(drays_o), _ptr(drays_d), _stream())
+
+
+def color_extras_bwd(d_ext, dirs, dir_div, multires_view, ddirs, accumulate=False):
+    """ddirs [R,3] (+)= view-encoding gradient of d_ext -- cn_color_extras_bwd."""
+    _need(d_ext, "d_ext")
+    _need(dirs, "dirs")
+    _lib.call("cn_color_extras_bwd", dirs.shape[0], dir_div, _ptr(d_ext), _ld(d_ext), _ptr(dirs), _ld(dirs),
+              multires_view, _ptr(ddirs), 1 if accumulate else 0, _stream())
+    return ddirs

@@ -19,6 +19,34 @@ from . import ops
 from .fields import _empty
 
 
+class _PointsFn(torch.autograd.Function):
+    """Section midpoints along the rays (neus_renderer.py:337-350):
+    pts_time = [rays_o + rays_d * mid_z, t]; backward gives the ray gradients."""
+
+    @staticmethod
+    def forward(ctx, rays_o, rays_d, z, time_step, near, far, n_coarse):
+        R, S = z.shape
+        pts = torch.empty(R * S, 4, device=z.device)
+        ops.points(rays_o, rays_d, z, time_step, pts, mid=True, near=near, far=far, n_coarse=n_coarse)
+        ctx.save_for_backward(z, near, far)
+        ctx.n_coarse = n_coarse
+        return pts
+
+    @staticmethod
+    def backward(ctx, dpts):
+        z, near, far = ctx.saved_tensors
+        R = z.shape[0]
+        want_o, want_d = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        if dpts is None or not (want_o or want_d):
+            return (None,) * 7
+        if dpts.stride(1) != 1:
+            dpts = dpts.contiguous()
+        do = torch.empty(R, 3, device=z.device) if want_o else None
+        dd = torch.empty(R, 3, device=z.device) if want_d else None
+        ops.points_bwd(z, dpts, do, dd, mid=True, near=near, far=far, n_coarse=ctx.n_coarse)
+        return do, dd, None, None, None, None, None
+
+
 class _CompositeFn(torch.autograd.Function):
     """(z, sdf, ∇ₓSDF, rgb, rays_d, inv_s) -> (colour, weighted z, weights, cdf)."""
 
@@ -38,9 +66,7 @@ class _CompositeFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dcolor, ddepth, dweights, dcdf):
-        if ctx.needs_input_grad[4] or ctx.needs_input_grad[0]:
-            raise NotImplementedError("copenerf: compositing gradients w.r.t. rays / z (pose optimisation) "
-                                      "are not implemented yet")
+        # z is sampled under no_grad in the reference (neus_renderer.py:492-525): no gradient
         z, sdf, G, rgb, rays_d, inv_s, near, far = ctx.saved_tensors
         R, S = z.shape
         M, dev = R * S, z.device
@@ -49,11 +75,12 @@ class _CompositeFn(torch.autograd.Function):
         drgb = _empty(M, 3, dev)
         dinv = torch.empty(R, device=dev)
         c = lambda t: None if t is None else t.contiguous()  # noqa: E731
+        drays_d = torch.empty(R, 3, device=dev) if ctx.needs_input_grad[4] else None
         ops.composite_bwd(z, sdf, G, rgb, rays_d, inv_s, near, far, ctx.n_coarse, ctx.car, c(dcolor), c(ddepth),
-                          c(dweights), c(dcdf), dsdf, dG, drgb, dinv)
+                          c(dweights), c(dcdf), dsdf, dG, drgb, dinv, drays_d)
         dinv_s = dinv.sum().reshape(inv_s.shape) if ctx.needs_input_grad[5] else None
         return (None, dsdf if ctx.needs_input_grad[1] else None, dG if ctx.needs_input_grad[2] else None,
-                drgb if ctx.needs_input_grad[3] else None, None, dinv_s, None, None, None, None)
+                drgb if ctx.needs_input_grad[3] else None, drays_d, dinv_s, None, None, None, None)
 
 
 class NeuSRenderer(nn.Module):
@@ -120,8 +147,6 @@ class NeuSRenderer(nn.Module):
         """Reference signature (neus_renderer.py:453) plus two test hooks: `t_rand`
         injects the stratified jitter, `z_vals` [R, S] skips the sampler and renders
         at the given sample positions (the render_core seam)."""
-        if rays_o.requires_grad or rays_d.requires_grad:
-            raise NotImplementedError("copenerf: ray gradients (eval.py pose optimisation) are not implemented yet")
         R = len(rays_o)
         dev = rays_o.device
         if it >= self.importance_sampling_start:
@@ -129,7 +154,7 @@ class NeuSRenderer(nn.Module):
         else:
             n_samples, n_importance = self.n_samples + self.n_importance, 0
         rays_o = rays_o.contiguous().float()
-        rays_d = rays_d.contiguous().float()
+        rays_d = rays_d.contiguous().float()  # differentiable: pose gradients flow through these
         near = near.contiguous().float()
         far = far.contiguous().float()
         time_step = time_step.reshape(-1)[:1].contiguous().float()
@@ -147,8 +172,11 @@ class NeuSRenderer(nn.Module):
         S = z.shape[1]
 
         # render_core (neus_renderer.py:307-450)
-        pts_time = torch.empty(R * S, 4, device=dev)
-        ops.points(rays_o, rays_d, z, time_step, pts_time, mid=True, near=near, far=far, n_coarse=n_samples)
+        if rays_o.requires_grad or rays_d.requires_grad:  # pose optimisation (eval.py:51-82, joint pose training)
+            pts_time = _PointsFn.apply(rays_o, rays_d, z, time_step, near, far, n_samples)
+        else:
+            pts_time = torch.empty(R * S, 4, device=dev)
+            ops.points(rays_o, rays_d, z, time_step, pts_time, mid=True, near=near, far=far, n_coarse=n_samples)
         sdf, feat, G = self.sdf_network.field(pts_time, want_feat=True, want_grad=True, packed=sdf_packed)
         rgb = self.color_network.color(pts_time, G, rays_d, S, feat, packed=col_packed)
         inv_s = self.deviation_network(torch.zeros([1, 3], device=dev))[:, :1].clip(1 / 1e3, 1 / 1e-3)

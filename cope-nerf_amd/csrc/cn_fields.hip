@@ -150,6 +150,37 @@ __global__ void color_extras_kernel(int M, const float* __restrict__ Gm, int64_t
     st4(ext + m * ld_ext + 4 * g, o);
 }
 
+// Gradient of the per-ray view directions through the view encoding.  Block =
+// 8 rays x 32 lanes; lane e < nv sums column 8+e of d_ext over the ray's rows
+// (double, fixed order), then lanes 0..2 apply the encoding's Jacobian.
+__global__ void __launch_bounds__(256) color_extras_bwd_kernel(int R, int rows, const float* __restrict__ d_ext,
+                                                               int64_t ld_ext, const float* __restrict__ dirs,
+                                                               int64_t ld_d, int L, float* ddirs, int accumulate) {
+    __shared__ double part[8][32];
+    const int rr = threadIdx.x >> 5, e = threadIdx.x & 31;
+    const int r = blockIdx.x * 8 + rr;
+    const int nv = 3 + 6 * L;
+    double acc = 0.0;
+    if (r < R && e < nv) {
+        const float* col = d_ext + (int64_t)r * rows * ld_ext + 8 + e;
+        for (int i = 0; i < rows; ++i) acc += (double)col[(int64_t)i * ld_ext];
+    }
+    part[rr][e] = acc;
+    __syncthreads();
+    if (r < R && e < 3) {
+        const float dc = dirs[(int64_t)r * ld_d + e];
+        double g = part[rr][e];
+        for (int k = 0; k < L; ++k) {
+            const float f = (float)(1 << k);
+            const float t = dc * f;
+            // ext column 3 + 6k + w: w < 3 sin(2^k d_w), w >= 3 cos(2^k d_{w-3})
+            g += (double)(f * cosf(t)) * part[rr][3 + 6 * k + e] - (double)(f * sinf(t)) * part[rr][3 + 6 * k + 3 + e];
+        }
+        float* o = ddirs + 3 * (int64_t)r + e;
+        *o = accumulate ? *o + (float)g : (float)g;
+    }
+}
+
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace cn
@@ -219,4 +250,17 @@ extern "C" int cn_color_extras(int32_t M, const float* G, int64_t ld_g, const fl
     color_extras_kernel<<<(int)((tot + 255) / 256), 256, 0, (hipStream_t)stream>>>(
         M, G, ld_g, pts, ld_p, dirs, ld_d, dir_div, multires_view, Gc, ext, ld_ext);
     return check_launch("cn_color_extras");
+}
+
+extern "C" int cn_color_extras_bwd(int32_t R, int32_t dir_div, const float* d_ext, int64_t ld_ext, const float* dirs,
+                                   int64_t ld_d, int32_t multires_view, float* ddirs, int32_t accumulate,
+                                   cn_stream_t stream) {
+    CN_REQUIRE(d_ext && dirs && ddirs, CN_ERR_ARG, "cn_color_extras_bwd: null pointer");
+    CN_REQUIRE(R >= 0 && dir_div >= 1 && multires_view >= 0 && 3 + 6 * multires_view <= 32 &&
+                   ld_ext >= 8 + 3 + 6 * multires_view && ld_d >= 3,
+               CN_ERR_SHAPE, "cn_color_extras_bwd: R=%d dir_div=%d multires_view=%d", R, dir_div, multires_view);
+    if (R == 0) return CN_OK;
+    color_extras_bwd_kernel<<<cdiv(R, 8), 256, 0, (hipStream_t)stream>>>(R, dir_div, d_ext, ld_ext, dirs, ld_d,
+                                                                        multires_view, ddirs, accumulate);
+    return check_launch("cn_color_extras_bwd");
 }

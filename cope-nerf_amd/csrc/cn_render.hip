@@ -93,6 +93,37 @@ __global__ void points_kernel(int R, int n, const float* __restrict__ o, const f
     *reinterpret_cast<floatx4*>(pts + 4 * idx) = p;
 }
 
+// Backward of points_kernel: one wavefront per ray, lanes stride the samples.
+__global__ void __launch_bounds__(256) points_bwd_kernel(int R, int n, const float* __restrict__ z, int mid,
+                                                         const float* __restrict__ near, const float* __restrict__ far,
+                                                         int n_coarse, const float* __restrict__ dP, int64_t ld_p,
+                                                         float* drays_o, float* drays_d) {
+    const int lane = threadIdx.x & 63;
+    const int r = blockIdx.x * kRaysPerBlock + (threadIdx.x >> 6);
+    if (r >= R) return;
+    double so[3] = {0.0, 0.0, 0.0}, sd[3] = {0.0, 0.0, 0.0};
+    for (int i = lane; i < n; i += 64) {
+        const int64_t idx = (int64_t)r * n + i;
+        float zz = z[idx];
+        if (mid) {
+            const float dist = i < n - 1 ? z[idx + 1] - zz : (far[0] - near[0]) / (float)n_coarse;
+            zz = zz + dist * 0.5f;
+        }
+        for (int c = 0; c < 3; ++c) {
+            const float g = dP[idx * ld_p + c];
+            so[c] += (double)g;
+            sd[c] += (double)(g * zz);
+        }
+    }
+    for (int c = 0; c < 3; ++c) {
+        const double a = wave_sum(so[c]), b = wave_sum(sd[c]);
+        if (lane == 0) {
+            if (drays_o) drays_o[3 * r + c] = (float)a;
+            if (drays_d) drays_d[3 * r + c] = (float)b;
+        }
+    }
+}
+
 // One NeuS up-sampling round (up_sample + sample_pdf(det) + cat_z_vals).
 __global__ void __launch_bounds__(256) up_sample_merge_kernel(int R, int n, int n_imp, float inv_s,
                                                               const float* __restrict__ z,
@@ -339,7 +370,7 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(
     const float* __restrict__ rgb, const float* __restrict__ rays_d, const float* __restrict__ inv_s_p,
     const float* __restrict__ near, const float* __restrict__ far, int n_coarse, float car,
     const float* __restrict__ dcolor, const float* __restrict__ ddepth, const float* __restrict__ dweights,
-    const float* __restrict__ dcdf, float* dsdf, float* dG, float* drgb, float* dinv_part) {
+    const float* __restrict__ dcdf, float* dsdf, float* dG, float* drgb, float* dinv_part, float* drays_d) {
     const int lane = threadIdx.x & 63;
     const int r = blockIdx.x * kRaysPerBlock + (threadIdx.x >> 6);
     if (r >= R) return;
@@ -393,6 +424,7 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(
     double after = __shfl_down(sincl, 1, 64);  // sum over lanes > lane
     if (lane == 63) after = 0.0;
     double dinv = 0.0;
+    double dd0 = 0.0, dd1 = 0.0, dd2 = 0.0;  // d rays_d from true_cos
 #pragma unroll
     for (int p = kMaxPerLane - 1; p >= 0; --p) {
         const int i = lane * P + p;
@@ -429,9 +461,24 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(
         dG[4 * m + 1] = dtc * d[1];
         dG[4 * m + 2] = dtc * d[2];
         dG[4 * m + 3] = 0.0f;
+        if (drays_d) {
+            dd0 += (double)(dtc * G[m * ld_g]);
+            dd1 += (double)(dtc * G[m * ld_g + 1]);
+            dd2 += (double)(dtc * G[m * ld_g + 2]);
+        }
     }
     dinv = wave_sum(dinv);
     if (lane == 0) dinv_part[r] = (float)dinv;
+    if (drays_d) {
+        dd0 = wave_sum(dd0);
+        dd1 = wave_sum(dd1);
+        dd2 = wave_sum(dd2);
+        if (lane == 0) {
+            drays_d[3 * r] = (float)dd0;
+            drays_d[3 * r + 1] = (float)dd1;
+            drays_d[3 * r + 2] = (float)dd2;
+        }
+    }
 }
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -463,6 +510,18 @@ extern "C" int cn_points(int32_t R, int32_t n, const float* rays_o, const float*
     return check_launch("cn_points");
 }
 
+extern "C" int cn_points_bwd(int32_t R, int32_t n, const float* z, int32_t mid, const float* near, const float* far,
+                             int32_t n_coarse, const float* dP, int64_t ld_p, float* drays_o, float* drays_d,
+                             cn_stream_t stream) {
+    CN_REQUIRE(z && dP && (drays_o || drays_d), CN_ERR_ARG, "cn_points_bwd: null pointer");
+    CN_REQUIRE(!mid || (near && far && n_coarse > 0), CN_ERR_ARG, "cn_points_bwd: mid needs near/far/n_coarse");
+    CN_REQUIRE(R >= 0 && n >= 1 && ld_p >= 3, CN_ERR_SHAPE, "cn_points_bwd: R=%d n=%d ld_p=%lld", R, n, (long long)ld_p);
+    if (R == 0) return CN_OK;
+    points_bwd_kernel<<<cdiv(R, kRaysPerBlock), 64 * kRaysPerBlock, 0, (hipStream_t)stream>>>(
+        R, n, z, mid, near, far, n_coarse, dP, ld_p, drays_o, drays_d);
+    return check_launch("cn_points_bwd");
+}
+
 extern "C" int cn_up_sample_merge(int32_t R, int32_t n, int32_t n_imp, float inv_s, const float* z, const float* sdf,
                                   float* z_out, float* z_new, float* sdf_out, int32_t* new_dst, cn_stream_t stream) {
     CN_REQUIRE(z && sdf && z_out && z_new, CN_ERR_ARG, "cn_up_sample_merge: null pointer");
@@ -492,7 +551,7 @@ extern "C" int cn_composite_bwd(int32_t R, int32_t S, const float* z, const floa
                                 const float* rgb, const float* rays_d, const float* inv_s, const float* near,
                                 const float* far, int32_t n_coarse, float cos_anneal_ratio, const float* dcolor,
                                 const float* ddepth, const float* dweights, const float* dcdf, float* dsdf, float* dG,
-                                float* drgb, float* dinv_s_part, cn_stream_t stream) {
+                                float* drgb, float* dinv_s_part, float* drays_d, cn_stream_t stream) {
     CN_REQUIRE(z && sdf && G && rgb && rays_d && inv_s && near && far && dsdf && dG && drgb && dinv_s_part,
                CN_ERR_ARG, "cn_composite_bwd: null pointer");
     CN_REQUIRE(S >= 1 && S <= 64 * kMaxPerLane && n_coarse > 0 && ld_g >= 3, CN_ERR_UNSUPPORTED,
@@ -500,6 +559,6 @@ extern "C" int cn_composite_bwd(int32_t R, int32_t S, const float* z, const floa
     if (R == 0) return CN_OK;
     composite_bwd_kernel<<<cdiv(R, kRaysPerBlock), 64 * kRaysPerBlock, 0, (hipStream_t)stream>>>(
         R, S, z, sdf, G, ld_g, rgb, rays_d, inv_s, near, far, n_coarse, cos_anneal_ratio, dcolor, ddepth, dweights,
-        dcdf, dsdf, dG, drgb, dinv_s_part);
+        dcdf, dsdf, dG, drgb, dinv_s_part, drays_d);
     return check_launch("cn_composite_bwd");
 }

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define CN_ABI_VERSION 1
+#define CN_ABI_VERSION 2
 
 typedef void* cn_stream_t; /* hipStream_t */
 
@@ -171,6 +171,16 @@ int cn_color_extras(int32_t M, const float* G, int64_t ld_g, const float* pts, i
                     const float* dirs, int64_t ld_d, int32_t dir_div, int32_t multires_view,
                     int32_t kpad, float* ext, int64_t ld_ext, cn_stream_t stream);
 
+/* Ray-direction gradient through the view encoding of cn_color_extras (the
+ * autograd of neus_embedder.py:17-36 on dirs, neus_renderer.py:345, 354):
+ * with d_ext [M][>=8+3+6L] the gradient of ext, rows r*dir_div .. r*dir_div +
+ * dir_div-1 sharing dirs[r],
+ *   ddirs[r][c] (+)= sum_rows d_ext[.][8+c]
+ *                  + sum_k 2^k (cos(2^k d_c) d_ext[.][11+6k+c] - sin(2^k d_c) d_ext[.][14+6k+c]). */
+int cn_color_extras_bwd(int32_t R, int32_t dir_div, const float* d_ext, int64_t ld_ext, const float* dirs,
+                        int64_t ld_d, int32_t multires_view, float* ddirs, int32_t accumulate,
+                        cn_stream_t stream);
+
 /* Backward of the colour head (sigmoid(Linear 256->3), neus_fields.py:367-373):
  *   dz3 = drgb*rgb*(1-rgb);  dZ2[m][k] = (H3[m][k] > 0) * sum_c dz3[m][c]*W3[c][k];
  *   dW3 = sum_m dz3ᵀ H3, db3 = sum_m dz3 (fixed-order slab reduction). */
@@ -194,6 +204,15 @@ int cn_points(int32_t R, int32_t n, const float* rays_o, const float* rays_d, co
               const float* t, int32_t mid, const float* near, const float* far, int32_t n_coarse,
               float* pts_time, cn_stream_t stream);
 
+/* Backward of cn_points for ray / pose gradients (the autograd of
+ * neus_renderer.py:343-350, pts = rays_o + rays_d * mid_z): with dP [R*n][>=3]
+ * (row stride ld_p) the upstream gradient of pts_time,
+ *   drays_o[r] = sum_i dP[r*n+i][0..3),  drays_d[r] = sum_i dP[r*n+i][0..3) * zz_i
+ * (zz as in cn_points).  One wavefront per ray, fixed-order double sums. */
+int cn_points_bwd(int32_t R, int32_t n, const float* z, int32_t mid, const float* near, const float* far,
+                  int32_t n_coarse, const float* dP, int64_t ld_p, float* drays_o, float* drays_d,
+                  cn_stream_t stream);
+
 /* One NeuS up-sampling round + merge (neus_renderer.py:178-224 up_sample,
  * 39-70 sample_pdf det=True, 282-298 cat_z_vals).  One wavefront per ray.
  *   z_out = sorted merge of z and the n_imp new samples;
@@ -214,12 +233,16 @@ int cn_composite_fwd(int32_t R, int32_t S, const float* z, const float* sdf, con
                      const float* near, const float* far, int32_t n_coarse, float cos_anneal_ratio,
                      float* color, float* depth, float* weights, float* cdf, cn_stream_t stream);
 
+/* Backward of cn_composite_fwd.  drays_d (nullable, [R][3]) receives the ray
+ * direction gradient of true_cos = rays_d . normals (neus_renderer.py:362);
+ * the normals are those of the detached-input gradient pass
+ * (neus_renderer.py:356), so no second-order term reaches the points. */
 int cn_composite_bwd(int32_t R, int32_t S, const float* z, const float* sdf, const float* G,
                      int64_t ld_g, const float* rgb, const float* rays_d, const float* inv_s,
                      const float* near, const float* far, int32_t n_coarse, float cos_anneal_ratio,
                      const float* dcolor, const float* ddepth, const float* dweights,
                      const float* dcdf, float* dsdf, float* dG, float* drgb, float* dinv_s_part,
-                     cn_stream_t stream);
+                     float* drays_d, cn_stream_t stream);
 
 #ifdef __cplusplus
 }
