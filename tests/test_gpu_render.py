@@ -135,3 +135,42 @@ def test_render_large_batch_properties():
     loss.backward()
     for n, p in named_params(*mods):
         assert p.grad is not None and torch.isfinite(p.grad).all(), n
+
+
+@pytest.mark.parametrize("n_samples,n_importance", [(64, 128), (32, 32)])
+def test_render_configs_c5_c1(n_samples, n_importance):
+    """C5 (coarse 64 + fine 128 = 192 samples, 4 rounds of 32) and C1 (32 + 32):
+    the sampler and compositing at other sample counts, end to end against the
+    oracle with the same jitter, and strict |Δ| <= 1e-4 on identical samples."""
+    from copenerf import NeuSRenderer
+    R = 256
+    g = torch.Generator().manual_seed(7)
+    mods_cpu = build_modules(55, 256, 256)
+    P, Pc, var, _ = oracle_params(*mods_cpu)
+    o = torch.tensor([0.05, -0.03, 1.6]).expand(R, 3).contiguous()
+    d = torch.cat([(torch.rand(R, 2, generator=g) - 0.5) * 0.6, -torch.ones(R, 1)], -1)
+    nrm = d.norm(dim=-1, keepdim=True)
+    d = d / nrm
+    t = torch.tensor([0.25])
+    near, far = torch.full((R, 1), 0.01), torch.full((R, 1), 3.0)
+    t_rand = torch.rand(R, n_samples, generator=g)
+    torch.set_num_threads(8)
+    ref = O.render(P, Pc, var, o, d, nrm, t, near, far, n_samples=n_samples, n_importance=n_importance, car=0.5,
+                   t_rand=t_rand)
+    cfg = dict(REN_CFG, n_samples=n_samples, n_importance=n_importance)
+    sdf, col, dev = build_modules(55, 256, 256, device=DEV)
+    r = NeuSRenderer(None, sdf, dev, col, None, **cfg).to(DEV)
+    args = tuple(x.to(DEV) for x in (o, d, nrm, t, near, far))
+    out = r(*args, cos_anneal_ratio=0.5, it=0, eval=False, z_vals=ref["z_vals"].to(DEV))
+    assert out["weights"].shape == (R, n_samples + n_importance)
+    for k in ("color_fine", "depth_pred"):
+        err = (out[k].detach().cpu() - ref[k].detach()).abs().max().item()
+        assert err <= TOL_RGB_DEPTH, (k, err)
+    out = r(*args, cos_anneal_ratio=0.5, it=0, eval=False, t_rand=t_rand.to(DEV))
+    zh = ((out["sampled_points"].cpu() - o[:, None]) * d[:, None]).sum(-1)
+    zr = ((ref["sampled_points"] - o[:, None]) * d[:, None]).sum(-1)
+    jumped = (zh - zr).abs().max(1)[0] > 1e-4
+    assert jumped.float().mean().item() <= 0.1
+    err = torch.maximum((out["depth_pred"].detach().cpu() - ref["depth_pred"].detach()).abs().squeeze(1),
+                        (out["color_fine"].detach().cpu() - ref["color_fine"].detach()).abs().max(1)[0])
+    assert (err > TOL_RGB_DEPTH).float().mean().item() <= 0.01
