@@ -8,7 +8,8 @@ from .fields import NeRF, RenderingNetwork, SDFNetwork, SingleVarianceNetwork  #
 from .renderer import NeuSRenderer  # noqa: F401
 from .losses import EdgePreservingSmoothnessLoss, SmoothnessLoss  # noqa: F401
 from .rays import PoseRetriever  # noqa: F401
+from .motion import MotionNetwork  # noqa: F401
 from . import _lib  # noqa: F401
 
 __all__ = ["NeuSRenderer", "SDFNetwork", "RenderingNetwork", "SingleVarianceNetwork", "NeRF",
-           "EdgePreservingSmoothnessLoss", "SmoothnessLoss", "PoseRetriever"]
+           "EdgePreservingSmoothnessLoss", "SmoothnessLoss", "PoseRetriever", "MotionNetwork"]

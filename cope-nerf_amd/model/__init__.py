@@ -2,8 +2,8 @@
 
 Put `cope-nerf_amd/` on sys.path ahead of the reference checkout and
 `from model import NeuSRenderer, SDFNetwork, ...` resolves to the HIP-backed
-classes.  Names outside the rendering hot path (Trainer, CheckpointIO,
-MotionNetwork) are out of scope for this build and are not exported.
+classes.  Trainer and CheckpointIO (outside the rendering hot path) are not
+exported; MotionNetwork is the stage-1 motion model of copenerf/motion.py.
 """
-from copenerf import (EdgePreservingSmoothnessLoss, NeRF, NeuSRenderer, PoseRetriever,  # noqa: F401
-                      RenderingNetwork, SDFNetwork, SingleVarianceNetwork, SmoothnessLoss)
+from copenerf import (EdgePreservingSmoothnessLoss, MotionNetwork, NeRF, NeuSRenderer,  # noqa: F401
+                      PoseRetriever, RenderingNetwork, SDFNetwork, SingleVarianceNetwork, SmoothnessLoss)

@@ -282,3 +282,15 @@ def train_loss(out, rgb_gt, *, patch=4, w_rgb=1.0, w_eik=0.1, w_edge=1.0, w_smoo
         g = rgb_gt.view(-1, patch, patch, 3)
         loss = loss + w_edge * (1 / (2 ** s)) * edge_smoothness(d, g) + w_smooth * (1 / (2 ** s)) * smoothness(d)
     return loss
+
+
+# ---------------------------------------------------------------------------
+# stage-1 scene-flow loss (train.py:467-477)
+def scene_flow_loss(pts, normals, sdf_flows, weights, omega, vel):
+    """sum |(ω × p + v) · n + ∂sdf/∂t| · w.detach() / (sum w + 1e-10) over all samples."""
+    pts = pts.reshape(-1, 3)
+    n = normals.reshape(-1, 3)
+    w = weights.reshape(-1).detach()
+    sf = torch.cross(omega.reshape(1, 3).repeat(pts.shape[0], 1), pts, dim=-1) + vel.reshape(1, 3).repeat(pts.shape[0], 1)
+    lhs = torch.sum(sf * n, dim=-1)
+    return torch.sum(torch.abs(lhs + sdf_flows.reshape(-1)) * w) / (torch.sum(w) + 1e-10)

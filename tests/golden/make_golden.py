@@ -235,8 +235,37 @@ def seams_case(fields, rend):
     print("wrote seams")
 
 
+MOTION_CFG = dict(d_out=6, d_in=1, d_hidden=256, n_layers=4, skip_in=[2], multires=6, bias=0.5, scale=1.0,
+                  geometric_init=False, weight_norm=True)
+
+
+def motion_case(fields):
+    """MotionNetwork (neus_fields.py:79-190): seeded weights, forward, relative
+    camera poses and world-to-camera chain, for the default config
+    (default.yaml:113-123) and for geometric_init=True."""
+    rec = {}
+    for tag, gi in (("", False), ("geo.", True)):
+        torch.manual_seed(681)
+        m = fields.MotionNetwork(**dict(MOTION_CFG, geometric_init=gi))
+        for k, v in m.state_dict().items():
+            rec[tag + "sd." + k] = v.detach().numpy()
+        t = torch.linspace(-1.0, 1.0, 9).view(-1, 1)
+        w, v = m(t)
+        rec[tag + "t"] = t.numpy()
+        rec[tag + "omega"] = w.detach().numpy()
+        rec[tag + "vel"] = v.detach().numpy()
+        dt, rel = m.compute_relative_camera_pose(target_cam_idx=2, final_ref_cam_idx=5, total_nb_images=10,
+                                                 nb_sample_timestep=10)
+        rec[tag + "dt"] = np.float32(dt)
+        rec[tag + "rel"] = torch.stack(rel).detach().numpy()
+        rec[tag + "w2c"] = m.compute_w2c_mappings(rel).detach().numpy()
+    np.savez_compressed(os.path.join(OUT, "motion.npz"), **rec)
+    print("wrote motion")
+
+
 def main():
     fields, rend = load_reference()
+    motion_case(fields)
     torch.set_num_threads(8)
     render_case(fields, rend, "render_small_train", seed=678, R=16, dh_sdf=64, dh_col=64, eval_mode=False,
                 car=0.5, full_grads=True)
@@ -247,5 +276,10 @@ def main():
     seams_case(fields, rend)
 
 
+def main_motion_only():
+    fields, _ = load_reference()
+    motion_case(fields)
+
+
 if __name__ == "__main__":
-    main()
+    main_motion_only() if "--motion-only" in sys.argv else main()
