@@ -97,41 +97,71 @@ def cpu_baseline(rays=256, steps=2):
                       f"torch {torch.__version__} CPU, {threads} threads, {dt:.1f} s"}
 
 
+CONFIGS = {
+    # name: (rays per GPU, trainer kwargs, workload text)
+    "c2": (4096, {}, "C2: synthetic scene, 4096 rays x 128 samples (64 coarse + 4x16 importance) per GPU, fp32, "
+                     "fixed poses, full train step (fwd + losses + bwd + Adam)"),
+    "c3": (4096, {"joint_pose": True, "stage1": True},
+           "C3-style: synthetic scene, 4096 rays x 128 samples per GPU, fp32 MFMA, joint pose optimisation "
+           "(learnable SE(3) poses -> ray gradients) + stage-1 scene-flow and SDF-consistency losses"),
+    "c4": (8192, {}, "C4: synthetic scene, 8192 rays x 128 samples per GPU, fp32, fixed poses, data-parallel"),
+    "c5": (4096, {"ren_cfg": dict(n_samples=64, n_importance=128, n_outside=0, up_sample_steps=4, perturb=1.0,
+                                  n_max_network_queries=64000, importance_sampling_start=0, naive_render=False),
+                  "graph": True},
+           "C5: synthetic scene, 4096 rays x 192 samples (coarse 64 + fine 4x32), fp32, HIP-graph-captured step"),
+}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rays", type=int, default=RAYS)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c2")
+    ap.add_argument("--rays", type=int, default=None, help="rays per GPU (default: the config's)")
+    ap.add_argument("--graph", action="store_true", help="replay the step from a captured HIP graph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    rays_cfg, kw, workload = CONFIGS[args.config]
+    kw = dict(kw)
+    graph = kw.pop("graph", False) or args.graph
+    rays = args.rays or rays_cfg
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    distributed = world > 1
+    # COPENERF_FORCE_DIST=1 runs the RCCL path (process group + flat all-reduce) even at one rank
+    distributed = world > 1 or os.environ.get("COPENERF_FORCE_DIST") == "1"
     torch.cuda.set_device(local)
     if distributed:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank, world_size=world)
+    if graph and distributed:
+        raise SystemExit("--graph captures the single-GPU step; the data-parallel all-reduce stays eager")
 
     from copenerf import ops
-    from copenerf.train_step import SyntheticTrainer
-    tr = SyntheticTrainer(f"cuda:{local}", rays=args.rays, distributed=distributed)
+    from copenerf.train_step import GraphedTrainer, SyntheticTrainer
+    tr = SyntheticTrainer(f"cuda:{local}", rays=rays, distributed=distributed, capturable=graph, **kw)
+    step = tr.step
+    if graph:
+        g = GraphedTrainer(tr, warmup=max(1, args.warmup))
+        step = g.step
 
     for _ in range(args.warmup):
-        tr.step()
+        step()
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
 
-    timer = ops.KernelTimer()
+    timer = None if graph else ops.KernelTimer()
     ops.set_kernel_timer(timer)
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = tr.step()
+        loss = step()
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
@@ -144,19 +174,13 @@ def main():
     if not torch.isfinite(loss).item():
         raise RuntimeError("non-finite loss in the timed steps")
 
-    agg = timer.summary()
-    # dominant single-kernel launch class (a cn_wgrad call is two kernels: the
-    # split-M MFMA kernel and its fixed-order slab reduction)
-    dom_key = max((k for k in agg if k[0] == "linear"), key=lambda k: agg[k]["ms"])
-    dom = agg[dom_key]
-    avg_ms = dom["ms"] / dom["launches"]
-    achieved = dom["flops"] / dom["launches"] / (avg_ms * 1e-3) / 1e12
-    symbol = kernel_symbol(dom_key)
-    traffic, traffic_src = pmc_traffic(symbol)
-    kernels_ms = sum(a["ms"] for a in agg.values()) / args.steps
-    rays_total = args.rays * world * args.steps
+    rays_total = rays * world * args.steps
+    S = 192 if args.config == "c5" else SAMPLES
+    metric = "rays/sec (train step incl. backward) at 4096 rays × 128 samples"
+    if args.config != "c2" or rays != RAYS:
+        metric = f"rays/sec (train step incl. backward) at {rays} rays × {S} samples ({args.config})"
     result = {
-        "metric": "rays/sec (train step incl. backward) at 4096 rays × 128 samples",
+        "metric": metric,
         "value": round(rays_total / elapsed, 1),
         "unit": "rays/s",
         "n_gpus": world,
@@ -167,31 +191,50 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": "synthetic (random 540x960 image, 4x4 patches, fixed identity pose, geometric-init SDF, seed 678)",
-        "config": {"workload": "C2: synthetic scene, 4096 rays x 128 samples (64 coarse + 4x16 importance) per GPU, "
-                               "fp32, fixed poses, full train step (fwd + losses + bwd + Adam)",
-                   "rays_per_gpu": args.rays, "samples_per_ray": SAMPLES, "global_rays": args.rays * world,
+        "data": "synthetic (random 540x960 image, 4x4 patches, " +
+                ("learnable SE(3) poses" if kw.get("joint_pose") else "fixed identity pose") +
+                ", geometric-init SDF, seed 678)",
+        "config": {"workload": workload, "rays_per_gpu": rays, "samples_per_ray": S,
+                   "global_rays": rays * world, "hip_graph": graph,
                    "parallelism": f"dp{world}" if world > 1 else "single"},
-        "roofline": {"bound": "mfma", "kernel": symbol, "achieved": round(achieved, 2),
-                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-                     "traffic": traffic, "traffic_source": traffic_src,
-                     "launches_per_step": dom["launches"] / args.steps, "avg_launch_ms": round(avg_ms, 4),
-                     "algorithmic_gflop_per_launch": round(dom["flops"] / dom["launches"] / 1e9, 3)},
-        "effective_ref_tflops": round(rays_total / elapsed * GFLOP_PER_RAY_REF / 1e3, 2),
-        "gemm_ms_per_step": round(kernels_ms, 3),
-        "gemm_tflops_avg": round(sum(a["flops"] for a in agg.values()) / sum(a["ms"] for a in agg.values()) / 1e9, 2),
-        "roofline_by_class": {"/".join(map(str, k)): round(v["flops"] / v["ms"] / 1e9, 1) for k, v in
-                              sorted(agg.items(), key=lambda kv: -kv[1]["ms"])},
-        "kernel_breakdown_ms_per_step": {"/".join(map(str, k)): round(v["ms"] / args.steps, 3) for k, v in
-                                         sorted(agg.items(), key=lambda kv: -kv[1]["ms"])},
+        "roofline": None,
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if timer is not None:
+        result.update(roofline_fields(timer, args.steps, rays_total / elapsed))
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
         result["cpu_baseline"] = cpu_baseline()
     if rank == 0:
         print(json.dumps(result), flush=True)
     if distributed:
         dist.destroy_process_group()
+
+
+def roofline_fields(timer, steps, rays_per_s):
+    agg = timer.summary()
+    # dominant single-kernel launch class (a cn_wgrad call is two kernels: the
+    # split-M MFMA kernel and its fixed-order slab reduction)
+    dom_key = max((k for k in agg if k[0] == "linear"), key=lambda k: agg[k]["ms"])
+    dom = agg[dom_key]
+    avg_ms = dom["ms"] / dom["launches"]
+    achieved = dom["flops"] / dom["launches"] / (avg_ms * 1e-3) / 1e12
+    symbol = kernel_symbol(dom_key)
+    traffic, traffic_src = pmc_traffic(symbol)
+    kernels_ms = sum(a["ms"] for a in agg.values()) / steps
+    return {
+        "roofline": {"bound": "mfma", "kernel": symbol, "achieved": round(achieved, 2),
+                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "launches_per_step": dom["launches"] / steps, "avg_launch_ms": round(avg_ms, 4),
+                     "algorithmic_gflop_per_launch": round(dom["flops"] / dom["launches"] / 1e9, 3)},
+        "effective_ref_tflops": round(rays_per_s * GFLOP_PER_RAY_REF / 1e3, 2),
+        "gemm_ms_per_step": round(kernels_ms, 3),
+        "gemm_tflops_avg": round(sum(a["flops"] for a in agg.values()) / sum(a["ms"] for a in agg.values()) / 1e9, 2),
+        "roofline_by_class": {"/".join(map(str, k)): round(v["flops"] / v["ms"] / 1e9, 1) for k, v in
+                              sorted(agg.items(), key=lambda kv: -kv[1]["ms"])},
+        "kernel_breakdown_ms_per_step": {"/".join(map(str, k)): round(v["ms"] / steps, 3) for k, v in
+                                         sorted(agg.items(), key=lambda kv: -kv[1]["ms"])},
+    }
 
 
 if __name__ == "__main__":

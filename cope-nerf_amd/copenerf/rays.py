@@ -46,9 +46,33 @@ def intrinsics_ndc(fx, fy, w, h, device="cpu"):
                         dtype=torch.float32, device=device)
 
 
+def inv4x4(m):
+    """Inverse of a 4x4 matrix by cofactors (adjugate / determinant).  Pure
+    elementwise device ops, differentiable and HIP-graph capturable (the LAPACK
+    path behind torch.inverse is not); agrees with it to fp32 rounding for the
+    well-conditioned camera / pose matrices on this path."""
+    a = m.reshape(16)
+    a0, a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11, a12, a13, a14, a15 = a.unbind(0)
+    s0, s1, s2 = a0 * a5 - a4 * a1, a0 * a6 - a4 * a2, a0 * a7 - a4 * a3
+    s3, s4, s5 = a1 * a6 - a5 * a2, a1 * a7 - a5 * a3, a2 * a7 - a6 * a3
+    c5, c4, c3 = a10 * a15 - a14 * a11, a9 * a15 - a13 * a11, a9 * a14 - a13 * a10
+    c2, c1, c0 = a8 * a15 - a12 * a11, a8 * a14 - a12 * a10, a8 * a13 - a12 * a9
+    det = s0 * c5 - s1 * c4 + s2 * c3 + s3 * c2 - s4 * c1 + s5 * c0
+    inv = torch.stack([
+        a5 * c5 - a6 * c4 + a7 * c3, -a1 * c5 + a2 * c4 - a3 * c3, a13 * s5 - a14 * s4 + a15 * s3,
+        -a9 * s5 + a10 * s4 - a11 * s3,
+        -a4 * c5 + a6 * c2 - a7 * c1, a0 * c5 - a2 * c2 + a3 * c1, -a12 * s5 + a14 * s2 - a15 * s1,
+        a8 * s5 - a10 * s2 + a11 * s1,
+        a4 * c4 - a5 * c2 + a7 * c0, -a0 * c4 + a1 * c2 - a3 * c0, a12 * s4 - a13 * s2 + a15 * s0,
+        -a8 * s4 + a9 * s2 - a11 * s0,
+        -a4 * c3 + a5 * c1 - a6 * c0, a0 * c3 - a1 * c1 + a2 * c0, -a12 * s3 + a13 * s1 - a14 * s0,
+        a8 * s3 - a9 * s1 + a10 * s0]) / det
+    return inv.reshape(4, 4)
+
+
 def world_rays(pixels_norm, camera_mat, world_mat, scale_mat):
     """rays_o [R,3], unit rays_d [R,3], |p - o| [R,1] (training.py:474-487)."""
-    inv = torch.inverse(scale_mat) @ torch.inverse(world_mat) @ torch.inverse(camera_mat)  # [4,4]
+    inv = inv4x4(scale_mat) @ inv4x4(world_mat) @ inv4x4(camera_mat)  # [4,4]
     o = inv[:3, 3]
     R = pixels_norm.shape[0]
     ph = torch.cat([pixels_norm, torch.ones(R, 2, device=pixels_norm.device)], -1)  # [x, y, 1, 1]

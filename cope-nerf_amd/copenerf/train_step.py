@@ -27,7 +27,7 @@ import torch.distributed as dist
 from .fields import RenderingNetwork, SDFNetwork, SingleVarianceNetwork
 from .losses import EdgePreservingSmoothnessLoss, SmoothnessLoss, eikonal_loss, rgb_l1
 from .motion import MotionNetwork, scene_flow_loss, world_points
-from .rays import (PoseRetriever, get_patch_indices, intrinsics_ndc, near_far_from_sphere, pixels_from_indices,
+from .rays import (PoseRetriever, get_patch_indices, inv4x4, intrinsics_ndc, near_far_from_sphere, pixels_from_indices,
                    world_rays)
 from .renderer import NeuSRenderer
 
@@ -61,7 +61,8 @@ class SyntheticTrainer:
     def __init__(self, device, rays=4096, H=540, W=960, patch=4, seed=678, depth_range=(0.01, 5.0),
                  cos_anneal_ratio=0.5, lr=1e-3, weights=dict(rgb=1.0, eikonal=0.1, edge=1.0, smooth=1e-4),
                  distributed=False, sdf_cfg=None, col_cfg=None, ren_cfg=None, joint_pose=False, stage1=False,
-                 n_images=10, nb_sample_timestep=10, sdf_weight=0.1, sdf_consistency_weight=1.0):
+                 n_images=10, nb_sample_timestep=10, sdf_weight=0.1, sdf_consistency_weight=1.0,
+                 capturable=False):
         self.device = torch.device(device)
         self.R, self.H, self.W, self.patch = rays, H, W, patch
         self.depth_range = depth_range
@@ -89,7 +90,7 @@ class SyntheticTrainer:
             self.motion = MotionNetwork(**MOTION_CFG).to(self.device)
             groups.append({"params": list(self.motion.parameters()), "lr": 5e-4})
         self.all_params = [p for g in groups for p in g["params"]]
-        self.opt = torch.optim.Adam(groups, lr=lr)
+        self.opt = torch.optim.Adam(groups, lr=lr, capturable=capturable)
         gen = torch.Generator(device=self.device).manual_seed(seed + (dist.get_rank() if distributed else 0))
         self.gen = gen
         self.image = torch.rand(3, H, W, device=self.device, generator=gen)
@@ -130,7 +131,7 @@ class SyntheticTrainer:
         l_sf = scene_flow_loss(pts, normals, out["sdf_flows"], out["weights"], omega, vel)
         _, rel = self.motion.compute_relative_camera_pose(0, img, self.n_images, self.nb_sample_timestep)
         c2c = self.motion.compute_w2c_mappings(rel)[-1]
-        pw = world_points(pts, torch.inverse(c2c))
+        pw = world_points(pts, inv4x4(c2c))
         t_world = torch.full((pw.shape[0], 1), -1.0, device=self.device)
         sdf_w = self.sdf.sdf(torch.cat([pw, t_world], 1))
         l_cons = torch.mean(torch.abs(sdf_w - out["sdf"]))
@@ -154,3 +155,44 @@ class SyntheticTrainer:
         self.opt.step()
         self.it += 1
         return loss
+
+
+class GraphedTrainer:
+    """The whole training step -- patch sampling and ray generation, the HIP
+    sampler / renderer forward, losses, the HIP backward and Adam -- captured
+    once into a HIP graph and replayed (config C5).
+
+    Everything on the step is stream-ordered device work on torch's current
+    stream with no host synchronisation: the library launches on the stream it
+    is given and allocates nothing, the RNG (patch corners, stratified jitter)
+    draws from generators registered with the graph so every replay advances
+    their Philox offsets, and Adam runs with capturable=True.  Buffers come from
+    the graph's private pool, so the replayed addresses are the captured ones.
+    Not supported with distributed=True (the all-reduce is left eager).  The
+    caller must not hold a loss (or any output) of an earlier eager step: a live
+    autograd graph keeps the leaves' AccumulateGrad nodes bound to the stream
+    they were created on, and capture then records work on two streams."""
+
+    def __init__(self, trainer: SyntheticTrainer, warmup: int = 3):
+        if trainer.distributed:
+            raise NotImplementedError("GraphedTrainer: capture the single-GPU step; DP all-reduce stays eager")
+        self.tr = trainer
+        s = torch.cuda.Stream(device=trainer.device)
+        s.wait_stream(torch.cuda.current_stream(trainer.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                trainer.step()  # result dropped: no autograd graph outlives its step
+        torch.cuda.current_stream(trainer.device).wait_stream(s)
+        torch.cuda.synchronize(trainer.device)
+        self.graph = torch.cuda.CUDAGraph()
+        reg = getattr(self.graph, "register_generator_state", None)
+        if reg is not None:
+            reg(trainer.gen)
+        trainer.opt.zero_grad(set_to_none=True)
+        with torch.cuda.graph(self.graph):
+            self.loss = trainer.step()
+
+    def step(self):
+        self.graph.replay()
+        self.tr.it += 1
+        return self.loss
