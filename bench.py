@@ -101,9 +101,14 @@ CONFIGS = {
     # name: (rays per GPU, trainer kwargs, workload text)
     "c2": (4096, {}, "C2: synthetic scene, 4096 rays x 128 samples (64 coarse + 4x16 importance) per GPU, fp32, "
                      "fixed poses, full train step (fwd + losses + bwd + Adam)"),
-    "c3": (4096, {"joint_pose": True, "stage1": True},
-           "C3-style: synthetic scene, 4096 rays x 128 samples per GPU, fp32 MFMA, joint pose optimisation "
-           "(learnable SE(3) poses -> ray gradients) + stage-1 scene-flow and SDF-consistency losses"),
+    "c3": (4096, {"joint_pose": True, "stage1": True, "mfma_dtype": "bf16"},
+           "C3-style: synthetic scene, 4096 rays x 128 samples per GPU, bf16 MLP MFMA (fp32 accumulate), joint "
+           "pose optimisation (learnable SE(3) poses -> ray gradients) + stage-1 scene-flow and SDF-consistency "
+           "losses"),
+    "c3fp32": (4096, {"joint_pose": True, "stage1": True},
+               "C3-style as c3 with exact fp32 MFMA"),
+    "c2bf16": (4096, {"mfma_dtype": "bf16"},
+               "C2 workload (4096 rays x 128 samples, fixed poses) with bf16 MLP MFMA (fp32 accumulate)"),
     "c4": (8192, {}, "C4: synthetic scene, 8192 rays x 128 samples per GPU, fp32, fixed poses, data-parallel"),
     "c5": (4096, {"ren_cfg": dict(n_samples=64, n_importance=128, n_outside=0, up_sample_steps=4, perturb=1.0,
                                   n_max_network_queries=64000, importance_sampling_start=0, naive_render=False),
@@ -190,7 +195,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": "bf16 MFMA operands, fp32 accumulate/activations" if kw.get("mfma_dtype") == "bf16" else "fp32",
         "data": "synthetic (random 540x960 image, 4x4 patches, " +
                 ("learnable SE(3) poses" if kw.get("joint_pose") else "fixed identity pose") +
                 ", geometric-init SDF, seed 678)",

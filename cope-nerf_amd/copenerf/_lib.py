@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libcopenerf.so"
 LIB_PATH = os.environ.get("COPENERF_LIB", os.path.join(_HERE, LIB_NAME))
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 c_f32p = ctypes.c_void_p  # device pointers are passed as integers
 c_i32 = ctypes.c_int32
@@ -43,6 +43,7 @@ class LinearDesc(ctypes.Structure):
         ("M", c_i32), ("N", c_i32), ("K", c_i32), ("K1", c_i32),
         ("nzero", c_i32), ("nsplit", c_i32), ("epilogue", c_i32), ("tile", c_i32),
         ("adiv", c_f32), ("odiv", c_f32), ("beta", c_f32), ("threshold", c_f32),
+        ("mfma_dtype", c_i32), ("reserved_", c_i32),
     ]
 
 

@@ -78,15 +78,20 @@ class SDFPack:
     bf8: torch.Tensor
 
 
-def pack_sdf(lay: SDFLayout, Ws, bs) -> SDFPack:
+def pack_sdf(lay: SDFLayout, Ws, bs, mfma_dtype: str = "fp32") -> SDFPack:
+    """Zero-padded GEMM images of the effective weights.  mfma_dtype "bf16": the
+    B images are bfloat16 with K padded to 64 (cn_linear's bf16 MFMA path)."""
+    bf = mfma_dtype == "bf16"
+    kq = 64 if bf else 32
+    cv = (lambda t: t.to(torch.bfloat16).contiguous()) if bf else (lambda t: t.contiguous())  # noqa: E731
     with torch.no_grad():
         Bf, Bt, b = [], [], []
         for l in range(lay.n_lin - 1):
             W = Ws[l].detach()
             o, i = W.shape
-            kp = lay.KE if l == 0 else rup(i, 32)
-            Bf.append(F.pad(W, (0, kp - i, 0, rup(o, 128) - o)).contiguous())
-            Bt.append(F.pad(W.t(), (0, rup(o, 32) - o, 0, rup(i, 128) - i)).contiguous())
+            kp = lay.KE if l == 0 else rup(i, kq)
+            Bf.append(cv(F.pad(W, (0, kp - i, 0, rup(o, 128) - o))))
+            Bt.append(cv(F.pad(W.t(), (0, rup(o, kq) - o, 0, rup(i, 128) - i))))
             b.append(bs[l].detach().contiguous())
         W8, b8 = Ws[-1].detach(), bs[-1].detach()
         s = float(lay.scale)
@@ -95,8 +100,8 @@ def pack_sdf(lay: SDFLayout, Ws, bs) -> SDFPack:
         w80p = F.pad(w80, (0, lay.HL - w80.shape[0])).contiguous()
         Wf = W8[1:]
         o, i = Wf.shape
-        Bf8 = F.pad(Wf, (0, rup(i, 32) - i, 0, rup(o, 128) - o)).contiguous()
-        Bt8 = F.pad(Wf.t(), (0, rup(o, 32) - o, 0, rup(i, 128) - i)).contiguous()
+        Bf8 = cv(F.pad(Wf, (0, rup(i, kq) - i, 0, rup(o, 128) - o)))
+        Bt8 = cv(F.pad(Wf.t(), (0, rup(o, kq) - o, 0, rup(i, 128) - i)))
         return SDFPack(Bf, Bt, b, w80.contiguous()[None], b80.contiguous(), w80p, Bf8, Bt8, b8[1:].contiguous())
 
 
@@ -363,6 +368,7 @@ class SDFNetwork(nn.Module):
             setattr(self, "lin" + str(l), lin)
         self.activation = nn.Softplus(beta=100)
         self._layout = None
+        self.mfma_dtype = "fp32"  # "bf16": bf16-operand MFMA GEMMs (config C3); not part of the state dict
 
     # -- kernel plumbing ---------------------------------------------------
     def layout(self) -> SDFLayout:
@@ -394,7 +400,7 @@ class SDFNetwork(nn.Module):
             lin = getattr(self, "lin" + str(l))
             Ws.append(effective_weight(lin))
             bs.append(lin.bias)
-        return Ws, bs, pack_sdf(lay, Ws, bs)
+        return Ws, bs, pack_sdf(lay, Ws, bs, self.mfma_dtype)
 
     def field(self, x, *, want_feat=True, want_grad=True, packed=None):
         """Fused (sdf, feature, ∇ₓsdf) of the points x [M, 4] in one launch sequence."""
@@ -450,7 +456,10 @@ class ColorPack:
     Bxt: torch.Tensor  # [64][Hpad]: extras columns [g | pts | emb(dirs)] of lin0, transposed (ray gradients)
 
 
-def pack_color(lay: ColorLayout, Ws, bs) -> ColorPack:
+def pack_color(lay: ColorLayout, Ws, bs, mfma_dtype: str = "fp32") -> ColorPack:
+    bf = mfma_dtype == "bf16"
+    kq = 64 if bf else 32
+    cv = (lambda t: t.to(torch.bfloat16).contiguous()) if bf else (lambda t: t.contiguous())  # noqa: E731
     with torch.no_grad():
         P, V, Gd, Fd = lay.P, lay.V, lay.Gd, lay.F
         W0 = Ws[0].detach()
@@ -458,18 +467,18 @@ def pack_color(lay: ColorLayout, Ws, bs) -> ColorPack:
         pts, emb, g, feat = (W0[:, 0:P], W0[:, P:P + V], W0[:, P + V:P + V + Gd], W0[:, P + V + Gd:])
         ext = torch.cat([g, pts, emb], 1)
         W0k = torch.cat([feat, F.pad(ext, (0, lay.KX - ext.shape[1]))], 1)
-        Bf = [F.pad(W0k, (0, 0, 0, rup(o, 128) - o)).contiguous()]
+        Bf = [cv(F.pad(W0k, (0, 0, 0, rup(o, 128) - o)))]
         Bt = [None]
         b = [bs[0].detach().contiguous()]
         for l in range(1, lay.n_lin - 1):
             W = Ws[l].detach()
             oo, ii = W.shape
-            Bf.append(F.pad(W, (0, rup(ii, 32) - ii, 0, rup(oo, 128) - oo)).contiguous())
-            Bt.append(F.pad(W.t(), (0, rup(oo, 32) - oo, 0, rup(ii, 128) - ii)).contiguous())
+            Bf.append(cv(F.pad(W, (0, rup(ii, kq) - ii, 0, rup(oo, 128) - oo))))
+            Bt.append(cv(F.pad(W.t(), (0, rup(oo, kq) - oo, 0, rup(ii, 128) - ii))))
             b.append(bs[l].detach().contiguous())
-        Btf = F.pad(feat.t(), (0, rup(o, 32) - o, 0, rup(Fd, 128) - Fd)).contiguous()
+        Btf = cv(F.pad(feat.t(), (0, rup(o, kq) - o, 0, rup(Fd, 128) - Fd)))
         Wg = g.t().contiguous()
-        Bxt = F.pad(ext.t(), (0, rup(o, 32) - o, 0, 64 - ext.shape[1])).contiguous()
+        Bxt = cv(F.pad(ext.t(), (0, rup(o, kq) - o, 0, 64 - ext.shape[1])))
         return ColorPack(Bf, Bt, b, Ws[-1].detach().contiguous(), bs[-1].detach().contiguous(), Btf, Wg, Bxt)
 
 
@@ -581,6 +590,7 @@ class RenderingNetwork(nn.Module):
             setattr(self, "lin" + str(l), lin)
         self.relu = nn.ReLU()
         self._layout = None
+        self.mfma_dtype = "fp32"  # see SDFNetwork.mfma_dtype
 
     def layout(self) -> ColorLayout:
         if self._layout is None:
@@ -611,7 +621,7 @@ class RenderingNetwork(nn.Module):
             lin = getattr(self, "lin" + str(l))
             Ws.append(effective_weight(lin))
             bs.append(lin.bias)
-        return Ws, bs, pack_color(lay, Ws, bs)
+        return Ws, bs, pack_color(lay, Ws, bs, self.mfma_dtype)
 
     def color(self, points, normals, dirs, dir_div, feature_vectors, packed=None):
         """rgb [M,3]; dirs is [M/dir_div, 3] (one row per ray when dir_div = S)."""

@@ -75,7 +75,7 @@ def _need(t, name, *, ndim=2):
     if not t.is_cuda:
         raise RuntimeError(f"copenerf: {name} must be a CUDA/HIP tensor (got {t.device}); "
                            "the HIP kernels have no CPU fallback")
-    if t.dtype != torch.float32 and t.dtype != torch.int32:
+    if t.dtype not in (torch.float32, torch.int32, torch.bfloat16):
         raise RuntimeError(f"copenerf: {name} must be float32 (got {t.dtype})")
     if ndim == 2 and (t.dim() != 2 or t.stride(1) != 1):
         raise RuntimeError(f"copenerf: {name} must be a row-major 2-D tensor (shape {tuple(t.shape)}, "
@@ -90,10 +90,20 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
            aux1=None, out1=None, out_split=None, nsplit=None, nzero=None, adiv=1.0, odiv=1.0, beta=100.0,
            threshold=20.0, tile=None, M=None, kalg=None):
     """out = epilogue((A|A2) @ B[:N].T / adiv) -- cn_linear.  kalg: the unpadded
-    inner dimension (for the FLOP count of the kernel timer only)."""
+    inner dimension (for the FLOP count of the kernel timer only).  A bfloat16 B
+    selects the bf16 MFMA path (A rounded to bf16 on load, fp32 accumulate); K is
+    then rounded up to 64, so A's columns up to that must exist (zero padding)."""
     for t, n in ((A, "A"), (A2, "A2"), (B, "B"), (out0, "out0"), (out1, "out1"), (aux0, "aux0"),
                  (aux1, "aux1"), (out_split, "out_split")):
         _need(t, n)
+        if t is not None and t is not B and t.dtype == torch.bfloat16:
+            raise RuntimeError(f"cn_linear: {n} must be float32 (only B may be bfloat16)")
+    bf = B.dtype == torch.bfloat16
+    if bf:
+        K = rup(K, 64)
+        K1 = rup(K1, 64) if K1 is not None else None
+        if (A.stride(0) < (K1 or K)) or (A2 is not None and A2.stride(0) < K - K1):
+            raise RuntimeError(f"cn_linear (bf16): A rows too short for K={K}")
     M = A.shape[0] if M is None else M
     # the epilogue reads bias / colv as float4
     bias = bias if bias is None or bias.data_ptr() % 16 == 0 else bias.clone()
@@ -117,10 +127,11 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     d.nsplit = nsplit if nsplit is not None else N
     d.epilogue, d.tile = epilogue, tile
     d.adiv, d.odiv, d.beta, d.threshold = adiv, odiv, beta, threshold
+    d.mfma_dtype = 1 if bf else 0
     if _timer is not None:
         e0 = _timer.start()
         _lib.check(_lib.load().cn_linear(d, _stream()), "cn_linear")
-        key = ("linear", tile, EPI_NAMES[epilogue])
+        key = ("linear", tile, EPI_NAMES[epilogue]) + (("bf16",) if bf else ())
         _timer.stop(key + ((M, N, K),) if _timer.detail else key, e0, 2.0 * M * N * (kalg or K))
     else:
         _lib.check(_lib.load().cn_linear(d, _stream()), "cn_linear")

@@ -108,6 +108,17 @@ class NeuSRenderer(nn.Module):
         if naive_render:
             raise NotImplementedError("naive_render (logistic up-sampler) is out of scope; every config uses False")
 
+    def set_mfma_dtype(self, dtype: str):
+        """"fp32" (default: exact fp32 MFMA products, the |Δ| <= 1e-4 parity path) or
+        "bf16" (config C3, "bf16 MLP MFMA": every MLP GEMM rounds its operands to
+        bf16 and accumulates in fp32; activations, epilogues, sampling and
+        compositing stay fp32)."""
+        if dtype not in ("fp32", "bf16"):
+            raise ValueError(f"mfma dtype {dtype!r}")
+        self.sdf_network.mfma_dtype = dtype
+        self.color_network.mfma_dtype = dtype
+        return self
+
     # -- sampling ------------------------------------------------------------
     @torch.no_grad()
     def sample_z(self, rays_o, rays_d, time_step, near, far, n_samples, n_importance, t_rand, sdf_packed):

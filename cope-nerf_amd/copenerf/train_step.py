@@ -62,7 +62,7 @@ class SyntheticTrainer:
                  cos_anneal_ratio=0.5, lr=1e-3, weights=dict(rgb=1.0, eikonal=0.1, edge=1.0, smooth=1e-4),
                  distributed=False, sdf_cfg=None, col_cfg=None, ren_cfg=None, joint_pose=False, stage1=False,
                  n_images=10, nb_sample_timestep=10, sdf_weight=0.1, sdf_consistency_weight=1.0,
-                 capturable=False):
+                 capturable=False, mfma_dtype="fp32"):
         self.device = torch.device(device)
         self.R, self.H, self.W, self.patch = rays, H, W, patch
         self.depth_range = depth_range
@@ -74,6 +74,7 @@ class SyntheticTrainer:
         self.col = RenderingNetwork(**(col_cfg or COL_CFG)).to(self.device)
         self.var = SingleVarianceNetwork(0.3).to(self.device)
         self.renderer = NeuSRenderer(None, self.sdf, self.var, self.col, None, **(ren_cfg or REN_CFG)).to(self.device)
+        self.renderer.set_mfma_dtype(mfma_dtype)
         self.params = list(self.sdf.parameters()) + list(self.var.parameters()) + list(self.col.parameters())
         self.joint_pose, self.stage1 = joint_pose, stage1
         self.n_images, self.nb_sample_timestep = n_images, nb_sample_timestep

@@ -43,6 +43,8 @@ struct LinearArgs {
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
 // Buffer views: every global access of the GEMM goes through a buffer resource
@@ -112,18 +114,27 @@ __device__ __forceinline__ void tile_coords(int vt, int T, int& tm, int& tn) {
 // virtual tiles; the first K-chunk of the next tile is fetched into registers
 // while the current tile's epilogue runs, so only the first tile of a
 // workgroup pays the cold-start latency.
-template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int EPI, bool ROWV>
+// BF = false: A and B fp32, v_mfma_f32_32x32x2_f32, BK fp32 k per chunk.
+// BF = true : A fp32 converted to bf16 (RNE) while staging, B bf16 [N][ldb]
+//             (ldb in bf16 elements), v_mfma_f32_32x32x16_bf16, BK = 64 bf16 k per
+//             chunk.  The LDS image has the same geometry in both modes (rows of
+//             36 dwords: conflict-free ds_read_b128 fragments) and the accumulator
+//             layout of the two MFMAs is the same, so the epilogue is shared.
+template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int EPI, bool ROWV, bool BF>
 __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel(LinearArgs p) {
     constexpr int NT = 64 * WM * WN;
     constexpr int BM = 32 * TM * WM;
     constexpr int BN = 32 * TN * WN;
-    constexpr int LS = BK + 4;  // padded LDS row (floats): conflict-free ds_read_b128 for BK = 16, 32
-    constexpr int KC4 = BK / 4; // float4 per staged row
+    constexpr int LS = (BF ? BK / 2 : BK) + 4;  // padded LDS row in dwords: 36 for BK = 32 (f32) / 64 (bf16)
+    constexpr int KC4 = BK / 4;                  // A: fp32 float4 per staged row
     static_assert(NT % KC4 == 0, "staging rows");
-    constexpr int RSTEP = NT / KC4;  // staged rows per load instruction
-    static_assert(BM % RSTEP == 0 && BN % RSTEP == 0, "tile/thread mismatch");
+    constexpr int RSTEP = NT / KC4;  // staged A rows per load instruction
+    constexpr int KCB = BF ? BK / 8 : BK / 4;    // B: 16-byte pieces per staged row
+    constexpr int RSTEPB = NT / KCB;
+    static_assert(BM % RSTEP == 0 && BN % RSTEPB == 0, "tile/thread mismatch");
     constexpr int ALD = BM / RSTEP;
-    constexpr int BLD = BN / RSTEP;
+    constexpr int BLD = BN / RSTEPB;
+    constexpr int ESZB = BF ? 2 : 4;             // bytes per B element
     constexpr int CS = BN + 4;
     constexpr int LDS_FLOATS = 2 * (BM + BN) * LS;
     // the epilogue parks the C tile in the staging LDS, in NPART row slabs if it does not fit
@@ -144,8 +155,10 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     const int ntiles = ((p.n_tiles_m + 7) / 8) * 8 * T;
     const int nk = p.K / BK;
 
-    // staging: thread tid loads rows tid/KC4 + q*RSTEP, float4 column tid%KC4
+    // staging: thread tid loads A rows tid/KC4 + q*RSTEP (fp32 float4 column tid%KC4)
+    // and B rows tid/KCB + q*RSTEPB (16-byte piece tid%KCB)
     const int srow = tid / KC4, sc4 = tid % KC4;
+    const int srowb = tid / KCB, scb = tid % KCB;
     int voA[ALD], voA2[ALD], voB[BLD];  // byte offsets of the staged rows (range-checked)
 #pragma unroll
     for (int q = 0; q < ALD; ++q) {
@@ -153,8 +166,10 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         voA2[q] = ((srow + q * RSTEP) * p.lda2 + sc4 * 4) * 4;
     }
 #pragma unroll
-    for (int q = 0; q < BLD; ++q) voB[q] = ((srow + q * RSTEP) * p.ldb + sc4 * 4) * 4;
-    const int lds_st = srow * LS + sc4 * 4;
+    for (int q = 0; q < BLD; ++q) voB[q] = (srowb + q * RSTEPB) * p.ldb * ESZB + scb * 16;
+    // LDS write offsets in dwords: A as fp32 float4 (4 dwords) or bf16x4 (2 dwords); B 16-byte pieces
+    const int lds_a = srow * LS + sc4 * (BF ? 2 : 4);
+    const int lds_b = srowb * LS + scb * 4;
 
     floatx4 ra[DEPTH][ALD], rb[DEPTH][BLD];
     auto gload = [&](int set, int kc, int m0, int n0) {
@@ -169,17 +184,24 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 #pragma unroll
             for (int q = 0; q < ALD; ++q) ra[set][q] = bload4(rA, voA2[q], (k0 - p.K1) * 4);
         }
-        const rsrc_t rB = make_view(p.B + (int64_t)n0 * p.ldb, BN * p.ldb * 4);
+        const rsrc_t rB = make_view(reinterpret_cast<const float*>(reinterpret_cast<const char*>(p.B) +
+                                                                   (int64_t)n0 * p.ldb * ESZB),
+                                    BN * p.ldb * ESZB);
 #pragma unroll
-        for (int q = 0; q < BLD; ++q) rb[set][q] = bload4(rB, voB[q], k0 * 4);
+        for (int q = 0; q < BLD; ++q) rb[set][q] = bload4(rB, voB[q], k0 * ESZB);
     };
     auto lstore = [&](int set, int buf) {
-        float* a = sA + buf * BM * LS + lds_st;
-        float* b = sB + buf * BN * LS + lds_st;
+        float* a = sA + buf * BM * LS + lds_a;
+        float* b = sB + buf * BN * LS + lds_b;
 #pragma unroll
-        for (int q = 0; q < ALD; ++q) *reinterpret_cast<floatx4*>(a + q * RSTEP * LS) = ra[set][q];
+        for (int q = 0; q < ALD; ++q) {
+            if constexpr (BF)
+                *reinterpret_cast<bf16x4*>(a + q * RSTEP * LS) = __builtin_convertvector(ra[set][q], bf16x4);
+            else
+                *reinterpret_cast<floatx4*>(a + q * RSTEP * LS) = ra[set][q];
+        }
 #pragma unroll
-        for (int q = 0; q < BLD; ++q) *reinterpret_cast<floatx4*>(b + q * RSTEP * LS) = rb[set][q];
+        for (int q = 0; q < BLD; ++q) *reinterpret_cast<floatx4*>(b + q * RSTEPB * LS) = rb[set][q];
     };
     auto next_valid = [&](int vt) {
         for (; vt < ntiles; vt += gridDim.x) {
@@ -241,6 +263,27 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
         auto compute = [&](int cur) {
+            if constexpr (BF) {
+                // lane half h holds k = 8h + j of each 16-deep MFMA step (8 bf16 = 4 dwords)
+                const float* a_base = sA + cur * BM * LS + arow * LS + 4 * (lane >> 5);
+                const float* b_base = sB + cur * BN * LS + brow * LS + 4 * (lane >> 5);
+#pragma unroll
+                for (int ks = 0; ks < BK / 16; ++ks) {
+                    bf16x8 af[TM], bf[TN];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+                        af[i] = *reinterpret_cast<const bf16x8*>(a_base + i * 32 * LS + ks * 8);
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        bf[j] = *reinterpret_cast<const bf16x8*>(b_base + j * 32 * LS + ks * 8);
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+                }
+                return;
+            }
             const float* a_base = sA + cur * BM * LS + arow * LS + kofs;
             const float* b_base = sB + cur * BN * LS + brow * LS + kofs;
 #pragma unroll
@@ -795,7 +838,7 @@ static int g_linear_variant = [] {
     return e ? atoi(e) : 0;
 }();
 
-template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH>
+template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, bool BF = false>
 static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_t s) {
     constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
     a.n_tiles_m = cdiv(d->M, BM);
@@ -811,8 +854,8 @@ static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_
     switch (d->epilogue) {
 #define CN_EPI_CASE(E)                                                                     \
         case E:                                                                            \
-            if (d->rowv) linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, E, true><<<grid, block, 0, s>>>(a); \
-            else linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, E, false><<<grid, block, 0, s>>>(a);        \
+            if (d->rowv) linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, E, true, BF><<<grid, block, 0, s>>>(a); \
+            else linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, E, false, BF><<<grid, block, 0, s>>>(a);        \
             break;
         CN_EPI_CASE(CN_EPI_STORE)
         CN_EPI_CASE(CN_EPI_SOFTPLUS)
@@ -822,7 +865,7 @@ static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_
         CN_EPI_CASE(CN_EPI_BWD_SOFTPLUS)
         CN_EPI_CASE(CN_EPI_BWD_RELU)
 #undef CN_EPI_CASE
-        case 7: linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, 7, false><<<grid, block, 0, s>>>(a); break;
+        case 7: linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, 7, false, BF><<<grid, block, 0, s>>>(a); break;
         default: set_error("cn_linear: bad epilogue %d", d->epilogue); return CN_ERR_ARG;
     }
     return check_launch("cn_linear");
@@ -834,13 +877,16 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     CN_REQUIRE(d, CN_ERR_ARG, "cn_linear: null desc");
     CN_REQUIRE(d->A && d->B && d->out0, CN_ERR_ARG, "cn_linear: A, B and out0 are required");
     CN_REQUIRE(d->M >= 0 && d->N > 0 && d->K > 0, CN_ERR_SHAPE, "cn_linear: bad M/N/K %d/%d/%d", d->M, d->N, d->K);
-    CN_REQUIRE(d->K % 32 == 0, CN_ERR_SHAPE, "cn_linear: K=%d must be a multiple of 32", d->K);
+    CN_REQUIRE(d->mfma_dtype == CN_MFMA_F32 || d->mfma_dtype == CN_MFMA_BF16, CN_ERR_ARG,
+               "cn_linear: bad mfma_dtype %d", d->mfma_dtype);
+    const bool bf = d->mfma_dtype == CN_MFMA_BF16;
+    CN_REQUIRE(d->K % (bf ? 64 : 32) == 0, CN_ERR_SHAPE, "cn_linear: K=%d must be a multiple of %d", d->K, bf ? 64 : 32);
     CN_REQUIRE(d->tile == 0 || d->tile == 1, CN_ERR_ARG, "cn_linear: bad tile %d", d->tile);
     const int K1 = d->A2 ? d->K1 : d->K;
-    CN_REQUIRE(K1 > 0 && K1 <= d->K && K1 % 32 == 0, CN_ERR_SHAPE, "cn_linear: bad K1=%d", K1);
+    CN_REQUIRE(K1 > 0 && K1 <= d->K && K1 % (bf ? 64 : 32) == 0, CN_ERR_SHAPE, "cn_linear: bad K1=%d", K1);
     CN_REQUIRE(d->lda >= K1 && d->lda % 4 == 0 && al16(d->A), CN_ERR_ALIGN, "cn_linear: A must be 16B aligned with lda>=K1, lda%%4==0");
     if (d->A2) CN_REQUIRE(d->lda2 >= d->K - K1 && d->lda2 % 4 == 0 && al16(d->A2), CN_ERR_ALIGN, "cn_linear: bad A2/lda2");
-    CN_REQUIRE(d->ldb >= d->K && d->ldb % 4 == 0 && al16(d->B), CN_ERR_ALIGN, "cn_linear: bad B/ldb");
+    CN_REQUIRE(d->ldb >= d->K && d->ldb % (bf ? 8 : 4) == 0 && al16(d->B), CN_ERR_ALIGN, "cn_linear: bad B/ldb");
     const int nzero = std::max(d->nzero, d->N);
     const int bn = d->tile == 0 ? 128 : 64;
     CN_REQUIRE(nzero <= cdiv(d->N, bn) * bn, CN_ERR_SHAPE,
@@ -888,6 +934,10 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     a.beta = d->beta;
     a.threshold = d->threshold;
     hipStream_t s = (hipStream_t)stream;
+    if (bf) {
+        if (d->tile == 0) return launch_linear_tile<2, 2, 2, 2, 64, 2, 1, true>(d, a, s);
+        return launch_linear_tile<4, 1, 1, 2, 64, 2, 1, true>(d, a, s);
+    }
     const bool even = (d->K % 64) == 0;  // DEPTH-2 prefetch consumes K in pairs of 32-chunks
     if (d->tile == 0) {
         if (g_linear_variant == 2) return launch_linear_tile<2, 2, 2, 2, 16, 3, 2>(d, a, s);

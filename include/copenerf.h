@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define CN_ABI_VERSION 2
+#define CN_ABI_VERSION 3
 
 typedef void* cn_stream_t; /* hipStream_t */
 
@@ -85,10 +85,17 @@ typedef struct cn_linear_desc {
     int32_t nzero, nsplit;
     int32_t epilogue;    /* cn_epilogue */
     int32_t tile;        /* 0: 128x128 block tile, 1: 128x64 */
-    float adiv, odiv;    /* divisors applied to A·Bᵀ and to the activation (0 means 1);
-                            divisions, not reciprocals, to round like torch's x / sqrt(2) */
+    float adiv, odiv;    /* divisors applied to A·Bᵀ and to the activation (0 means 1),
+                            applied as multiplies by their fp32 reciprocals */
     float beta, threshold; /* Softplus(beta, threshold) of neus_fields.py:266 */
+    int32_t mfma_dtype;  /* CN_MFMA_F32: A, B fp32, exact fp32 products (v_mfma_f32_32x32x2_f32);
+                            CN_MFMA_BF16: A fp32 rounded to bf16 (RNE) on load, B bf16 [N][ldb]
+                            (ldb in bf16 elements), fp32 accumulate (v_mfma_f32_32x32x16_bf16);
+                            K and K1 multiples of 64 (config C3's bf16 MLP MFMA) */
+    int32_t reserved_;
 } cn_linear_desc;
+
+enum cn_mfma_dtype { CN_MFMA_F32 = 0, CN_MFMA_BF16 = 1 };
 
 int cn_linear(const cn_linear_desc* d, cn_stream_t stream);
 

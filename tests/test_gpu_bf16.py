@@ -1,0 +1,101 @@
+"""bf16 MFMA mode (config C3, "bf16 MLP MFMA"): cn_linear with mfma_dtype
+CN_MFMA_BF16 against torch with the same operand rounding (A and B rounded to
+bf16 RNE, products and sums in double), every epilogue, both tiles, the
+virtual concat; and the renderer in bf16 mode against the fp32 oracle with the
+bf16 tolerance of DESIGN.md §4 (the fp32 path keeps the 1e-4 bar)."""
+import pytest
+import torch
+
+from helpers import REN_CFG, build_modules, oracle_params
+from oracle import neus_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rnd(*s, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return ((torch.rand(*s, generator=g) * 2 - 1) * scale).to(DEV)
+
+
+def _ref(A, Bb, N):
+    """(A rounded to bf16) @ B^T in double: the exact result the bf16 MFMA path rounds once per sum."""
+    return A.bfloat16().double() @ Bb[:N].double().t()
+
+
+@pytest.mark.parametrize("M,N,K,tile", [(1000, 256, 256, 0), (130, 204, 256, 0), (777, 52, 256, 1),
+                                        (64, 256, 64, 0), (4096, 128, 192, 0)])
+def test_linear_bf16_store(M, N, K, tile):
+    from copenerf import ops
+    A = _rnd(M, K, seed=1)
+    bn = 64 if tile else 128
+    B = torch.zeros(ops.rup(N, bn), K, device=DEV)
+    B[:N] = _rnd(N, K, seed=2, scale=0.1)
+    Bb = B.bfloat16().contiguous()
+    bias = _rnd(N, seed=3)
+    ld = ops.rup(N, bn)
+    out = torch.full((M, ld), float("nan"), device=DEV)
+    ops.linear(A, Bb, N, K, out, ops.EPI_STORE, bias=bias, nzero=ld, tile=tile)
+    ref = (_ref(A, Bb, N) + bias.double()).float()
+    torch.testing.assert_close(out[:, :N], ref, rtol=1e-5, atol=1e-5)
+    assert torch.all(out[:, N:] == 0)
+
+
+def test_linear_bf16_epilogues_and_concat():
+    from copenerf import ops
+    M, K1, K2, N = 517, 256, 64, 256
+    A, A2 = _rnd(M, K1, seed=4, scale=0.3), _rnd(M, K2, seed=5, scale=0.3)
+    Bb = _rnd(N, K1 + K2, seed=6, scale=0.05).bfloat16().contiguous()
+    bias = _rnd(N, seed=7, scale=0.3)
+    v = (torch.cat([A, A2], 1).bfloat16().double() @ Bb.double().t())
+    a, s = torch.empty(M, N, device=DEV), torch.empty(M, N, device=DEV)
+    ops.linear(A, Bb, N, K1 + K2, a, ops.EPI_SOFTPLUS, A2=A2, K1=K1, bias=bias, out1=s)
+    z = (v + bias.double()).float()
+    torch.testing.assert_close(a, torch.nn.functional.softplus(z, beta=100), rtol=1e-5, atol=2e-5)
+    torch.testing.assert_close(s, torch.where(z * 100 > 20, torch.ones_like(z), torch.sigmoid(100 * z)),
+                               rtol=1e-4, atol=1e-5)
+    aux0, aux1 = torch.rand(M, N, device=DEV), _rnd(M, N, seed=8)
+    o0, o1 = torch.empty(M, N, device=DEV), torch.empty(M, N, device=DEV)
+    ops.linear(A, Bb, N, K1 + K2, o0, ops.EPI_TANGENT, A2=A2, K1=K1, aux0=aux0, aux1=aux1, out1=o1)
+    vf = v.float()
+    torch.testing.assert_close(o0, vf * aux0, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(o1, 100.0 * aux1 * (1 - aux0) * vf, rtol=1e-4, atol=1e-4)
+    o2 = torch.empty(M, N, device=DEV)
+    ops.linear(A, Bb, N, K1 + K2, o2, ops.EPI_BWD_SOFTPLUS, A2=A2, K1=K1, aux0=aux0, aux1=aux1)
+    torch.testing.assert_close(o2, vf * aux0 + aux1, rtol=1e-5, atol=1e-5)
+
+
+def test_render_bf16_mode_against_fp32_oracle():
+    """bf16 operands cannot meet the fp32 1e-4 bar; measured against the fp32
+    oracle on identical samples (1024 rays) the bf16 path stays within the bounds
+    asserted here, and training gradients stay finite."""
+    from copenerf import NeuSRenderer
+    R = 1024
+    g = torch.Generator().manual_seed(R)
+    mods_cpu = build_modules(55, 256, 256)
+    P, Pc, var, _ = oracle_params(*mods_cpu)
+    o = torch.tensor([0.05, -0.03, 1.6]).expand(R, 3).contiguous()
+    d = torch.cat([(torch.rand(R, 2, generator=g) - 0.5) * 0.6, -torch.ones(R, 1)], -1)
+    nrm = d.norm(dim=-1, keepdim=True)
+    d = d / nrm
+    t = torch.tensor([0.25])
+    near, far = torch.full((R, 1), 0.01), torch.full((R, 1), 3.0)
+    t_rand = torch.rand(R, 64, generator=g)
+    torch.set_num_threads(8)
+    ref = O.render(P, Pc, var, o, d, nrm, t, near, far, car=0.5, t_rand=t_rand)
+    sdf, col, dev = build_modules(55, 256, 256, device=DEV)
+    r = NeuSRenderer(None, sdf, dev, col, None, **REN_CFG).to(DEV).set_mfma_dtype("bf16")
+    args = tuple(x.to(DEV) for x in (o, d, nrm, t, near, far))
+    out = r(*args, cos_anneal_ratio=0.5, it=0, eval=False, z_vals=ref["z_vals"].to(DEV))
+    errs = {}
+    for k in ("color_fine", "depth_pred"):
+        e = (out[k].detach().cpu() - ref[k].detach()).abs()
+        errs[k] = (e.max().item(), e.mean().item())
+    print("bf16 vs fp32 oracle (max, mean):", errs)
+    # measured on MI355X: rgb max 1.8e-3 / mean 2.0e-4, depth max 5.0e-3 / mean 5.6e-4
+    assert errs["color_fine"][0] <= 5e-3 and errs["color_fine"][1] <= 5e-4, errs
+    assert errs["depth_pred"][0] <= 1.5e-2 and errs["depth_pred"][1] <= 1.5e-3, errs
+    loss = O.train_loss(out, torch.rand(R, 3, generator=g).to(DEV))
+    loss.backward()
+    for p in list(sdf.parameters()) + list(col.parameters()):
+        assert p.grad is not None and torch.isfinite(p.grad).all()

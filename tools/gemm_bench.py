@@ -47,6 +47,13 @@ def main():
                           ("relu", ops.EPI_RELU, dict(bias=bias)),
                           ("main loop only (bench)", 7, {})):
         res["cn_linear " + name] = timeit(lambda: ops.linear(A, B, N, K, o0, epi, **kw))
+    Bb = B.bfloat16().contiguous()
+    for name, epi, kw in (("store", ops.EPI_STORE, dict(bias=bias)),
+                          ("softplus", ops.EPI_SOFTPLUS, dict(bias=bias, out1=o1)),
+                          ("tangent", ops.EPI_TANGENT, dict(aux0=aux0, aux1=aux1, out1=o1)),
+                          ("main loop only (bench)", 7, {})):
+        res["cn_linear bf16 " + name] = timeit(lambda: ops.linear(A, Bb, N, K, o0, epi, **kw))
+    res["torch.matmul bf16 (hipBLASLt)"] = timeit(lambda: torch.matmul(A.bfloat16(), Bb.t()))
     dW = torch.empty(N, K, device=dev)
     db = torch.empty(N, device=dev)
     res["cn_wgrad 1 pair"] = timeit(lambda: ops.wgrad(A, A, N, K, dW, db=db))
