@@ -107,6 +107,9 @@ CONFIGS = {
            "losses"),
     "c3fp32": (4096, {"joint_pose": True, "stage1": True},
                "C3-style as c3 with exact fp32 MFMA"),
+    "infer": (518400, {"infer": True},
+              "inference: full 540x960 image (518,400 rays x 128 samples, eval mode, no jitter), forward only "
+              "(sampler + SDF + ∇SDF + colour + compositing), 65,536-ray chunks, fp32"),
     "c2bf16": (4096, {"mfma_dtype": "bf16"},
                "C2 workload (4096 rays x 128 samples, fixed poses) with bf16 MLP MFMA (fp32 accumulate)"),
     "c4": (8192, {}, "C4: synthetic scene, 8192 rays x 128 samples per GPU, fp32, fixed poses, data-parallel"),
@@ -147,8 +150,17 @@ def main():
 
     from copenerf import ops
     from copenerf.train_step import GraphedTrainer, SyntheticTrainer
-    tr = SyntheticTrainer(f"cuda:{local}", rays=rays, distributed=distributed, capturable=graph, **kw)
+    infer = kw.pop("infer", False)
+    tr = SyntheticTrainer(f"cuda:{local}", rays=4096 if infer else rays, distributed=distributed and not infer,
+                          capturable=graph, **kw)
     step = tr.step
+    if infer:
+        from copenerf.inference import render_image
+        t_img = torch.zeros(1, device=f"cuda:{local}")
+
+        def step():
+            out = render_image(tr.renderer, tr.K, tr.I, tr.I, (tr.H, tr.W), t_img, chunk=65536)
+            return out["rgb"].sum()
     if graph:
         g = GraphedTrainer(tr, warmup=max(1, args.warmup))
         step = g.step
@@ -184,6 +196,8 @@ def main():
     metric = "rays/sec (train step incl. backward) at 4096 rays × 128 samples"
     if args.config != "c2" or rays != RAYS:
         metric = f"rays/sec (train step incl. backward) at {rays} rays × {S} samples ({args.config})"
+    if infer:
+        metric = f"rays/sec (inference render, forward only) at 540x960 × {S} samples"
     result = {
         "metric": metric,
         "value": round(rays_total / elapsed, 1),

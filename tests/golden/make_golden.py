@@ -163,6 +163,47 @@ def render_case(fields, rend, name, *, seed, R, dh_sdf, dh_col, eval_mode, car, 
     print("wrote", name, sorted(rec)[:6], "...")
 
 
+def pretrained_case(fields, rend, name="render_pretrained", seed=690, R=256):
+    """The reference's shipped pretrained SDF (pretrained_sdf/model.pt, loaded with
+    weights_only=True) rendered from a camera at the origin looking down -z
+    (near/far 0.01/5.0 as the Co3D config): a trained, non-spherical surface.
+    The SDF weights travel in the fixture (sdfw.*) so the GPU test can load them."""
+    sdf, col, dev, r = build_nets(fields, rend, seed)
+    sd = torch.load(os.path.join(REF, "pretrained_sdf", "model.pt"), map_location="cpu", weights_only=True)
+    sdf.load_state_dict(sd, strict=True)
+    g = torch.Generator().manual_seed(seed + 1)
+    d = torch.cat([(torch.rand(R, 2, generator=g) - 0.5) * 1.0, -torch.ones(R, 1)], -1)
+    norm = d.norm(dim=-1, keepdim=True)
+    rays_d = (d / norm).contiguous()
+    rays_o = torch.zeros(R, 3)
+    t_rand = torch.rand(R, REN_CFG["n_samples"], generator=g)
+    rgb_gt = torch.rand(R, 3, generator=g)
+    t = torch.tensor([0.0])
+    near, far = torch.full((R, 1), 0.01), torch.full((R, 1), 5.0)
+    out, z = run_render(r, rays_o, rays_d, norm, t, near, far, t_rand, 0.5, False)
+    edge, smooth = make_losses()
+    rec = {"rays_o": rays_o, "rays_d": rays_d, "rays_d_norm": norm, "t": t, "near": near, "far": far,
+           "t_rand": t_rand, "rgb_gt": rgb_gt, "car": np.float32(0.5), "eval": np.int32(0),
+           "seed": np.int32(seed), "dh_sdf": np.int32(256), "dh_col": np.int32(256),
+           "variance": dev.variance.detach(), "z_vals": z}
+    for k, v in sd.items():
+        rec["sdfw." + k] = v.detach()
+    for k in ("color_fine", "depth_pred", "weighted_z_vals", "weights", "sdf", "normals", "sdf_flows",
+              "cdf_fine", "s_val", "sampled_points", "weight_sum", "weight_max"):
+        rec["out_" + k] = out[k].detach()
+    params = [("sdf." + k, p) for k, p in sdf.named_parameters()] + \
+             [("col." + k, p) for k, p in col.named_parameters()] + [("dev.variance", dev.variance)]
+    loss = train_loss(out, rgb_gt, edge, smooth)
+    grads = torch.autograd.grad(loss, [p for _, p in params])
+    rec["loss"] = loss.detach()
+    gen = torch.Generator().manual_seed(1234)
+    for (k, p), gr in zip(params, grads):
+        put_grad(rec, k, gr, False, gen)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"),
+                        **{k: (v.numpy() if torch.is_tensor(v) else v) for k, v in rec.items()})
+    print("wrote", name)
+
+
 def put_grad(rec, key, gr, full, gen):
     if full or gr.numel() <= 512:
         rec["grad." + key] = gr
@@ -274,6 +315,7 @@ def main():
     render_case(fields, rend, "render_full_train", seed=680, R=32, dh_sdf=256, dh_col=256, eval_mode=False,
                 car=0.5, full_grads=False)
     seams_case(fields, rend)
+    pretrained_case(fields, rend)
 
 
 def main_motion_only():
@@ -281,5 +323,16 @@ def main_motion_only():
     motion_case(fields)
 
 
+def main_pretrained_only():
+    fields, rend = load_reference()
+    torch.set_num_threads(8)
+    pretrained_case(fields, rend)
+
+
 if __name__ == "__main__":
-    main_motion_only() if "--motion-only" in sys.argv else main()
+    if "--motion-only" in sys.argv:
+        main_motion_only()
+    elif "--pretrained-only" in sys.argv:
+        main_pretrained_only()
+    else:
+        main()

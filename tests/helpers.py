@@ -78,3 +78,11 @@ def check_grad(name, got, fx, rtol, atol):
                                    msg=lambda m: f"{name} (sampled): {m}")
         n = fx["gradnorm." + name].float()
         assert abs(got.norm().item() - n.item()) <= rtol * n.item() + atol, (name, got.norm().item(), n.item())
+
+
+def load_pretrained_sdf(sdf, fx):
+    """Load the reference's pretrained SDF weights carried by a fixture (sdfw.*)
+    into an SDFNetwork with strict key matching (checkpoint compatibility)."""
+    sd = {k[5:]: v for k, v in fx.items() if k.startswith("sdfw.")}
+    sdf.load_state_dict({k: v.to(next(sdf.parameters()).device) for k, v in sd.items()}, strict=True)
+    return sdf

@@ -174,3 +174,30 @@ def test_render_configs_c5_c1(n_samples, n_importance):
     err = torch.maximum((out["depth_pred"].detach().cpu() - ref["depth_pred"].detach()).abs().squeeze(1),
                         (out["color_fine"].detach().cpu() - ref["color_fine"].detach()).abs().max(1)[0])
     assert (err > TOL_RGB_DEPTH).float().mean().item() <= 0.01
+
+
+def test_render_pretrained_sdf_matches_reference():
+    """The reference's trained SDF (pretrained_sdf/model.pt via the fixture): strict
+    |Δ rgb|, |Δ depth| <= 1e-4 on the reference's own sample positions, the
+    end-to-end path within the sampler-flip statistics, and the loss gradients."""
+    from helpers import load_pretrained_sdf
+    fx = fixture("render_pretrained")
+    mods = build_modules(int(fx["seed"]), device=DEV)
+    load_pretrained_sdf(mods[0], fx)
+    r = _renderer(mods)
+    g = lambda k: fx[k].to(DEV)  # noqa: E731
+    args = (g("rays_o"), g("rays_d"), g("rays_d_norm"), g("t"), g("near"), g("far"))
+    out = r(*args, cos_anneal_ratio=float(fx["car"]), it=0, eval=False, z_vals=g("z_vals"))
+    for k in ("color_fine", "depth_pred"):
+        err = (out[k].detach().cpu() - fx["out_" + k]).abs().max().item()
+        assert err <= TOL_RGB_DEPTH, (k, err)
+    loss = O.train_loss(out, fx["rgb_gt"].to(DEV))
+    assert abs(loss.item() - fx["loss"].item()) <= 1e-4 * abs(fx["loss"].item()) + 1e-5
+    params = named_params(*mods)
+    grads = torch.autograd.grad(loss, [p for _, p in params])
+    for (n, _), gr in zip(params, grads):
+        check_grad(n, gr, fx, rtol=2e-2, atol=2e-4 * (gr.abs().max().item() + 1e-3))
+    out = r(*args, cos_anneal_ratio=float(fx["car"]), it=0, eval=False, t_rand=g("t_rand"))
+    err = torch.maximum((out["depth_pred"].detach().cpu() - fx["out_depth_pred"]).abs().squeeze(1),
+                        (out["color_fine"].detach().cpu() - fx["out_color_fine"]).abs().max(1)[0])
+    assert (err > TOL_RGB_DEPTH).float().mean().item() <= 0.02, err.max().item()
