@@ -172,21 +172,23 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     const int lds_b = srowb * LS + scb * 4;
 
     floatx4 ra[DEPTH][ALD], rb[DEPTH][BLD];
-    auto gload = [&](int set, int kc, int m0, int n0) {
+    // Straight-line staging: every call issues exactly ALD + BLD loads (an empty
+    // view when `valid` is false, reads return zero) with no data-dependent branch,
+    // so the compiler tracks vmcnt precisely and the LDS writes of one register
+    // set wait only for that set's loads, not for the prefetch issued after them.
+    auto gload = [&](int set, int kc, int m0, int n0, bool valid) {
         const int k0 = kc * BK;
-        const int rows = min(BM, p.M - m0);
-        if (k0 < p.K1) {
-            const rsrc_t rA = make_view(p.A + (int64_t)m0 * p.lda, rows * p.lda * 4);
+        const int rows = valid ? min(BM, p.M - m0) : 0;
+        const bool second = k0 >= p.K1;  // wave-uniform: A2 half of a virtual concat
+        const float* abase = second ? p.A2 + (int64_t)m0 * p.lda2 : p.A + (int64_t)m0 * p.lda;
+        const int ald = second ? p.lda2 : p.lda;
+        const int ak = second ? k0 - p.K1 : k0;
+        const rsrc_t rA = make_view(abase, rows * ald * 4);
 #pragma unroll
-            for (int q = 0; q < ALD; ++q) ra[set][q] = bload4(rA, voA[q], k0 * 4);
-        } else {
-            const rsrc_t rA = make_view(p.A2 + (int64_t)m0 * p.lda2, rows * p.lda2 * 4);
-#pragma unroll
-            for (int q = 0; q < ALD; ++q) ra[set][q] = bload4(rA, voA2[q], (k0 - p.K1) * 4);
-        }
+        for (int q = 0; q < ALD; ++q) ra[set][q] = bload4(rA, second ? voA2[q] : voA[q], ak * 4);
         const rsrc_t rB = make_view(reinterpret_cast<const float*>(reinterpret_cast<const char*>(p.B) +
                                                                    (int64_t)n0 * p.ldb * ESZB),
-                                    BN * p.ldb * ESZB);
+                                    valid ? BN * p.ldb * ESZB : 0);
 #pragma unroll
         for (int q = 0; q < BLD; ++q) rb[set][q] = bload4(rB, voB[q], k0 * ESZB);
     };
@@ -242,7 +244,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     if (vt >= ntiles) return;
     int tm, tn;
     tile_coords(vt, T, tm, tn);
-    gload(0, 0, tm * BM, tn * BN);
+    gload(0, 0, tm * BM, tn * BN, true);
 
     while (vt < ntiles) {
         const int m0 = tm * BM, n0 = tn * BN;
@@ -252,7 +254,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 
         lstore(0, 0);
         __syncthreads();
-        if (DEPTH == 2) gload(1, 1, m0, n0);  // nk is even for DEPTH 2
+        if (DEPTH == 2) gload(1, 1, m0, n0, true);  // nk is even for DEPTH 2
 
         floatx16 acc[TM][TN];
 #pragma unroll
@@ -305,30 +307,29 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             }
         };
 
+        const int m_next = tm_next * BM, n_next = tn_next * BN;
+        const bool has_next = vt_next < ntiles;
         if constexpr (DEPTH == 1) {
             for (int kc = 0; kc < nk; ++kc) {
                 const int cur = kc & 1;
-                if (kc + 1 < nk)
-                    gload(0, kc + 1, m0, n0);
-                else if (vt_next < ntiles)
-                    gload(0, 0, tm_next * BM, tn_next * BN);  // next tile's first chunk, consumed after the epilogue
+                // chunk kc+1 of this tile, or the next tile's first chunk (consumed after the epilogue)
+                const bool more = kc + 1 < nk;
+                gload(0, more ? kc + 1 : 0, more ? m0 : m_next, more ? n0 : n_next, more || has_next);
                 compute(cur);
-                if (kc + 1 < nk) lstore(0, cur ^ 1);
+                if (more) lstore(0, cur ^ 1);
                 __syncthreads();
             }
         } else {
             // chunk k+1 is in flight in set (k+1)&1 while chunk k is computed from LDS buffer k&1
             for (int kc = 0; kc < nk; kc += 2) {
-                if (kc + 2 < nk)
-                    gload(0, kc + 2, m0, n0);
-                else if (vt_next < ntiles)
-                    gload(0, 0, tm_next * BM, tn_next * BN);
+                const bool more = kc + 2 < nk;
+                gload(0, more ? kc + 2 : 0, more ? m0 : m_next, more ? n0 : n_next, more || has_next);
                 compute(0);
                 lstore(1, 1);
                 __syncthreads();
-                if (kc + 3 < nk) gload(1, kc + 3, m0, n0);
+                gload(1, kc + 3 < nk ? kc + 3 : 0, m0, n0, kc + 3 < nk);
                 compute(1);
-                if (kc + 2 < nk) lstore(0, 0);
+                if (more) lstore(0, 0);
                 __syncthreads();
             }
         }
