@@ -820,7 +820,11 @@ static void wgrad_geometry(int M, int N, int K, int* tile, int* Npad, int* Kpad,
     *Npad = cdiv(N, BNo) * BNo;
     *Kpad = cdiv(K, BKo) * BKo;
     const int tiles = (*Npad / BNo) * (*Kpad / BKo);
-    int ns = std::max(1, 1024 / tiles);
+    static const int kTarget = [] {  // workgroups per cn_wgrad (benchmarking aid: COPENERF_WGRAD_BLOCKS)
+        const char* e = getenv("COPENERF_WGRAD_BLOCKS");
+        return e ? atoi(e) : 512;
+    }();
+    int ns = std::max(1, kTarget / tiles);
     ns = std::min(ns, std::max(1, cdiv(M, 512)));
     int rps = cdiv(cdiv(M, ns), 32) * 32;
     ns = std::max(1, cdiv(M, rps));
