@@ -42,13 +42,19 @@ GFLOP_PER_RAY_REF = 1.4809  # reference GEMM FLOPs per ray per t
 
 
 def kernel_symbol(key):
-    """rocprofv3 name of the kernel a KernelTimer key times (cn_gemm.hip template
-    arguments: waves, tiles, BK 32, 2 workgroups/CU, 2-deep prefetch (every K on
-    the C2 path is a multiple of 64), epilogue, no row vector)."""
+    """rocprofv3 name of the kernel a KernelTimer key times (cn_gemm.hip's
+    cn_linear dispatch: waves, tiles, BK, workgroups/CU, prefetch depth,
+    epilogue, row vector, bf16).  fp32: BK 32 with the 2-deep prefetch (every K
+    on the C2 path is a multiple of 64); bf16: BK 64, 1-deep."""
     if key[0] == "linear":
         tiles = {0: "2, 2, 2, 2", 1: "4, 1, 1, 2"}
         epi = {"store": 0, "softplus": 1, "relu": 2, "mul": 3, "tangent": 4, "bwd_softplus": 5, "bwd_relu": 6}
-        return f"void cn::linear_kernel<{tiles[key[1]]}, 32, 2, 2, {epi[key[2]]}, false>(cn::LinearArgs)"
+        bf = "bf16" in key[3:]
+        mid = "64, 2, 1" if bf else "32, 2, 2"
+        return (f"void cn::linear_kernel<{tiles[key[1]]}, {mid}, {epi[key[2]]}, false, "
+                f"{'true' if bf else 'false'}>(cn::LinearArgs)")
+    if "bf16" in key[2:]:
+        return "void cn::wgrad_bf16_kernel<2, 2, 2, 2>(cn::WgradArgs) + cn::slab_reduce_kernel"
     return "void cn::wgrad_kernel<2, 2, 2, 2>(cn::WgradArgs) + cn::slab_reduce_kernel"
 
 

@@ -54,7 +54,7 @@ class WgradDesc(ctypes.Structure):
         ("ldy0", c_i64), ("ldx0", c_i64), ("ldy1", c_i64), ("ldx1", c_i64), ("ld_dw", c_i64),
         ("workspace_bytes", c_i64),
         ("M", c_i32), ("N", c_i32), ("K", c_i32), ("npairs", c_i32),
-        ("n_out", c_i32), ("k_out", c_i32), ("accumulate", c_i32), ("pad_", c_i32),
+        ("n_out", c_i32), ("k_out", c_i32), ("accumulate", c_i32), ("mfma_dtype", c_i32),
     ]
 
 

@@ -213,6 +213,7 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG):
     where s_l are the ∇ pass adjoints kept from the forward.  Six GEMMs per
     layer instead of autograd's nine.
     """
+    bf = pk.Bf[0].dtype == torch.bfloat16  # the pack's MFMA dtype also selects the wgrad MFMA
     U, Sig, S = st["U"], st["Sig"], st["S"]
     M, dev = U[0].shape[0], U[0].device
     nl, sk, HL, KE = lay.n_lin, lay.skip, lay.HL, lay.KE
@@ -244,7 +245,7 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG):
     dW8 = torch.empty(o8, i8, device=dev)
     db8 = torch.empty(o8, device=dev)
     if dfeat is not None:
-        ops.wgrad(dfeat, U[L8], lay.H_feat, i8, dW8[1:], db=db8[1:])
+        ops.wgrad(dfeat, U[L8], lay.H_feat, i8, dW8[1:], db=db8[1:], bf16=bf)
     else:
         dW8[1:].zero_()
         db8[1:].zero_()
@@ -276,7 +277,7 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG):
         dW = torch.empty(lay.out_dim[l], lay.in_dim[l], device=dev)
         db = torch.empty(lay.out_dim[l], device=dev)
         ops.wgrad(Zl, U[l], lay.out_dim[l], lay.in_dim[l], dW, db=db,
-                  Y1=S[l] if second else None, X1=Ud[l] if second else None)
+                  Y1=S[l] if second else None, X1=Ud[l] if second else None, bf16=bf)
         dWs[l], dbs[l] = dW, db
         R[l] = None
     return dWs, dbs
@@ -509,6 +510,7 @@ class _ColorFieldFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, drgb):
         lay, pk = ctx.lay, ctx.pk
+        bf = pk.Bf[0].dtype == torch.bfloat16
         feat, ext, H, rgb = ctx.bufs
         ctx.bufs = None
         nparams = 2 * lay.n_lin
@@ -525,7 +527,7 @@ class _ColorFieldFn(torch.autograd.Function):
         for l in range(n - 2, 0, -1):
             dW = torch.empty(lay.out_dim[l], lay.in_dim[l], device=dev)
             db = torch.empty(lay.out_dim[l], device=dev)
-            ops.wgrad(dZ, H[l - 1], lay.out_dim[l], lay.in_dim[l], dW, db=db)
+            ops.wgrad(dZ, H[l - 1], lay.out_dim[l], lay.in_dim[l], dW, db=db, bf16=bf)
             dWs[l], dbs[l] = dW, db
             dZp = _empty(M, lay.HL, dev)
             ops.linear(dZ, pk.Bt[l], lay.out_dim[l - 1], rup(lay.out_dim[l], 32), dZp, EPI_BWD_RELU, aux0=H[l - 1],
@@ -534,9 +536,9 @@ class _ColorFieldFn(torch.autograd.Function):
         o0 = lay.out_dim[0]
         dWf = torch.empty(o0, lay.F, device=dev)
         db0 = torch.empty(o0, device=dev)
-        ops.wgrad(dZ, feat, o0, lay.F, dWf, db=db0)
+        ops.wgrad(dZ, feat, o0, lay.F, dWf, db=db0, bf16=bf)
         dWx = torch.empty(o0, lay.KX, device=dev)
-        ops.wgrad(dZ, ext, o0, lay.KX, dWx)
+        ops.wgrad(dZ, ext, o0, lay.KX, dWx, bf16=bf)
         P, V, Gd = lay.P, lay.V, lay.Gd
         # back to the reference column order [pts | emb(dirs) | gradients | feature]
         dWs[0] = torch.cat([dWx[:, Gd:Gd + P], dWx[:, Gd + P:Gd + P + V], dWx[:, 0:Gd], dWf], 1)

@@ -138,8 +138,9 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     return out0
 
 
-def wgrad(Y0, X0, N, K, dW, *, db=None, Y1=None, X1=None, accumulate=False):
-    """dW[:n_out, :k_out] (+)= Y0ᵀX0 (+ Y1ᵀX1), db = colsum(Y0) -- cn_wgrad."""
+def wgrad(Y0, X0, N, K, dW, *, db=None, Y1=None, X1=None, accumulate=False, bf16=False):
+    """dW[:n_out, :k_out] (+)= Y0ᵀX0 (+ Y1ᵀX1), db = colsum(Y0) -- cn_wgrad.
+    bf16=True: operands rounded to bf16 on load (config C3's bf16 MFMA)."""
     for t, n in ((Y0, "Y0"), (X0, "X0"), (Y1, "Y1"), (X1, "X1"), (dW, "dW")):
         _need(t, n)
     M = Y0.shape[0]
@@ -155,10 +156,11 @@ def wgrad(Y0, X0, N, K, dW, *, db=None, Y1=None, X1=None, accumulate=False):
     d.npairs = 2 if Y1 is not None else 1
     d.n_out, d.k_out = dW.shape[0], dW.shape[1]
     d.accumulate = 1 if accumulate else 0
+    d.mfma_dtype = 1 if bf16 else 0
     if _timer is not None:
         e0 = _timer.start()
         _lib.check(lib.cn_wgrad(d, _stream()), "cn_wgrad")
-        key = ("wgrad", d.npairs)
+        key = ("wgrad", d.npairs) + (("bf16",) if bf16 else ())
         _timer.stop(key + ((M, d.n_out, d.k_out),) if _timer.detail else key, e0,
                     2.0 * M * d.n_out * d.k_out * d.npairs)
     else:

@@ -617,6 +617,166 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) wgrad_kernel(WgradArgs p) {
     if (do_bias && tid < BNo) p.bpart[(int64_t)slice * p.Npad + n0 + tid] = bacc;
 }
 
+// bf16-operand weight gradient (config C3): the same tiles and slabs as
+// wgrad_kernel, with Y and X rounded to bf16 while staging and written
+// TRANSPOSED into LDS ([n][m] and [k][m], 64 m per row + 8 pad = 36 dwords), so
+// one ds_read_b128 gives a lane the 8 consecutive m of its
+// v_mfma_f32_32x32x16_bf16 fragment.  A thread stages 4 rows x 4 columns per
+// pass and packs each column's 4 m into one ds_write_b64; the 16-byte blocks of
+// a row are XOR-swizzled so those writes do not collide on banks.  db is summed from the
+// fp32 values in registers (partials reduced through LDS at the end).
+template <int WM, int WN, int TM, int TN>
+__global__ void __launch_bounds__(64 * WM * WN, 2) wgrad_bf16_kernel(WgradArgs p) {
+    constexpr int NT = 64 * WM * WN;
+    constexpr int BNo = 32 * TM * WM;
+    constexpr int BKo = 32 * TN * WN;
+    constexpr int MC = 64;
+    constexpr int LSB = MC / 2 + 4;  // dwords per LDS row
+    constexpr int YC = BNo / 4, XC = BKo / 4;        // float4 column groups per staged row
+    constexpr int YMQ = NT / YC, XMQ = NT / XC;      // m-quads per pass
+    constexpr int YP = (MC / 4) / YMQ, XP = (MC / 4) / XMQ;
+    static_assert(YP >= 1 && XP >= 1 && YMQ * YC == NT && XMQ * XC == NT, "staging geometry");
+    static_assert(2 * BNo <= (BNo + BKo) * LSB, "bias partials fit in LDS");
+
+    __shared__ __attribute__((aligned(16))) float smem[2 * (BNo + BKo) * LSB];
+    float* sY = smem;
+    float* sX = smem + 2 * BNo * LSB;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave / WN;
+    const int wn = wave % WN;
+    const int T = p.n_tiles_n * p.n_tiles_k;
+    const int b = blockIdx.x;
+    const int tile = (b >> 3) % T;
+    const int slice = (b & 7) + 8 * ((b >> 3) / T);
+    if (slice >= p.nslices) return;
+    const int tn = tile / p.n_tiles_k;
+    const int tk = tile % p.n_tiles_k;
+    const int n0 = tn * BNo;
+    const int k0 = tk * BKo;
+    const int mbeg = slice * p.rows_per_slice;
+    const int mend = min(p.M, mbeg + p.rows_per_slice);
+    const int nch = mend > mbeg ? cdiv(mend - mbeg, MC) : 0;
+    const int total = nch * p.npairs;
+    const bool do_bias = (tk == 0) && (p.bpart != nullptr);
+
+    const int yc = tid % YC, ymq = tid / YC;
+    const int xc = tid % XC, xmq = tid / XC;
+    floatx4 ry[YP][4], rx[XP][4];
+    float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+    auto gload = [&](int c) {
+        const int pair = c >= nch;
+        const int mrow = mbeg + (c - pair * nch) * MC;
+        const float* Y = pair ? p.Y1 : p.Y0;
+        const float* X = pair ? p.X1 : p.X0;
+        const int ly = pair ? p.ldy1 : p.ldy0;
+        const int lx = pair ? p.ldx1 : p.ldx0;
+        const int nrows = min(MC, mend - mrow);
+        const rsrc_t vY = make_view(Y + (int64_t)mrow * ly + n0, (nrows * ly - n0) * 4);
+        const rsrc_t vX = make_view(X + (int64_t)mrow * lx + k0, (nrows * lx - k0) * 4);
+#pragma unroll
+        for (int pp = 0; pp < YP; ++pp)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                ry[pp][r] = bload4(vY, (((ymq + pp * YMQ) * 4 + r) * ly + yc * 4) * 4, 0);
+#pragma unroll
+        for (int pp = 0; pp < XP; ++pp)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                rx[pp][r] = bload4(vX, (((xmq + pp * XMQ) * 4 + r) * lx + xc * 4) * 4, 0);
+    };
+    // XOR swizzle of the 16-byte blocks of a row by (row >> 2) & 7: the staging
+    // writes (threads on rows 4 apart) spread over all banks; reads undo it
+    auto swz = [&](int row, int mq) { return row * LSB + (((mq >> 1) ^ ((row >> 2) & 7)) << 2) + ((mq & 1) << 1); };
+    auto lstore = [&](int buf, bool bias) {
+        float* y = sY + buf * BNo * LSB;
+        float* x = sX + buf * BKo * LSB;
+#pragma unroll
+        for (int pp = 0; pp < YP; ++pp)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const floatx4 col = {ry[pp][0][e], ry[pp][1][e], ry[pp][2][e], ry[pp][3][e]};
+                if (bias) bsum[e] += (col[0] + col[1]) + (col[2] + col[3]);
+                *reinterpret_cast<bf16x4*>(y + swz(yc * 4 + e, ymq + pp * YMQ)) = __builtin_convertvector(col, bf16x4);
+            }
+#pragma unroll
+        for (int pp = 0; pp < XP; ++pp)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const floatx4 col = {rx[pp][0][e], rx[pp][1][e], rx[pp][2][e], rx[pp][3][e]};
+                *reinterpret_cast<bf16x4*>(x + swz(xc * 4 + e, xmq + pp * XMQ)) = __builtin_convertvector(col, bf16x4);
+            }
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+    if (total > 0) {
+        gload(0);
+        lstore(0, do_bias && nch > 0);
+    }
+    __syncthreads();
+    const int h = lane >> 5;
+    const int ycol = wm * TM * 32 + (lane & 31);
+    const int xcol = wn * TN * 32 + (lane & 31);
+    for (int c = 0; c < total; ++c) {
+        const int cur = c & 1;
+        const bool more = c + 1 < total;
+        if (more) gload(c + 1);
+        const float* yb = sY + cur * BNo * LSB + ycol * LSB;
+        const float* xb = sX + cur * BKo * LSB + xcol * LSB;
+        const int sw = ((lane & 31) >> 2) & 7;  // (row >> 2) & 7 of this lane's rows
+#pragma unroll
+        for (int ks = 0; ks < MC / 16; ++ks) {
+            const int blk = ((2 * ks + h) ^ sw) << 2;
+            bf16x8 af[TM], bf[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(yb + i * 32 * LSB + blk);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const bf16x8*>(xb + j * 32 * LSB + blk);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
+        if (more) lstore(cur ^ 1, do_bias && c + 1 < nch);
+        __syncthreads();
+    }
+
+    const rsrc_t vP = make_view(p.part + (int64_t)slice * p.Npad * p.Kpad, p.Npad * p.Kpad * 4);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = k0 + wn * TN * 32 + j * 32 + (lane & 31);
+            const int rbase = n0 + wm * TM * 32 + i * 32 + 4 * (lane >> 5);
+            const int vo = (rbase * p.Kpad + col) * 4;
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                bstore1(vP, vo, ((r & 3) + 8 * (r >> 2)) * p.Kpad * 4, acc[i][j][r]);
+        }
+    }
+    if (do_bias) {  // reduce the per-thread column partials over the m-quads (fixed order)
+        float* red = smem;  // [YMQ][BNo]
+#pragma unroll
+        for (int e = 0; e < 4; ++e) red[ymq * BNo + yc * 4 + e] = bsum[e];
+        __syncthreads();
+        if (tid < BNo) {
+            float t = 0.0f;
+            for (int q = 0; q < YMQ; ++q) t += red[q * BNo + tid];
+            p.bpart[(int64_t)slice * p.Npad + n0 + tid] = t;
+        }
+    }
+}
+
 // Sum of nslab fp32 slabs: out[r*ldo + c] (+)= (sum_s part[s*stride + r*ldp + c]) / div
 // for r < rows, c < cols.  A workgroup owns 64 float4 column groups x 4 slab
 // groups; each thread sums its slab group in double with 4 loads in flight, the 4
@@ -826,7 +986,7 @@ static void wgrad_geometry(int M, int N, int K, int* tile, int* Npad, int* Kpad,
     }();
     int ns = std::max(1, kTarget / tiles);
     ns = std::min(ns, std::max(1, cdiv(M, 512)));
-    int rps = cdiv(cdiv(M, ns), 32) * 32;
+    int rps = cdiv(cdiv(M, ns), 64) * 64;  // whole 32-row (fp32) / 64-row (bf16) chunks
     ns = std::max(1, cdiv(M, rps));
     *nslices = ns;
     *rows_per_slice = rps;
@@ -989,10 +1149,18 @@ extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
     a.n_tiles_n = Npad / 128;
     a.nslices = ns;
     dim3 grid(cdiv(ns, 8) * 8 * a.n_tiles_n * a.n_tiles_k);
-    if (tile == 0)
+    CN_REQUIRE(d->mfma_dtype == CN_MFMA_F32 || d->mfma_dtype == CN_MFMA_BF16, CN_ERR_ARG,
+               "cn_wgrad: bad mfma_dtype %d", d->mfma_dtype);
+    if (d->mfma_dtype == CN_MFMA_BF16) {
+        if (tile == 0)
+            wgrad_bf16_kernel<2, 2, 2, 2><<<grid, 256, 0, s>>>(a);
+        else
+            wgrad_bf16_kernel<2, 2, 2, 1><<<grid, 256, 0, s>>>(a);
+    } else if (tile == 0) {
         wgrad_kernel<2, 2, 2, 2><<<grid, 256, 0, s>>>(a);
-    else
+    } else {
         wgrad_kernel<2, 2, 2, 1><<<grid, 256, 0, s>>>(a);
+    }
     int rc = check_launch("cn_wgrad");
     if (rc) return rc;
     rc = launch_slab_reduce(a.part, ns, (int64_t)Npad * Kpad, d->n_out, d->k_out, Kpad, d->dW, d->ld_dw, 1.0f,

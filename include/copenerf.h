@@ -120,7 +120,9 @@ typedef struct cn_wgrad_desc {
     int32_t npairs;
     int32_t n_out, k_out;
     int32_t accumulate;  /* 1: dW += result (db too), 0: dW = result */
-    int32_t pad_;
+    int32_t mfma_dtype;  /* CN_MFMA_F32, or CN_MFMA_BF16: Y and X rounded to bf16 (RNE) on load,
+                            v_mfma_f32_32x32x16_bf16, fp32 accumulation and slab reduction;
+                            db is summed from the fp32 values either way */
 } cn_wgrad_desc;
 
 size_t cn_wgrad_workspace_bytes(int32_t M, int32_t N, int32_t K);

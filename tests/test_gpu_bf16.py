@@ -65,6 +65,30 @@ def test_linear_bf16_epilogues_and_concat():
     torch.testing.assert_close(o2, vf * aux0 + aux1, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("M,N,K,pairs", [(70000, 256, 256, 2), (1000, 204, 64, 1), (5, 256, 256, 1),
+                                         (4097, 256, 320, 1), (300, 52, 192, 2)])
+def test_wgrad_bf16(M, N, K, pairs):
+    """cn_wgrad with mfma_dtype CN_MFMA_BF16: dW against the bf16-rounded operands
+    in double; db is the column sum of the fp32 Y0 (not rounded)."""
+    from copenerf import ops
+    ldn, ldk = ops.rup(N, 128), ops.rup(K, 128 if K % 128 == 0 else 64)
+    Y0, X0 = _rnd(M, ldn, seed=15), _rnd(M, ldk, seed=16)
+    Y1, X1 = (_rnd(M, ldn, seed=17), _rnd(M, ldk, seed=18)) if pairs == 2 else (None, None)
+    dW = torch.empty(N, K, device=DEV)
+    db = torch.empty(N, device=DEV)
+    ops.wgrad(Y0, X0, N, K, dW, db=db, Y1=Y1, X1=X1, bf16=True)
+    r = lambda t, n: t[:, :n].bfloat16().double()  # noqa: E731
+    ref = r(Y0, N).t() @ r(X0, K)
+    if pairs == 2:
+        ref = ref + r(Y1, N).t() @ r(X1, K)
+    tol = 1e-6 * M ** 0.5 + 1e-5
+    torch.testing.assert_close(dW, ref.float(), rtol=1e-4, atol=tol)
+    torch.testing.assert_close(db, Y0[:, :N].double().sum(0).float(), rtol=1e-4, atol=tol)
+    dW2 = torch.empty_like(dW)
+    ops.wgrad(Y0, X0, N, K, dW2, Y1=Y1, X1=X1, bf16=True)
+    assert torch.equal(dW, dW2)
+
+
 def test_render_bf16_mode_against_fp32_oracle():
     """bf16 operands cannot meet the fp32 1e-4 bar; measured against the fp32
     oracle on identical samples (1024 rays) the bf16 path stays within the bounds
