@@ -44,17 +44,19 @@ GFLOP_PER_RAY_REF = 1.4809  # reference GEMM FLOPs per ray per t
 def kernel_symbol(key):
     """rocprofv3 name of the kernel a KernelTimer key times (cn_gemm.hip's
     cn_linear dispatch: waves, tiles, BK, workgroups/CU, prefetch depth,
-    epilogue, row vector, bf16).  fp32: BK 32 with the 2-deep prefetch (every K
-    on the C2 path is a multiple of 64); bf16: BK 64, 1-deep."""
+    epilogue, row vector, operand mode).  fp32: BK 32 with the 2-deep prefetch
+    (every K on the C2 path is a multiple of 64); bf16: BK 64, 1-deep; bf16x6
+    (split fp32): BK 16, 2-deep."""
     if key[0] == "linear":
         tiles = {0: "2, 2, 2, 2", 1: "4, 1, 1, 2"}
         epi = {"store": 0, "softplus": 1, "relu": 2, "mul": 3, "tangent": 4, "bwd_softplus": 5, "bwd_relu": 6}
-        bf = "bf16" in key[3:]
-        mid = "64, 2, 1" if bf else "32, 2, 2"
-        return (f"void cn::linear_kernel<{tiles[key[1]]}, {mid}, {epi[key[2]]}, false, "
-                f"{'true' if bf else 'false'}>(cn::LinearArgs)")
+        mode = 1 if "bf16" in key[3:] else 2 if "x6" in key[3:] else 0
+        mid = {0: "32, 2, 2", 1: "64, 2, 1", 2: "16, 2, 2"}[mode]
+        return f"void cn::linear_kernel<{tiles[key[1]]}, {mid}, {epi[key[2]]}, false, {mode}>(cn::LinearArgs)"
     if "bf16" in key[2:]:
         return "void cn::wgrad_bf16_kernel<2, 2, 2, 2>(cn::WgradArgs) + cn::slab_reduce_kernel"
+    if "x6" in key[2:]:
+        return "cn::wgrad_x6_kernel(cn::WgradArgs) + cn::slab_reduce_kernel"
     return "void cn::wgrad_kernel<2, 2, 2, 2>(cn::WgradArgs) + cn::slab_reduce_kernel"
 
 
@@ -118,6 +120,9 @@ CONFIGS = {
               "(sampler + SDF + ∇SDF + colour + compositing), 65,536-ray chunks, fp32"),
     "c2bf16": (4096, {"mfma_dtype": "bf16"},
                "C2 workload (4096 rays x 128 samples, fixed poses) with bf16 MLP MFMA (fp32 accumulate)"),
+    "c2x6": (4096, {"mfma_dtype": "bf16x6"},
+             "C2 workload (4096 rays x 128 samples, fixed poses), fp32 MLP GEMMs on the bf16 MFMA (three-term "
+             "bf16 split of both operands, six products, fp32 accumulate)"),
     "c4": (8192, {}, "C4: synthetic scene, 8192 rays x 128 samples per GPU, fp32, fixed poses, data-parallel"),
     "c5": (4096, {"ren_cfg": dict(n_samples=64, n_importance=128, n_outside=0, up_sample_steps=4, perturb=1.0,
                                   n_max_network_queries=64000, importance_sampling_start=0, naive_render=False),

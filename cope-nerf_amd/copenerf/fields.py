@@ -78,12 +78,32 @@ class SDFPack:
     bf8: torch.Tensor
 
 
+MFMA_DTYPES = ("fp32", "bf16", "bf16x6")
+
+
+def _image_fmt(mfma_dtype: str):
+    """(K padding multiple, converter) of the B images for an MFMA mode."""
+    if mfma_dtype == "bf16":
+        return 64, lambda t: t.to(torch.bfloat16).contiguous()
+    if mfma_dtype == "bf16x6":
+        return 32, ops.split_bf16x3
+    if mfma_dtype == "fp32":
+        return 32, lambda t: t.contiguous()
+    raise ValueError(f"mfma_dtype must be one of {MFMA_DTYPES} (got {mfma_dtype!r})")
+
+
+def _wgrad_mode(pk) -> str:
+    """The weight gradients run in the pack's MFMA mode."""
+    if pk.Bf[0].dtype != torch.bfloat16:
+        return "fp32"
+    return "bf16x6" if pk.Bf[0].dim() == 3 else "bf16"
+
+
 def pack_sdf(lay: SDFLayout, Ws, bs, mfma_dtype: str = "fp32") -> SDFPack:
     """Zero-padded GEMM images of the effective weights.  mfma_dtype "bf16": the
-    B images are bfloat16 with K padded to 64 (cn_linear's bf16 MFMA path)."""
-    bf = mfma_dtype == "bf16"
-    kq = 64 if bf else 32
-    cv = (lambda t: t.to(torch.bfloat16).contiguous()) if bf else (lambda t: t.contiguous())  # noqa: E731
+    B images are bfloat16 with K padded to 64 (cn_linear's bf16 MFMA path);
+    "bf16x6": [N, 3, K] bf16 term images (fp32 GEMMs on the bf16 MFMA)."""
+    kq, cv = _image_fmt(mfma_dtype)
     with torch.no_grad():
         Bf, Bt, b = [], [], []
         for l in range(lay.n_lin - 1):
@@ -213,7 +233,7 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG):
     where s_l are the ∇ pass adjoints kept from the forward.  Six GEMMs per
     layer instead of autograd's nine.
     """
-    bf = pk.Bf[0].dtype == torch.bfloat16  # the pack's MFMA dtype also selects the wgrad MFMA
+    wmode = _wgrad_mode(pk)
     U, Sig, S = st["U"], st["Sig"], st["S"]
     M, dev = U[0].shape[0], U[0].device
     nl, sk, HL, KE = lay.n_lin, lay.skip, lay.HL, lay.KE
@@ -245,7 +265,7 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG):
     dW8 = torch.empty(o8, i8, device=dev)
     db8 = torch.empty(o8, device=dev)
     if dfeat is not None:
-        ops.wgrad(dfeat, U[L8], lay.H_feat, i8, dW8[1:], db=db8[1:], bf16=bf)
+        ops.wgrad(dfeat, U[L8], lay.H_feat, i8, dW8[1:], db=db8[1:], mode=wmode)
     else:
         dW8[1:].zero_()
         db8[1:].zero_()
@@ -277,7 +297,7 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG):
         dW = torch.empty(lay.out_dim[l], lay.in_dim[l], device=dev)
         db = torch.empty(lay.out_dim[l], device=dev)
         ops.wgrad(Zl, U[l], lay.out_dim[l], lay.in_dim[l], dW, db=db,
-                  Y1=S[l] if second else None, X1=Ud[l] if second else None, bf16=bf)
+                  Y1=S[l] if second else None, X1=Ud[l] if second else None, mode=wmode)
         dWs[l], dbs[l] = dW, db
         R[l] = None
     return dWs, dbs
@@ -458,9 +478,7 @@ class ColorPack:
 
 
 def pack_color(lay: ColorLayout, Ws, bs, mfma_dtype: str = "fp32") -> ColorPack:
-    bf = mfma_dtype == "bf16"
-    kq = 64 if bf else 32
-    cv = (lambda t: t.to(torch.bfloat16).contiguous()) if bf else (lambda t: t.contiguous())  # noqa: E731
+    kq, cv = _image_fmt(mfma_dtype)
     with torch.no_grad():
         P, V, Gd, Fd = lay.P, lay.V, lay.Gd, lay.F
         W0 = Ws[0].detach()
@@ -510,7 +528,7 @@ class _ColorFieldFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, drgb):
         lay, pk = ctx.lay, ctx.pk
-        bf = pk.Bf[0].dtype == torch.bfloat16
+        wmode = _wgrad_mode(pk)
         feat, ext, H, rgb = ctx.bufs
         ctx.bufs = None
         nparams = 2 * lay.n_lin
@@ -527,7 +545,7 @@ class _ColorFieldFn(torch.autograd.Function):
         for l in range(n - 2, 0, -1):
             dW = torch.empty(lay.out_dim[l], lay.in_dim[l], device=dev)
             db = torch.empty(lay.out_dim[l], device=dev)
-            ops.wgrad(dZ, H[l - 1], lay.out_dim[l], lay.in_dim[l], dW, db=db, bf16=bf)
+            ops.wgrad(dZ, H[l - 1], lay.out_dim[l], lay.in_dim[l], dW, db=db, mode=wmode)
             dWs[l], dbs[l] = dW, db
             dZp = _empty(M, lay.HL, dev)
             ops.linear(dZ, pk.Bt[l], lay.out_dim[l - 1], rup(lay.out_dim[l], 32), dZp, EPI_BWD_RELU, aux0=H[l - 1],
@@ -536,9 +554,9 @@ class _ColorFieldFn(torch.autograd.Function):
         o0 = lay.out_dim[0]
         dWf = torch.empty(o0, lay.F, device=dev)
         db0 = torch.empty(o0, device=dev)
-        ops.wgrad(dZ, feat, o0, lay.F, dWf, db=db0, bf16=bf)
+        ops.wgrad(dZ, feat, o0, lay.F, dWf, db=db0, mode=wmode)
         dWx = torch.empty(o0, lay.KX, device=dev)
-        ops.wgrad(dZ, ext, o0, lay.KX, dWx, bf16=bf)
+        ops.wgrad(dZ, ext, o0, lay.KX, dWx, mode=wmode)
         P, V, Gd = lay.P, lay.V, lay.Gd
         # back to the reference column order [pts | emb(dirs) | gradients | feature]
         dWs[0] = torch.cat([dWx[:, Gd:Gd + P], dWx[:, Gd + P:Gd + P + V], dWx[:, 0:Gd], dWf], 1)

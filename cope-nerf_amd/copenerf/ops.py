@@ -86,19 +86,35 @@ def _ld(t):
     return 0 if t is None else t.stride(0)
 
 
+def split_bf16x3(W: torch.Tensor) -> torch.Tensor:
+    """[N, K] fp32 -> [N, 3, K] bf16 terms w0 + w1 + w2 = W (each RNE of the
+    remainder; |W - Σ| <= 2^-27 |W|): the B image of CN_MFMA_F32_BF16X6."""
+    w0 = W.to(torch.bfloat16)
+    r = W - w0.float()
+    w1 = r.to(torch.bfloat16)
+    w2 = (r - w1.float()).to(torch.bfloat16)
+    return torch.stack([w0, w1, w2], 1).contiguous()
+
+
 def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None, colv=None, aux0=None,
            aux1=None, out1=None, out_split=None, nsplit=None, nzero=None, adiv=1.0, odiv=1.0, beta=100.0,
            threshold=20.0, tile=None, M=None, kalg=None):
     """out = epilogue((A|A2) @ B[:N].T / adiv) -- cn_linear.  kalg: the unpadded
     inner dimension (for the FLOP count of the kernel timer only).  A bfloat16 B
     selects the bf16 MFMA path (A rounded to bf16 on load, fp32 accumulate); K is
-    then rounded up to 64, so A's columns up to that must exist (zero padding)."""
+    then rounded up to 64, so A's columns up to that must exist (zero padding).
+    A [N, 3, K] bfloat16 B (split_bf16x3) selects CN_MFMA_F32_BF16X6: the fp32
+    GEMM computed from three bf16 terms per operand on the bf16 MFMA."""
+    x6 = B.dim() == 3
+    if x6 and (B.dtype != torch.bfloat16 or B.shape[1] != 3 or B.stride(2) != 1 or B.stride(0) != 3 * B.stride(1)):
+        raise RuntimeError(f"cn_linear: a 3-D B must be split_bf16x3's [N, 3, K] bfloat16 (got {tuple(B.shape)}, "
+                           f"{B.dtype}, strides {B.stride()})")
     for t, n in ((A, "A"), (A2, "A2"), (B, "B"), (out0, "out0"), (out1, "out1"), (aux0, "aux0"),
                  (aux1, "aux1"), (out_split, "out_split")):
-        _need(t, n)
+        _need(t, n, ndim=3 if (x6 and t is B) else 2)
         if t is not None and t is not B and t.dtype == torch.bfloat16:
             raise RuntimeError(f"cn_linear: {n} must be float32 (only B may be bfloat16)")
-    bf = B.dtype == torch.bfloat16
+    bf = B.dtype == torch.bfloat16 and not x6
     if bf:
         K = rup(K, 64)
         K1 = rup(K1, 64) if K1 is not None else None
@@ -111,7 +127,7 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     if tile is None:
         tile = 1 if max(N, nzero or 0) <= 64 else 0
     bn = 64 if tile == 1 else 128
-    if B.shape[0] < rup(N, bn) or B.shape[1] < K:
+    if B.shape[0] < rup(N, bn) or B.shape[-1] < K:
         raise RuntimeError(f"cn_linear: B {tuple(B.shape)} too small for N={N}, K={K} (tile {tile})")
     if out0.shape[0] < M:
         raise RuntimeError("cn_linear: out0 has fewer rows than A")
@@ -119,7 +135,7 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     d.A, d.A2, d.B, d.bias = _ptr(A), _ptr(A2), _ptr(B), _ptr(bias)
     d.rowv, d.colv, d.aux0, d.aux1 = _ptr(rowv), _ptr(colv), _ptr(aux0), _ptr(aux1)
     d.out0, d.out1, d.out_split = _ptr(out0), _ptr(out1), _ptr(out_split)
-    d.lda, d.lda2, d.ldb = _ld(A), _ld(A2), _ld(B)
+    d.lda, d.lda2, d.ldb = _ld(A), _ld(A2), (B.stride(1) if x6 else _ld(B))
     d.ld_aux0, d.ld_aux1, d.ld_out0, d.ld_out1, d.ld_split = _ld(aux0), _ld(aux1), _ld(out0), _ld(out1), _ld(out_split)
     d.M, d.N, d.K = M, N, K
     d.K1 = K1 if K1 is not None else K
@@ -127,20 +143,27 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     d.nsplit = nsplit if nsplit is not None else N
     d.epilogue, d.tile = epilogue, tile
     d.adiv, d.odiv, d.beta, d.threshold = adiv, odiv, beta, threshold
-    d.mfma_dtype = 1 if bf else 0
+    d.mfma_dtype = 2 if x6 else (1 if bf else 0)
     if _timer is not None:
         e0 = _timer.start()
         _lib.check(_lib.load().cn_linear(d, _stream()), "cn_linear")
-        key = ("linear", tile, EPI_NAMES[epilogue]) + (("bf16",) if bf else ())
+        key = ("linear", tile, EPI_NAMES[epilogue]) + (("bf16",) if bf else ("x6",) if x6 else ())
         _timer.stop(key + ((M, N, K),) if _timer.detail else key, e0, 2.0 * M * N * (kalg or K))
     else:
         _lib.check(_lib.load().cn_linear(d, _stream()), "cn_linear")
     return out0
 
 
-def wgrad(Y0, X0, N, K, dW, *, db=None, Y1=None, X1=None, accumulate=False, bf16=False):
+WGRAD_MODES = {"fp32": 0, "bf16": 1, "bf16x6": 2}
+
+
+def wgrad(Y0, X0, N, K, dW, *, db=None, Y1=None, X1=None, accumulate=False, mode="fp32"):
     """dW[:n_out, :k_out] (+)= Y0ᵀX0 (+ Y1ᵀX1), db = colsum(Y0) -- cn_wgrad.
-    bf16=True: operands rounded to bf16 on load (config C3's bf16 MFMA)."""
+    mode: "fp32" (exact fp32 MFMA), "bf16x6" (fp32 from three bf16 terms per
+    operand on the bf16 MFMA) or "bf16" (operands rounded to bf16 on load,
+    config C3's reduced-precision mode)."""
+    if mode not in WGRAD_MODES:
+        raise ValueError(f"wgrad: mode must be one of {tuple(WGRAD_MODES)} (got {mode!r})")
     for t, n in ((Y0, "Y0"), (X0, "X0"), (Y1, "Y1"), (X1, "X1"), (dW, "dW")):
         _need(t, n)
     M = Y0.shape[0]
@@ -156,11 +179,11 @@ def wgrad(Y0, X0, N, K, dW, *, db=None, Y1=None, X1=None, accumulate=False, bf16
     d.npairs = 2 if Y1 is not None else 1
     d.n_out, d.k_out = dW.shape[0], dW.shape[1]
     d.accumulate = 1 if accumulate else 0
-    d.mfma_dtype = 1 if bf16 else 0
+    d.mfma_dtype = WGRAD_MODES[mode]
     if _timer is not None:
         e0 = _timer.start()
         _lib.check(lib.cn_wgrad(d, _stream()), "cn_wgrad")
-        key = ("wgrad", d.npairs) + (("bf16",) if bf16 else ())
+        key = ("wgrad", d.npairs) + (("bf16",) if mode == "bf16" else ("x6",) if mode == "bf16x6" else ())
         _timer.stop(key + ((M, d.n_out, d.k_out),) if _timer.detail else key, e0,
                     2.0 * M * d.n_out * d.k_out * d.npairs)
     else:

@@ -109,11 +109,13 @@ class NeuSRenderer(nn.Module):
             raise NotImplementedError("naive_render (logistic up-sampler) is out of scope; every config uses False")
 
     def set_mfma_dtype(self, dtype: str):
-        """"fp32" (default: exact fp32 MFMA products, the |Δ| <= 1e-4 parity path) or
+        """"fp32" (default: exact fp32 MFMA products, the |Δ| <= 1e-4 parity path),
+        "bf16x6" (fp32 GEMMs on the bf16 MFMA: both operands split into three bf16
+        terms, six term products accumulated in fp32; same parity bar) or
         "bf16" (config C3, "bf16 MLP MFMA": every MLP GEMM rounds its operands to
         bf16 and accumulates in fp32; activations, epilogues, sampling and
         compositing stay fp32)."""
-        if dtype not in ("fp32", "bf16"):
+        if dtype not in ("fp32", "bf16", "bf16x6"):
             raise ValueError(f"mfma dtype {dtype!r}")
         self.sdf_network.mfma_dtype = dtype
         self.color_network.mfma_dtype = dtype

@@ -100,6 +100,33 @@ __device__ __forceinline__ void softplus_hw(float z, float c_exp, float c_thr, f
     sg = lin ? 1.0f : e * __builtin_amdgcn_rcpf(t);
 }
 
+// Three-term bf16 split of 4 fp32 values (CN_MFMA_F32_BF16X6): v = t0 + t1 + t2
+// with every term the RNE bf16 of the remainder.  Written on packed pairs: the
+// bf16 -> fp32 widening of a v_cvt_pk_bf16_f32 result is a shift (low half) and
+// a mask (high half), the remainders are v_pk_add_f32: 18 VALU per 4 values
+// (the per-element convertvector round trip compiles to 30).
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ floatx2 widen_bf16x2(unsigned p) {
+    return floatx2{__builtin_bit_cast(float, p << 16), __builtin_bit_cast(float, p & 0xffff0000u)};
+}
+__device__ __forceinline__ void split3(floatx4 v, bf16x4& t0, bf16x4& t1, bf16x4& t2) {
+    unsigned p0[2], p1[2], p2[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const floatx2 x = {v[2 * h], v[2 * h + 1]};
+        p0[h] = __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf16x2));
+        const floatx2 r = x - widen_bf16x2(p0[h]);
+        p1[h] = __builtin_bit_cast(unsigned, __builtin_convertvector(r, bf16x2));
+        const floatx2 q = r - widen_bf16x2(p1[h]);
+        p2[h] = __builtin_bit_cast(unsigned, __builtin_convertvector(q, bf16x2));
+    }
+    t0 = __builtin_bit_cast(bf16x4, (u32x2){p0[0], p0[1]});
+    t1 = __builtin_bit_cast(bf16x4, (u32x2){p1[0], p1[1]});
+    t2 = __builtin_bit_cast(bf16x4, (u32x2){p2[0], p2[1]});
+}
+
 // Virtual tile vt -> (tm, tn).  XCD-aware: blocks b and b+8 are dispatched to
 // the same XCD, so the T N-tiles of one M-tile are placed 8 apart and share that
 // XCD's L2 copy of the A rows.  Tiles are padded to a multiple of 8 M-tiles.
@@ -114,27 +141,44 @@ __device__ __forceinline__ void tile_coords(int vt, int T, int& tm, int& tn) {
 // virtual tiles; the first K-chunk of the next tile is fetched into registers
 // while the current tile's epilogue runs, so only the first tile of a
 // workgroup pays the cold-start latency.
-// BF = false: A and B fp32, v_mfma_f32_32x32x2_f32, BK fp32 k per chunk.
-// BF = true : A fp32 converted to bf16 (RNE) while staging, B bf16 [N][ldb]
-//             (ldb in bf16 elements), v_mfma_f32_32x32x16_bf16, BK = 64 bf16 k per
-//             chunk.  The LDS image has the same geometry in both modes (rows of
-//             36 dwords: conflict-free ds_read_b128 fragments) and the accumulator
-//             layout of the two MFMAs is the same, so the epilogue is shared.
-template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int EPI, bool ROWV, bool BF>
+// MODE 0: A and B fp32, v_mfma_f32_32x32x2_f32, BK fp32 k per chunk.
+// MODE 1: A fp32 converted to bf16 (RNE) while staging, B bf16 [N][ldb]
+//         (ldb in bf16 elements), v_mfma_f32_32x32x16_bf16, BK = 64 bf16 k per
+//         chunk.  The LDS image has the fp32 geometry (rows of 36 dwords:
+//         conflict-free ds_read_b128 fragments).
+// MODE 2: fp32 GEMM on the bf16 MFMA (CN_MFMA_F32_BF16X6).  Each fp32 operand is
+//         the sum of three bf16 terms x = x0 + x1 + x2 (x0 = bf16(x), x1 =
+//         bf16(x - x0), x2 = bf16(x - x0 - x1), all RNE; |x - Σ| <= 2^-27 |x|);
+//         A is split while staging, B arrives split ([N][3][ldb] bf16).  The six
+//         products with i + j <= 2 are issued (small terms first) into one fp32
+//         accumulator; the three dropped ones are below 2^-26 |a b|, under the
+//         rounding of the fp32 accumulation itself.  BK = 16 k per chunk; an LDS
+//         row holds the three 16-term planes (24 dwords) + 4 pad = 28 dwords
+//         (conflict-free ds_read_b128 over 16 consecutive rows).
+// The accumulator layout of the two MFMAs is the same, so the epilogue is shared.
+#ifndef X6_PAD
+#define X6_PAD 12
+#endif
+template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int EPI, bool ROWV, int MODE>
 __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel(LinearArgs p) {
     constexpr int NT = 64 * WM * WN;
     constexpr int BM = 32 * TM * WM;
     constexpr int BN = 32 * TN * WN;
-    constexpr int LS = (BF ? BK / 2 : BK) + 4;  // padded LDS row in dwords: 36 for BK = 32 (f32) / 64 (bf16)
+    constexpr bool BF = MODE != 0;               // bf16 MFMA (modes 1, 2)
+    constexpr int NPL = MODE == 2 ? 3 : 1;       // bf16 planes per operand
+    // padded LDS row in dwords: 36 for BK = 32 (f32) / 64 (bf16); 28 for BK = 16 (split)
+    constexpr int LS = (BF ? NPL * BK / 2 : BK) + (MODE == 2 ? X6_PAD : 4);
     constexpr int KC4 = BK / 4;                  // A: fp32 float4 per staged row
     static_assert(NT % KC4 == 0, "staging rows");
     constexpr int RSTEP = NT / KC4;  // staged A rows per load instruction
-    constexpr int KCB = BF ? BK / 8 : BK / 4;    // B: 16-byte pieces per staged row
-    constexpr int RSTEPB = NT / KCB;
-    static_assert(BM % RSTEP == 0 && BN % RSTEPB == 0, "tile/thread mismatch");
+    constexpr int KCB = BF ? NPL * BK / 8 : BK / 4;  // B: 16-byte pieces per staged row (all planes)
+    // modes 0/1: B rows tid/KCB + q*RSTEPB; mode 2 (6 pieces per row): piece tid + q*NT
+    constexpr int RSTEPB = MODE == 2 ? 1 : NT / KCB;
+    static_assert(BM % RSTEP == 0 && (MODE == 2 || (NT % KCB == 0 && BN % RSTEPB == 0)), "tile/thread mismatch");
     constexpr int ALD = BM / RSTEP;
-    constexpr int BLD = BN / RSTEPB;
+    constexpr int BLD = MODE == 2 ? (BN * KCB + NT - 1) / NT : BN / RSTEPB;
     constexpr int ESZB = BF ? 2 : 4;             // bytes per B element
+    constexpr int PIECES_PL = BK / 8;            // MODE 2: 16-byte pieces per plane of a staged row
     constexpr int CS = BN + 4;
     constexpr int LDS_FLOATS = 2 * (BM + BN) * LS;
     // the epilogue parks the C tile in the staging LDS, in NPART row slabs if it does not fit
@@ -166,7 +210,14 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         voA2[q] = ((srow + q * RSTEP) * p.lda2 + sc4 * 4) * 4;
     }
 #pragma unroll
-    for (int q = 0; q < BLD; ++q) voB[q] = (srowb + q * RSTEPB) * p.ldb * ESZB + scb * 16;
+    for (int q = 0; q < BLD; ++q) {
+        if constexpr (MODE == 2) {  // piece pc = plane * PIECES_PL + half; a B row is 3 planes of ldb
+            const int idx = tid + q * NT, row = idx / KCB, pc = idx % KCB;
+            voB[q] = idx < BN * KCB ? row * 3 * p.ldb * 2 + (pc / PIECES_PL) * p.ldb * 2 + (pc % PIECES_PL) * 16 : 0;
+        } else {
+            voB[q] = (srowb + q * RSTEPB) * p.ldb * ESZB + scb * 16;
+        }
+    }
     // LDS write offsets in dwords: A as fp32 float4 (4 dwords) or bf16x4 (2 dwords); B 16-byte pieces
     const int lds_a = srow * LS + sc4 * (BF ? 2 : 4);
     const int lds_b = srowb * LS + scb * 4;
@@ -187,8 +238,8 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 #pragma unroll
         for (int q = 0; q < ALD; ++q) ra[set][q] = bload4(rA, second ? voA2[q] : voA[q], ak * 4);
         const rsrc_t rB = make_view(reinterpret_cast<const float*>(reinterpret_cast<const char*>(p.B) +
-                                                                   (int64_t)n0 * p.ldb * ESZB),
-                                    valid ? BN * p.ldb * ESZB : 0);
+                                                                   (int64_t)n0 * NPL * p.ldb * ESZB),
+                                    valid ? BN * NPL * p.ldb * ESZB : 0);
 #pragma unroll
         for (int q = 0; q < BLD; ++q) rb[set][q] = bload4(rB, voB[q], k0 * ESZB);
     };
@@ -197,13 +248,27 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         float* b = sB + buf * BN * LS + lds_b;
 #pragma unroll
         for (int q = 0; q < ALD; ++q) {
-            if constexpr (BF)
+            if constexpr (MODE == 2) {
+                bf16x4 x0, x1, x2;
+                split3(ra[set][q], x0, x1, x2);
+                *reinterpret_cast<bf16x4*>(a + q * RSTEP * LS) = x0;
+                *reinterpret_cast<bf16x4*>(a + q * RSTEP * LS + BK / 2) = x1;
+                *reinterpret_cast<bf16x4*>(a + q * RSTEP * LS + BK) = x2;
+            } else if constexpr (BF)
                 *reinterpret_cast<bf16x4*>(a + q * RSTEP * LS) = __builtin_convertvector(ra[set][q], bf16x4);
             else
                 *reinterpret_cast<floatx4*>(a + q * RSTEP * LS) = ra[set][q];
         }
 #pragma unroll
-        for (int q = 0; q < BLD; ++q) *reinterpret_cast<floatx4*>(b + q * RSTEPB * LS) = rb[set][q];
+        for (int q = 0; q < BLD; ++q) {
+            if constexpr (MODE == 2) {
+                const int idx = tid + q * NT;
+                if (BN * KCB % NT == 0 || idx < BN * KCB)  // wave-uniform (NT, BN*KCB multiples of 64)
+                    *reinterpret_cast<floatx4*>(sB + buf * BN * LS + (idx / KCB) * LS + (idx % KCB) * 4) = rb[set][q];
+            } else {
+                *reinterpret_cast<floatx4*>(b + q * RSTEPB * LS) = rb[set][q];
+            }
+        }
     };
     auto next_valid = [&](int vt) {
         for (; vt < ntiles; vt += gridDim.x) {
@@ -265,7 +330,36 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
         auto compute = [&](int cur) {
-            if constexpr (BF) {
+            if constexpr (MODE == 2) {
+                const float* a_base = sA + cur * BM * LS + arow * LS + 4 * (lane >> 5);
+                const float* b_base = sB + cur * BN * LS + brow * LS + 4 * (lane >> 5);
+#pragma unroll
+                for (int ks = 0; ks < BK / 16; ++ks) {
+                    bf16x8 af[3][TM], bf[3][TN];
+#pragma unroll
+                    for (int t = 0; t < 3; ++t) {
+#pragma unroll
+                        for (int i = 0; i < TM; ++i)
+                            af[t][i] = *reinterpret_cast<const bf16x8*>(a_base + i * 32 * LS + t * (BK / 2) + ks * 8);
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+                            bf[t][j] = *reinterpret_cast<const bf16x8*>(b_base + j * 32 * LS + t * (BK / 2) + ks * 8);
+                    }
+                    // term pairs (ta, tb), ta + tb <= 2, in the order the fragments
+                    // arrive (t = 0 first): the first MFMAs wait only for a0, b0
+                    constexpr int TA[6] = {0, 1, 0, 2, 1, 0};
+                    constexpr int TB[6] = {0, 0, 1, 0, 1, 2};
+#pragma unroll
+                    for (int u = 0; u < 6; ++u)
+#pragma unroll
+                        for (int i = 0; i < TM; ++i)
+#pragma unroll
+                            for (int j = 0; j < TN; ++j)
+                                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[TA[u]][i], bf[TB[u]][j], acc[i][j],
+                                                                                     0, 0, 0);
+                }
+                return;
+            } else if constexpr (BF) {
                 // lane half h holds k = 8h + j of each 16-deep MFMA step (8 bf16 = 4 dwords)
                 const float* a_base = sA + cur * BM * LS + arow * LS + 4 * (lane >> 5);
                 const float* b_base = sB + cur * BN * LS + brow * LS + 4 * (lane >> 5);
@@ -777,6 +871,155 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) wgrad_bf16_kernel(WgradArgs p
     }
 }
 
+// fp32 weight gradient on the bf16 MFMA (CN_MFMA_F32_BF16X6), 128x128 output
+// tiles: Y and X are split into three bf16 terms while staging (split3) and the
+// six term products with i + j <= 2 accumulate in fp32, as in linear_kernel
+// MODE 2.  Staging is transposed like wgrad_bf16_kernel's, 32 sample rows per
+// chunk: thread t holds m-quad t % 8 of column group t / 8 (4 m x 4 columns of
+// Y and of X), so 16 contiguous lanes write two LDS rows 4 apart whose 64-byte
+// segments fall on the two halves of the 32 write banks; an LDS row is the three
+// 16-dword term planes + 4 pad (52 dwords: the ds_read_b128 fragment reads of 16
+// consecutive rows hit 16 distinct bank quads).  One LDS buffer (53 KB, two
+// workgroups per CU): the next chunk's loads fly during the MFMAs.
+__global__ void __launch_bounds__(256, 2) wgrad_x6_kernel(WgradArgs p) {
+    constexpr int TM = 2, TN = 2, WN = 2;
+    constexpr int BNo = 128, BKo = 128, MC = 32, MQ = MC / 4;
+    constexpr int PL = MC / 2;       // dwords per term plane of a row
+    constexpr int LSB = 3 * PL + 4;  // 52
+    static_assert(MQ * (BNo / 4) == 256 && MQ * (BKo / 4) == 256, "staging geometry");
+    static_assert(MQ * BNo <= (BNo + BKo) * LSB, "bias partials fit in LDS");
+    __shared__ __attribute__((aligned(16))) float smem[(BNo + BKo) * LSB];
+    float* sY = smem;
+    float* sX = smem + BNo * LSB;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave / WN;
+    const int wn = wave % WN;
+    const int T = p.n_tiles_n * p.n_tiles_k;
+    const int b = blockIdx.x;
+    const int tile = (b >> 3) % T;
+    const int slice = (b & 7) + 8 * ((b >> 3) / T);
+    if (slice >= p.nslices) return;
+    const int tn = tile / p.n_tiles_k;
+    const int tk = tile % p.n_tiles_k;
+    const int n0 = tn * BNo;
+    const int k0 = tk * BKo;
+    const int mbeg = slice * p.rows_per_slice;
+    const int mend = min(p.M, mbeg + p.rows_per_slice);
+    const int nch = mend > mbeg ? cdiv(mend - mbeg, MC) : 0;
+    const int total = nch * p.npairs;
+    const bool do_bias = (tk == 0) && (p.bpart != nullptr);
+
+    const int mq = tid % MQ, cg = tid / MQ;
+    floatx4 ry[4], rx[4];
+    float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+    auto gload = [&](int c) {
+        const int pair = c >= nch;
+        const int mrow = mbeg + (c - pair * nch) * MC;
+        const float* Y = pair ? p.Y1 : p.Y0;
+        const float* X = pair ? p.X1 : p.X0;
+        const int ly = pair ? p.ldy1 : p.ldy0;
+        const int lx = pair ? p.ldx1 : p.ldx0;
+        const int nrows = min(MC, mend - mrow);
+        const rsrc_t vY = make_view(Y + (int64_t)mrow * ly + n0, (nrows * ly - n0) * 4);
+        const rsrc_t vX = make_view(X + (int64_t)mrow * lx + k0, (nrows * lx - k0) * 4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ry[r] = bload4(vY, ((mq * 4 + r) * ly + cg * 4) * 4, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rx[r] = bload4(vX, ((mq * 4 + r) * lx + cg * 4) * 4, 0);
+    };
+    auto lstore = [&](bool bias) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const floatx4 col = {ry[0][e], ry[1][e], ry[2][e], ry[3][e]};
+            if (bias) bsum[e] += (col[0] + col[1]) + (col[2] + col[3]);
+            bf16x4 t0, t1, t2;
+            split3(col, t0, t1, t2);
+            float* y = sY + (cg * 4 + e) * LSB + mq * 2;
+            *reinterpret_cast<bf16x4*>(y) = t0;
+            *reinterpret_cast<bf16x4*>(y + PL) = t1;
+            *reinterpret_cast<bf16x4*>(y + 2 * PL) = t2;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const floatx4 col = {rx[0][e], rx[1][e], rx[2][e], rx[3][e]};
+            bf16x4 t0, t1, t2;
+            split3(col, t0, t1, t2);
+            float* x = sX + (cg * 4 + e) * LSB + mq * 2;
+            *reinterpret_cast<bf16x4*>(x) = t0;
+            *reinterpret_cast<bf16x4*>(x + PL) = t1;
+            *reinterpret_cast<bf16x4*>(x + 2 * PL) = t2;
+        }
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+    const int h = lane >> 5;
+    const float* yb = sY + (wm * TM * 32 + (lane & 31)) * LSB + 4 * h;
+    const float* xb = sX + (wn * TN * 32 + (lane & 31)) * LSB + 4 * h;
+    if (total > 0) gload(0);
+    for (int c = 0; c < total; ++c) {
+        if (c > 0) __syncthreads();  // the previous chunk's fragment reads are done
+        lstore(do_bias && c < nch);
+        __syncthreads();
+        if (c + 1 < total) gload(c + 1);
+#pragma unroll
+        for (int ks = 0; ks < MC / 16; ++ks) {
+            bf16x8 af[3][TM], bf[3][TN];
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i) af[t][i] = *reinterpret_cast<const bf16x8*>(yb + i * 32 * LSB + t * PL + ks * 8);
+#pragma unroll
+                for (int j = 0; j < TN; ++j) bf[t][j] = *reinterpret_cast<const bf16x8*>(xb + j * 32 * LSB + t * PL + ks * 8);
+            }
+            constexpr int TA[6] = {0, 1, 0, 2, 1, 0};
+            constexpr int TB[6] = {0, 0, 1, 0, 1, 2};
+#pragma unroll
+            for (int u = 0; u < 6; ++u)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[TA[u]][i], bf[TB[u]][j], acc[i][j], 0, 0, 0);
+        }
+    }
+    __syncthreads();  // LDS is reused for the bias partials
+
+    const rsrc_t vP = make_view(p.part + (int64_t)slice * p.Npad * p.Kpad, p.Npad * p.Kpad * 4);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = k0 + wn * TN * 32 + j * 32 + (lane & 31);
+            const int rbase = n0 + wm * TM * 32 + i * 32 + 4 * (lane >> 5);
+            const int vo = (rbase * p.Kpad + col) * 4;
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                bstore1(vP, vo, ((r & 3) + 8 * (r >> 2)) * p.Kpad * 4, acc[i][j][r]);
+        }
+    }
+    if (do_bias) {  // reduce the per-thread column partials over the m-quads (fixed order)
+        float* red = smem;  // [MQ][BNo]
+#pragma unroll
+        for (int e = 0; e < 4; ++e) red[mq * BNo + cg * 4 + e] = bsum[e];
+        __syncthreads();
+        if (tid < BNo) {
+            float t = 0.0f;
+            for (int q = 0; q < MQ; ++q) t += red[q * BNo + tid];
+            p.bpart[(int64_t)slice * p.Npad + n0 + tid] = t;
+        }
+    }
+}
+
 // Sum of nslab fp32 slabs: out[r*ldo + c] (+)= (sum_s part[s*stride + r*ldp + c]) / div
 // for r < rows, c < cols.  A workgroup owns 64 float4 column groups x 4 slab
 // groups; each thread sums its slab group in double with 4 loads in flight, the 4
@@ -1003,7 +1246,7 @@ static int g_linear_variant = [] {
     return e ? atoi(e) : 0;
 }();
 
-template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, bool BF = false>
+template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int MODE = 0>
 static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_t s) {
     constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
     a.n_tiles_m = cdiv(d->M, BM);
@@ -1019,8 +1262,8 @@ static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_
     switch (d->epilogue) {
 #define CN_EPI_CASE(E)                                                                     \
         case E:                                                                            \
-            if (d->rowv) linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, E, true, BF><<<grid, block, 0, s>>>(a); \
-            else linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, E, false, BF><<<grid, block, 0, s>>>(a);        \
+            if (d->rowv) linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, E, true, MODE><<<grid, block, 0, s>>>(a); \
+            else linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, E, false, MODE><<<grid, block, 0, s>>>(a);        \
             break;
         CN_EPI_CASE(CN_EPI_STORE)
         CN_EPI_CASE(CN_EPI_SOFTPLUS)
@@ -1030,7 +1273,7 @@ static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_
         CN_EPI_CASE(CN_EPI_BWD_SOFTPLUS)
         CN_EPI_CASE(CN_EPI_BWD_RELU)
 #undef CN_EPI_CASE
-        case 7: linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, 7, false, BF><<<grid, block, 0, s>>>(a); break;
+        case 7: linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, 7, false, MODE><<<grid, block, 0, s>>>(a); break;
         default: set_error("cn_linear: bad epilogue %d", d->epilogue); return CN_ERR_ARG;
     }
     return check_launch("cn_linear");
@@ -1042,16 +1285,17 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     CN_REQUIRE(d, CN_ERR_ARG, "cn_linear: null desc");
     CN_REQUIRE(d->A && d->B && d->out0, CN_ERR_ARG, "cn_linear: A, B and out0 are required");
     CN_REQUIRE(d->M >= 0 && d->N > 0 && d->K > 0, CN_ERR_SHAPE, "cn_linear: bad M/N/K %d/%d/%d", d->M, d->N, d->K);
-    CN_REQUIRE(d->mfma_dtype == CN_MFMA_F32 || d->mfma_dtype == CN_MFMA_BF16, CN_ERR_ARG,
-               "cn_linear: bad mfma_dtype %d", d->mfma_dtype);
+    CN_REQUIRE(d->mfma_dtype == CN_MFMA_F32 || d->mfma_dtype == CN_MFMA_BF16 || d->mfma_dtype == CN_MFMA_F32_BF16X6,
+               CN_ERR_ARG, "cn_linear: bad mfma_dtype %d", d->mfma_dtype);
     const bool bf = d->mfma_dtype == CN_MFMA_BF16;
+    const bool x6 = d->mfma_dtype == CN_MFMA_F32_BF16X6;
     CN_REQUIRE(d->K % (bf ? 64 : 32) == 0, CN_ERR_SHAPE, "cn_linear: K=%d must be a multiple of %d", d->K, bf ? 64 : 32);
     CN_REQUIRE(d->tile == 0 || d->tile == 1, CN_ERR_ARG, "cn_linear: bad tile %d", d->tile);
     const int K1 = d->A2 ? d->K1 : d->K;
     CN_REQUIRE(K1 > 0 && K1 <= d->K && K1 % (bf ? 64 : 32) == 0, CN_ERR_SHAPE, "cn_linear: bad K1=%d", K1);
     CN_REQUIRE(d->lda >= K1 && d->lda % 4 == 0 && al16(d->A), CN_ERR_ALIGN, "cn_linear: A must be 16B aligned with lda>=K1, lda%%4==0");
     if (d->A2) CN_REQUIRE(d->lda2 >= d->K - K1 && d->lda2 % 4 == 0 && al16(d->A2), CN_ERR_ALIGN, "cn_linear: bad A2/lda2");
-    CN_REQUIRE(d->ldb >= d->K && d->ldb % (bf ? 8 : 4) == 0 && al16(d->B), CN_ERR_ALIGN, "cn_linear: bad B/ldb");
+    CN_REQUIRE(d->ldb >= d->K && d->ldb % (bf || x6 ? 8 : 4) == 0 && al16(d->B), CN_ERR_ALIGN, "cn_linear: bad B/ldb");
     const int nzero = std::max(d->nzero, d->N);
     const int bn = d->tile == 0 ? 128 : 64;
     CN_REQUIRE(nzero <= cdiv(d->N, bn) * bn, CN_ERR_SHAPE,
@@ -1100,8 +1344,12 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     a.threshold = d->threshold;
     hipStream_t s = (hipStream_t)stream;
     if (bf) {
-        if (d->tile == 0) return launch_linear_tile<2, 2, 2, 2, 64, 2, 1, true>(d, a, s);
-        return launch_linear_tile<4, 1, 1, 2, 64, 2, 1, true>(d, a, s);
+        if (d->tile == 0) return launch_linear_tile<2, 2, 2, 2, 64, 2, 1, 1>(d, a, s);
+        return launch_linear_tile<4, 1, 1, 2, 64, 2, 1, 1>(d, a, s);
+    }
+    if (x6) {  // K % 32 == 0: an even number of 16-deep chunks for the 2-deep prefetch
+        if (d->tile == 0) return launch_linear_tile<2, 2, 2, 2, 16, 2, 2, 2>(d, a, s);
+        return launch_linear_tile<4, 1, 1, 2, 16, 2, 2, 2>(d, a, s);
     }
     const bool even = (d->K % 64) == 0;  // DEPTH-2 prefetch consumes K in pairs of 32-chunks
     if (d->tile == 0) {
@@ -1149,9 +1397,11 @@ extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
     a.n_tiles_n = Npad / 128;
     a.nslices = ns;
     dim3 grid(cdiv(ns, 8) * 8 * a.n_tiles_n * a.n_tiles_k);
-    CN_REQUIRE(d->mfma_dtype == CN_MFMA_F32 || d->mfma_dtype == CN_MFMA_BF16, CN_ERR_ARG,
-               "cn_wgrad: bad mfma_dtype %d", d->mfma_dtype);
-    if (d->mfma_dtype == CN_MFMA_BF16) {
+    CN_REQUIRE(d->mfma_dtype == CN_MFMA_F32 || d->mfma_dtype == CN_MFMA_BF16 || d->mfma_dtype == CN_MFMA_F32_BF16X6,
+               CN_ERR_ARG, "cn_wgrad: bad mfma_dtype %d", d->mfma_dtype);
+    if (d->mfma_dtype == CN_MFMA_F32_BF16X6 && tile == 0) {
+        wgrad_x6_kernel<<<grid, 256, 0, s>>>(a);
+    } else if (d->mfma_dtype == CN_MFMA_BF16) {
         if (tile == 0)
             wgrad_bf16_kernel<2, 2, 2, 2><<<grid, 256, 0, s>>>(a);
         else

@@ -91,11 +91,15 @@ typedef struct cn_linear_desc {
     int32_t mfma_dtype;  /* CN_MFMA_F32: A, B fp32, exact fp32 products (v_mfma_f32_32x32x2_f32);
                             CN_MFMA_BF16: A fp32 rounded to bf16 (RNE) on load, B bf16 [N][ldb]
                             (ldb in bf16 elements), fp32 accumulate (v_mfma_f32_32x32x16_bf16);
-                            K and K1 multiples of 64 (config C3's bf16 MLP MFMA) */
+                            K and K1 multiples of 64 (config C3's bf16 MLP MFMA);
+                            CN_MFMA_F32_BF16X6: fp32 GEMM on the bf16 MFMA: A fp32 split on load
+                            into three bf16 terms, B pre-split [N][3][ldb] bf16 (plane t of row n
+                            at B + (3n + t) ldb), six term products accumulated in fp32
+                            (error at the level of fp32 accumulation; K, K1 multiples of 32) */
     int32_t reserved_;
 } cn_linear_desc;
 
-enum cn_mfma_dtype { CN_MFMA_F32 = 0, CN_MFMA_BF16 = 1 };
+enum cn_mfma_dtype { CN_MFMA_F32 = 0, CN_MFMA_BF16 = 1, CN_MFMA_F32_BF16X6 = 2 };
 
 int cn_linear(const cn_linear_desc* d, cn_stream_t stream);
 
@@ -122,7 +126,9 @@ typedef struct cn_wgrad_desc {
     int32_t accumulate;  /* 1: dW += result (db too), 0: dW = result */
     int32_t mfma_dtype;  /* CN_MFMA_F32, or CN_MFMA_BF16: Y and X rounded to bf16 (RNE) on load,
                             v_mfma_f32_32x32x16_bf16, fp32 accumulation and slab reduction;
-                            db is summed from the fp32 values either way */
+                            db is summed from the fp32 values either way;
+                            CN_MFMA_F32_BF16X6: fp32 gradient from three bf16 terms per operand
+                            (six products) on 128x128 output tiles, exact fp32 MFMA on 64-wide ones */
 } cn_wgrad_desc;
 
 size_t cn_wgrad_workspace_bytes(int32_t M, int32_t N, int32_t K);

@@ -76,7 +76,7 @@ def test_wgrad_bf16(M, N, K, pairs):
     Y1, X1 = (_rnd(M, ldn, seed=17), _rnd(M, ldk, seed=18)) if pairs == 2 else (None, None)
     dW = torch.empty(N, K, device=DEV)
     db = torch.empty(N, device=DEV)
-    ops.wgrad(Y0, X0, N, K, dW, db=db, Y1=Y1, X1=X1, bf16=True)
+    ops.wgrad(Y0, X0, N, K, dW, db=db, Y1=Y1, X1=X1, mode="bf16")
     r = lambda t, n: t[:, :n].bfloat16().double()  # noqa: E731
     ref = r(Y0, N).t() @ r(X0, K)
     if pairs == 2:
@@ -85,7 +85,7 @@ def test_wgrad_bf16(M, N, K, pairs):
     torch.testing.assert_close(dW, ref.float(), rtol=1e-4, atol=tol)
     torch.testing.assert_close(db, Y0[:, :N].double().sum(0).float(), rtol=1e-4, atol=tol)
     dW2 = torch.empty_like(dW)
-    ops.wgrad(Y0, X0, N, K, dW2, Y1=Y1, X1=X1, bf16=True)
+    ops.wgrad(Y0, X0, N, K, dW2, Y1=Y1, X1=X1, mode="bf16")
     assert torch.equal(dW, dW2)
 
 

@@ -12,10 +12,15 @@ DEV = "cuda"
 TOL_RGB_DEPTH = 1e-4
 
 
-def _renderer(mods):
+# the two fp32 GEMM modes: exact fp32 MFMA products, and fp32 operands split into
+# three bf16 terms on the bf16 MFMA (both held to the same bars)
+FP32_MODES = ["fp32", "bf16x6"]
+
+
+def _renderer(mods, mode="fp32"):
     from copenerf import NeuSRenderer
     sdf, col, dev = mods
-    return NeuSRenderer(None, sdf, dev, col, None, **REN_CFG).to(DEV)
+    return NeuSRenderer(None, sdf, dev, col, None, **REN_CFG).to(DEV).set_mfma_dtype(mode)
 
 
 def _run(r, fx):
@@ -24,11 +29,12 @@ def _run(r, fx):
              cos_anneal_ratio=float(fx["car"]), it=0, eval=bool(fx["eval"]), t_rand=g("t_rand"))
 
 
+@pytest.mark.parametrize("mode", FP32_MODES)
 @pytest.mark.parametrize("name", ["render_small_train", "render_small_eval", "render_full_train"])
-def test_render_matches_reference_golden(name):
+def test_render_matches_reference_golden(name, mode):
     fx = fixture(name)
     mods = build_modules(int(fx["seed"]), int(fx["dh_sdf"]), int(fx["dh_col"]), device=DEV)
-    r = _renderer(mods)
+    r = _renderer(mods, mode)
     out = _run(r, fx)
     for k in ("color_fine", "depth_pred"):
         err = (out[k].detach().cpu() - fx["out_" + k]).abs().max().item()
@@ -53,7 +59,7 @@ def test_render_matches_reference_golden(name):
             check_grad(n, gr, fx, rtol=2e-2, atol=2e-4 * (gr.abs().max().item() + 1e-3))
 
 
-def _oracle_case(R, dh, seed=55):
+def _oracle_case(R, dh, seed=55, mode="fp32"):
     g = torch.Generator().manual_seed(R)
     mods_cpu = build_modules(seed, dh, dh)
     P, Pc, var, leaves = oracle_params(*mods_cpu)
@@ -66,16 +72,17 @@ def _oracle_case(R, dh, seed=55):
     t_rand = torch.rand(R, 64, generator=g)
     torch.set_num_threads(8)
     ref = O.render(P, Pc, var, o, d, nrm, t, near, far, car=0.5, t_rand=t_rand)
-    r = _renderer(build_modules(seed, dh, dh, device=DEV))
+    r = _renderer(build_modules(seed, dh, dh, device=DEV), mode)
     args = tuple(x.to(DEV) for x in (o, d, nrm, t, near, far))
     return ref, r, args, t_rand.to(DEV), (o, d)
 
 
+@pytest.mark.parametrize("mode", FP32_MODES)
 @pytest.mark.parametrize("R", [256, 2048])
-def test_render_core_matches_oracle_on_identical_samples(R):
+def test_render_core_matches_oracle_on_identical_samples(R, mode):
     """The north-star parity bar, |Δ rgb|, |Δ depth| <= 1e-4 (fp32), for every ray,
     with the sample positions held identical (the oracle's z-values)."""
-    ref, r, args, t_rand, _ = _oracle_case(R, 256)
+    ref, r, args, t_rand, _ = _oracle_case(R, 256, mode=mode)
     out = r(*args, cos_anneal_ratio=0.5, it=0, eval=False, z_vals=ref["z_vals"].to(DEV))
     for k in ("color_fine", "depth_pred"):
         err = (out[k].detach().cpu() - ref[k].detach()).abs().max().item()
@@ -83,8 +90,9 @@ def test_render_core_matches_oracle_on_identical_samples(R):
     torch.testing.assert_close(out["weights"].detach().cpu(), ref["weights"].detach(), rtol=1e-3, atol=2e-5)
 
 
+@pytest.mark.parametrize("mode", FP32_MODES)
 @pytest.mark.parametrize("R", [256, 1024])
-def test_render_end_to_end_matches_oracle(R):
+def test_render_end_to_end_matches_oracle(R, mode):
     """Full path incl. the hierarchical sampler.  Sample positions come from a
     searchsorted on an SDF-derived cdf (neus_renderer.py:56), so a last-ulp SDF
     difference can move an importance sample to a neighbouring bin; the reference's
@@ -92,7 +100,7 @@ def test_render_end_to_end_matches_oracle(R):
     samples all agree to 1e-5 must meet 1e-5; rays with a moved sample must stay
     <= 5e-4, at most 0.5 % of rays may exceed the 1e-4 bar, and at most 10 % of
     rays may see a bin jump (> 1e-4) of an importance sample."""
-    ref, r, args, t_rand, (o, d) = _oracle_case(R, 256)
+    ref, r, args, t_rand, (o, d) = _oracle_case(R, 256, mode=mode)
     out = r(*args, cos_anneal_ratio=0.5, it=0, eval=False, t_rand=t_rand)
     de = (out["depth_pred"].detach().cpu() - ref["depth_pred"].detach()).abs().squeeze(1)
     ce = (out["color_fine"].detach().cpu() - ref["color_fine"].detach()).abs().max(1)[0]

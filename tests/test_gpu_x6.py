@@ -1,0 +1,132 @@
+"""fp32 GEMMs on the bf16 MFMA (CN_MFMA_F32_BF16X6): both operands split into
+three bf16 terms, the six term products with i + j <= 2 accumulated in fp32.
+
+The bar is the native fp32 MFMA path's own accuracy: against a float64 GEMM of
+the unrounded fp32 operands, the split path's error must stay within a small
+factor of the exact-product fp32 MFMA's error on the same inputs, every
+epilogue and both tiles.  (Renderer-level parity of this mode against the
+reference golden vectors and the oracle at |Δ| <= 1e-4 runs in
+test_gpu_render.py, parametrized over FP32_MODES.)"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rnd(*s, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return ((torch.rand(*s, generator=g) * 2 - 1) * scale).to(DEV)
+
+
+def test_split_terms_reconstruct():
+    from copenerf import ops
+    W = _rnd(256, 320, seed=1) * torch.logspace(-6, 3, 320, device=DEV)
+    S = ops.split_bf16x3(W)
+    assert S.shape == (256, 3, 320) and S.dtype == torch.bfloat16
+    rec = S[:, 0].double() + S[:, 1].double() + S[:, 2].double()
+    rel = ((rec - W.double()).abs() / W.double().abs().clamp_min(1e-30)).max().item()
+    assert rel <= 2.0 ** -26, rel
+
+
+@pytest.mark.parametrize("M,N,K,tile", [(1000, 256, 256, 0), (130, 204, 256, 0), (777, 52, 256, 1),
+                                        (64, 256, 64, 0), (4096, 128, 192, 0), (300, 64, 288, 1)])
+def test_linear_x6_store_matches_fp32_accuracy(M, N, K, tile):
+    from copenerf import ops
+    A = _rnd(M, K, seed=2)
+    bn = 64 if tile else 128
+    B = torch.zeros(ops.rup(N, bn), K, device=DEV)
+    B[:N] = _rnd(N, K, seed=3, scale=0.1)
+    bias = _rnd(N, seed=4)
+    ld = ops.rup(N, bn)
+    exact = A.double() @ B[:N].double().t() + bias.double()
+    o32 = torch.empty(M, ld, device=DEV)
+    ops.linear(A, B, N, K, o32, ops.EPI_STORE, bias=bias, nzero=ld, tile=tile)
+    o6 = torch.full((M, ld), float("nan"), device=DEV)
+    ops.linear(A, ops.split_bf16x3(B), N, K, o6, ops.EPI_STORE, bias=bias, nzero=ld, tile=tile)
+    e32 = (o32[:, :N].double() - exact).abs()
+    e6 = (o6[:, :N].double() - exact).abs()
+    scale = exact.abs().max().item()
+    print(f"fp32 MFMA max {e32.max().item():.3e} mean {e32.mean().item():.3e} | "
+          f"bf16x6 max {e6.max().item():.3e} mean {e6.mean().item():.3e} (|C| max {scale:.2f})")
+    assert e6.max().item() <= 2.0 * e32.max().item() + 1e-7 * scale
+    assert e6.mean().item() <= 1.5 * e32.mean().item() + 1e-8 * scale
+    assert torch.all(o6[:, N:] == 0)
+
+
+def test_linear_x6_epilogues_and_concat():
+    from copenerf import ops
+    M, K1, K2, N = 517, 256, 64, 256
+    A, A2 = _rnd(M, K1, seed=5, scale=0.3), _rnd(M, K2, seed=6, scale=0.3)
+    B = _rnd(N, K1 + K2, seed=7, scale=0.05)
+    Bs = ops.split_bf16x3(B)
+    bias = _rnd(N, seed=8, scale=0.3)
+    aux0, aux1 = torch.rand(M, N, device=DEV), _rnd(M, N, seed=9)
+    for epi, kw in ((ops.EPI_SOFTPLUS, dict(bias=bias, out1=True)), (ops.EPI_TANGENT, dict(aux0=aux0, aux1=aux1, out1=True)),
+                    (ops.EPI_BWD_SOFTPLUS, dict(aux0=aux0, aux1=aux1)), (ops.EPI_RELU, dict(bias=bias)),
+                    (ops.EPI_MUL, dict(aux0=aux0)), (ops.EPI_BWD_RELU, dict(aux0=aux1))):
+        outs = []
+        for Bimg in (B, Bs):
+            o0 = torch.empty(M, N, device=DEV)
+            o1 = torch.empty(M, N, device=DEV) if kw.get("out1") else None
+            args = {k: v for k, v in kw.items() if k != "out1"}
+            ops.linear(A, Bimg, N, K1 + K2, o0, epi, A2=A2, K1=K1, out1=o1, **args)
+            outs.append((o0, o1))
+        (a0, a1), (b0, b1) = outs
+        torch.testing.assert_close(b0, a0, rtol=2e-5, atol=2e-6 if epi != ops.EPI_TANGENT else 2e-5)
+        if a1 is not None:
+            torch.testing.assert_close(b1, a1, rtol=1e-4, atol=1e-5 if epi != ops.EPI_TANGENT else 1e-3)
+
+
+def test_sdf_field_x6_gradients_match_fp32():
+    """SDF forward, ∇ₓSDF and the double backward in bf16x6 mode against the fp32
+    mode on the same weights and points."""
+    from copenerf import SDFNetwork
+    from helpers import SDF_CFG
+    torch.manual_seed(3)
+    net = SDFNetwork(**SDF_CFG).to(DEV)
+    x = (torch.rand(8192, 4, device=DEV) * 2 - 1)
+    res = {}
+    for mode in ("fp32", "bf16x6"):
+        net.mfma_dtype = mode
+        sdf, feat, g = net.field(x)
+        loss = ((g.norm(dim=-1) - 1) ** 2).mean() + sdf.abs().mean() + 1e-2 * feat.square().mean()
+        grads = torch.autograd.grad(loss, list(net.parameters()))
+        res[mode] = (sdf.detach(), g.detach(), grads)
+    a, b = res["fp32"], res["bf16x6"]
+    torch.testing.assert_close(b[0], a[0], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(b[1], a[1], rtol=1e-4, atol=1e-4)
+    for ga, gb in zip(a[2], b[2]):
+        torch.testing.assert_close(gb, ga, rtol=1e-3, atol=1e-5 * (ga.abs().max().item() + 1e-6))
+
+
+@pytest.mark.parametrize("M,N,K,pairs", [(70000, 256, 256, 2), (1000, 204, 64, 1), (5, 256, 256, 1),
+                                         (4097, 256, 320, 1), (300, 52, 192, 2), (33, 128, 128, 2)])
+def test_wgrad_x6_matches_fp32_accuracy(M, N, K, pairs):
+    """cn_wgrad in bf16x6 mode: dW's error against float64 within a small factor
+    of the exact fp32 MFMA kernel's on the same inputs; db (summed from the fp32
+    values in both modes) within fp32 rounding; deterministic."""
+    from copenerf import ops
+    ldn, ldk = ops.rup(N, 128), ops.rup(K, 128 if K % 128 == 0 else 64)
+    Y0, X0 = _rnd(M, ldn, seed=15), _rnd(M, ldk, seed=16)
+    Y1, X1 = (_rnd(M, ldn, seed=17), _rnd(M, ldk, seed=18)) if pairs == 2 else (None, None)
+    exact = Y0[:, :N].double().t() @ X0[:, :K].double()
+    if pairs == 2:
+        exact = exact + Y1[:, :N].double().t() @ X1[:, :K].double()
+    res = {}
+    for mode in ("fp32", "bf16x6"):
+        dW = torch.empty(N, K, device=DEV)
+        db = torch.empty(N, device=DEV)
+        ops.wgrad(Y0, X0, N, K, dW, db=db, Y1=Y1, X1=X1, mode=mode)
+        res[mode] = (dW, db)
+    e32 = (res["fp32"][0].double() - exact).abs()
+    e6 = (res["bf16x6"][0].double() - exact).abs()
+    scale = exact.abs().max().item() + 1e-30
+    print(f"wgrad fp32 max {e32.max().item():.3e} | bf16x6 max {e6.max().item():.3e} (|dW| max {scale:.2f})")
+    assert e6.max().item() <= 2.0 * e32.max().item() + 1e-7 * scale
+    assert e6.mean().item() <= 1.5 * e32.mean().item() + 1e-8 * scale
+    tol = 1e-6 * M ** 0.5 + 1e-5
+    torch.testing.assert_close(res["bf16x6"][1], Y0[:, :N].double().sum(0).float(), rtol=1e-4, atol=tol)
+    dW2 = torch.empty_like(res["bf16x6"][0])
+    ops.wgrad(Y0, X0, N, K, dW2, Y1=Y1, X1=X1, mode="bf16x6")
+    assert torch.equal(dW2, res["bf16x6"][0])

@@ -53,11 +53,21 @@ def main():
                           ("tangent", ops.EPI_TANGENT, dict(aux0=aux0, aux1=aux1, out1=o1)),
                           ("main loop only (bench)", 7, {})):
         res["cn_linear bf16 " + name] = timeit(lambda: ops.linear(A, Bb, N, K, o0, epi, **kw))
+    Bs = ops.split_bf16x3(B)
+    for name, epi, kw in (("store", ops.EPI_STORE, dict(bias=bias)),
+                          ("softplus", ops.EPI_SOFTPLUS, dict(bias=bias, out1=o1)),
+                          ("tangent", ops.EPI_TANGENT, dict(aux0=aux0, aux1=aux1, out1=o1)),
+                          ("bwd_softplus", ops.EPI_BWD_SOFTPLUS, dict(aux0=aux0, aux1=aux1)),
+                          ("main loop only (bench)", 7, {})):
+        res["cn_linear x6 " + name] = timeit(lambda: ops.linear(A, Bs, N, K, o0, epi, **kw))
     res["torch.matmul bf16 (hipBLASLt)"] = timeit(lambda: torch.matmul(A.bfloat16(), Bb.t()))
     dW = torch.empty(N, K, device=dev)
     db = torch.empty(N, device=dev)
     res["cn_wgrad 1 pair"] = timeit(lambda: ops.wgrad(A, A, N, K, dW, db=db))
     res["cn_wgrad 2 pairs"] = timeit(lambda: ops.wgrad(A, A, N, K, dW, db=db, Y1=aux1, X1=aux0)) / 2
+    res["cn_wgrad x6 1 pair"] = timeit(lambda: ops.wgrad(A, A, N, K, dW, db=db, mode="bf16x6"))
+    res["cn_wgrad x6 2 pairs"] = timeit(lambda: ops.wgrad(A, A, N, K, dW, db=db, Y1=aux1, X1=aux0, mode="bf16x6")) / 2
+    res["cn_wgrad bf16 2 pairs"] = timeit(lambda: ops.wgrad(A, A, N, K, dW, db=db, Y1=aux1, X1=aux0, mode="bf16")) / 2
     res["torch A^T A"] = timeit(lambda: torch.matmul(A.t(), A, out=dW))
     for k, ms in res.items():
         print(f"{k:32s} {ms*1e3:9.1f} us  {fl / ms / 1e9:8.1f} TFLOP/s")

@@ -21,6 +21,11 @@ def main():
     aux1 = torch.randn(M, N, device=dev)
     o0 = torch.empty(M, N, device=dev)
     o1 = torch.empty(M, N, device=dev)
+    mode = os.environ.get("GEMM_MODE", "fp32")  # fp32 | bf16 | x6
+    if mode == "bf16":
+        B = B.bfloat16().contiguous()
+    elif mode == "x6":
+        B = ops.split_bf16x3(B)
     for epi, kw in ((ops.EPI_STORE, dict(bias=bias)), (ops.EPI_SOFTPLUS, dict(bias=bias, out1=o1)),
                     (ops.EPI_TANGENT, dict(aux0=aux0, aux1=aux1, out1=o1)), (7, {})):
         for _ in range(int(os.environ.get("REPS", 5))):
