@@ -36,6 +36,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(ROOT, "cope-nerf_amd"), ROOT]
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, = fp32 vector peak
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 (v_mfma_f32_32x32x16_bf16, 32 cycles)
+# fp32-GEMM FLOP/s ceiling of each operand mode: bf16x6 issues six bf16 MFMAs per fp32 product
+MODE_PEAK_TFLOPS = {"fp32": FP32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS,
+                    "bf16x6": BF16_MFMA_PEAK_TFLOPS / 6.0}
+MODE_TEXT = {"fp32": "exact fp32 MFMA products (v_mfma_f32_32x32x2_f32)",
+             "bf16x6": "fp32 GEMMs on the bf16 MFMA: both operands split into three bf16 terms, six products, "
+                       "fp32 accumulate (error vs float64 <= the exact fp32 MFMA's; tests/test_gpu_x6.py)",
+             "bf16": "bf16 MFMA operands (reduced precision), fp32 accumulate / activations"}
 RAYS = 4096
 SAMPLES = 128
 GFLOP_PER_RAY_REF = 1.4809  # reference GEMM FLOPs per ray per train step (64+4x16)
@@ -56,7 +64,7 @@ def kernel_symbol(key):
     if "bf16" in key[2:]:
         return "void cn::wgrad_bf16_kernel<2, 2, 2, 2>(cn::WgradArgs) + cn::slab_reduce_kernel"
     if "x6" in key[2:]:
-        return "cn::wgrad_x6_kernel(cn::WgradArgs) + cn::slab_reduce_kernel"
+        return "void cn::wgrad_x6_kernel<2>(cn::WgradArgs) + cn::slab_reduce_kernel"
     return "void cn::wgrad_kernel<2, 2, 2, 2>(cn::WgradArgs) + cn::slab_reduce_kernel"
 
 
@@ -107,26 +115,25 @@ def cpu_baseline(rays=256, steps=2):
 
 CONFIGS = {
     # name: (rays per GPU, trainer kwargs, workload text)
-    "c2": (4096, {}, "C2: synthetic scene, 4096 rays x 128 samples (64 coarse + 4x16 importance) per GPU, fp32, "
-                     "fixed poses, full train step (fwd + losses + bwd + Adam)"),
+    "c2": (4096, {"mfma_dtype": "bf16x6"},
+           "C2: synthetic scene, 4096 rays x 128 samples (64 coarse + 4x16 importance) per GPU, fp32, "
+           "fixed poses, full train step (fwd + losses + bwd + Adam)"),
+    "c2fp32": (4096, {"mfma_dtype": "fp32"}, "C2 with the exact-product fp32 MFMA GEMMs"),
     "c3": (4096, {"joint_pose": True, "stage1": True, "mfma_dtype": "bf16"},
            "C3-style: synthetic scene, 4096 rays x 128 samples per GPU, bf16 MLP MFMA (fp32 accumulate), joint "
            "pose optimisation (learnable SE(3) poses -> ray gradients) + stage-1 scene-flow and SDF-consistency "
            "losses"),
-    "c3fp32": (4096, {"joint_pose": True, "stage1": True},
-               "C3-style as c3 with exact fp32 MFMA"),
-    "infer": (518400, {"infer": True},
+    "c3fp32": (4096, {"joint_pose": True, "stage1": True, "mfma_dtype": "bf16x6"},
+               "C3-style as c3 with fp32 GEMMs (bf16x6)"),
+    "infer": (518400, {"infer": True, "mfma_dtype": "bf16x6"},
               "inference: full 540x960 image (518,400 rays x 128 samples, eval mode, no jitter), forward only "
               "(sampler + SDF + ∇SDF + colour + compositing), 65,536-ray chunks, fp32"),
     "c2bf16": (4096, {"mfma_dtype": "bf16"},
                "C2 workload (4096 rays x 128 samples, fixed poses) with bf16 MLP MFMA (fp32 accumulate)"),
-    "c2x6": (4096, {"mfma_dtype": "bf16x6"},
-             "C2 workload (4096 rays x 128 samples, fixed poses), fp32 MLP GEMMs on the bf16 MFMA (three-term "
-             "bf16 split of both operands, six products, fp32 accumulate)"),
-    "c4": (8192, {}, "C4: synthetic scene, 8192 rays x 128 samples per GPU, fp32, fixed poses, data-parallel"),
+    "c4": (8192, {"mfma_dtype": "bf16x6"}, "C4: synthetic scene, 8192 rays x 128 samples per GPU, fp32, fixed poses, data-parallel"),
     "c5": (4096, {"ren_cfg": dict(n_samples=64, n_importance=128, n_outside=0, up_sample_steps=4, perturb=1.0,
                                   n_max_network_queries=64000, importance_sampling_start=0, naive_render=False),
-                  "graph": True},
+                  "graph": True, "mfma_dtype": "bf16x6"},
            "C5: synthetic scene, 4096 rays x 192 samples (coarse 64 + fine 4x32), fp32, HIP-graph-captured step"),
 }
 
@@ -162,6 +169,7 @@ def main():
     from copenerf import ops
     from copenerf.train_step import GraphedTrainer, SyntheticTrainer
     infer = kw.pop("infer", False)
+    mode = kw.get("mfma_dtype", "fp32")
     tr = SyntheticTrainer(f"cuda:{local}", rays=4096 if infer else rays, distributed=distributed and not infer,
                           capturable=graph, **kw)
     step = tr.step
@@ -220,18 +228,18 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16 MFMA operands, fp32 accumulate/activations" if kw.get("mfma_dtype") == "bf16" else "fp32",
+        "dtype": "bf16 MFMA operands, fp32 accumulate/activations" if mode == "bf16" else "fp32",
         "data": "synthetic (random 540x960 image, 4x4 patches, " +
                 ("learnable SE(3) poses" if kw.get("joint_pose") else "fixed identity pose") +
                 ", geometric-init SDF, seed 678)",
-        "config": {"workload": workload, "rays_per_gpu": rays, "samples_per_ray": S,
+        "config": {"workload": workload, "gemm": MODE_TEXT[mode], "rays_per_gpu": rays, "samples_per_ray": S,
                    "global_rays": rays * world, "hip_graph": graph,
                    "parallelism": f"dp{world}" if world > 1 else "single"},
         "roofline": None,
         "cpu_baseline": None,
     }
     if timer is not None:
-        result.update(roofline_fields(timer, args.steps, rays_total / elapsed))
+        result.update(roofline_fields(timer, args.steps, rays_total / elapsed, mode))
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
         result["cpu_baseline"] = cpu_baseline()
     if rank == 0:
@@ -240,7 +248,7 @@ def main():
         dist.destroy_process_group()
 
 
-def roofline_fields(timer, steps, rays_per_s):
+def roofline_fields(timer, steps, rays_per_s, mode):
     agg = timer.summary()
     # dominant single-kernel launch class (a cn_wgrad call is two kernels: the
     # split-M MFMA kernel and its fixed-order slab reduction)
@@ -253,7 +261,10 @@ def roofline_fields(timer, steps, rays_per_s):
     kernels_ms = sum(a["ms"] for a in agg.values()) / steps
     return {
         "roofline": {"bound": "mfma", "kernel": symbol, "achieved": round(achieved, 2),
-                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                     "peak": round(MODE_PEAK_TFLOPS[mode], 1), "unit": "TFLOP/s",
+                     "frac": round(achieved / MODE_PEAK_TFLOPS[mode], 4),
+                     "peak_basis": {"fp32": "fp32 MFMA dense", "bf16": "bf16 MFMA dense",
+                                    "bf16x6": "bf16 MFMA dense / 6 products"}[mode],
                      "traffic": traffic, "traffic_source": traffic_src,
                      "launches_per_step": dom["launches"] / steps, "avg_launch_ms": round(avg_ms, 4),
                      "algorithmic_gflop_per_launch": round(dom["flops"] / dom["launches"] / 1e9, 3)},

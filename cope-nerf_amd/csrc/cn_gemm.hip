@@ -880,13 +880,16 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) wgrad_bf16_kernel(WgradArgs p
 // segments fall on the two halves of the 32 write banks; an LDS row is the three
 // 16-dword term planes + 4 pad (52 dwords: the ds_read_b128 fragment reads of 16
 // consecutive rows hit 16 distinct bank quads).  One LDS buffer (53 KB, two
-// workgroups per CU): the next chunk's loads fly during the MFMAs.
+// workgroups per CU): the next chunk's loads fly during the MFMAs.  TN = 1: 64
+// output columns, X staged by the first two waves.
+template <int TN>
 __global__ void __launch_bounds__(256, 2) wgrad_x6_kernel(WgradArgs p) {
-    constexpr int TM = 2, TN = 2, WN = 2;
-    constexpr int BNo = 128, BKo = 128, MC = 32, MQ = MC / 4;
+    constexpr int TM = 2, WN = 2;
+    constexpr int BNo = 128, BKo = 64 * TN, MC = 32, MQ = MC / 4;
     constexpr int PL = MC / 2;       // dwords per term plane of a row
     constexpr int LSB = 3 * PL + 4;  // 52
-    static_assert(MQ * (BNo / 4) == 256 && MQ * (BKo / 4) == 256, "staging geometry");
+    constexpr int XT = MQ * (BKo / 4);  // threads staging X (256 or 128: whole waves)
+    static_assert(MQ * (BNo / 4) == 256 && (XT == 256 || XT == 128), "staging geometry");
     static_assert(MQ * BNo <= (BNo + BKo) * LSB, "bias partials fit in LDS");
     __shared__ __attribute__((aligned(16))) float smem[(BNo + BKo) * LSB];
     float* sY = smem;
@@ -927,8 +930,10 @@ __global__ void __launch_bounds__(256, 2) wgrad_x6_kernel(WgradArgs p) {
         const rsrc_t vX = make_view(X + (int64_t)mrow * lx + k0, (nrows * lx - k0) * 4);
 #pragma unroll
         for (int r = 0; r < 4; ++r) ry[r] = bload4(vY, ((mq * 4 + r) * ly + cg * 4) * 4, 0);
+        if (XT == 256 || tid < XT) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) rx[r] = bload4(vX, ((mq * 4 + r) * lx + cg * 4) * 4, 0);
+            for (int r = 0; r < 4; ++r) rx[r] = bload4(vX, ((mq * 4 + r) * lx + cg * 4) * 4, 0);
+        }
     };
     auto lstore = [&](bool bias) {
 #pragma unroll
@@ -942,6 +947,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_x6_kernel(WgradArgs p) {
             *reinterpret_cast<bf16x4*>(y + PL) = t1;
             *reinterpret_cast<bf16x4*>(y + 2 * PL) = t2;
         }
+        if (XT < 256 && tid >= XT) return;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const floatx4 col = {rx[0][e], rx[1][e], rx[2][e], rx[3][e]};
@@ -1399,8 +1405,11 @@ extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
     dim3 grid(cdiv(ns, 8) * 8 * a.n_tiles_n * a.n_tiles_k);
     CN_REQUIRE(d->mfma_dtype == CN_MFMA_F32 || d->mfma_dtype == CN_MFMA_BF16 || d->mfma_dtype == CN_MFMA_F32_BF16X6,
                CN_ERR_ARG, "cn_wgrad: bad mfma_dtype %d", d->mfma_dtype);
-    if (d->mfma_dtype == CN_MFMA_F32_BF16X6 && tile == 0) {
-        wgrad_x6_kernel<<<grid, 256, 0, s>>>(a);
+    if (d->mfma_dtype == CN_MFMA_F32_BF16X6) {
+        if (tile == 0)
+            wgrad_x6_kernel<2><<<grid, 256, 0, s>>>(a);
+        else
+            wgrad_x6_kernel<1><<<grid, 256, 0, s>>>(a);
     } else if (d->mfma_dtype == CN_MFMA_BF16) {
         if (tile == 0)
             wgrad_bf16_kernel<2, 2, 2, 2><<<grid, 256, 0, s>>>(a);

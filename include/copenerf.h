@@ -128,7 +128,7 @@ typedef struct cn_wgrad_desc {
                             v_mfma_f32_32x32x16_bf16, fp32 accumulation and slab reduction;
                             db is summed from the fp32 values either way;
                             CN_MFMA_F32_BF16X6: fp32 gradient from three bf16 terms per operand
-                            (six products) on 128x128 output tiles, exact fp32 MFMA on 64-wide ones */
+                            (six products) */
 } cn_wgrad_desc;
 
 size_t cn_wgrad_workspace_bytes(int32_t M, int32_t N, int32_t K);
