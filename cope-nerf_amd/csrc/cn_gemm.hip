@@ -153,12 +153,10 @@ __device__ __forceinline__ void tile_coords(int vt, int T, int& tm, int& tn) {
 //         products with i + j <= 2 are issued (small terms first) into one fp32
 //         accumulator; the three dropped ones are below 2^-26 |a b|, under the
 //         rounding of the fp32 accumulation itself.  BK = 16 k per chunk; an LDS
-//         row holds the three 16-term planes (24 dwords) + 4 pad = 28 dwords
-//         (conflict-free ds_read_b128 over 16 consecutive rows).
+//         row holds the three 16-term planes (24 dwords) + 12 pad = 36 dwords,
+//         the fp32 image's geometry (conflict-free fragment reads, and the C tile
+//         parks in one slab).
 // The accumulator layout of the two MFMAs is the same, so the epilogue is shared.
-#ifndef X6_PAD
-#define X6_PAD 12
-#endif
 template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int EPI, bool ROWV, int MODE>
 __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel(LinearArgs p) {
     constexpr int NT = 64 * WM * WN;
@@ -166,8 +164,8 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     constexpr int BN = 32 * TN * WN;
     constexpr bool BF = MODE != 0;               // bf16 MFMA (modes 1, 2)
     constexpr int NPL = MODE == 2 ? 3 : 1;       // bf16 planes per operand
-    // padded LDS row in dwords: 36 for BK = 32 (f32) / 64 (bf16); 28 for BK = 16 (split)
-    constexpr int LS = (BF ? NPL * BK / 2 : BK) + (MODE == 2 ? X6_PAD : 4);
+    // padded LDS row in dwords: 36 in every mode (BK = 32 f32 / 64 bf16 / 16 split: 3 x 8 + 12 pad)
+    constexpr int LS = (BF ? NPL * BK / 2 : BK) + (MODE == 2 ? 12 : 4);
     constexpr int KC4 = BK / 4;                  // A: fp32 float4 per staged row
     static_assert(NT % KC4 == 0, "staging rows");
     constexpr int RSTEP = NT / KC4;  // staged A rows per load instruction
