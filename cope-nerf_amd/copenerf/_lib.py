@@ -58,6 +58,14 @@ class WgradDesc(ctypes.Structure):
     ]
 
 
+class PackJob(ctypes.Structure):
+    _fields_ = [
+        ("src", c_ptr), ("dst", c_ptr), ("src_ld", c_i64), ("dst_ld", c_i64),
+        ("rows", c_i32), ("cols", c_i32), ("r0", c_i32), ("r1", c_i32), ("c0", c_i32), ("c1", c_i32),
+        ("transpose", c_i32), ("format", c_i32),
+    ]
+
+
 # name -> (restype, argtypes); mirrors include/copenerf.h one to one.
 SIGNATURES = {
     "cn_abi_version": (c_i32, []),
@@ -65,6 +73,7 @@ SIGNATURES = {
     "cn_linear": (c_i32, [ctypes.POINTER(LinearDesc), c_ptr]),
     "cn_wgrad_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32]),
     "cn_wgrad": (c_i32, [ctypes.POINTER(WgradDesc), c_ptr]),
+    "cn_pack_weights": (c_i32, [ctypes.POINTER(PackJob), c_i32, c_ptr]),
     "cn_row_head": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i32, c_i32, c_ptr, c_i64,
                             c_ptr, c_ptr]),
     "cn_scale_cols": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr]),

@@ -81,15 +81,11 @@ class SDFPack:
 MFMA_DTYPES = ("fp32", "bf16", "bf16x6")
 
 
-def _image_fmt(mfma_dtype: str):
-    """(K padding multiple, converter) of the B images for an MFMA mode."""
-    if mfma_dtype == "bf16":
-        return 64, lambda t: t.to(torch.bfloat16).contiguous()
-    if mfma_dtype == "bf16x6":
-        return 32, ops.split_bf16x3
-    if mfma_dtype == "fp32":
-        return 32, lambda t: t.contiguous()
-    raise ValueError(f"mfma_dtype must be one of {MFMA_DTYPES} (got {mfma_dtype!r})")
+def _kq(mfma_dtype: str) -> int:
+    """K padding multiple of the B images for an MFMA mode (bf16 MFMA steps are 64 deep)."""
+    if mfma_dtype not in MFMA_DTYPES:
+        raise ValueError(f"mfma_dtype must be one of {MFMA_DTYPES} (got {mfma_dtype!r})")
+    return 64 if mfma_dtype == "bf16" else 32
 
 
 def _wgrad_mode(pk) -> str:
@@ -100,28 +96,32 @@ def _wgrad_mode(pk) -> str:
 
 
 def pack_sdf(lay: SDFLayout, Ws, bs, mfma_dtype: str = "fp32") -> SDFPack:
-    """Zero-padded GEMM images of the effective weights.  mfma_dtype "bf16": the
-    B images are bfloat16 with K padded to 64 (cn_linear's bf16 MFMA path);
-    "bf16x6": [N, 3, K] bf16 term images (fp32 GEMMs on the bf16 MFMA)."""
-    kq, cv = _image_fmt(mfma_dtype)
+    """Zero-padded GEMM images of the effective weights, built in one
+    cn_pack_weights launch.  mfma_dtype "bf16": bfloat16 images with K padded
+    to 64 (cn_linear's bf16 MFMA path); "bf16x6": [N, 3, K] bf16 term images
+    (fp32 GEMMs on the bf16 MFMA)."""
+    kq = _kq(mfma_dtype)
+    pk = ops.ImagePacker(mfma_dtype)
     with torch.no_grad():
+        dev = Ws[0].device
         Bf, Bt, b = [], [], []
         for l in range(lay.n_lin - 1):
-            W = Ws[l].detach()
+            W = Ws[l].detach().contiguous()
             o, i = W.shape
             kp = lay.KE if l == 0 else rup(i, kq)
-            Bf.append(cv(F.pad(W, (0, kp - i, 0, rup(o, 128) - o))))
-            Bt.append(cv(F.pad(W.t(), (0, rup(o, kq) - o, 0, rup(i, 128) - i))))
+            Bf.append(pk.put(pk.image(rup(o, 128), kp, dev), W))
+            Bt.append(pk.put(pk.image(rup(i, 128), rup(o, kq), dev), W, transpose=True))
             b.append(bs[l].detach().contiguous())
-        W8, b8 = Ws[-1].detach(), bs[-1].detach()
+        W8, b8 = Ws[-1].detach().contiguous(), bs[-1].detach()
         s = float(lay.scale)
         w80 = (W8[0] / s) if s != 1.0 else W8[0]
         b80 = (b8[:1] / s) if s != 1.0 else b8[:1]
         w80p = F.pad(w80, (0, lay.HL - w80.shape[0])).contiguous()
         Wf = W8[1:]
         o, i = Wf.shape
-        Bf8 = cv(F.pad(Wf, (0, rup(i, kq) - i, 0, rup(o, 128) - o)))
-        Bt8 = cv(F.pad(Wf.t(), (0, rup(o, kq) - o, 0, rup(i, 128) - i)))
+        Bf8 = pk.put(pk.image(rup(o, 128), rup(i, kq), dev), Wf)
+        Bt8 = pk.put(pk.image(rup(i, 128), rup(o, kq), dev), Wf, transpose=True)
+        pk.run()
         return SDFPack(Bf, Bt, b, w80.contiguous()[None], b80.contiguous(), w80p, Bf8, Bt8, b8[1:].contiguous())
 
 
@@ -478,26 +478,39 @@ class ColorPack:
 
 
 def pack_color(lay: ColorLayout, Ws, bs, mfma_dtype: str = "fp32") -> ColorPack:
-    kq, cv = _image_fmt(mfma_dtype)
+    """GEMM images of the colour network in one cn_pack_weights launch.  lin0's
+    columns [pts | emb(dirs) | gradient | feature] (neus_fields.py:352-356) are
+    permuted to [feature | gradient | pts | emb | 0] to match the operands
+    (feature, extras) of the first GEMM."""
+    kq = _kq(mfma_dtype)
+    pk = ops.ImagePacker(mfma_dtype)
     with torch.no_grad():
+        dev = Ws[0].device
         P, V, Gd, Fd = lay.P, lay.V, lay.Gd, lay.F
-        W0 = Ws[0].detach()
+        W0 = Ws[0].detach().contiguous()
         o = W0.shape[0]
         pts, emb, g, feat = (W0[:, 0:P], W0[:, P:P + V], W0[:, P + V:P + V + Gd], W0[:, P + V + Gd:])
-        ext = torch.cat([g, pts, emb], 1)
-        W0k = torch.cat([feat, F.pad(ext, (0, lay.KX - ext.shape[1]))], 1)
-        Bf = [cv(F.pad(W0k, (0, 0, 0, rup(o, 128) - o)))]
-        Bt = [None]
+        B0 = pk.image(rup(o, 128), Fd + lay.KX, dev)
+        pk.put(B0, feat, c0=0, c1=Fd)
+        pk.put(B0, g, c0=Fd, c1=Fd + Gd)
+        pk.put(B0, pts, c0=Fd + Gd, c1=Fd + Gd + P)
+        pk.put(B0, emb, c0=Fd + Gd + P, c1=Fd + lay.KX)
+        Bf, Bt = [B0], [None]
         b = [bs[0].detach().contiguous()]
         for l in range(1, lay.n_lin - 1):
-            W = Ws[l].detach()
+            W = Ws[l].detach().contiguous()
             oo, ii = W.shape
-            Bf.append(cv(F.pad(W, (0, rup(ii, kq) - ii, 0, rup(oo, 128) - oo))))
-            Bt.append(cv(F.pad(W.t(), (0, rup(oo, kq) - oo, 0, rup(ii, 128) - ii))))
+            Bf.append(pk.put(pk.image(rup(oo, 128), rup(ii, kq), dev), W))
+            Bt.append(pk.put(pk.image(rup(ii, 128), rup(oo, kq), dev), W, transpose=True))
             b.append(bs[l].detach().contiguous())
-        Btf = cv(F.pad(feat.t(), (0, rup(o, kq) - o, 0, rup(Fd, 128) - Fd)))
-        Wg = g.t().contiguous()
-        Bxt = cv(F.pad(ext.t(), (0, rup(o, kq) - o, 0, 64 - ext.shape[1])))
+        Btf = pk.put(pk.image(rup(Fd, 128), rup(o, kq), dev), feat, transpose=True)
+        Wg = pk.put(pk.image(Gd, o, dev, fmt="fp32"), g, transpose=True, fmt="fp32")
+        # extras columns [g | pts | emb] of lin0, transposed, rows padded to 64
+        Bxt = pk.image(64, rup(o, kq), dev)
+        pk.put(Bxt, g, transpose=True, r0=0, r1=Gd)
+        pk.put(Bxt, pts, transpose=True, r0=Gd, r1=Gd + P)
+        pk.put(Bxt, emb, transpose=True, r0=Gd + P, r1=64)
+        pk.run()
         return ColorPack(Bf, Bt, b, Ws[-1].detach().contiguous(), bs[-1].detach().contiguous(), Btf, Wg, Bxt)
 
 

@@ -96,6 +96,54 @@ def split_bf16x3(W: torch.Tensor) -> torch.Tensor:
     return torch.stack([w0, w1, w2], 1).contiguous()
 
 
+FORMATS = {"fp32": 0, "bf16": 1, "bf16x6": 2}
+
+
+class ImagePacker:
+    """Collects cn_pack_job regions of weight images and builds them in one
+    cn_pack_weights launch (the per-call weight packing of fields.py)."""
+
+    def __init__(self, mode: str):
+        if mode not in FORMATS:
+            raise ValueError(f"mode must be one of {tuple(FORMATS)} (got {mode!r})")
+        self.mode = mode
+        self.jobs = []
+        self.keep = []  # sources must stay alive until the launch is queued
+
+    def image(self, rows: int, cols: int, device, fmt: str | None = None) -> torch.Tensor:
+        """An uninitialised image of the packer's format: fp32 / bf16 [rows, cols], bf16x6 [rows, 3, cols]."""
+        fmt = fmt or self.mode
+        if fmt == "bf16x6":
+            return torch.empty(rows, 3, cols, device=device, dtype=torch.bfloat16)
+        return torch.empty(rows, cols, device=device, dtype=torch.bfloat16 if fmt == "bf16" else torch.float32)
+
+    def put(self, dst: torch.Tensor, src: torch.Tensor, *, transpose=False, r0=0, r1=None, c0=0, c1=None, fmt=None):
+        """Region [r0, r1) x [c0, c1) of dst (default: all of it) = src (or srcᵀ) at (r0, c0), zero elsewhere."""
+        fmt = fmt or self.mode
+        _need(src, "pack src")
+        _need(dst, "pack dst", ndim=dst.dim())
+        if src.dtype != torch.float32:
+            raise RuntimeError("pack: src must be float32")
+        rows, cols = (src.shape[1], src.shape[0]) if transpose else (src.shape[0], src.shape[1])
+        j = _lib.PackJob()
+        j.src, j.dst = src.data_ptr(), dst.data_ptr()
+        j.src_ld = src.stride(0)
+        j.dst_ld = dst.shape[-1]
+        j.rows, j.cols = rows, cols
+        j.r0, j.r1 = r0, dst.shape[0] if r1 is None else r1
+        j.c0, j.c1 = c0, dst.shape[-1] if c1 is None else c1
+        j.transpose, j.format = int(transpose), FORMATS[fmt]
+        self.jobs.append(j)
+        self.keep.append(src)
+        return dst
+
+    def run(self):
+        if self.jobs:
+            arr = (_lib.PackJob * len(self.jobs))(*self.jobs)
+            _lib.check(_lib.load().cn_pack_weights(arr, len(self.jobs), _stream()), "cn_pack_weights")
+        self.jobs, self.keep = [], []
+
+
 def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None, colv=None, aux0=None,
            aux1=None, out1=None, out_split=None, nsplit=None, nzero=None, adiv=1.0, odiv=1.0, beta=100.0,
            threshold=20.0, tile=None, M=None, kalg=None):

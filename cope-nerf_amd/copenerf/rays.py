@@ -46,33 +46,49 @@ def intrinsics_ndc(fx, fy, w, h, device="cpu"):
                         dtype=torch.float32, device=device)
 
 
+def _cofactor_tables():
+    """Flat indices [16, 6, 3] and signs [16, 6] of the six permutation terms of
+    every 3x3 minor's determinant, (-1)^(i+j) folded in: cofactor C_ij =
+    sum_p sign[ij, p] * prod_k a[idx[ij, p, k]]."""
+    perms = (((0, 1, 2), 1), ((0, 2, 1), -1), ((1, 0, 2), -1), ((1, 2, 0), 1), ((2, 0, 1), 1), ((2, 1, 0), -1))
+    idx = np.zeros((16, 6, 3), np.int64)
+    sgn = np.zeros((16, 6), np.float32)
+    for i in range(4):
+        for j in range(4):
+            rows = [r for r in range(4) if r != i]
+            cols = [c for c in range(4) if c != j]
+            for p, (perm, s) in enumerate(perms):
+                idx[4 * i + j, p] = [rows[k] * 4 + cols[perm[k]] for k in range(3)]
+                sgn[4 * i + j, p] = s * (-1) ** (i + j)
+    return idx, sgn
+
+
+_COF = _cofactor_tables()
+_COF_DEV = {}
+
+
 def inv4x4(m):
-    """Inverse of a 4x4 matrix by cofactors (adjugate / determinant).  Pure
-    elementwise device ops, differentiable and HIP-graph capturable (the LAPACK
-    path behind torch.inverse is not); agrees with it to fp32 rounding for the
-    well-conditioned camera / pose matrices on this path."""
-    a = m.reshape(16)
-    a0, a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11, a12, a13, a14, a15 = a.unbind(0)
-    s0, s1, s2 = a0 * a5 - a4 * a1, a0 * a6 - a4 * a2, a0 * a7 - a4 * a3
-    s3, s4, s5 = a1 * a6 - a5 * a2, a1 * a7 - a5 * a3, a2 * a7 - a6 * a3
-    c5, c4, c3 = a10 * a15 - a14 * a11, a9 * a15 - a13 * a11, a9 * a14 - a13 * a10
-    c2, c1, c0 = a8 * a15 - a12 * a11, a8 * a14 - a12 * a10, a8 * a13 - a12 * a9
-    det = s0 * c5 - s1 * c4 + s2 * c3 + s3 * c2 - s4 * c1 + s5 * c0
-    inv = torch.stack([
-        a5 * c5 - a6 * c4 + a7 * c3, -a1 * c5 + a2 * c4 - a3 * c3, a13 * s5 - a14 * s4 + a15 * s3,
-        -a9 * s5 + a10 * s4 - a11 * s3,
-        -a4 * c5 + a6 * c2 - a7 * c1, a0 * c5 - a2 * c2 + a3 * c1, -a12 * s5 + a14 * s2 - a15 * s1,
-        a8 * s5 - a10 * s2 + a11 * s1,
-        a4 * c4 - a5 * c2 + a7 * c0, -a0 * c4 + a1 * c2 - a3 * c0, a12 * s4 - a13 * s2 + a15 * s0,
-        -a8 * s4 + a9 * s2 - a11 * s0,
-        -a4 * c3 + a5 * c1 - a6 * c0, a0 * c3 - a1 * c1 + a2 * c0, -a12 * s3 + a13 * s1 - a14 * s0,
-        a8 * s3 - a9 * s1 + a10 * s0]) / det
-    return inv.reshape(4, 4)
+    """Inverse of 4x4 matrices [..., 4, 4] by cofactors (adjugate / determinant):
+    one gather of the 96 minor-term triples, their products and signed sums,
+    a determinant and a division -- a handful of device ops, differentiable and
+    HIP-graph capturable (the LAPACK path behind torch.inverse is not); agrees
+    with torch.inverse to fp32 rounding on the well-conditioned camera / pose
+    matrices of this path."""
+    key = (m.device, m.dtype)
+    if key not in _COF_DEV:  # first use is outside any graph capture (warmup steps)
+        _COF_DEV[key] = (torch.as_tensor(_COF[0], device=m.device), torch.as_tensor(_COF[1], device=m.device,
+                                                                                    dtype=m.dtype))
+    idx, sgn = _COF_DEV[key]
+    a = m.reshape(*m.shape[:-2], 16)
+    cof = (a[..., idx].prod(-1) * sgn).sum(-1).reshape(*m.shape[:-2], 4, 4)  # C_ij
+    det = (m[..., 0, :] * cof[..., 0, :]).sum(-1)
+    return cof.transpose(-1, -2) / det[..., None, None]
 
 
 def world_rays(pixels_norm, camera_mat, world_mat, scale_mat):
     """rays_o [R,3], unit rays_d [R,3], |p - o| [R,1] (training.py:474-487)."""
-    inv = inv4x4(scale_mat) @ inv4x4(world_mat) @ inv4x4(camera_mat)  # [4,4]
+    inv_s, inv_w, inv_c = inv4x4(torch.stack([scale_mat, world_mat, camera_mat])).unbind(0)
+    inv = inv_s @ inv_w @ inv_c  # [4,4]
     o = inv[:3, 3]
     R = pixels_norm.shape[0]
     ph = torch.cat([pixels_norm, torch.ones(R, 2, device=pixels_norm.device)], -1)  # [x, y, 1, 1]

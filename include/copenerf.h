@@ -104,6 +104,29 @@ enum cn_mfma_dtype { CN_MFMA_F32 = 0, CN_MFMA_BF16 = 1, CN_MFMA_F32_BF16X6 = 2 }
 int cn_linear(const cn_linear_desc* d, cn_stream_t stream);
 
 /* ------------------------------------------------------------------------ *
+ * Weight images for cn_linear (the per-call `pack` of the effective weights,
+ * neus_fields.py:273-283 / 364-373 weight_norm outputs): one launch builds
+ * every padded / transposed / column-permuted B image of a network.  Job j
+ * writes the region [r0, r1) x [c0, c1) of its image: the source matrix
+ * S (rows x cols; S[r][c] = src[r*src_ld + c], or src[c*src_ld + r] when
+ * transpose) lands at (r0, c0), the rest of the region is zero.  format is a
+ * cn_mfma_dtype: CN_MFMA_F32 copies fp32 (element (r, c) at dst[r*dst_ld + c]),
+ * CN_MFMA_BF16 rounds to bf16 (RNE, same indexing), CN_MFMA_F32_BF16X6 writes
+ * the three bf16 terms of each value (term t at dst[(3r + t)*dst_ld + c]).
+ * ------------------------------------------------------------------------ */
+typedef struct cn_pack_job {
+    const float* src;
+    void* dst;
+    int64_t src_ld, dst_ld;
+    int32_t rows, cols;
+    int32_t r0, r1, c0, c1;
+    int32_t transpose;
+    int32_t format;
+} cn_pack_job;
+
+int cn_pack_weights(const cn_pack_job* jobs, int32_t njobs, cn_stream_t stream);
+
+/* ------------------------------------------------------------------------ *
  * Weight gradient: dW[n][k] = sum_m ( Y0[m][n]*X0[m][k] + Y1[m][n]*X1[m][k] ),
  * db[n] = sum_m Y0[m][n].  Reduction over the M = R*S sample rows is split
  * over workgroups into fp32 slabs (workspace) and summed in a fixed order, so

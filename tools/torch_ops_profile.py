@@ -10,7 +10,7 @@ from copenerf.train_step import SyntheticTrainer  # noqa: E402
 
 
 def main():
-    tr = SyntheticTrainer("cuda:0", rays=4096)
+    tr = SyntheticTrainer("cuda:0", rays=4096, mfma_dtype=os.environ.get("MODE", "bf16x6"))
     for _ in range(3):
         tr.step()
     torch.cuda.synchronize()
