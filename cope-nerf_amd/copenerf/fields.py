@@ -98,7 +98,7 @@ def _wgrad_mode(pk) -> str:
 def pack_sdf(lay: SDFLayout, Ws, bs, mfma_dtype: str = "fp32") -> SDFPack:
     """Zero-padded GEMM images of the effective weights, built in one
     cn_pack_weights launch.  mfma_dtype "bf16": bfloat16 images with K padded
-    to 64 (cn_linear's bf16 MFMA path); "bf16x6": [N, 3, K] bf16 term images
+    to 64 (cn_linear's bf16 MFMA path); "bf16x6": chunk-major bf16 term images [K/16, N, 48]
     (fp32 GEMMs on the bf16 MFMA)."""
     kq = _kq(mfma_dtype)
     pk = ops.ImagePacker(mfma_dtype)

@@ -87,13 +87,25 @@ def _ld(t):
 
 
 def split_bf16x3(W: torch.Tensor) -> torch.Tensor:
-    """[N, K] fp32 -> [N, 3, K] bf16 terms w0 + w1 + w2 = W (each RNE of the
-    remainder; |W - Σ| <= 2^-27 |W|): the B image of CN_MFMA_F32_BF16X6."""
+    """[N, K] fp32 (K % 16 == 0) -> the chunk-major B image of
+    CN_MFMA_F32_BF16X6, bf16 [K/16, N, 48]: entry [c, n, 16 t + j] is term t of
+    W[n, 16 c + j], with W = w0 + w1 + w2 (each the RNE bf16 of the remainder;
+    |W - Σ| <= 2^-27 |W|)."""
+    N, K = W.shape
+    if K % 16:
+        raise ValueError(f"split_bf16x3: K={K} must be a multiple of 16")
     w0 = W.to(torch.bfloat16)
     r = W - w0.float()
     w1 = r.to(torch.bfloat16)
     w2 = (r - w1.float()).to(torch.bfloat16)
-    return torch.stack([w0, w1, w2], 1).contiguous()
+    t = torch.stack([w0, w1, w2], 1).view(N, 3, K // 16, 16)
+    return t.permute(2, 0, 1, 3).reshape(K // 16, N, 48).contiguous()
+
+
+def unsplit_bf16x3(B: torch.Tensor) -> torch.Tensor:
+    """The three terms [3, N, K] (bf16) of a split_bf16x3 image."""
+    C, N, _ = B.shape
+    return B.view(C, N, 3, 16).permute(2, 1, 0, 3).reshape(3, N, C * 16)
 
 
 FORMATS = {"fp32": 0, "bf16": 1, "bf16x6": 2}
@@ -111,10 +123,13 @@ class ImagePacker:
         self.keep = []  # sources must stay alive until the launch is queued
 
     def image(self, rows: int, cols: int, device, fmt: str | None = None) -> torch.Tensor:
-        """An uninitialised image of the packer's format: fp32 / bf16 [rows, cols], bf16x6 [rows, 3, cols]."""
+        """An uninitialised image of the packer's format: fp32 / bf16 [rows, cols], bf16x6 the
+        chunk-major [cols/16, rows, 48] (split_bf16x3's layout)."""
         fmt = fmt or self.mode
         if fmt == "bf16x6":
-            return torch.empty(rows, 3, cols, device=device, dtype=torch.bfloat16)
+            if cols % 16:
+                raise ValueError(f"pack: bf16x6 image width {cols} must be a multiple of 16")
+            return torch.empty(cols // 16, rows, 48, device=device, dtype=torch.bfloat16)
         return torch.empty(rows, cols, device=device, dtype=torch.bfloat16 if fmt == "bf16" else torch.float32)
 
     def put(self, dst: torch.Tensor, src: torch.Tensor, *, transpose=False, r0=0, r1=None, c0=0, c1=None, fmt=None):
@@ -128,10 +143,12 @@ class ImagePacker:
         j = _lib.PackJob()
         j.src, j.dst = src.data_ptr(), dst.data_ptr()
         j.src_ld = src.stride(0)
-        j.dst_ld = dst.shape[-1]
+        x6 = fmt == "bf16x6"
+        d_rows, d_cols = (dst.shape[1], 16 * dst.shape[0]) if x6 else (dst.shape[0], dst.shape[1])
+        j.dst_ld = d_rows if x6 else d_cols
         j.rows, j.cols = rows, cols
-        j.r0, j.r1 = r0, dst.shape[0] if r1 is None else r1
-        j.c0, j.c1 = c0, dst.shape[-1] if c1 is None else c1
+        j.r0, j.r1 = r0, d_rows if r1 is None else r1
+        j.c0, j.c1 = c0, d_cols if c1 is None else c1
         j.transpose, j.format = int(transpose), FORMATS[fmt]
         self.jobs.append(j)
         self.keep.append(src)
@@ -151,12 +168,12 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     inner dimension (for the FLOP count of the kernel timer only).  A bfloat16 B
     selects the bf16 MFMA path (A rounded to bf16 on load, fp32 accumulate); K is
     then rounded up to 64, so A's columns up to that must exist (zero padding).
-    A [N, 3, K] bfloat16 B (split_bf16x3) selects CN_MFMA_F32_BF16X6: the fp32
+    A [K/16, N, 48] bfloat16 B (split_bf16x3) selects CN_MFMA_F32_BF16X6: the fp32
     GEMM computed from three bf16 terms per operand on the bf16 MFMA."""
     x6 = B.dim() == 3
-    if x6 and (B.dtype != torch.bfloat16 or B.shape[1] != 3 or B.stride(2) != 1 or B.stride(0) != 3 * B.stride(1)):
-        raise RuntimeError(f"cn_linear: a 3-D B must be split_bf16x3's [N, 3, K] bfloat16 (got {tuple(B.shape)}, "
-                           f"{B.dtype}, strides {B.stride()})")
+    if x6 and (B.dtype != torch.bfloat16 or B.shape[2] != 48 or not B.is_contiguous()):
+        raise RuntimeError(f"cn_linear: a 3-D B must be split_bf16x3's [K/16, N, 48] bfloat16 image (got "
+                           f"{tuple(B.shape)}, {B.dtype}, strides {B.stride()})")
     for t, n in ((A, "A"), (A2, "A2"), (B, "B"), (out0, "out0"), (out1, "out1"), (aux0, "aux0"),
                  (aux1, "aux1"), (out_split, "out_split")):
         _need(t, n, ndim=3 if (x6 and t is B) else 2)
@@ -175,7 +192,8 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     if tile is None:
         tile = 1 if max(N, nzero or 0) <= 64 else 0
     bn = 64 if tile == 1 else 128
-    if B.shape[0] < rup(N, bn) or B.shape[-1] < K:
+    b_rows, b_k = (B.shape[1], 16 * B.shape[0]) if x6 else (B.shape[0], B.shape[1])
+    if b_rows < rup(N, bn) or b_k < K:
         raise RuntimeError(f"cn_linear: B {tuple(B.shape)} too small for N={N}, K={K} (tile {tile})")
     if out0.shape[0] < M:
         raise RuntimeError("cn_linear: out0 has fewer rows than A")
@@ -183,7 +201,7 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     d.A, d.A2, d.B, d.bias = _ptr(A), _ptr(A2), _ptr(B), _ptr(bias)
     d.rowv, d.colv, d.aux0, d.aux1 = _ptr(rowv), _ptr(colv), _ptr(aux0), _ptr(aux1)
     d.out0, d.out1, d.out_split = _ptr(out0), _ptr(out1), _ptr(out_split)
-    d.lda, d.lda2, d.ldb = _ld(A), _ld(A2), (B.stride(1) if x6 else _ld(B))
+    d.lda, d.lda2, d.ldb = _ld(A), _ld(A2), (B.shape[1] if x6 else _ld(B))
     d.ld_aux0, d.ld_aux1, d.ld_out0, d.ld_out1, d.ld_split = _ld(aux0), _ld(aux1), _ld(out0), _ld(out1), _ld(out_split)
     d.M, d.N, d.K = M, N, K
     d.K1 = K1 if K1 is not None else K

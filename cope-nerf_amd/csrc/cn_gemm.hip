@@ -149,7 +149,10 @@ __device__ __forceinline__ void tile_coords(int vt, int T, int& tm, int& tn) {
 // MODE 2: fp32 GEMM on the bf16 MFMA (CN_MFMA_F32_BF16X6).  Each fp32 operand is
 //         the sum of three bf16 terms x = x0 + x1 + x2 (x0 = bf16(x), x1 =
 //         bf16(x - x0), x2 = bf16(x - x0 - x1), all RNE; |x - Σ| <= 2^-27 |x|);
-//         A is split while staging, B arrives split ([N][3][ldb] bf16).  The six
+//         A is split while staging, B arrives split and chunk-major: chunk c
+//         (k = 16c .. 16c+15) is [ldb rows][3 terms][16 k] bf16, so a tile's B
+//         chunk is one contiguous 96 * BN-byte block (coalesced 16-byte pieces
+//         that land on LDS rows as they are).  The six
 //         products with i + j <= 2 are issued (small terms first) into one fp32
 //         accumulator; the three dropped ones are below 2^-26 |a b|, under the
 //         rounding of the fp32 accumulation itself.  BK = 16 k per chunk; an LDS
@@ -157,6 +160,9 @@ __device__ __forceinline__ void tile_coords(int vt, int T, int& tm, int& tn) {
 //         the fp32 image's geometry (conflict-free fragment reads, and the C tile
 //         parks in one slab).
 // The accumulator layout of the two MFMAs is the same, so the epilogue is shared.
+#ifndef X6_EXP
+#define X6_EXP 0  // benchmark-only ablations of the bf16x6 main loop (tools/x6_ablation.sh)
+#endif
 template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int EPI, bool ROWV, int MODE>
 __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel(LinearArgs p) {
     constexpr int NT = 64 * WM * WN;
@@ -209,9 +215,9 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     }
 #pragma unroll
     for (int q = 0; q < BLD; ++q) {
-        if constexpr (MODE == 2) {  // piece pc = plane * PIECES_PL + half; a B row is 3 planes of ldb
-            const int idx = tid + q * NT, row = idx / KCB, pc = idx % KCB;
-            voB[q] = idx < BN * KCB ? row * 3 * p.ldb * 2 + (pc / PIECES_PL) * p.ldb * 2 + (pc % PIECES_PL) * 16 : 0;
+        if constexpr (MODE == 2) {  // the chunk's B tile is contiguous: piece idx at byte 16 idx
+            const int idx = tid + q * NT;
+            voB[q] = idx < BN * KCB ? idx * 16 : 0;
         } else {
             voB[q] = (srowb + q * RSTEPB) * p.ldb * ESZB + scb * 16;
         }
@@ -234,12 +240,23 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         const int ak = second ? k0 - p.K1 : k0;
         const rsrc_t rA = make_view(abase, rows * ald * 4);
 #pragma unroll
-        for (int q = 0; q < ALD; ++q) ra[set][q] = bload4(rA, second ? voA2[q] : voA[q], ak * 4);
-        const rsrc_t rB = make_view(reinterpret_cast<const float*>(reinterpret_cast<const char*>(p.B) +
-                                                                   (int64_t)n0 * NPL * p.ldb * ESZB),
-                                    valid ? BN * NPL * p.ldb * ESZB : 0);
+        for (int q = 0; q < ALD; ++q) {
+#if X6_EXP == 4
+            if (MODE == 2) { ra[set][q] = floatx4{(float)k0, (float)rows, (float)q, 1.0f}; continue; }
+#endif
+            ra[set][q] = bload4(rA, second ? voA2[q] : voA[q], ak * 4);
+        }
+        // MODE 2: chunk kc of the image is [ldb rows][48 bf16]; the tile's BN rows are 96 * BN contiguous bytes
+        const int64_t bofs = MODE == 2 ? ((int64_t)kc * p.ldb + n0) * 96 : (int64_t)n0 * p.ldb * ESZB;
+        const rsrc_t rB = make_view(reinterpret_cast<const float*>(reinterpret_cast<const char*>(p.B) + bofs),
+                                    valid ? (MODE == 2 ? BN * 96 : BN * p.ldb * ESZB) : 0);
 #pragma unroll
-        for (int q = 0; q < BLD; ++q) rb[set][q] = bload4(rB, voB[q], k0 * ESZB);
+        for (int q = 0; q < BLD; ++q) {
+#if X6_EXP == 4 || X6_EXP == 5
+            if (MODE == 2) { rb[set][q] = floatx4{(float)k0, (float)n0, (float)q, 1.0f}; continue; }
+#endif
+            rb[set][q] = bload4(rB, voB[q], MODE == 2 ? 0 : k0 * ESZB);
+        }
     };
     auto lstore = [&](int set, int buf) {
         float* a = sA + buf * BM * LS + lds_a;
@@ -248,7 +265,11 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         for (int q = 0; q < ALD; ++q) {
             if constexpr (MODE == 2) {
                 bf16x4 x0, x1, x2;
+#if X6_EXP == 1
+                x0 = x1 = x2 = __builtin_convertvector(ra[set][q], bf16x4);
+#else
                 split3(ra[set][q], x0, x1, x2);
+#endif
                 *reinterpret_cast<bf16x4*>(a + q * RSTEP * LS) = x0;
                 *reinterpret_cast<bf16x4*>(a + q * RSTEP * LS + BK / 2) = x1;
                 *reinterpret_cast<bf16x4*>(a + q * RSTEP * LS + BK) = x2;
@@ -336,6 +357,13 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                     bf16x8 af[3][TM], bf[3][TN];
 #pragma unroll
                     for (int t = 0; t < 3; ++t) {
+#if X6_EXP == 3
+                        if (t > 0) {
+                            for (int i = 0; i < TM; ++i) af[t][i] = af[0][i];
+                            for (int j = 0; j < TN; ++j) bf[t][j] = bf[0][j];
+                            continue;
+                        }
+#endif
 #pragma unroll
                         for (int i = 0; i < TM; ++i)
                             af[t][i] = *reinterpret_cast<const bf16x8*>(a_base + i * 32 * LS + t * (BK / 2) + ks * 8);
@@ -348,7 +376,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                     constexpr int TA[6] = {0, 1, 0, 2, 1, 0};
                     constexpr int TB[6] = {0, 0, 1, 0, 1, 2};
 #pragma unroll
-                    for (int u = 0; u < 6; ++u)
+                    for (int u = 0; u < (X6_EXP == 2 ? 3 : 6); ++u)
 #pragma unroll
                         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1299,7 +1327,11 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     CN_REQUIRE(K1 > 0 && K1 <= d->K && K1 % (bf ? 64 : 32) == 0, CN_ERR_SHAPE, "cn_linear: bad K1=%d", K1);
     CN_REQUIRE(d->lda >= K1 && d->lda % 4 == 0 && al16(d->A), CN_ERR_ALIGN, "cn_linear: A must be 16B aligned with lda>=K1, lda%%4==0");
     if (d->A2) CN_REQUIRE(d->lda2 >= d->K - K1 && d->lda2 % 4 == 0 && al16(d->A2), CN_ERR_ALIGN, "cn_linear: bad A2/lda2");
-    CN_REQUIRE(d->ldb >= d->K && d->ldb % (bf || x6 ? 8 : 4) == 0 && al16(d->B), CN_ERR_ALIGN, "cn_linear: bad B/ldb");
+    if (x6)  // ldb = rows of the chunk-major term image
+        CN_REQUIRE(d->ldb >= cdiv(d->N, d->tile == 0 ? 128 : 64) * (d->tile == 0 ? 128 : 64) && al16(d->B), CN_ERR_ALIGN,
+                   "cn_linear: bf16x6 B image rows (ldb=%lld) must cover the N tiles", (long long)d->ldb);
+    else
+        CN_REQUIRE(d->ldb >= d->K && d->ldb % (bf ? 8 : 4) == 0 && al16(d->B), CN_ERR_ALIGN, "cn_linear: bad B/ldb");
     const int nzero = std::max(d->nzero, d->N);
     const int bn = d->tile == 0 ? 128 : 64;
     CN_REQUIRE(nzero <= cdiv(d->N, bn) * bn, CN_ERR_SHAPE,

@@ -45,14 +45,15 @@ __global__ void __launch_bounds__(256) pack_kernel(PackBatch b) {
         } else if (j.format == CN_MFMA_BF16) {
             static_cast<unsigned short*>(j.dst)[r * j.dst_ld + c] = bf16_rne(v);
         } else {
-            unsigned short* d = static_cast<unsigned short*>(j.dst);
+            // chunk-major term image: (c / 16, r, t, c % 16), dst_ld = image rows
+            unsigned short* d = static_cast<unsigned short*>(j.dst) + ((c >> 4) * j.dst_ld + r) * 48 + (c & 15);
             const unsigned short t0 = bf16_rne(v);
             const float q = v - bf16_to_f32(t0);
             const unsigned short t1 = bf16_rne(q);
             const unsigned short t2 = bf16_rne(q - bf16_to_f32(t1));
-            d[(3 * r + 0) * j.dst_ld + c] = t0;
-            d[(3 * r + 1) * j.dst_ld + c] = t1;
-            d[(3 * r + 2) * j.dst_ld + c] = t2;
+            d[0] = t0;
+            d[16] = t1;
+            d[32] = t2;
         }
     }
 }
@@ -69,7 +70,8 @@ extern "C" int cn_pack_weights(const cn_pack_job* jobs, int32_t njobs, cn_stream
         CN_REQUIRE(j.format == CN_MFMA_F32 || j.format == CN_MFMA_BF16 || j.format == CN_MFMA_F32_BF16X6, CN_ERR_ARG,
                    "cn_pack_weights: job %d bad format %d", i, j.format);
         CN_REQUIRE(0 <= j.r0 && j.r0 <= j.r1 && 0 <= j.c0 && j.c0 <= j.c1 && j.rows >= 0 && j.cols >= 0 &&
-                       j.rows <= j.r1 - j.r0 && j.cols <= j.c1 - j.c0 && j.c1 <= j.dst_ld &&
+                       j.rows <= j.r1 - j.r0 && j.cols <= j.c1 - j.c0 &&
+                       (j.format == CN_MFMA_F32_BF16X6 ? j.r1 <= j.dst_ld : j.c1 <= j.dst_ld) &&
                        (j.rows == 0 || j.cols == 0 || j.src_ld >= (j.transpose ? j.rows : j.cols)),
                    CN_ERR_SHAPE, "cn_pack_weights: job %d region [%d,%d)x[%d,%d) src %dx%d ld %lld dst ld %lld", i, j.r0,
                    j.r1, j.c0, j.c1, j.rows, j.cols, (long long)j.src_ld, (long long)j.dst_ld);

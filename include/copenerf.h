@@ -93,9 +93,11 @@ typedef struct cn_linear_desc {
                             (ldb in bf16 elements), fp32 accumulate (v_mfma_f32_32x32x16_bf16);
                             K and K1 multiples of 64 (config C3's bf16 MLP MFMA);
                             CN_MFMA_F32_BF16X6: fp32 GEMM on the bf16 MFMA: A fp32 split on load
-                            into three bf16 terms, B pre-split [N][3][ldb] bf16 (plane t of row n
-                            at B + (3n + t) ldb), six term products accumulated in fp32
-                            (error at the level of fp32 accumulation; K, K1 multiples of 32) */
+                            into three bf16 terms, B pre-split and chunk-major: bf16
+                            [K/16][ldb][3][16], term t of element (n, k) at
+                            B + ((k/16) ldb + n) 48 + 16 t + k%16, ldb = image rows >= the N
+                            tiles; six term products accumulated in fp32 (error at the level
+                            of fp32 accumulation; K, K1 multiples of 32) */
     int32_t reserved_;
 } cn_linear_desc;
 
@@ -112,7 +114,8 @@ int cn_linear(const cn_linear_desc* d, cn_stream_t stream);
  * transpose) lands at (r0, c0), the rest of the region is zero.  format is a
  * cn_mfma_dtype: CN_MFMA_F32 copies fp32 (element (r, c) at dst[r*dst_ld + c]),
  * CN_MFMA_BF16 rounds to bf16 (RNE, same indexing), CN_MFMA_F32_BF16X6 writes
- * the three bf16 terms of each value (term t at dst[(3r + t)*dst_ld + c]).
+ * the three bf16 terms of each value into cn_linear's chunk-major image (term t
+ * at dst[((c/16)*dst_ld + r)*48 + 16t + c%16]; dst_ld = the image's rows).
  * ------------------------------------------------------------------------ */
 typedef struct cn_pack_job {
     const float* src;

@@ -23,8 +23,10 @@ def test_split_terms_reconstruct():
     from copenerf import ops
     W = _rnd(256, 320, seed=1) * torch.logspace(-6, 3, 320, device=DEV)
     S = ops.split_bf16x3(W)
-    assert S.shape == (256, 3, 320) and S.dtype == torch.bfloat16
-    rec = S[:, 0].double() + S[:, 1].double() + S[:, 2].double()
+    assert S.shape == (20, 256, 48) and S.dtype == torch.bfloat16
+    T = ops.unsplit_bf16x3(S)
+    assert torch.equal(T[0], W.to(torch.bfloat16))
+    rec = T[0].double() + T[1].double() + T[2].double()
     rel = ((rec - W.double()).abs() / W.double().abs().clamp_min(1e-30)).max().item()
     assert rel <= 2.0 ** -26, rel
 
