@@ -23,6 +23,14 @@ def timeit(fn, iters=20):
     return e0.elapsed_time(e1) / iters
 
 
+ONLY = os.environ.get("ONLY", "")  # substring filter on the variant names
+
+
+def bench(res, key, fn, div=1):
+    if ONLY in key:
+        res[key] = timeit(fn) / div
+
+
 def main():
     M = int(os.environ.get("M", 524288))
     N = K = 256
@@ -36,8 +44,8 @@ def main():
     o1 = torch.empty(M, N, device=dev)
     fl = 2.0 * M * N * K
     res = {}
-    res["torch.matmul (hipBLASLt)"] = timeit(lambda: torch.matmul(A, B.t(), out=o0))
-    res["torch addmm+softplus"] = timeit(lambda: torch.nn.functional.softplus(torch.addmm(bias, A, B.t()), beta=100))
+    bench(res, "torch.matmul (hipBLASLt)", lambda: torch.matmul(A, B.t(), out=o0))
+    bench(res, "torch addmm+softplus", lambda: torch.nn.functional.softplus(torch.addmm(bias, A, B.t()), beta=100))
     for name, epi, kw in (("store", ops.EPI_STORE, dict(bias=bias)),
                           ("softplus", ops.EPI_SOFTPLUS, dict(bias=bias, out1=o1)),
                           ("softplus(no sig)", ops.EPI_SOFTPLUS, dict(bias=bias)),
@@ -46,29 +54,29 @@ def main():
                           ("bwd_softplus", ops.EPI_BWD_SOFTPLUS, dict(aux0=aux0, aux1=aux1)),
                           ("relu", ops.EPI_RELU, dict(bias=bias)),
                           ("main loop only (bench)", 7, {})):
-        res["cn_linear " + name] = timeit(lambda: ops.linear(A, B, N, K, o0, epi, **kw))
+        bench(res, "cn_linear " + name, lambda: ops.linear(A, B, N, K, o0, epi, **kw))
     Bb = B.bfloat16().contiguous()
     for name, epi, kw in (("store", ops.EPI_STORE, dict(bias=bias)),
                           ("softplus", ops.EPI_SOFTPLUS, dict(bias=bias, out1=o1)),
                           ("tangent", ops.EPI_TANGENT, dict(aux0=aux0, aux1=aux1, out1=o1)),
                           ("main loop only (bench)", 7, {})):
-        res["cn_linear bf16 " + name] = timeit(lambda: ops.linear(A, Bb, N, K, o0, epi, **kw))
+        bench(res, "cn_linear bf16 " + name, lambda: ops.linear(A, Bb, N, K, o0, epi, **kw))
     Bs = ops.split_bf16x3(B)
     for name, epi, kw in (("store", ops.EPI_STORE, dict(bias=bias)),
                           ("softplus", ops.EPI_SOFTPLUS, dict(bias=bias, out1=o1)),
                           ("tangent", ops.EPI_TANGENT, dict(aux0=aux0, aux1=aux1, out1=o1)),
                           ("bwd_softplus", ops.EPI_BWD_SOFTPLUS, dict(aux0=aux0, aux1=aux1)),
                           ("main loop only (bench)", 7, {})):
-        res["cn_linear x6 " + name] = timeit(lambda: ops.linear(A, Bs, N, K, o0, epi, **kw))
-    res["torch.matmul bf16 (hipBLASLt)"] = timeit(lambda: torch.matmul(A.bfloat16(), Bb.t()))
+        bench(res, "cn_linear x6 " + name, lambda: ops.linear(A, Bs, N, K, o0, epi, **kw))
+    bench(res, "torch.matmul bf16 (hipBLASLt)", lambda: torch.matmul(A.bfloat16(), Bb.t()))
     dW = torch.empty(N, K, device=dev)
     db = torch.empty(N, device=dev)
-    res["cn_wgrad 1 pair"] = timeit(lambda: ops.wgrad(A, A, N, K, dW, db=db))
-    res["cn_wgrad 2 pairs"] = timeit(lambda: ops.wgrad(A, A, N, K, dW, db=db, Y1=aux1, X1=aux0)) / 2
-    res["cn_wgrad x6 1 pair"] = timeit(lambda: ops.wgrad(A, A, N, K, dW, db=db, mode="bf16x6"))
-    res["cn_wgrad x6 2 pairs"] = timeit(lambda: ops.wgrad(A, A, N, K, dW, db=db, Y1=aux1, X1=aux0, mode="bf16x6")) / 2
-    res["cn_wgrad bf16 2 pairs"] = timeit(lambda: ops.wgrad(A, A, N, K, dW, db=db, Y1=aux1, X1=aux0, mode="bf16")) / 2
-    res["torch A^T A"] = timeit(lambda: torch.matmul(A.t(), A, out=dW))
+    bench(res, "cn_wgrad 1 pair", lambda: ops.wgrad(A, A, N, K, dW, db=db))
+    bench(res, "cn_wgrad 2 pairs", lambda: ops.wgrad(A, A, N, K, dW, db=db, Y1=aux1, X1=aux0), 2)
+    bench(res, "cn_wgrad x6 1 pair", lambda: ops.wgrad(A, A, N, K, dW, db=db, mode="bf16x6"))
+    bench(res, "cn_wgrad x6 2 pairs", lambda: ops.wgrad(A, A, N, K, dW, db=db, Y1=aux1, X1=aux0, mode="bf16x6"), 2)
+    bench(res, "cn_wgrad bf16 2 pairs", lambda: ops.wgrad(A, A, N, K, dW, db=db, Y1=aux1, X1=aux0, mode="bf16"), 2)
+    bench(res, "torch A^T A", lambda: torch.matmul(A.t(), A, out=dW))
     for k, ms in res.items():
         print(f"{k:32s} {ms*1e3:9.1f} us  {fl / ms / 1e9:8.1f} TFLOP/s")
 
