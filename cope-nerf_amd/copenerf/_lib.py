@@ -102,6 +102,9 @@ SIGNATURES = {
     "cn_points_bwd": (c_i32, [c_i32, c_i32, c_ptr, c_i32, c_ptr, c_ptr, c_i32, c_ptr, c_i64, c_ptr, c_ptr,
                               c_ptr]),
     "cn_color_extras_bwd": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_i32, c_ptr, c_i32, c_ptr]),
+    "cn_train_loss_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32]),
+    "cn_train_loss": (c_i32, [c_i32, c_i32, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_f32, c_f32, c_f32, c_f32,
+                              c_f32, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr]),
 }
 
 _lock = threading.Lock()

@@ -3,14 +3,18 @@
   SmoothnessLoss / EdgePreservingSmoothnessLoss   model/losses.py:7-38
   rgb L1 + mse, weighted sum, NaN guard           model/training.py:490-549
   eikonal                                         train.py:526
-They act on [R,3] / [R/16,4,4] / [M,3] tensors -- a few µs of elementwise work
-on the device next to the ~10^2 ms of MLP work -- and stay torch expressions so
-train.py's loss code runs unchanged on the HIP renderer's outputs.
+The classes and functions below are the reference's own torch expressions, so
+train.py's loss code runs unchanged on the HIP renderer's outputs.  Those
+expressions launch ~150 small kernels per step (forward + autograd);
+`train_losses` computes the same weighted sum and its input gradients with one
+HIP call (cn_train_loss: three launches) and is what the training step uses.
 """
 from __future__ import annotations
 
 import torch
 from torch import nn
+
+from . import ops
 
 
 def _l1mean(x):
@@ -53,3 +57,33 @@ def eikonal_loss(normals):
 
 def rgb_l1(rgb, gt):
     return torch.sum(torch.abs(rgb - gt)) / float(rgb.shape[0])
+
+
+class _TrainLossFn(torch.autograd.Function):
+    """(color, gt, depth, normals) -> weighted loss; the input gradients come out of
+    the same cn_train_loss call and are scaled by the upstream gradient."""
+
+    @staticmethod
+    def forward(ctx, color, gt, depth, normals, w_rgb, w_eik, w_edge, w_smooth, patch, gamma):
+        shape = normals.shape
+        loss, dc, dd, dn = ops.train_loss(color.contiguous(), gt.contiguous(), depth.contiguous(),
+                                          normals.reshape(-1, 3), w_rgb=w_rgb, w_eik=w_eik, w_edge=w_edge,
+                                          w_smooth=w_smooth, patch=patch, gamma=gamma)
+        ctx.save_for_backward(dc, dd.view(depth.shape), dn.view(shape))
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        dc, dd, dn = ctx.saved_tensors
+        dc, dd, dn = torch._foreach_mul([dc, dd, dn], g)
+        return dc, None, dd, dn, None, None, None, None, None, None
+
+
+def train_losses(color, gt, depth, normals, *, w_rgb=1.0, w_eik=0.1, w_edge=1.0, w_smooth=1e-4, patch=4,
+                 gamma=0.1):
+    """w_rgb rgb_l1 + w_eik eikonal + w_edge EdgePreservingSmoothnessLoss + w_smooth
+    SmoothnessLoss on patch x patch ray patches, on the device in one call
+    (color [R,3], gt [R,3], depth [R,1], normals [..., 3] sample normals)."""
+    return _TrainLossFn.apply(color, gt, depth, normals, float(w_rgb), float(w_eik),
+                              float(w_edge if patch > 1 else 0.0), float(w_smooth if patch > 1 else 0.0),
+                              int(patch), float(gamma))

@@ -373,3 +373,25 @@ def color_extras_bwd(d_ext, dirs, dir_div, multires_view, ddirs, accumulate=Fals
     _lib.call("cn_color_extras_bwd", dirs.shape[0], dir_div, _ptr(d_ext), _ld(d_ext), _ptr(dirs), _ld(dirs),
               multires_view, _ptr(ddirs), 1 if accumulate else 0, _stream())
     return ddirs
+
+
+def train_loss(color, gt, depth, normals, *, w_rgb=1.0, w_eik=0.1, w_edge=1.0, w_smooth=1e-4, patch=4, gamma=0.1):
+    """(loss [], dcolor [R,3], ddepth [R,1], dnormals [M,3]) -- cn_train_loss: the colour
+    L1, eikonal, edge-aware and plain smoothness terms and their input gradients.
+    normals may be any [M,3] row view (e.g. the first three columns of ∇ₓSDF)."""
+    for t, n in ((color, "color"), (gt, "gt"), (normals, "normals")):
+        _need(t, n)
+    _need(depth.reshape(-1, 1), "depth")
+    R, M, dev = color.shape[0], normals.shape[0], color.device
+    if not (color.is_contiguous() and gt.is_contiguous() and depth.is_contiguous()):
+        raise RuntimeError("train_loss: color, gt and depth must be contiguous")
+    lib = _lib.load()
+    ws = torch.empty(lib.cn_train_loss_workspace_bytes(R, patch) // 8 + 1, device=dev, dtype=torch.float64)
+    loss = torch.empty((), device=dev)
+    dcolor = torch.empty_like(color)
+    ddepth = torch.empty(R, 1, device=dev)
+    dn = torch.empty(M, 3, device=dev)
+    _lib.call("cn_train_loss", R, patch, M, _ptr(color), _ptr(gt), _ptr(depth), _ptr(normals), _ld(normals),
+              float(w_rgb), float(w_eik), float(w_edge), float(w_smooth), float(gamma), _ptr(loss), _ptr(dcolor),
+              _ptr(ddepth), _ptr(dn), 3, _ptr(ws), ws.numel() * 8, _stream())
+    return loss, dcolor, ddepth, dn

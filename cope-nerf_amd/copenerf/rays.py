@@ -23,7 +23,10 @@ def get_patch_indices(h, w, patch_size, n_points, generator=None, device="cpu"):
     n_patches = n_points // (patch_size ** 2)
     h_adj, w_adj = h - patch_size + 1, w - patch_size + 1
     n_patches = min(n_patches, h_adj * w_adj)
-    corners = torch.randperm(h_adj * w_adj, generator=generator, device=device)[:n_patches]
+    # a uniformly random n_patches-subset of the corners, as randperm(...)[:n_patches]
+    # (training.py:422), by the top-k of random keys instead of a full device sort
+    keys = torch.rand(h_adj * w_adj, generator=generator, device=device)
+    corners = torch.topk(keys, n_patches, sorted=False).indices
     rows, cols = corners // w_adj, corners % w_adj
     offs = torch.arange(patch_size, device=device).repeat(patch_size, 1)
     offs = (offs + offs.t() * w).flatten()

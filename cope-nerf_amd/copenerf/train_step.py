@@ -25,7 +25,7 @@ import torch
 import torch.distributed as dist
 
 from .fields import RenderingNetwork, SDFNetwork, SingleVarianceNetwork
-from .losses import EdgePreservingSmoothnessLoss, SmoothnessLoss, eikonal_loss, rgb_l1
+from .losses import EdgePreservingSmoothnessLoss, SmoothnessLoss, eikonal_loss, rgb_l1, train_losses
 from .motion import MotionNetwork, scene_flow_loss, world_points
 from .rays import (PoseRetriever, get_patch_indices, inv4x4, intrinsics_ndc, near_far_from_sphere, pixels_from_indices,
                    world_rays)
@@ -50,11 +50,8 @@ def flat_allreduce_mean(params, group=None):
     flat = torch.cat([g.reshape(-1) for g in grads])
     dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
     flat.div_(world)
-    off = 0
-    for g in grads:
-        n = g.numel()
-        g.copy_(flat[off:off + n].view_as(g))
-        off += n
+    views = [v.view_as(g) for v, g in zip(flat.split([g.numel() for g in grads]), grads)]
+    torch._foreach_copy_(grads, views)  # one multi-tensor launch instead of a copy per parameter
 
 
 class SyntheticTrainer:
@@ -115,6 +112,14 @@ class SyntheticTrainer:
         return rays_o, rays_d, norm, rgb_gt
 
     def loss(self, out, rgb_gt):
+        """L1 rgb + eikonal + edge-aware / plain depth smoothness (training.py:506-533,
+        train.py:519-526) in one HIP call; `loss_torch` is the same sum as torch
+        expressions of the reference's loss classes."""
+        w = self.w
+        return train_losses(out["color_fine"], rgb_gt, out["depth_pred"], out["normals"], w_rgb=w["rgb"],
+                            w_eik=w["eikonal"], w_edge=w["edge"], w_smooth=w["smooth"], patch=self.patch)
+
+    def loss_torch(self, out, rgb_gt):
         w = self.w
         loss = w["rgb"] * rgb_l1(out["color_fine"], rgb_gt) + w["eikonal"] * eikonal_loss(out["normals"])
         if self.patch > 1:

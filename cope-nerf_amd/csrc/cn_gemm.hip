@@ -1118,51 +1118,86 @@ static int launch_slab_reduce(const float* part, int nslab, int64_t stride, int 
 
 
 // ---------------------------------------------------------------------------
-// Per-row heads: out[dst(m)][c] = act(sum_k A[m][k] W[c][k] + b[c]).  One
-// wavefront per row (K <= 256: one float4 per lane), shuffle reduction.
-__global__ void row_head_kernel(int M, int K, const float* __restrict__ A, int64_t lda,
-                                const float* __restrict__ W, int64_t ldw, const float* __restrict__ b,
-                                int C, int act, float* out, int64_t ld_out, const int* dst) {
+// Per-row heads: out[dst(m)][c] = act(sum_k A[m][k] W[c][k] + b[c]).  A row is
+// read by a 16-lane group (lane g holds columns 4g + 64j, j < 4: four coalesced
+// 256-byte segments), so a wavefront covers 4 rows per pass and 2 passes are
+// unrolled: 8 independent 16-byte loads per lane in flight.  The 16 partial sums
+// of a row meet in a fixed xor-shuffle tree (deterministic).
+__global__ void __launch_bounds__(256) row_head_kernel(int M, int K, const float* __restrict__ A, int64_t lda,
+                                                       const float* __restrict__ W, int64_t ldw,
+                                                       const float* __restrict__ b, int C, int act, float* out,
+                                                       int64_t ld_out, const int* dst) {
     const int lane = threadIdx.x & 63;
-    const int wpb = blockDim.x >> 6;
-    const int64_t wave0 = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6);
-    const int64_t nw = (int64_t)gridDim.x * wpb;
-    const int k = lane * 4;
-    floatx4 wv[4];
+    const int g = lane & 15;   // column group of the lane
+    const int sub = lane >> 4; // row of the wave's 4-row pass
+    const int64_t wave0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    floatx4 wv[4][4];
 #pragma unroll
     for (int c = 0; c < 4; ++c)
-        wv[c] = (c < C && k < K) ? *reinterpret_cast<const floatx4*>(W + c * ldw + k)
-                                 : floatx4{0.f, 0.f, 0.f, 0.f};
-    for (int64_t m = wave0; m < M; m += nw) {
-        const floatx4 a = k < K ? *reinterpret_cast<const floatx4*>(A + m * lda + k) : floatx4{0.f, 0.f, 0.f, 0.f};
-        float s[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) s[c] = a[0] * wv[c][0] + a[1] * wv[c][1] + a[2] * wv[c][2] + a[3] * wv[c][3];
+        for (int j = 0; j < 4; ++j) {
+            const int k = 4 * g + 64 * j;
+            wv[c][j] = (c < C && k < K) ? *reinterpret_cast<const floatx4*>(W + c * ldw + k) : floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+    float bias[4];
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1)
+    for (int c = 0; c < 4; ++c) bias[c] = (b && c < C) ? b[c] : 0.0f;
+    constexpr int U = 2;  // 4-row passes per iteration
+    for (int64_t m0 = wave0 * 4 * U; m0 < M; m0 += nw * 4 * U) {
+        floatx4 a[U][4];
 #pragma unroll
-            for (int c = 0; c < 4; ++c) s[c] += __shfl_xor(s[c], off);
-        if (lane < C) {
-            float v = s[0];
+        for (int u = 0; u < U; ++u) {
+            const int64_t m = m0 + 4 * u + sub;
 #pragma unroll
-            for (int c = 1; c < 4; ++c)
-                if (lane == c) v = s[c];
-            if (b) v = v + b[lane];
-            if (act == 1) v = sigmoidf_ref(v);
-            const int64_t o = dst ? (int64_t)dst[m] : m;
-            out[o * ld_out + lane] = v;
+            for (int j = 0; j < 4; ++j) {
+                const int k = 4 * g + 64 * j;
+                a[u][j] = (m < M && k < K) ? *reinterpret_cast<const floatx4*>(A + m * lda + k) : floatx4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            float s[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                float t = 0.0f;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    t += (a[u][j][0] * wv[c][j][0] + a[u][j][1] * wv[c][j][1]) + (a[u][j][2] * wv[c][j][2] + a[u][j][3] * wv[c][j][3]);
+                s[c] = t;
+            }
+#pragma unroll
+            for (int off = 8; off > 0; off >>= 1)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) s[c] += __shfl_xor(s[c], off);
+            const int64_t m = m0 + 4 * u + sub;
+            if (g < C && m < M) {
+                float v = s[0];
+#pragma unroll
+                for (int c = 1; c < 4; ++c)
+                    if (g == c) v = s[c];
+                v = v + bias[g];
+                if (act == 1) v = sigmoidf_ref(v);
+                const int64_t o = dst ? (int64_t)dst[m] : m;
+                out[o * ld_out + g] = v;
+            }
         }
     }
 }
 
-__global__ void scale_cols_kernel(int M, int N, const float* __restrict__ X, int64_t ldx,
-                                  const float* __restrict__ w, float* out, int64_t ldo) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t tot = (int64_t)M * N;
-    if (idx >= tot) return;
-    const int64_t m = idx / N;
-    const int n = idx % N;
-    out[m * ldo + n] = X[m * ldx + n] * w[n];
+// out[m][n] = X[m][n] * w[n], float4-vectorized (N, the leading dimensions and
+// the pointers are multiples of 4 floats / 16-byte aligned: checked by the host).
+__global__ void __launch_bounds__(256) scale_cols_kernel(int M, int N4, const float* __restrict__ X, int64_t ldx,
+                                                         const float* __restrict__ w, float* out, int64_t ldo) {
+    const int64_t tot = (int64_t)M * N4;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += stride) {
+        const int64_t m = idx / N4;
+        const int n = (int)(idx - m * N4) * 4;
+        const floatx4 x = *reinterpret_cast<const floatx4*>(X + m * ldx + n);
+        const floatx4 s = *reinterpret_cast<const floatx4*>(w + n);
+        *reinterpret_cast<floatx4*>(out + m * ldo + n) = x * s;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1184,22 +1219,37 @@ __global__ void rgb_head_bwd_kernel(int M, int K, const float* __restrict__ drgb
         w2 = W3[2 * K + k];
     }
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, ab = 0.f;
-    for (int m = m0; m < m1; ++m) {
-        const float g0 = drgb[3 * (int64_t)m], g1 = drgb[3 * (int64_t)m + 1], g2 = drgb[3 * (int64_t)m + 2];
-        const float y0 = rgb[3 * (int64_t)m], y1 = rgb[3 * (int64_t)m + 1], y2 = rgb[3 * (int64_t)m + 2];
-        // torch sigmoid_backward: grad * (1 - y) * y
-        const float d0 = g0 * (1.0f - y0) * y0;
-        const float d1 = g1 * (1.0f - y1) * y1;
-        const float d2 = g2 * (1.0f - y2) * y2;
-        if (kv) {
-            const float hv = H3[(int64_t)m * ld_h + k];
-            const float dh = d0 * w0 + d1 * w1 + d2 * w2;
-            dZ2[(int64_t)m * ld_dz + k] = hv > 0.0f ? dh : 0.0f;
-            a0 += d0 * hv;
-            a1 += d1 * hv;
-            a2 += d2 * hv;
+    // 4 rows per iteration: their H3 loads are issued together (the sums keep row order)
+    constexpr int U = 4;
+    for (int mb = m0; mb < m1; mb += U) {
+        float hv[U], g[U][3], y[U][3];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int m = mb + u < m1 ? mb + u : m1 - 1;  // clamped: rows past m1 are loaded, not used
+            hv[u] = kv ? H3[(int64_t)m * ld_h + k] : 0.0f;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                g[u][c] = drgb[3 * (int64_t)m + c];
+                y[u][c] = rgb[3 * (int64_t)m + c];
+            }
         }
-        if (k < 3) ab += (k == 0 ? d0 : (k == 1 ? d1 : d2));
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (mb + u >= m1) break;
+            const int m = mb + u;
+            // torch sigmoid_backward: grad * (1 - y) * y
+            const float d0 = g[u][0] * (1.0f - y[u][0]) * y[u][0];
+            const float d1 = g[u][1] * (1.0f - y[u][1]) * y[u][1];
+            const float d2 = g[u][2] * (1.0f - y[u][2]) * y[u][2];
+            if (kv) {
+                const float dh = d0 * w0 + d1 * w1 + d2 * w2;
+                dZ2[(int64_t)m * ld_dz + k] = hv[u] > 0.0f ? dh : 0.0f;
+                a0 += d0 * hv[u];
+                a1 += d1 * hv[u];
+                a2 += d2 * hv[u];
+            }
+            if (k < 3) ab += (k == 0 ? d0 : (k == 1 ? d1 : d2));
+        }
     }
     float* pb = part + (int64_t)blockIdx.x * 4 * K;
     if (kv) {
@@ -1222,20 +1272,30 @@ __global__ void __launch_bounds__(256) colsum_kernel(int M, int K, const float* 
     const int rg = threadIdx.x >> 6;
     const int m0 = blockIdx.x * kColsumRows;
     const int m1 = min(M, m0 + kColsumRows);
-    floatx4 a = {0.f, 0.f, 0.f, 0.f};
+    // four independent row streams per thread (rows m0 + rg + 4i, by i mod 4), combined in a fixed order
+    floatx4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     const bool vec = (c + 3 < K) && (ldx % 4 == 0);
     if (c < K) {
-        for (int m = m0 + rg; m < m1; m += 4) {
-            floatx4 x;
-            if (vec) {
-                x = *reinterpret_cast<const floatx4*>(X + (int64_t)m * ldx + c);
-            } else {
-                for (int e = 0; e < 4; ++e) x[e] = (c + e < K) ? X[(int64_t)m * ldx + c + e] : 0.0f;
+        for (int mb = m0 + rg; mb < m1; mb += 16) {
+            floatx4 x[4];
+            float wm[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int m = mb + 4 * u;
+                const bool in = m < m1;
+                if (vec) {
+                    x[u] = in ? *reinterpret_cast<const floatx4*>(X + (int64_t)m * ldx + c) : floatx4{0.f, 0.f, 0.f, 0.f};
+                } else {
+                    for (int e = 0; e < 4; ++e) x[u][e] = (in && c + e < K) ? X[(int64_t)m * ldx + c + e] : 0.0f;
+                }
+                wm[u] = (w && in) ? w[m] : 1.0f;
             }
-            const float wm = w ? w[m] : 1.0f;
-            for (int e = 0; e < 4; ++e) a[e] += w ? wm * x[e] : x[e];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                for (int e = 0; e < 4; ++e) acc[u][e] += w ? wm[u] * x[u][e] : x[u][e];
         }
     }
+    const floatx4 a = (acc[0] + acc[1]) + (acc[2] + acc[3]);
     for (int e = 0; e < 4; ++e) red[rg][(threadIdx.x & 63) * 4 + e] = a[e];
     __syncthreads();
     if (rg == 0 && c < K) {
@@ -1470,7 +1530,7 @@ extern "C" int cn_row_head(int32_t M, int32_t K, const float* A, int64_t lda, co
     CN_REQUIRE(lda % 4 == 0 && ldw % 4 == 0 && al16(A) && al16(W), CN_ERR_ALIGN, "cn_row_head: alignment");
     CN_REQUIRE(act == 0 || act == 1, CN_ERR_ARG, "cn_row_head: act");
     if (M == 0) return CN_OK;
-    const int blocks = std::min(cdiv(M, 4), 4096);
+    const int blocks = std::min(cdiv(M, 32), 8192);  // 4 waves x 8 rows per iteration
     row_head_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(M, K, A, lda, W, ldw, b, C, act, out, ld_out, dst_index);
     return check_launch("cn_row_head");
 }
@@ -1478,9 +1538,12 @@ extern "C" int cn_row_head(int32_t M, int32_t K, const float* A, int64_t lda, co
 extern "C" int cn_scale_cols(int32_t M, int32_t N, const float* X, int64_t ldx, const float* w, float* out,
                              int64_t ld_out, cn_stream_t stream) {
     CN_REQUIRE(X && w && out, CN_ERR_ARG, "cn_scale_cols: null pointer");
+    CN_REQUIRE(N % 4 == 0 && ldx % 4 == 0 && ld_out % 4 == 0 && al16(X) && al16(w) && al16(out), CN_ERR_ALIGN,
+               "cn_scale_cols: N, leading dimensions and pointers must be multiples of 4 floats");
     if ((int64_t)M * N == 0) return CN_OK;
-    const int64_t tot = (int64_t)M * N;
-    scale_cols_kernel<<<(int)((tot + 255) / 256), 256, 0, (hipStream_t)stream>>>(M, N, X, ldx, w, out, ld_out);
+    const int64_t tot = (int64_t)M * (N / 4);
+    const int blocks = (int)std::min<int64_t>((tot + 255) / 256, 8192);
+    scale_cols_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(M, N / 4, X, ldx, w, out, ld_out);
     return check_launch("cn_scale_cols");
 }
 

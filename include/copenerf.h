@@ -285,6 +285,23 @@ int cn_composite_bwd(int32_t R, int32_t S, const float* z, const float* sdf, con
                      const float* dcdf, float* dsdf, float* dG, float* drgb, float* dinv_s_part,
                      float* drays_d, cn_stream_t stream);
 
+/* ------------------------------------------------------------------------ *
+ * Training losses in one pass: the loss value and its input gradients
+ * (model/training.py:506-509 colour L1, train.py:526 eikonal, model/losses.py:7-38
+ * with train.py:519-525 edge-aware and plain depth smoothness on patch x patch
+ * ray patches, patch in 1..4; R rays, M samples):
+ *   loss = w_rgb sum|color - gt| / R + w_eik mean_m (|n_m| - 1)^2
+ *        + w_edge EdgePreservingSmoothness(depth, gt; gamma) + w_smooth Smoothness(depth)
+ *   color, gt [R][3]; depth [R]; normals [M][ld_n] (columns 0..2); loss [1];
+ *   dcolor [R][3], ddepth [R], dnormals [M][ld_dn] (columns 0..2) = d loss / d input.
+ * Partial sums are reduced in double in a fixed order (bitwise reproducible).
+ * ------------------------------------------------------------------------ */
+size_t cn_train_loss_workspace_bytes(int32_t R, int32_t patch);
+int cn_train_loss(int32_t R, int32_t patch, int64_t M, const float* color, const float* gt, const float* depth,
+                  const float* normals, int64_t ld_n, float w_rgb, float w_eik, float w_edge, float w_smooth,
+                  float gamma, float* loss, float* dcolor, float* ddepth, float* dnormals, int64_t ld_dn,
+                  void* workspace, int64_t workspace_bytes, cn_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -63,6 +63,11 @@ def test_argument_validation_without_gpu():
     w = _lib.WgradDesc()
     assert lib.cn_wgrad(ctypes.byref(w), None) == -1
     assert lib.cn_wgrad_workspace_bytes(524288, 256, 256) >= 4 * 256 * 256
+    ws = lib.cn_train_loss_workspace_bytes(4096, 4)
+    assert ws >= 8 * (4096 // 16 // 256)
+    assert lib.cn_train_loss(4096, 5, 0, 16, 16, 16, None, 0, 1.0, 0.1, 1.0, 1e-4, 0.1, 16, 16, 16, None, 0, 16, ws,
+                             None) == -5
+    assert b"patch 5" in lib.cn_last_error()
 
 
 def test_product_path_refuses_cpu_tensors():

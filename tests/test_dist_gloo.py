@@ -1,9 +1,11 @@
-"""Data-parallel gradient exchange (train_step.flat_allreduce_mean) on 2 gloo
-ranks: each rank differentiates the oracle on its half of the rays; after the
-flat all-reduce every rank holds the single-process gradient of the full batch."""
+"""Data-parallel gradient exchange (train_step.flat_allreduce_mean) on 2 and 4
+gloo ranks: each rank differentiates the oracle on its share of the rays (whole
+4x4 patches); after the flat all-reduce every rank holds the single-process
+gradient of the full batch."""
 import os
 import socket
 
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -48,9 +50,9 @@ def _worker(rank, world, port, q):
     torch.set_num_threads(1)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     from copenerf.train_step import flat_allreduce_mean
-    full = _batch(32, 0)
-    half = tuple(t[rank * 16:(rank + 1) * 16] for t in full)  # whole 4x4 patches per rank
-    names, gr = _grads(half)
+    full = _batch(16 * world, 0)
+    part = tuple(t[rank * 16:(rank + 1) * 16] for t in full)  # one whole 4x4 patch group per rank
+    names, gr = _grads(part)
     params = [torch.nn.Parameter(torch.zeros_like(g)) for g in gr]
     for p, g in zip(params, gr):
         p.grad = g.clone()
@@ -60,8 +62,9 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_allreduce_equals_full_batch():
-    world, port = 2, _free_port()
+@pytest.mark.parametrize("world", [2, 4])
+def test_allreduce_equals_full_batch(world):
+    port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
@@ -71,7 +74,7 @@ def test_two_rank_allreduce_equals_full_batch():
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    names, ref = _grads(_batch(32, 0))
+    names, ref = _grads(_batch(16 * world, 0))
     for n, r in zip(names, ref):
         for rank in range(world):
             torch.testing.assert_close(torch.from_numpy(res[rank][n]), r, rtol=1e-4, atol=1e-6, msg=lambda m: f"{n} rank {rank}: {m}")

@@ -258,3 +258,64 @@ def test_up_sample_merge_matches_reference_seams(n):
     pos_old[dst.long()] = float("nan")
     kept = pos_old[~torch.isnan(pos_old)].reshape(R, n)
     torch.testing.assert_close(kept.cpu(), sd, rtol=0, atol=0)
+
+
+def test_row_head_edge_cases_and_rgb_head_bwd():
+    """row_head with one output scattered through dst_index, K < 256 and a row
+    count that is not a multiple of the 8-row pass; rgb_head_bwd (sigmoid + Linear
+    256 -> 3 backward, neus_fields.py:367-373) against torch autograd."""
+    ops = _ops()
+    M, K = 5003, 64
+    A = _rnd(M, K, seed=23)
+    W = _rnd(1, K, seed=24, scale=0.2)
+    b = _rnd(1, seed=25)
+    dst = torch.randperm(M, device=DEV).to(torch.int32)
+    out = torch.full((M, 1), float("nan"), device=DEV)
+    ops.row_head(A, K, W, b, 1, 0, out, dst_index=dst)
+    ref = torch.empty(M, 1, device=DEV)
+    ref[dst.long()] = A @ W.t() + b
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-6)
+    M, K = 3001, 256
+    H3 = torch.relu(_rnd(M, K, seed=26))
+    W3 = _rnd(3, K, seed=27, scale=0.1).requires_grad_(True)
+    b3 = _rnd(3, seed=28).requires_grad_(True)
+    Z = _rnd(M, K, seed=29)  # pre-activation whose relu is H3's pattern
+    Z = torch.where(H3 > 0, H3, -Z.abs()).requires_grad_(True)
+    rgb = torch.sigmoid(torch.relu(Z) @ W3.t() + b3)
+    drgb = _rnd(M, 3, seed=30)
+    gZ, gW, gb = torch.autograd.grad(rgb, [Z, W3, b3], drgb)
+    dZ = torch.empty(M, K, device=DEV)
+    dW = torch.empty(3, K, device=DEV)
+    db = torch.empty(3, device=DEV)
+    ops.rgb_head_bwd(drgb, rgb.detach().contiguous(), torch.relu(Z).detach(), K, W3.detach().contiguous(), dZ, dW, db)
+    torch.testing.assert_close(dZ, gZ, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(dW, gW, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(db, gb, rtol=1e-4, atol=1e-5)
+    cs = torch.empty(K, device=DEV)
+    ops.colsum(H3, K, cs)
+    torch.testing.assert_close(cs, H3.double().sum(0).float(), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("patch", [4, 2, 1])
+def test_train_loss_matches_reference_losses(patch):
+    """cn_train_loss (value and input gradients) against the oracle's torch
+    statement of training.py:506-509, train.py:519-526 and losses.py:7-38."""
+    from copenerf.losses import train_losses
+    R, S = 4096, 32
+    g = torch.Generator(device=DEV).manual_seed(31)
+    color = torch.rand(R, 3, device=DEV, generator=g).requires_grad_(True)
+    gt = torch.rand(R, 3, device=DEV, generator=g)
+    depth = (torch.rand(R, 1, device=DEV, generator=g) * 3).requires_grad_(True)
+    G = torch.randn(R * S, 4, device=DEV, generator=g)
+    G[:7, :3] = 0.0  # zero normals: the norm's gradient is 0 there
+    G.requires_grad_(True)
+    normals = G[:, :3].reshape(R, S, 3)
+    w = dict(w_rgb=1.0, w_eik=0.1, w_edge=1.0, w_smooth=1e-4)
+    ref = O.train_loss({"color_fine": color, "normals": normals, "depth_pred": depth}, gt, patch=patch, **w)
+    r_grads = torch.autograd.grad(ref, [color, depth, G], allow_unused=True)  # patch 1: depth unused
+    r_grads = [torch.zeros_like(t) if gr is None else gr for gr, t in zip(r_grads, (color, depth, G))]
+    got = train_losses(color, gt, depth, normals, patch=patch, **w)
+    g_grads = torch.autograd.grad(got * 2.0, [color, depth, G])  # upstream gradient scales the inputs'
+    assert abs(got.item() - ref.item()) <= 1e-6 * abs(ref.item()), (got.item(), ref.item())
+    for a, b, n in zip(g_grads, r_grads, ("color", "depth", "G")):
+        torch.testing.assert_close(a, 2.0 * b, rtol=1e-5, atol=1e-9, msg=lambda m: f"{n}: {m}")
