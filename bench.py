@@ -54,12 +54,14 @@ def kernel_symbol(key):
     cn_linear dispatch: waves, tiles, BK, workgroups/CU, prefetch depth,
     epilogue, row vector, operand mode).  fp32: BK 32 with the 2-deep prefetch
     (every K on the C2 path is a multiple of 64); bf16: BK 64, 1-deep; bf16x6
-    (split fp32): BK 16, 2-deep."""
+    (split fp32): 256x128 tiles, BK 32, one workgroup per CU for STORE / SOFTPLUS
+    / RELU at K % 64 == 0 (every such K on C2), else 128x128, BK 16, 2-deep."""
     if key[0] == "linear":
-        tiles = {0: "2, 2, 2, 2", 1: "4, 1, 1, 2"}
+        wide = "x6" in key[3:] and key[1] == 0 and key[2] in ("store", "softplus", "relu")  # K % 64 == 0 on C2
+        tiles = {0: "4, 2, 2, 2" if wide else "2, 2, 2, 2", 1: "4, 1, 1, 2"}
         epi = {"store": 0, "softplus": 1, "relu": 2, "mul": 3, "tangent": 4, "bwd_softplus": 5, "bwd_relu": 6}
         mode = 1 if "bf16" in key[3:] else 2 if "x6" in key[3:] else 0
-        mid = {0: "32, 2, 2", 1: "64, 2, 1", 2: "16, 2, 2"}[mode]
+        mid = {0: "32, 2, 2", 1: "64, 2, 1", 2: "32, 1, 2" if wide else "16, 2, 2"}[mode]
         return f"void cn::linear_kernel<{tiles[key[1]]}, {mid}, {epi[key[2]]}, false, {mode}>(cn::LinearArgs)"
     if "bf16" in key[2:]:
         return "void cn::wgrad_bf16_kernel<2, 2, 2, 2>(cn::WgradArgs) + cn::slab_reduce_kernel"

@@ -171,7 +171,8 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     constexpr bool BF = MODE != 0;               // bf16 MFMA (modes 1, 2)
     constexpr int NPL = MODE == 2 ? 3 : 1;       // bf16 planes per operand
     // padded LDS row in dwords: 36 in every mode (BK = 32 f32 / 64 bf16 / 16 split: 3 x 8 + 12 pad)
-    constexpr int LS = (BF ? NPL * BK / 2 : BK) + (MODE == 2 ? 12 : 4);
+    // (BK = 32 split: 3 x 16 + 4 pad = 52, conflict-free like wgrad_x6_kernel's rows)
+    constexpr int LS = (BF ? NPL * BK / 2 : BK) + (MODE == 2 && BK == 16 ? 12 : 4);
     constexpr int KC4 = BK / 4;                  // A: fp32 float4 per staged row
     static_assert(NT % KC4 == 0, "staging rows");
     constexpr int RSTEP = NT / KC4;  // staged A rows per load instruction
@@ -208,6 +209,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     const int srow = tid / KC4, sc4 = tid % KC4;
     const int srowb = tid / KCB, scb = tid % KCB;
     int voA[ALD], voA2[ALD], voB[BLD];  // byte offsets of the staged rows (range-checked)
+    int ldsB[BLD];                      // MODE 2: LDS dword offset of B piece q within a buffer
 #pragma unroll
     for (int q = 0; q < ALD; ++q) {
         voA[q] = ((srow + q * RSTEP) * p.lda + sc4 * 4) * 4;
@@ -215,9 +217,14 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     }
 #pragma unroll
     for (int q = 0; q < BLD; ++q) {
-        if constexpr (MODE == 2) {  // the chunk's B tile is contiguous: piece idx at byte 16 idx
+        if constexpr (MODE == 2) {
+            // a stage is BK/16 image chunks; a chunk's B tile is contiguous ([BN rows][6 pieces of
+            // 16 bytes]), consecutive chunks ldb * 96 bytes apart.  Piece idx: chunk h, row w / 6,
+            // term (w % 6) / 2, k half w % 2 -> LDS dword term * BK/2 + 8 h + 4 (w % 2) of the row.
             const int idx = tid + q * NT;
-            voB[q] = idx < BN * KCB ? idx * 16 : 0;
+            const int h = idx / (BN * 6), w = idx % (BN * 6);
+            voB[q] = idx < BN * KCB ? h * p.ldb * 96 + w * 16 : 0;
+            ldsB[q] = (w / 6) * LS + ((w % 6) >> 1) * (BK / 2) + 8 * h + 4 * (w & 1);
         } else {
             voB[q] = (srowb + q * RSTEPB) * p.ldb * ESZB + scb * 16;
         }
@@ -247,9 +254,9 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             ra[set][q] = bload4(rA, second ? voA2[q] : voA[q], ak * 4);
         }
         // MODE 2: chunk kc of the image is [ldb rows][48 bf16]; the tile's BN rows are 96 * BN contiguous bytes
-        const int64_t bofs = MODE == 2 ? ((int64_t)kc * p.ldb + n0) * 96 : (int64_t)n0 * p.ldb * ESZB;
+        const int64_t bofs = MODE == 2 ? ((int64_t)kc * (BK / 16) * p.ldb + n0) * 96 : (int64_t)n0 * p.ldb * ESZB;
         const rsrc_t rB = make_view(reinterpret_cast<const float*>(reinterpret_cast<const char*>(p.B) + bofs),
-                                    valid ? (MODE == 2 ? BN * 96 : BN * p.ldb * ESZB) : 0);
+                                    valid ? (MODE == 2 ? ((BK / 16 - 1) * p.ldb + BN) * 96 : BN * p.ldb * ESZB) : 0);
 #pragma unroll
         for (int q = 0; q < BLD; ++q) {
 #if X6_EXP == 4 || X6_EXP == 5
@@ -283,7 +290,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             if constexpr (MODE == 2) {
                 const int idx = tid + q * NT;
                 if (BN * KCB % NT == 0 || idx < BN * KCB)  // wave-uniform (NT, BN*KCB multiples of 64)
-                    *reinterpret_cast<floatx4*>(sB + buf * BN * LS + (idx / KCB) * LS + (idx % KCB) * 4) = rb[set][q];
+                    *reinterpret_cast<floatx4*>(sB + buf * BN * LS + ldsB[q]) = rb[set][q];
             } else {
                 *reinterpret_cast<floatx4*>(b + q * RSTEPB * LS) = rb[set][q];
             }
@@ -338,7 +345,8 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 
         lstore(0, 0);
         __syncthreads();
-        if (DEPTH == 2) gload(1, 1, m0, n0, true);  // nk is even for DEPTH 2
+#pragma unroll
+        for (int d = 1; d < DEPTH; ++d) gload(d, d, m0, n0, true);  // nk is a multiple of DEPTH
 
         floatx16 acc[TM][TN];
 #pragma unroll
@@ -440,17 +448,20 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 __syncthreads();
             }
         } else {
-            // chunk k+1 is in flight in set (k+1)&1 while chunk k is computed from LDS buffer k&1
-            for (int kc = 0; kc < nk; kc += 2) {
-                const bool more = kc + 2 < nk;
-                gload(0, more ? kc + 2 : 0, more ? m0 : m_next, more ? n0 : n_next, more || has_next);
-                compute(0);
-                lstore(1, 1);
-                __syncthreads();
-                gload(1, kc + 3 < nk ? kc + 3 : 0, m0, n0, kc + 3 < nk);
-                compute(1);
-                if (more) lstore(0, 0);
-                __syncthreads();
+            // DEPTH register sets: chunks c+1 .. c+DEPTH-1 are in flight while chunk c
+            // is computed from LDS buffer c&1; set c%DEPTH (already in LDS) then takes
+            // chunk c+DEPTH, or the next tile's first chunk when c+DEPTH == nk.
+            static_assert(DEPTH % 2 == 0, "LDS buffer of chunk kc+j is j&1");
+            for (int kc = 0; kc < nk; kc += DEPTH) {
+#pragma unroll
+                for (int j = 0; j < DEPTH; ++j) {
+                    const int cn = kc + j + DEPTH;
+                    const bool here = cn < nk;
+                    gload(j, here ? cn : 0, here ? m0 : m_next, here ? n0 : n_next, here || (cn == nk && has_next));
+                    compute(j & 1);
+                    if (kc + j + 1 < nk) lstore((j + 1) % DEPTH, (j + 1) & 1);
+                    __syncthreads();
+                }
             }
         }
 
@@ -1332,7 +1343,8 @@ static void wgrad_geometry(int M, int N, int K, int* tile, int* Npad, int* Kpad,
 using namespace cn;
 
 // Kernel variant (benchmarking aid, process-wide): 0 = 2-deep register prefetch
-// when K % 64 == 0 (else 1-deep), 1 = always 1-deep, 2 = BK 16 at 3 workgroups/CU.
+// when K % 64 == 0 (else 1-deep), 1 = always 1-deep, 2 = BK 16 at 3 workgroups/CU; bf16x6:
+// 0 = 256x128 tiles when K % 64 == 0, 3 = 128x128 tiles only, 4 = 128x128 with a 4-deep prefetch.
 static int g_linear_variant = [] {
     const char* e = getenv("COPENERF_LINEAR_VARIANT");
     return e ? atoi(e) : 0;
@@ -1443,8 +1455,19 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
         if (d->tile == 0) return launch_linear_tile<2, 2, 2, 2, 64, 2, 1, 1>(d, a, s);
         return launch_linear_tile<4, 1, 1, 2, 64, 2, 1, 1>(d, a, s);
     }
-    if (x6) {  // K % 32 == 0: an even number of 16-deep chunks for the 2-deep prefetch
-        if (d->tile == 0) return launch_linear_tile<2, 2, 2, 2, 16, 2, 2, 2>(d, a, s);
+    if (x6) {
+        // K % 64 == 0, STORE / SOFTPLUS / RELU: 256x128 tiles of 8 waves, one workgroup per CU,
+        // 32-deep stages (whole 128-byte A row segments per load, half the barriers per K; main
+        // loop 366 vs 385 us at C2's layer shape); else 128x128 tiles of 16-deep chunks (K % 32
+        // == 0: an even number of chunks for the 2-deep prefetch)
+        if (d->tile == 0) {
+            // (the wide tile only for the light epilogues: with one workgroup per CU an aux-reading
+            // epilogue no longer overlaps a partner workgroup's main loop, measured slower)
+            const bool light = d->epilogue == CN_EPI_STORE || d->epilogue == CN_EPI_SOFTPLUS || d->epilogue == CN_EPI_RELU;
+            if (d->K % 64 == 0 && g_linear_variant == 0 && light) return launch_linear_tile<4, 2, 2, 2, 32, 1, 2, 2>(d, a, s);
+            if (d->K % 64 == 0 && g_linear_variant == 4) return launch_linear_tile<2, 2, 2, 2, 16, 2, 4, 2>(d, a, s);
+            return launch_linear_tile<2, 2, 2, 2, 16, 2, 2, 2>(d, a, s);
+        }
         return launch_linear_tile<4, 1, 1, 2, 16, 2, 2, 2>(d, a, s);
     }
     const bool even = (d->K % 64) == 0;  // DEPTH-2 prefetch consumes K in pairs of 32-chunks

@@ -9,7 +9,7 @@ if [ "$1" = build ]; then
   cd $R/cope-nerf_amd/csrc
   for n in $V; do
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -D$FLAG=$n \
-      -o $R/tools/abl/lib_${FLAG}_$n.so cn_abi.hip cn_gemm.hip cn_fields.hip cn_render.hip cn_pack.hip &
+      -o $R/tools/abl/lib_${FLAG}_$n.so cn_abi.hip cn_gemm.hip cn_fields.hip cn_render.hip cn_pack.hip cn_loss.hip &
   done
   wait
 else
