@@ -66,7 +66,7 @@ def kernel_symbol(key):
     if "bf16" in key[2:]:
         return "void cn::wgrad_bf16_kernel<2, 2, 2, 2>(cn::WgradArgs) + cn::slab_reduce_kernel"
     if "x6" in key[2:]:
-        return "void cn::wgrad_x6_kernel<2>(cn::WgradArgs) + cn::slab_reduce_kernel"
+        return "void cn::wgrad_x6_kernel<4, 4>(cn::WgradArgs) + cn::slab_reduce_kernel"
     return "void cn::wgrad_kernel<2, 2, 2, 2>(cn::WgradArgs) + cn::slab_reduce_kernel"
 
 

@@ -918,15 +918,17 @@ __global__ void __launch_bounds__(64 * WM * WN, 2) wgrad_bf16_kernel(WgradArgs p
 // 16-dword term planes + 4 pad (52 dwords: the ds_read_b128 fragment reads of 16
 // consecutive rows hit 16 distinct bank quads).  One LDS buffer (53 KB, two
 // workgroups per CU): the next chunk's loads fly during the MFMAs.  TN = 1: 64
-// output columns, X staged by the first two waves.
-template <int TN>
-__global__ void __launch_bounds__(256, 2) wgrad_x6_kernel(WgradArgs p) {
-    constexpr int TM = 2, WN = 2;
-    constexpr int BNo = 128, BKo = 64 * TN, MC = 32, MQ = MC / 4;
+// output columns, X staged by the first two waves.  WM = 4, TN = 4: a whole
+// 256x256 layer per workgroup of 8 waves (one per CU, 106 KB LDS): every staged
+// element feeds twice the MFMA work of the 128x128 tile.
+template <int WM, int TN>
+__global__ void __launch_bounds__(128 * WM, 2) wgrad_x6_kernel(WgradArgs p) {
+    constexpr int TM = 2, WN = 2, NT = 128 * WM;
+    constexpr int BNo = 64 * WM, BKo = 64 * TN, MC = 32, MQ = MC / 4;
     constexpr int PL = MC / 2;       // dwords per term plane of a row
     constexpr int LSB = 3 * PL + 4;  // 52
     constexpr int XT = MQ * (BKo / 4);  // threads staging X (256 or 128: whole waves)
-    static_assert(MQ * (BNo / 4) == 256 && (XT == 256 || XT == 128), "staging geometry");
+    static_assert(MQ * (BNo / 4) == NT && XT <= NT && XT % 64 == 0, "staging geometry: whole waves");
     static_assert(MQ * BNo <= (BNo + BKo) * LSB, "bias partials fit in LDS");
     __shared__ __attribute__((aligned(16))) float smem[(BNo + BKo) * LSB];
     float* sY = smem;
@@ -967,7 +969,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_x6_kernel(WgradArgs p) {
         const rsrc_t vX = make_view(X + (int64_t)mrow * lx + k0, (nrows * lx - k0) * 4);
 #pragma unroll
         for (int r = 0; r < 4; ++r) ry[r] = bload4(vY, ((mq * 4 + r) * ly + cg * 4) * 4, 0);
-        if (XT == 256 || tid < XT) {
+        if (XT == NT || tid < XT) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) rx[r] = bload4(vX, ((mq * 4 + r) * lx + cg * 4) * 4, 0);
         }
@@ -984,7 +986,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_x6_kernel(WgradArgs p) {
             *reinterpret_cast<bf16x4*>(y + PL) = t1;
             *reinterpret_cast<bf16x4*>(y + 2 * PL) = t2;
         }
-        if (XT < 256 && tid >= XT) return;
+        if (XT < NT && tid >= XT) return;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const floatx4 col = {rx[0][e], rx[1][e], rx[2][e], rx[3][e]};
@@ -1318,10 +1320,20 @@ __global__ void __launch_bounds__(256) colsum_kernel(int M, int K, const float* 
 }
 
 // ---------------------------------------------------------------------------
-static void wgrad_geometry(int M, int N, int K, int* tile, int* Npad, int* Kpad, int* nslices,
+// tile 0: 128x128 output tiles, 1: 128x64, 2 (bf16x6, N and K multiples of 256): 256x256
+// tiles of 512-thread workgroups, one per CU (half the workgroup target)
+static bool wgrad_wide(int mfma_dtype, int N, int K) {
+    static const bool on = [] {  // benchmarking aid: COPENERF_WGRAD_WIDE=0 keeps the 128x128 tiles
+        const char* e = getenv("COPENERF_WGRAD_WIDE");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return on && mfma_dtype == CN_MFMA_F32_BF16X6 && N % 256 == 0 && K % 256 == 0;
+}
+
+static void wgrad_geometry(int M, int N, int K, bool wide, int* tile, int* Npad, int* Kpad, int* nslices,
                            int* rows_per_slice) {
-    const int t = (K % 128 == 0) ? 0 : 1;
-    const int BNo = 128, BKo = t == 0 ? 128 : 64;
+    const int t = wide ? 2 : (K % 128 == 0) ? 0 : 1;
+    const int BNo = t == 2 ? 256 : 128, BKo = t == 2 ? 256 : t == 0 ? 128 : 64;
     *tile = t;
     *Npad = cdiv(N, BNo) * BNo;
     *Kpad = cdiv(K, BKo) * BKo;
@@ -1330,7 +1342,7 @@ static void wgrad_geometry(int M, int N, int K, int* tile, int* Npad, int* Kpad,
         const char* e = getenv("COPENERF_WGRAD_BLOCKS");
         return e ? atoi(e) : 512;
     }();
-    int ns = std::max(1, kTarget / tiles);
+    int ns = std::max(1, (t == 2 ? kTarget / 2 : kTarget) / tiles);
     ns = std::min(ns, std::max(1, cdiv(M, 512)));
     int rps = cdiv(cdiv(M, ns), 64) * 64;  // whole 32-row (fp32) / 64-row (bf16) chunks
     ns = std::max(1, cdiv(M, rps));
@@ -1481,9 +1493,13 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
 }
 
 extern "C" size_t cn_wgrad_workspace_bytes(int32_t M, int32_t N, int32_t K) {
-    int tile, Npad, Kpad, ns, rps;
-    wgrad_geometry(std::max(M, 1), N, K, &tile, &Npad, &Kpad, &ns, &rps);
-    return sizeof(float) * ((size_t)ns * Npad * Kpad + (size_t)ns * Npad);
+    size_t need = 0;  // the larger of the two tilings (the call's mfma_dtype picks one)
+    for (int w = 0; w < 2; ++w) {
+        int tile, Npad, Kpad, ns, rps;
+        wgrad_geometry(std::max(M, 1), N, K, w && wgrad_wide(CN_MFMA_F32_BF16X6, N, K), &tile, &Npad, &Kpad, &ns, &rps);
+        need = std::max(need, sizeof(float) * ((size_t)ns * Npad * Kpad + (size_t)ns * Npad));
+    }
+    return need;
 }
 
 extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
@@ -1493,7 +1509,7 @@ extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
     CN_REQUIRE(d->M >= 0 && d->N > 0 && d->K > 0 && d->K % 64 == 0, CN_ERR_SHAPE,
                "cn_wgrad: bad shape M=%d N=%d K=%d (K must be a multiple of 64)", d->M, d->N, d->K);
     int tile, Npad, Kpad, ns, rps;
-    wgrad_geometry(std::max(d->M, 1), d->N, d->K, &tile, &Npad, &Kpad, &ns, &rps);
+    wgrad_geometry(std::max(d->M, 1), d->N, d->K, wgrad_wide(d->mfma_dtype, d->N, d->K), &tile, &Npad, &Kpad, &ns, &rps);
     CN_REQUIRE(d->n_out <= Npad && d->k_out <= Kpad && d->n_out > 0 && d->k_out > 0, CN_ERR_SHAPE, "cn_wgrad: bad n_out/k_out");
     CN_REQUIRE(d->ldy0 >= Npad && d->ldx0 >= Kpad && d->ldy0 % 4 == 0 && d->ldx0 % 4 == 0 && al16(d->Y0) && al16(d->X0),
                CN_ERR_ALIGN, "cn_wgrad: Y0/X0 must be 16B aligned with ld >= padded tile (%d, %d)", Npad, Kpad);
@@ -1511,18 +1527,20 @@ extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
     a.bpart = d->db ? d->workspace + (size_t)ns * Npad * Kpad : nullptr;
     a.ldy0 = (int)d->ldy0; a.ldx0 = (int)d->ldx0; a.ldy1 = (int)d->ldy1; a.ldx1 = (int)d->ldx1;
     a.M = d->M; a.Npad = Npad; a.Kpad = Kpad; a.npairs = d->npairs; a.rows_per_slice = rps;
-    const int BKo = tile == 0 ? 128 : 64;
+    const int BNo = tile == 2 ? 256 : 128, BKo = tile == 2 ? 256 : tile == 0 ? 128 : 64;
     a.n_tiles_k = Kpad / BKo;
-    a.n_tiles_n = Npad / 128;
+    a.n_tiles_n = Npad / BNo;
     a.nslices = ns;
     dim3 grid(cdiv(ns, 8) * 8 * a.n_tiles_n * a.n_tiles_k);
     CN_REQUIRE(d->mfma_dtype == CN_MFMA_F32 || d->mfma_dtype == CN_MFMA_BF16 || d->mfma_dtype == CN_MFMA_F32_BF16X6,
                CN_ERR_ARG, "cn_wgrad: bad mfma_dtype %d", d->mfma_dtype);
     if (d->mfma_dtype == CN_MFMA_F32_BF16X6) {
-        if (tile == 0)
-            wgrad_x6_kernel<2><<<grid, 256, 0, s>>>(a);
+        if (tile == 2)
+            wgrad_x6_kernel<4, 4><<<grid, 512, 0, s>>>(a);
+        else if (tile == 0)
+            wgrad_x6_kernel<2, 2><<<grid, 256, 0, s>>>(a);
         else
-            wgrad_x6_kernel<1><<<grid, 256, 0, s>>>(a);
+            wgrad_x6_kernel<2, 1><<<grid, 256, 0, s>>>(a);
     } else if (d->mfma_dtype == CN_MFMA_BF16) {
         if (tile == 0)
             wgrad_bf16_kernel<2, 2, 2, 2><<<grid, 256, 0, s>>>(a);
