@@ -1320,14 +1320,21 @@ __global__ void __launch_bounds__(256) colsum_kernel(int M, int K, const float* 
 }
 
 // ---------------------------------------------------------------------------
-// tile 0: 128x128 output tiles, 1: 128x64, 2 (bf16x6, N and K multiples of 256): 256x256
-// tiles of 512-thread workgroups, one per CU (half the workgroup target)
-static bool wgrad_wide(int mfma_dtype, int N, int K) {
+// tile 0: 128x128 output tiles, 1: 128x64, 2 (bf16x6, operand rows at least 256-padded):
+// 256x256 tiles of 512-thread workgroups, one per CU (half the workgroup target).  Padding
+// columns of Y / X only feed output rows / columns past n_out / k_out, which the slab
+// reduction never reads.
+static bool wgrad_wide_on() {
     static const bool on = [] {  // benchmarking aid: COPENERF_WGRAD_WIDE=0 keeps the 128x128 tiles
         const char* e = getenv("COPENERF_WGRAD_WIDE");
         return e ? atoi(e) != 0 : true;
     }();
-    return on && mfma_dtype == CN_MFMA_F32_BF16X6 && N % 256 == 0 && K % 256 == 0;
+    return on;
+}
+static bool wgrad_wide(const cn_wgrad_desc* d) {
+    const int64_t np = (int64_t)cdiv(d->N, 256) * 256, kp = (int64_t)cdiv(d->K, 256) * 256;
+    return wgrad_wide_on() && d->mfma_dtype == CN_MFMA_F32_BF16X6 && d->ldy0 >= np && d->ldx0 >= kp &&
+           (d->npairs == 1 || (d->ldy1 >= np && d->ldx1 >= kp));
 }
 
 static void wgrad_geometry(int M, int N, int K, bool wide, int* tile, int* Npad, int* Kpad, int* nslices,
@@ -1496,7 +1503,7 @@ extern "C" size_t cn_wgrad_workspace_bytes(int32_t M, int32_t N, int32_t K) {
     size_t need = 0;  // the larger of the two tilings (the call's mfma_dtype picks one)
     for (int w = 0; w < 2; ++w) {
         int tile, Npad, Kpad, ns, rps;
-        wgrad_geometry(std::max(M, 1), N, K, w && wgrad_wide(CN_MFMA_F32_BF16X6, N, K), &tile, &Npad, &Kpad, &ns, &rps);
+        wgrad_geometry(std::max(M, 1), N, K, w && wgrad_wide_on(), &tile, &Npad, &Kpad, &ns, &rps);
         need = std::max(need, sizeof(float) * ((size_t)ns * Npad * Kpad + (size_t)ns * Npad));
     }
     return need;
@@ -1509,7 +1516,7 @@ extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
     CN_REQUIRE(d->M >= 0 && d->N > 0 && d->K > 0 && d->K % 64 == 0, CN_ERR_SHAPE,
                "cn_wgrad: bad shape M=%d N=%d K=%d (K must be a multiple of 64)", d->M, d->N, d->K);
     int tile, Npad, Kpad, ns, rps;
-    wgrad_geometry(std::max(d->M, 1), d->N, d->K, wgrad_wide(d->mfma_dtype, d->N, d->K), &tile, &Npad, &Kpad, &ns, &rps);
+    wgrad_geometry(std::max(d->M, 1), d->N, d->K, wgrad_wide(d), &tile, &Npad, &Kpad, &ns, &rps);
     CN_REQUIRE(d->n_out <= Npad && d->k_out <= Kpad && d->n_out > 0 && d->k_out > 0, CN_ERR_SHAPE, "cn_wgrad: bad n_out/k_out");
     CN_REQUIRE(d->ldy0 >= Npad && d->ldx0 >= Kpad && d->ldy0 % 4 == 0 && d->ldx0 % 4 == 0 && al16(d->Y0) && al16(d->X0),
                CN_ERR_ALIGN, "cn_wgrad: Y0/X0 must be 16B aligned with ld >= padded tile (%d, %d)", Npad, Kpad);
