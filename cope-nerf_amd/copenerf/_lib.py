@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libcopenerf.so"
 LIB_PATH = os.environ.get("COPENERF_LIB", os.path.join(_HERE, LIB_NAME))
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 c_f32p = ctypes.c_void_p  # device pointers are passed as integers
 c_i32 = ctypes.c_int32
@@ -43,7 +43,8 @@ class LinearDesc(ctypes.Structure):
         ("M", c_i32), ("N", c_i32), ("K", c_i32), ("K1", c_i32),
         ("nzero", c_i32), ("nsplit", c_i32), ("epilogue", c_i32), ("tile", c_i32),
         ("adiv", c_f32), ("odiv", c_f32), ("beta", c_f32), ("threshold", c_f32),
-        ("mfma_dtype", c_i32), ("reserved_", c_i32),
+        ("mfma_dtype", c_i32), ("aux_beta", c_f32), ("aux2", c_ptr), ("ld_aux2", c_i64),
+        ("aux2_scale", c_f32), ("reserved_", c_i32),
     ]
 
 
@@ -76,7 +77,7 @@ SIGNATURES = {
     "cn_pack_weights": (c_i32, [ctypes.POINTER(PackJob), c_i32, c_ptr]),
     "cn_row_head": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i32, c_i32, c_ptr, c_i64,
                             c_ptr, c_ptr]),
-    "cn_scale_cols": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr]),
+    "cn_scale_cols": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_f32, c_ptr]),
     "cn_sdf_embed": (c_i32, [c_i32, c_ptr, c_i64, c_i32, c_f32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_f32,
                              c_ptr]),
     "cn_sdf_grad_assemble": (c_i32, [c_i32, c_i32, c_f32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr,
@@ -95,16 +96,16 @@ SIGNATURES = {
     "cn_up_sample_merge": (c_i32, [c_i32, c_i32, c_i32, c_f32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
                                    c_ptr]),
     "cn_composite_fwd": (c_i32, [c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
-                                 c_i32, c_f32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr]),
+                                 c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr]),
     "cn_composite_bwd": (c_i32, [c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
-                                 c_i32, c_f32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
+                                 c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
                                  c_ptr, c_ptr]),
     "cn_points_bwd": (c_i32, [c_i32, c_i32, c_ptr, c_i32, c_ptr, c_ptr, c_i32, c_ptr, c_i64, c_ptr, c_ptr,
                               c_ptr]),
     "cn_color_extras_bwd": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_i32, c_ptr, c_i32, c_ptr]),
     "cn_train_loss_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32]),
-    "cn_train_loss": (c_i32, [c_i32, c_i32, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_f32, c_f32, c_f32, c_f32,
-                              c_f32, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr]),
+    "cn_train_loss": (c_i32, [c_i32, c_i32, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_f32, c_ptr, c_ptr,
+                              c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr]),
 }
 
 _lock = threading.Lock()

@@ -125,19 +125,26 @@ def pack_sdf(lay: SDFLayout, Ws, bs, mfma_dtype: str = "fp32") -> SDFPack:
         return SDFPack(Bf, Bt, b, w80.contiguous()[None], b80.contiguous(), w80p, Bf8, Bt8, b8[1:].contiguous())
 
 
+def sig_beta(lay: SDFLayout, l: int) -> float:
+    """aux_beta of softplus' σ_l read from the stored activation U[l+1] = a_l / c
+    (c = √2 for the layer feeding the skip concat, neus_fields.py:276-277):
+    σ_l = 1 - exp(-β c U[l+1])."""
+    return lay.beta * (SQRT2 if (l + 1) == lay.skip else 1.0)
+
+
 def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool, want_grad: bool, keep: bool,
                 sdf_out: Optional[torch.Tensor] = None, dst: Optional[torch.Tensor] = None):
     """Forward of SDFNetwork (neus_fields.py:268-283) and, with want_grad, the
     ∇ₓSDF pass of SDFNetwork.gradient (neus_fields.py:291-303).
 
     Returns a dict of device buffers; with keep=True everything the backward
-    needs (layer inputs U_l, softplus' σ_l, ∇ pass adjoints S_l) is retained.
+    needs (layer inputs U_l and the ∇ pass adjoints S_l) is retained.  softplus'
+    σ_l is never stored: its consumers recover it from U[l+1] (sig_beta).
     """
     M, dev = x.shape[0], x.device
     nl, sk, HL, KE = lay.n_lin, lay.skip, lay.HL, lay.KE
-    keep_sig = keep or want_grad
+    keep_u = keep or want_grad
     U = [None] * nl
-    Sig = [None] * (nl - 1)
     U[0] = _empty(M, KE, dev)
     Usk, e_view = None, None
     if sk >= 0:
@@ -148,13 +155,12 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
     for l in range(nl - 1):
         into = (l + 1) == sk
         out = Usk if into else _empty(M, HL, dev)
-        sig = _empty(M, HL, dev) if keep_sig else None
         K = KE if l == 0 else rup(lay.in_dim[l], 32)
-        ops.linear(U[l], pk.Bf[l], lay.out_dim[l], K, out, EPI_SOFTPLUS, bias=pk.b[l], out1=sig,
+        ops.linear(U[l], pk.Bf[l], lay.out_dim[l], K, out, EPI_SOFTPLUS, bias=pk.b[l],
                    nzero=lay.out_dim[l] if into else HL, odiv=SQRT2 if into else 1.0, beta=lay.beta,
                    threshold=lay.threshold, kalg=lay.in_dim[l])
-        U[l + 1], Sig[l] = out, sig
-        if not keep_sig and l >= 1 and (l != sk):
+        U[l + 1] = out
+        if not keep_u and l >= 1 and (l != sk):
             U[l] = None  # free as we go on the no-grad sampler path
     L8 = nl - 1
     sdf = sdf_out if sdf_out is not None else _empty(M, 1, dev)
@@ -168,22 +174,22 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
     if want_grad:
         S = [None] * (nl - 1)
         S[L8 - 1] = _empty(M, HL, dev)
-        ops.scale_cols(Sig[L8 - 1], HL, pk.w80p, S[L8 - 1])
+        ops.scale_cols(U[L8], HL, pk.w80p, S[L8 - 1], act_beta=sig_beta(lay, L8 - 1))
         QE = _empty(M, KE, dev) if sk >= 0 else None
         for l in range(L8 - 1, 0, -1):
             Kl = rup(lay.out_dim[l], 32)
             S[l - 1] = _empty(M, HL, dev)
             if l == sk:
-                ops.linear(S[l], pk.Bt[l], lay.in_dim[l], Kl, S[l - 1], EPI_MUL, aux0=Sig[l - 1],
+                ops.linear(S[l], pk.Bt[l], lay.in_dim[l], Kl, S[l - 1], EPI_MUL, aux0=U[l], aux_beta=sig_beta(lay, l - 1),
                            nsplit=lay.out_dim[l - 1], out_split=QE, nzero=HL, adiv=SQRT2, kalg=lay.out_dim[l])
             else:
-                ops.linear(S[l], pk.Bt[l], lay.out_dim[l - 1], Kl, S[l - 1], EPI_MUL, aux0=Sig[l - 1], nzero=HL,
-                           kalg=lay.out_dim[l])
+                ops.linear(S[l], pk.Bt[l], lay.out_dim[l - 1], Kl, S[l - 1], EPI_MUL, aux0=U[l],
+                           aux_beta=sig_beta(lay, l - 1), nzero=HL, kalg=lay.out_dim[l])
         Q0 = _empty(M, KE, dev)
         ops.linear(S[0], pk.Bt[0], lay.E, rup(lay.out_dim[0], 32), Q0, EPI_STORE, nzero=KE, kalg=lay.out_dim[0])
         G = _empty(M, 4, dev)
         ops.sdf_grad_assemble(lay.multires, lay.scale, U[0], Q0, QE, G)
-    return {"U": U, "Sig": Sig, "S": S, "sdf": sdf, "feat": feat, "G": G}
+    return {"U": U, "S": S, "sdf": sdf, "feat": feat, "G": G}
 
 
 def sdf_input_grad(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat):
@@ -192,7 +198,7 @@ def sdf_input_grad(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat):
     neus_renderer.py:356, so it contributes nothing here).  Primal adjoint chain
     P_{l-1} = (W_lᵀ P_l) ⊙ σ_{l-1} from P_7 = (W_8fᵀ dfeat + dsdf w80) ⊙ σ_7, then
     dx = scale · J_emb(x)ᵀ (W_0ᵀ P_0 + skip-embedding part)."""
-    U, Sig = st["U"], st["Sig"]
+    U = st["U"]
     M, dev = U[0].shape[0], U[0].device
     nl, sk, HL, KE = lay.n_lin, lay.skip, lay.HL, lay.KE
     L8 = nl - 1
@@ -203,17 +209,18 @@ def sdf_input_grad(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat):
     phi = dfeat if dfeat is not None else torch.zeros(M, lay.H_feat, device=dev)
     P = _empty(M, HL, dev)
     ops.linear(phi, pk.Bt8, lay.out_dim[L8 - 1], rup(lay.H_feat, 32), P, EPI_BWD_SOFTPLUS,
-               rowv=dsdf_flat, colv=pk.w80p if dsdf_flat is not None else None, aux0=Sig[L8 - 1], nzero=HL)
+               rowv=dsdf_flat, colv=pk.w80p if dsdf_flat is not None else None, aux0=U[L8],
+               aux_beta=sig_beta(lay, L8 - 1), nzero=HL)
     PE = _empty(M, KE, dev) if sk >= 0 else None
     for l in range(L8 - 1, 0, -1):
         Kl = rup(lay.out_dim[l], 32)
         Pn = _empty(M, HL, dev)
         if l == sk:
-            ops.linear(P, pk.Bt[l], lay.in_dim[l], Kl, Pn, EPI_MUL, aux0=Sig[l - 1], nsplit=lay.out_dim[l - 1],
-                       out_split=PE, nzero=HL, adiv=SQRT2, kalg=lay.out_dim[l])
+            ops.linear(P, pk.Bt[l], lay.in_dim[l], Kl, Pn, EPI_MUL, aux0=U[l], aux_beta=sig_beta(lay, l - 1),
+                       nsplit=lay.out_dim[l - 1], out_split=PE, nzero=HL, adiv=SQRT2, kalg=lay.out_dim[l])
         else:
-            ops.linear(P, pk.Bt[l], lay.out_dim[l - 1], Kl, Pn, EPI_MUL, aux0=Sig[l - 1], nzero=HL,
-                       kalg=lay.out_dim[l])
+            ops.linear(P, pk.Bt[l], lay.out_dim[l - 1], Kl, Pn, EPI_MUL, aux0=U[l], aux_beta=sig_beta(lay, l - 1),
+                       nzero=HL, kalg=lay.out_dim[l])
         P = Pn
     P0 = _empty(M, KE, dev)
     ops.linear(P, pk.Bt[0], lay.E, rup(lay.out_dim[0], 32), P0, EPI_STORE, nzero=KE, kalg=lay.out_dim[0])
@@ -231,17 +238,20 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG):
       weights   dW_l = Σ_m Z_l u_lᵀ + s_l u̇_lᵀ,   db_l = Σ_m Z_l
 
     where s_l are the ∇ pass adjoints kept from the forward.  Six GEMMs per
-    layer instead of autograd's nine.
+    layer instead of autograd's nine.  σ_l is recovered from
+    U[l+1] inside every epilogue (sig_beta), and the second-order term is rebuilt
+    by the adjoint's epilogue from s_l and u̇_{l+1} (ż_l = u̇_{l+1} c / σ_l), so the
+    tangent pass writes one buffer per layer, not two.
     """
     wmode = _wgrad_mode(pk)
-    U, Sig, S = st["U"], st["Sig"], st["S"]
+    U, S = st["U"], st["S"]
     M, dev = U[0].shape[0], U[0].device
     nl, sk, HL, KE = lay.n_lin, lay.skip, lay.HL, lay.KE
     L8 = nl - 1
     second = dG is not None
     if second and S is None:
         raise RuntimeError("SDF double backward needs the ∇ pass buffers (want_grad=True in forward)")
-    Ud, R = None, [None] * (nl - 1)
+    Ud = None
     if second:
         Ud = [None] * nl
         Ud[0] = _empty(M, KE, dev)
@@ -254,9 +264,8 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG):
         for l in range(nl - 1):
             into = (l + 1) == sk
             out = Usk_d if into else _empty(M, HL, dev)
-            R[l] = _empty(M, HL, dev)
             K = KE if l == 0 else rup(lay.in_dim[l], 32)
-            ops.linear(Ud[l], pk.Bf[l], lay.out_dim[l], K, out, EPI_TANGENT, aux0=Sig[l], aux1=S[l], out1=R[l],
+            ops.linear(Ud[l], pk.Bf[l], lay.out_dim[l], K, out, EPI_TANGENT, aux0=U[l + 1], aux_beta=sig_beta(lay, l),
                        nzero=lay.out_dim[l] if into else HL, odiv=SQRT2 if into else 1.0, beta=lay.beta,
                        kalg=lay.in_dim[l])
             Ud[l + 1] = out
@@ -281,11 +290,16 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG):
     if second:
         ops.colsum(Ud[L8], i8, dW8[0], wdiv=lay.scale, accumulate=True)
 
+    def second_order(l):  # BWD_SOFTPLUS inputs of β s_l (1-σ_l) ż_l, ż_l = u̇_{l+1} c_l / σ_l
+        if not second:
+            return {}
+        return dict(aux1=S[l], aux2=Ud[l + 1], aux2_scale=lay.beta * (SQRT2 if (l + 1) == sk else 1.0))
+
     phi = dfeat if dfeat is not None else torch.zeros(M, lay.H_feat, device=dev)
     Z = _empty(M, HL, dev)
     ops.linear(phi, pk.Bt8, lay.out_dim[L8 - 1], rup(lay.H_feat, 32), Z, EPI_BWD_SOFTPLUS,
-               rowv=dsdf_flat, colv=pk.w80p if dsdf_flat is not None else None, aux0=Sig[L8 - 1],
-               aux1=R[L8 - 1], nzero=HL)
+               rowv=dsdf_flat, colv=pk.w80p if dsdf_flat is not None else None, aux0=U[L8],
+               aux_beta=sig_beta(lay, L8 - 1), nzero=HL, **second_order(L8 - 1))
     dWs, dbs = [None] * nl, [None] * nl
     dWs[L8], dbs[L8] = dW8, db8
     for l in range(L8 - 1, -1, -1):
@@ -293,13 +307,13 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG):
         if l > 0:
             Z = _empty(M, HL, dev)
             ops.linear(Zl, pk.Bt[l], lay.out_dim[l - 1], rup(lay.out_dim[l], 32), Z, EPI_BWD_SOFTPLUS,
-                       aux0=Sig[l - 1], aux1=R[l - 1], nzero=HL, adiv=SQRT2 if l == sk else 1.0, kalg=lay.out_dim[l])
+                       aux0=U[l], aux_beta=sig_beta(lay, l - 1), nzero=HL, adiv=SQRT2 if l == sk else 1.0,
+                       kalg=lay.out_dim[l], **second_order(l - 1))
         dW = torch.empty(lay.out_dim[l], lay.in_dim[l], device=dev)
         db = torch.empty(lay.out_dim[l], device=dev)
         ops.wgrad(Zl, U[l], lay.out_dim[l], lay.in_dim[l], dW, db=db,
                   Y1=S[l] if second else None, X1=Ud[l] if second else None, mode=wmode)
         dWs[l], dbs[l] = dW, db
-        R[l] = None
     return dWs, dbs
 
 

@@ -64,11 +64,11 @@ class _TrainLossFn(torch.autograd.Function):
     the same cn_train_loss call and are scaled by the upstream gradient."""
 
     @staticmethod
-    def forward(ctx, color, gt, depth, normals, w_rgb, w_eik, w_edge, w_smooth, patch, gamma):
+    def forward(ctx, color, gt, depth, normals, weights, patch, gamma, nonfinite):
         shape = normals.shape
         loss, dc, dd, dn = ops.train_loss(color.contiguous(), gt.contiguous(), depth.contiguous(),
-                                          normals.reshape(-1, 3), w_rgb=w_rgb, w_eik=w_eik, w_edge=w_edge,
-                                          w_smooth=w_smooth, patch=patch, gamma=gamma)
+                                          normals.reshape(-1, 3), weights=weights, patch=patch, gamma=gamma,
+                                          nonfinite=nonfinite)
         ctx.save_for_backward(dc, dd.view(depth.shape), dn.view(shape))
         return loss
 
@@ -76,14 +76,24 @@ class _TrainLossFn(torch.autograd.Function):
     def backward(ctx, g):
         dc, dd, dn = ctx.saved_tensors
         dc, dd, dn = torch._foreach_mul([dc, dd, dn], g)
-        return dc, None, dd, dn, None, None, None, None, None, None
+        return dc, None, dd, dn, None, None, None, None
+
+
+def loss_weight_vector(w_rgb=1.0, w_eik=0.1, w_edge=1.0, w_smooth=1e-4, device=None):
+    """The device weight vector cn_train_loss reads: (w_rgb, w_eik, w_edge, w_smooth)."""
+    return torch.tensor([w_rgb, w_eik, w_edge, w_smooth], dtype=torch.float32, device=device)
 
 
 def train_losses(color, gt, depth, normals, *, w_rgb=1.0, w_eik=0.1, w_edge=1.0, w_smooth=1e-4, patch=4,
-                 gamma=0.1):
+                 gamma=0.1, weights=None, nonfinite=None):
     """w_rgb rgb_l1 + w_eik eikonal + w_edge EdgePreservingSmoothnessLoss + w_smooth
     SmoothnessLoss on patch x patch ray patches, on the device in one call
-    (color [R,3], gt [R,3], depth [R,1], normals [..., 3] sample normals)."""
-    return _TrainLossFn.apply(color, gt, depth, normals, float(w_rgb), float(w_eik),
-                              float(w_edge if patch > 1 else 0.0), float(w_smooth if patch > 1 else 0.0),
-                              int(patch), float(gamma))
+    (color [R,3], gt [R,3], depth [R,1], normals [..., 3] sample normals).
+    weights: optional device [4] tensor replacing the floats (updated in place by a
+    schedule, read by the kernels at run time: graph-replay safe); nonfinite: optional
+    device int32 [1] sticky flag, the device form of model/training.py:532-533's
+    `assert not torch.isnan(loss)`."""
+    if weights is None:
+        weights = torch.tensor([w_rgb, w_eik, w_edge, w_smooth], dtype=torch.float32).to(color.device,
+                                                                                         non_blocking=True)
+    return _TrainLossFn.apply(color, gt, depth, normals, weights, int(patch), float(gamma), nonfinite)

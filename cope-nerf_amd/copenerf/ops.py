@@ -162,9 +162,11 @@ class ImagePacker:
 
 
 def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None, colv=None, aux0=None,
-           aux1=None, out1=None, out_split=None, nsplit=None, nzero=None, adiv=1.0, odiv=1.0, beta=100.0,
-           threshold=20.0, tile=None, M=None, kalg=None):
-    """out = epilogue((A|A2) @ B[:N].T / adiv) -- cn_linear.  kalg: the unpadded
+           aux1=None, aux2=None, out_split=None, nsplit=None, nzero=None, adiv=1.0, odiv=1.0, beta=100.0,
+           threshold=20.0, aux_beta=0.0, aux2_scale=0.0, tile=None, M=None, kalg=None):
+    """out = epilogue((A|A2) @ B[:N].T / adiv) -- cn_linear.  MUL / TANGENT /
+    BWD_SOFTPLUS read softplus' as sg = 1 - exp(-aux_beta * aux0) from the stored
+    softplus output aux0 (include/copenerf.h).  kalg: the unpadded
     inner dimension (for the FLOP count of the kernel timer only).  A bfloat16 B
     selects the bf16 MFMA path (A rounded to bf16 on load, fp32 accumulate); K is
     then rounded up to 64, so A's columns up to that must exist (zero padding).
@@ -174,8 +176,8 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     if x6 and (B.dtype != torch.bfloat16 or B.shape[2] != 48 or not B.is_contiguous()):
         raise RuntimeError(f"cn_linear: a 3-D B must be split_bf16x3's [K/16, N, 48] bfloat16 image (got "
                            f"{tuple(B.shape)}, {B.dtype}, strides {B.stride()})")
-    for t, n in ((A, "A"), (A2, "A2"), (B, "B"), (out0, "out0"), (out1, "out1"), (aux0, "aux0"),
-                 (aux1, "aux1"), (out_split, "out_split")):
+    for t, n in ((A, "A"), (A2, "A2"), (B, "B"), (out0, "out0"), (aux0, "aux0"), (aux1, "aux1"), (aux2, "aux2"),
+                 (out_split, "out_split")):
         _need(t, n, ndim=3 if (x6 and t is B) else 2)
         if t is not None and t is not B and t.dtype == torch.bfloat16:
             raise RuntimeError(f"cn_linear: {n} must be float32 (only B may be bfloat16)")
@@ -200,9 +202,11 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     d = _lib.LinearDesc()
     d.A, d.A2, d.B, d.bias = _ptr(A), _ptr(A2), _ptr(B), _ptr(bias)
     d.rowv, d.colv, d.aux0, d.aux1 = _ptr(rowv), _ptr(colv), _ptr(aux0), _ptr(aux1)
-    d.out0, d.out1, d.out_split = _ptr(out0), _ptr(out1), _ptr(out_split)
+    d.out0, d.out1, d.out_split = _ptr(out0), None, _ptr(out_split)
+    d.aux2, d.ld_aux2 = _ptr(aux2), _ld(aux2)
+    d.aux_beta, d.aux2_scale = aux_beta, aux2_scale
     d.lda, d.lda2, d.ldb = _ld(A), _ld(A2), (B.shape[1] if x6 else _ld(B))
-    d.ld_aux0, d.ld_aux1, d.ld_out0, d.ld_out1, d.ld_split = _ld(aux0), _ld(aux1), _ld(out0), _ld(out1), _ld(out_split)
+    d.ld_aux0, d.ld_aux1, d.ld_out0, d.ld_out1, d.ld_split = _ld(aux0), _ld(aux1), _ld(out0), 0, _ld(out_split)
     d.M, d.N, d.K = M, N, K
     d.K1 = K1 if K1 is not None else K
     d.nzero = nzero if nzero is not None else N
@@ -270,10 +274,12 @@ def row_head(A, K, W, b, C, act, out, dst_index=None, ld_out=None):
     return out
 
 
-def scale_cols(X, N, w, out):
+def scale_cols(X, N, w, out, act_beta=0.0):
+    """out = X * w (act_beta 0) or (1 - exp(-act_beta X)) * w: softplus' of stored activations."""
     _need(X, "X")
     _need(out, "out")
-    _lib.call("cn_scale_cols", X.shape[0], N, _ptr(X), _ld(X), _ptr(w), _ptr(out), _ld(out), _stream())
+    _lib.call("cn_scale_cols", X.shape[0], N, _ptr(X), _ld(X), _ptr(w), _ptr(out), _ld(out), float(act_beta),
+              _stream())
     return out
 
 
@@ -342,10 +348,22 @@ def up_sample_merge(z, sdf, n_imp, inv_s, z_out, z_new, sdf_out=None, new_dst=No
               _ptr(sdf_out), _ptr(new_dst), _stream())
 
 
+def device_scalar(x, device) -> torch.Tensor:
+    """A float / 0-d tensor as a 1-element fp32 device tensor (the kernels read schedule
+    values such as cos_anneal_ratio from device memory, so a replayed graph sees updates)."""
+    if isinstance(x, torch.Tensor):
+        t = x.reshape(-1)[:1]
+        if t.device != device or t.dtype != torch.float32:
+            t = t.to(device=device, dtype=torch.float32)
+        return t.contiguous()
+    return torch.full((1,), float(x), device=device, dtype=torch.float32)
+
+
 def composite_fwd(z, sdf, G, rgb, rays_d, inv_s, near, far, n_coarse, car, color, depth, weights, cdf):
+    """car: cos_anneal_ratio as a 1-element device tensor (device_scalar)."""
     R, S = z.shape
     _lib.call("cn_composite_fwd", R, S, _ptr(z), _ptr(sdf), _ptr(G), G.stride(0), _ptr(rgb), _ptr(rays_d),
-              _ptr(inv_s), _ptr(near), _ptr(far), n_coarse, float(car), _ptr(color), _ptr(depth), _ptr(weights),
+              _ptr(inv_s), _ptr(near), _ptr(far), n_coarse, _ptr(car), _ptr(color), _ptr(depth), _ptr(weights),
               _ptr(cdf), _stream())
 
 
@@ -353,7 +371,7 @@ def composite_bwd(z, sdf, G, rgb, rays_d, inv_s, near, far, n_coarse, car, dcolo
                   dsdf, dG, drgb, dinv_part, drays_d=None):
     R, S = z.shape
     _lib.call("cn_composite_bwd", R, S, _ptr(z), _ptr(sdf), _ptr(G), G.stride(0), _ptr(rgb), _ptr(rays_d),
-              _ptr(inv_s), _ptr(near), _ptr(far), n_coarse, float(car), _ptr(dcolor), _ptr(ddepth),
+              _ptr(inv_s), _ptr(near), _ptr(far), n_coarse, _ptr(car), _ptr(dcolor), _ptr(ddepth),
               _ptr(dweights), _ptr(dcdf), _ptr(dsdf), _ptr(dG), _ptr(drgb), _ptr(dinv_part), _ptr(drays_d),
               _stream())
 
@@ -375,10 +393,14 @@ def color_extras_bwd(d_ext, dirs, dir_div, multires_view, ddirs, accumulate=Fals
     return ddirs
 
 
-def train_loss(color, gt, depth, normals, *, w_rgb=1.0, w_eik=0.1, w_edge=1.0, w_smooth=1e-4, patch=4, gamma=0.1):
+def train_loss(color, gt, depth, normals, *, w_rgb=1.0, w_eik=0.1, w_edge=1.0, w_smooth=1e-4, patch=4, gamma=0.1,
+               weights=None, nonfinite=None):
     """(loss [], dcolor [R,3], ddepth [R,1], dnormals [M,3]) -- cn_train_loss: the colour
     L1, eikonal, edge-aware and plain smoothness terms and their input gradients.
-    normals may be any [M,3] row view (e.g. the first three columns of ∇ₓSDF)."""
+    normals may be any [M,3] row view (e.g. the first three columns of ∇ₓSDF).
+    weights: optional device tensor [4] (w_rgb, w_eik, w_edge, w_smooth) read by the
+    kernels (overrides the floats); nonfinite: optional device int32 [1] flag set when
+    the loss is not finite."""
     for t, n in ((color, "color"), (gt, "gt"), (normals, "normals")):
         _need(t, n)
     _need(depth.reshape(-1, 1), "depth")
@@ -386,12 +408,18 @@ def train_loss(color, gt, depth, normals, *, w_rgb=1.0, w_eik=0.1, w_edge=1.0, w
     if not (color.is_contiguous() and gt.is_contiguous() and depth.is_contiguous()):
         raise RuntimeError("train_loss: color, gt and depth must be contiguous")
     lib = _lib.load()
+    if weights is None:
+        weights = torch.tensor([w_rgb, w_eik, w_edge, w_smooth], dtype=torch.float32).to(dev, non_blocking=True)
+    elif weights.dtype != torch.float32 or weights.numel() != 4 or not weights.is_contiguous() or weights.device != dev:
+        raise RuntimeError("train_loss: weights must be a contiguous fp32 [4] tensor on the loss device")
+    if nonfinite is not None and (nonfinite.dtype != torch.int32 or nonfinite.device != dev):
+        raise RuntimeError("train_loss: nonfinite must be an int32 tensor on the loss device")
     ws = torch.empty(lib.cn_train_loss_workspace_bytes(R, patch) // 8 + 1, device=dev, dtype=torch.float64)
     loss = torch.empty((), device=dev)
     dcolor = torch.empty_like(color)
     ddepth = torch.empty(R, 1, device=dev)
     dn = torch.empty(M, 3, device=dev)
     _lib.call("cn_train_loss", R, patch, M, _ptr(color), _ptr(gt), _ptr(depth), _ptr(normals), _ld(normals),
-              float(w_rgb), float(w_eik), float(w_edge), float(w_smooth), float(gamma), _ptr(loss), _ptr(dcolor),
-              _ptr(ddepth), _ptr(dn), 3, _ptr(ws), ws.numel() * 8, _stream())
+              _ptr(weights), float(gamma), _ptr(loss), _ptr(dcolor), _ptr(ddepth), _ptr(dn), 3, _ptr(nonfinite),
+              _ptr(ws), ws.numel() * 8, _stream())
     return loss, dcolor, ddepth, dn

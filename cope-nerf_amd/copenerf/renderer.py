@@ -55,6 +55,7 @@ class _CompositeFn(torch.autograd.Function):
         ctx.set_materialize_grads(False)
         R, S = z.shape
         dev = z.device
+        car = ops.device_scalar(car, dev)  # cos_anneal_ratio: float or device tensor (no host sync)
         color = _empty(R, 3, dev)
         depth = _empty(R, 1, dev)
         weights = _empty(R, S, dev)
@@ -193,8 +194,8 @@ class NeuSRenderer(nn.Module):
         sdf, feat, G = self.sdf_network.field(pts_time, want_feat=True, want_grad=True, packed=sdf_packed)
         rgb = self.color_network.color(pts_time, G, rays_d, S, feat, packed=col_packed)
         inv_s = self.deviation_network(torch.zeros([1, 3], device=dev))[:, :1].clip(1 / 1e3, 1 / 1e-3)
-        color, depth, weights, cdf = _CompositeFn.apply(z, sdf, G, rgb, rays_d, inv_s, near, far, n_samples,
-                                                        float(cos_anneal_ratio))
+        car = ops.device_scalar(cos_anneal_ratio, dev)  # a device scalar: graph replays read the current ratio
+        color, depth, weights, cdf = _CompositeFn.apply(z, sdf, G, rgb, rays_d, inv_s, near, far, n_samples, car)
         weighted_z_vals = depth.detach().clone()
         depth_pred = depth / ray_d_norm if eval else depth
         if background_rgb is not None:

@@ -34,12 +34,15 @@ struct LinearArgs {
     const float* colv;
     const float* aux0;
     const float* aux1;
+    const float* aux2;
     float* out0;
     float* out1;
     float* out_split;
-    int lda, lda2, ldb, ld_aux0, ld_aux1, ld_out0, ld_out1, ld_split;
+    int lda, lda2, ldb, ld_aux0, ld_aux1, ld_aux2, ld_out0, ld_out1, ld_split;
     int M, N, K, K1, nzero, nsplit, n_tiles_m, n_tiles_n;
     float inv_adiv, inv_odiv, beta, threshold;
+    float aux_c;       // -aux_beta * log2(e): sigma = 1 - 2^(aux_c * aux0)
+    float aux2_scale;  // BWD_SOFTPLUS second-order term scale
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -86,18 +89,24 @@ __device__ __forceinline__ void bstore4(rsrc_t r, int voff, int soff, floatx4 v)
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, soff, 0);
 }
 
-// torch.nn.Softplus(beta, threshold) and its derivative from one exponential,
-// on the hardware transcendentals: e = 2^(z beta log2 e), a = log2(1 + e) ln2 / beta,
-// sg = e / (1 + e); the linear branch (beta z > threshold) exactly as torch.
-// Absolute error of a is ~1e-9 (log2 of the rounded 1 + e; v_exp/v_log/v_rcp are
-// 1 ulp), far below the fp32 GEMM rounding of the layer that produced z.
-__device__ __forceinline__ void softplus_hw(float z, float c_exp, float c_thr, float c_log, float& a, float& sg) {
+// torch.nn.Softplus(beta, threshold) on the hardware transcendentals: e = 2^(z beta
+// log2 e), a = log2(1 + e) ln2 / beta; the linear branch (beta z > threshold) exactly
+// as torch.  Absolute error of a is ~1e-9 (log2 of the rounded 1 + e; v_exp/v_log
+// are 1 ulp), far below the fp32 GEMM rounding of the layer that produced z.
+__device__ __forceinline__ float softplus_hw(float z, float c_exp, float c_thr, float c_log) {
     const float y = z * c_exp;  // beta z log2(e)
     const float e = __builtin_amdgcn_exp2f(y);
-    const float t = 1.0f + e;
     const bool lin = y > c_thr;  // beta z > threshold (boundary moved by <= 1 ulp; the branches agree to 1e-10 there)
-    a = lin ? z : __builtin_amdgcn_logf(t) * c_log;
-    sg = lin ? 1.0f : e * __builtin_amdgcn_rcpf(t);
+    return lin ? z : __builtin_amdgcn_logf(1.0f + e) * c_log;
+}
+
+// softplus'(z) = sigmoid(beta z) recovered from the softplus output a = softplus(z):
+// exp(beta a) = 1 + exp(beta z), so sigma = 1 - exp(-beta a) (= 1 exactly in fp32 on
+// torch's linear branch, beta z > 20).  aux_c = -beta * log2(e) (times the divisor the
+// stored activation carries).  Absolute error <= ~1e-7: the backward never stores
+// sigma, every consumer reads the activation it already has.
+__device__ __forceinline__ float sigma_from_act(float a, float aux_c) {
+    return 1.0f - __builtin_amdgcn_exp2f(a * aux_c);
 }
 
 // Three-term bf16 split of 4 fp32 values (CN_MFMA_F32_BF16X6): v = t0 + t1 + t2
@@ -316,8 +325,8 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     static_assert((PROWS / RPP) % GROUP == 0, "epilogue passes");
     constexpr bool kAux0 = EPI == CN_EPI_MUL || EPI == CN_EPI_TANGENT || EPI == CN_EPI_BWD_SOFTPLUS ||
                            EPI == CN_EPI_BWD_RELU;
-    constexpr bool kAux1 = EPI == CN_EPI_TANGENT || EPI == CN_EPI_BWD_SOFTPLUS;
-    constexpr bool kOut1 = EPI == CN_EPI_SOFTPLUS || EPI == CN_EPI_TANGENT;
+    constexpr bool kAux1 = EPI == CN_EPI_BWD_SOFTPLUS;  // aux1 = s, aux2 = u' (second-order term)
+    constexpr bool kOut1 = false;
 
     // epilogue thread geometry: row rr + k*RPP of the slab, columns 4*c4 .. 4*c4+3
     const int c4 = tid % C4;
@@ -326,6 +335,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     const int voO1 = (rr * p.ld_out1 + 4 * c4) * 4;
     const int voX0 = (rr * p.ld_aux0 + 4 * c4) * 4;
     const int voX1 = (rr * p.ld_aux1 + 4 * c4) * 4;
+    const int voX2 = (rr * p.ld_aux2 + 4 * c4) * 4;
     const int voS = (rr * p.ld_split + 4 * c4) * 4;
     const float c_exp = p.beta * 1.44269504088896341f;        // beta log2(e)
     const float c_thr = p.threshold * 1.44269504088896341f;   // threshold in the log2 domain
@@ -490,6 +500,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         const TileView tO1 = {p.out1 + (int64_t)m0 * p.ld_out1 + n0, p.ld_out1, p.out1 ? (rows * p.ld_out1 - n0) * 4 : 0};
         const TileView tX0 = {p.aux0 + (int64_t)m0 * p.ld_aux0 + n0, p.ld_aux0, p.aux0 ? (rows * p.ld_aux0 - n0) * 4 : 0};
         const TileView tX1 = {p.aux1 + (int64_t)m0 * p.ld_aux1 + n0, p.ld_aux1, p.aux1 ? (rows * p.ld_aux1 - n0) * 4 : 0};
+        const TileView tX2 = {p.aux2 + (int64_t)m0 * p.ld_aux2 + n0, p.ld_aux2, p.aux2 ? (rows * p.ld_aux2 - n0) * 4 : 0};
         const TileView tR = {p.rowv + m0, 1, ROWV ? rows * 4 : 0};
         const int sh = n0 - p.nsplit;  // out_split column of this tile's first column
         const TileView tS = {p.out_split + (int64_t)m0 * p.ld_split + sh, p.ld_split,
@@ -521,7 +532,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             if (region == 3) continue;
 #pragma unroll
             for (int pb = 0; pb < PROWS / RPP; pb += GROUP) {
-                floatx4 v[GROUP], x0[GROUP], x1[GROUP];
+                floatx4 v[GROUP], x0[GROUP], x1[GROUP], x2[GROUP];
                 float rv[GROUP];
 #pragma unroll
                 for (int q = 0; q < GROUP; ++q) {
@@ -531,6 +542,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                     // past the last row harmless, and only region-0 lanes use the values
                     if (kAux0) x0[q] = bload4(view_at(tX0, lrow), voX0, 0);
                     if (kAux1) x1[q] = bload4(view_at(tX1, lrow), voX1, 0);
+                    if (kAux1) x2[q] = bload4(view_at(tX2, lrow), voX2, 0);
                     if (ROWV) rv[q] = bload1(view_at(tR, lrow), rr * 4, 0);
                 }
                 // main-region values of pass q (the EPI's math on 4 columns)
@@ -544,20 +556,24 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         if constexpr (EPI == CN_EPI_STORE) {
                             o0[e] = u + bias[e];
                         } else if constexpr (EPI == CN_EPI_SOFTPLUS) {
-                            float a, sg;
-                            softplus_hw(u + bias[e], c_exp, c_thr, c_log, a, sg);
-                            o0[e] = a * p.inv_odiv;
-                            o1[e] = sg;
+                            o0[e] = softplus_hw(u + bias[e], c_exp, c_thr, c_log) * p.inv_odiv;
                         } else if constexpr (EPI == CN_EPI_RELU) {
                             const float z = u + bias[e];
                             o0[e] = z > 0.0f ? z : 0.0f;
                         } else if constexpr (EPI == CN_EPI_MUL) {
-                            o0[e] = u * x0[q][e];
+                            o0[e] = u * sigma_from_act(x0[q][e], p.aux_c);
                         } else if constexpr (EPI == CN_EPI_TANGENT) {
-                            o0[e] = u * x0[q][e] * p.inv_odiv;
-                            o1[e] = p.beta * x1[q][e] * (1.0f - x0[q][e]) * u;
+                            o0[e] = u * sigma_from_act(x0[q][e], p.aux_c) * p.inv_odiv;
                         } else if constexpr (EPI == CN_EPI_BWD_SOFTPLUS) {
-                            o0[e] = u * x0[q][e] + x1[q][e];  // aux1 absent: a zero-record view reads 0
+                            // Z = v sigma + beta s (1 - sigma) z', with z' = u' / sigma from the
+                            // stored tangent u' = sigma z' (aux2_scale = beta * its divisor):
+                            // the second-order term of softplus is rebuilt here instead of
+                            // being written by the tangent pass and read back.  sigma = 0
+                            // implies s = u' = 0 (both carry the factor sigma): term 0.
+                            // aux1 / aux2 absent: zero-record views read 0.
+                            const float sg = sigma_from_act(x0[q][e], p.aux_c);
+                            const float rr = sg > 0.0f ? (1.0f - sg) * __builtin_amdgcn_rcpf(sg) : 0.0f;
+                            o0[e] = u * sg + x1[q][e] * x2[q][e] * (p.aux2_scale * rr);
                         } else if constexpr (EPI == CN_EPI_BWD_RELU) {
                             o0[e] = x0[q][e] > 0.0f ? u : 0.0f;
                         }
@@ -1201,14 +1217,17 @@ __global__ void __launch_bounds__(256) row_head_kernel(int M, int K, const float
 // out[m][n] = X[m][n] * w[n], float4-vectorized (N, the leading dimensions and
 // the pointers are multiples of 4 floats / 16-byte aligned: checked by the host).
 __global__ void __launch_bounds__(256) scale_cols_kernel(int M, int N4, const float* __restrict__ X, int64_t ldx,
-                                                         const float* __restrict__ w, float* out, int64_t ldo) {
+                                                         const float* __restrict__ w, float* out, int64_t ldo,
+                                                         float aux_c) {
     const int64_t tot = (int64_t)M * N4;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += stride) {
         const int64_t m = idx / N4;
         const int n = (int)(idx - m * N4) * 4;
-        const floatx4 x = *reinterpret_cast<const floatx4*>(X + m * ldx + n);
+        floatx4 x = *reinterpret_cast<const floatx4*>(X + m * ldx + n);
         const floatx4 s = *reinterpret_cast<const floatx4*>(w + n);
+        if (aux_c != 0.0f)  // X holds softplus outputs: scale softplus' = 1 - exp(-beta X)
+            for (int e = 0; e < 4; ++e) x[e] = sigma_from_act(x[e], aux_c);
         *reinterpret_cast<floatx4*>(out + m * ldo + n) = x * s;
     }
 }
@@ -1368,6 +1387,13 @@ static int g_linear_variant = [] {
     const char* e = getenv("COPENERF_LINEAR_VARIANT");
     return e ? atoi(e) : 0;
 }();
+// bf16x6 epilogues that run on the 256x128 one-workgroup-per-CU tile (bit e = cn_epilogue e;
+// benchmarking aid: COPENERF_WIDE_EPIS).  Default: the epilogues that read at most one aux
+// stream (STORE, SOFTPLUS, RELU, MUL, TANGENT).
+static int g_wide_epis = [] {
+    const char* e = getenv("COPENERF_WIDE_EPIS");
+    return e ? (int)strtol(e, nullptr, 0) : 0x1f;
+}();
 
 template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int MODE = 0>
 static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_t s) {
@@ -1431,10 +1457,15 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     const int e = d->epilogue;
     if (e == CN_EPI_MUL || e == CN_EPI_TANGENT || e == CN_EPI_BWD_SOFTPLUS || e == CN_EPI_BWD_RELU)
         CN_REQUIRE(d->aux0 && d->ld_aux0 >= d->N, CN_ERR_ARG, "cn_linear: epilogue %d needs aux0", e);
-    if (e == CN_EPI_TANGENT)
-        CN_REQUIRE(d->aux1 && d->out1 && d->ld_aux1 >= d->N && d->ld_out1 >= nzero, CN_ERR_ARG,
-                   "cn_linear: tangent epilogue needs aux1/out1");
-    if (e == CN_EPI_SOFTPLUS && d->out1) CN_REQUIRE(d->ld_out1 >= nzero, CN_ERR_SHAPE, "cn_linear: ld_out1");
+    if (e == CN_EPI_MUL || e == CN_EPI_TANGENT || e == CN_EPI_BWD_SOFTPLUS)
+        CN_REQUIRE(d->aux_beta > 0.0f, CN_ERR_ARG, "cn_linear: epilogue %d needs aux_beta > 0 (sigma from aux0)", e);
+    CN_REQUIRE(d->out1 == nullptr, CN_ERR_ARG, "cn_linear: out1 is not produced by any epilogue (ABI v4)");
+    if (e == CN_EPI_BWD_SOFTPLUS)
+        CN_REQUIRE((d->aux1 == nullptr) == (d->aux2 == nullptr) &&
+                       (!d->aux1 || (d->ld_aux1 >= d->N && d->ld_aux2 >= d->N)),
+                   CN_ERR_ARG, "cn_linear: BWD_SOFTPLUS takes aux1 (s) and aux2 (u') together");
+    else
+        CN_REQUIRE(d->aux1 == nullptr && d->aux2 == nullptr, CN_ERR_ARG, "cn_linear: aux1/aux2 only for BWD_SOFTPLUS");
     if (e == CN_EPI_MUL && d->nsplit < d->N)
         CN_REQUIRE(d->out_split && d->nsplit >= 0 && d->ld_split >= d->N - d->nsplit, CN_ERR_ARG,
                    "cn_linear: split output required");
@@ -1446,20 +1477,23 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     CN_REQUIRE(al16(d->out0) && d->ld_out0 % 4 == 0 && (!d->out1 || (al16(d->out1) && d->ld_out1 % 4 == 0)) &&
                    (!d->aux0 || (al16(d->aux0) && d->ld_aux0 % 4 == 0)) &&
                    (!d->aux1 || (al16(d->aux1) && d->ld_aux1 % 4 == 0)) &&
+                   (!d->aux2 || (al16(d->aux2) && d->ld_aux2 % 4 == 0)) &&
                    (!d->out_split || (al16(d->out_split) && d->ld_split % 4 == 0)),
                CN_ERR_ALIGN, "cn_linear: outputs / aux must be 16-byte aligned with leading dims % 4 == 0");
     // buffer views address a 128-row tile with 32-bit byte offsets
     constexpr int64_t kMaxLd = 1 << 20;
-    CN_REQUIRE(d->lda < kMaxLd && d->lda2 < kMaxLd && d->ldb < kMaxLd && d->ld_aux0 < kMaxLd && d->ld_aux1 < kMaxLd &&
+    CN_REQUIRE(d->lda < kMaxLd && d->lda2 < kMaxLd && d->ldb < kMaxLd && d->ld_aux0 < kMaxLd && d->ld_aux1 < kMaxLd && d->ld_aux2 < kMaxLd &&
                    d->ld_out0 < kMaxLd && d->ld_out1 < kMaxLd && d->ld_split < kMaxLd,
                CN_ERR_SHAPE, "cn_linear: leading dimensions must be < 2^20");
     if (d->M == 0) return CN_OK;
 
     LinearArgs a;
     a.A = d->A; a.A2 = d->A2; a.B = d->B; a.bias = d->bias; a.rowv = d->rowv; a.colv = d->colv;
-    a.aux0 = d->aux0; a.aux1 = d->aux1; a.out0 = d->out0; a.out1 = d->out1; a.out_split = d->out_split;
+    a.aux0 = d->aux0; a.aux1 = d->aux1; a.aux2 = d->aux2; a.out0 = d->out0; a.out1 = d->out1; a.out_split = d->out_split;
     a.lda = (int)d->lda; a.lda2 = (int)d->lda2; a.ldb = (int)d->ldb;
-    a.ld_aux0 = (int)d->ld_aux0; a.ld_aux1 = (int)d->ld_aux1;
+    a.ld_aux0 = (int)d->ld_aux0; a.ld_aux1 = (int)d->ld_aux1; a.ld_aux2 = (int)d->ld_aux2;
+    a.aux_c = -d->aux_beta * 1.44269504088896341f;
+    a.aux2_scale = d->aux2_scale;
     a.ld_out0 = (int)d->ld_out0; a.ld_out1 = (int)d->ld_out1; a.ld_split = (int)d->ld_split;
     a.M = d->M; a.N = d->N; a.K = d->K; a.K1 = K1; a.nzero = nzero;
     a.nsplit = (e == CN_EPI_MUL && d->out_split) ? d->nsplit : d->N;
@@ -1482,7 +1516,7 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
         if (d->tile == 0) {
             // (the wide tile only for the light epilogues: with one workgroup per CU an aux-reading
             // epilogue no longer overlaps a partner workgroup's main loop, measured slower)
-            const bool light = d->epilogue == CN_EPI_STORE || d->epilogue == CN_EPI_SOFTPLUS || d->epilogue == CN_EPI_RELU;
+            const bool light = (g_wide_epis >> d->epilogue) & 1;
             if (d->K % 64 == 0 && g_linear_variant == 0 && light) return launch_linear_tile<4, 2, 2, 2, 32, 1, 2, 2>(d, a, s);
             if (d->K % 64 == 0 && g_linear_variant == 4) return launch_linear_tile<2, 2, 2, 2, 16, 2, 4, 2>(d, a, s);
             return launch_linear_tile<2, 2, 2, 2, 16, 2, 2, 2>(d, a, s);
@@ -1584,14 +1618,16 @@ extern "C" int cn_row_head(int32_t M, int32_t K, const float* A, int64_t lda, co
 }
 
 extern "C" int cn_scale_cols(int32_t M, int32_t N, const float* X, int64_t ldx, const float* w, float* out,
-                             int64_t ld_out, cn_stream_t stream) {
+                             int64_t ld_out, float act_beta, cn_stream_t stream) {
+    CN_REQUIRE(act_beta >= 0.0f, CN_ERR_ARG, "cn_scale_cols: act_beta must be >= 0");
     CN_REQUIRE(X && w && out, CN_ERR_ARG, "cn_scale_cols: null pointer");
     CN_REQUIRE(N % 4 == 0 && ldx % 4 == 0 && ld_out % 4 == 0 && al16(X) && al16(w) && al16(out), CN_ERR_ALIGN,
                "cn_scale_cols: N, leading dimensions and pointers must be multiples of 4 floats");
     if ((int64_t)M * N == 0) return CN_OK;
     const int64_t tot = (int64_t)M * (N / 4);
     const int blocks = (int)std::min<int64_t>((tot + 255) / 256, 8192);
-    scale_cols_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(M, N / 4, X, ldx, w, out, ld_out);
+    scale_cols_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(M, N / 4, X, ldx, w, out, ld_out,
+                                                               -act_beta * 1.44269504088896341f);
     return check_launch("cn_scale_cols");
 }
 

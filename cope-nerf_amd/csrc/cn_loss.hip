@@ -39,11 +39,12 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 template <int P>
 __global__ void __launch_bounds__(kLossThreads) patch_loss_kernel(int npatch, const float* __restrict__ color,
                                                                   const float* __restrict__ gt,
-                                                                  const float* __restrict__ depth, float w_rgb,
-                                                                  float w_edge, float w_smooth, float gamma, int R,
+                                                                  const float* __restrict__ depth,
+                                                                  const float* __restrict__ wts, float gamma, int R,
                                                                   float* dcolor, float* ddepth, double* part) {
     __shared__ double red[kLossThreads];
     constexpr int Q = P * P;
+    const float w_rgb = wts[0], w_edge = wts[2], w_smooth = wts[3];
     const int p = blockIdx.x * kLossThreads + threadIdx.x;
     double acc = 0.0;
     if (p < npatch) {
@@ -111,10 +112,12 @@ __global__ void __launch_bounds__(kLossThreads) patch_loss_kernel(int npatch, co
     if (threadIdx.x == 0) part[blockIdx.x] = tot;
 }
 
-// Eikonal term over every sample: (|n| - 1)^2, gradient coef * 2 (|n| - 1) n / |n|.
+// Eikonal term over every sample: (|n| - 1)^2, gradient coef * 2 (|n| - 1) n / |n|, coef = w_eik / M.
 __global__ void __launch_bounds__(kLossThreads) eikonal_kernel(int64_t M, const float* __restrict__ nrm, int64_t ldn,
-                                                               float coef, float* dn, int64_t ld_dn, double* part) {
+                                                               const float* __restrict__ wts, float* dn, int64_t ld_dn,
+                                                               double* part) {
     __shared__ double red[kLossThreads];
+    const float coef = wts[1] / (float)M;
     double acc = 0.0;
     const int64_t stride = (int64_t)gridDim.x * kLossThreads;
     for (int64_t m = (int64_t)blockIdx.x * kLossThreads + threadIdx.x; m < M; m += stride) {
@@ -131,10 +134,14 @@ __global__ void __launch_bounds__(kLossThreads) eikonal_kernel(int64_t M, const 
     if (threadIdx.x == 0) part[blockIdx.x] = tot;
 }
 
-// loss = sum(part_a) + coef_b * sum(part_b), each summed in a fixed order.
+// loss = sum(part_a) + (w_eik / M) sum(part_b), each summed in a fixed order.  The
+// device-side NaN guard of model/training.py:532-533 (assert not torch.isnan(loss)):
+// a non-finite loss sets the sticky flag *nonfinite, which the host reads when it
+// syncs anyway -- no per-step host sync, so the step stays graph-capturable.
 __global__ void __launch_bounds__(kLossThreads) loss_finalize_kernel(const double* part_a, int na,
-                                                                     const double* part_b, int nb, double coef_b,
-                                                                     float* loss) {
+                                                                     const double* part_b, int nb, int64_t M,
+                                                                     const float* __restrict__ wts, float* loss,
+                                                                     int* nonfinite) {
     __shared__ double red[kLossThreads];
     double a = 0.0, b = 0.0;
     for (int i = threadIdx.x; i < na; i += kLossThreads) a += part_a[i];
@@ -142,7 +149,12 @@ __global__ void __launch_bounds__(kLossThreads) loss_finalize_kernel(const doubl
     const double sa = block_sum(a, red);
     __syncthreads();
     const double sb = block_sum(b, red);
-    if (threadIdx.x == 0) *loss = (float)(sa + coef_b * sb);
+    if (threadIdx.x == 0) {
+        const double coef_b = M > 0 ? (double)wts[1] / (double)M : 0.0;
+        const float l = (float)(sa + coef_b * sb);
+        *loss = l;
+        if (nonfinite && !isfinite(l)) *nonfinite = 1;
+    }
 }
 
 // patch threads (patches, or rays for P = 1) and their workgroups
@@ -158,11 +170,10 @@ extern "C" size_t cn_train_loss_workspace_bytes(int32_t R, int32_t patch) {
 }
 
 extern "C" int cn_train_loss(int32_t R, int32_t patch, int64_t M, const float* color, const float* gt,
-                             const float* depth, const float* normals, int64_t ld_n, float w_rgb, float w_eik,
-                             float w_edge, float w_smooth, float gamma, float* loss, float* dcolor, float* ddepth,
-                             float* dnormals, int64_t ld_dn, void* workspace, int64_t workspace_bytes,
-                             cn_stream_t stream) {
-    CN_REQUIRE(color && gt && depth && loss && dcolor && ddepth && workspace, CN_ERR_ARG,
+                             const float* depth, const float* normals, int64_t ld_n, const float* weights,
+                             float gamma, float* loss, float* dcolor, float* ddepth, float* dnormals, int64_t ld_dn,
+                             int32_t* nonfinite, void* workspace, int64_t workspace_bytes, cn_stream_t stream) {
+    CN_REQUIRE(color && gt && depth && weights && loss && dcolor && ddepth && workspace, CN_ERR_ARG,
                "cn_train_loss: null pointer");
     CN_REQUIRE(R > 0 && M >= 0 && (M == 0 || (normals && dnormals && ld_n >= 3 && ld_dn >= 3)), CN_ERR_SHAPE,
                "cn_train_loss: bad R=%d / M=%lld / normals", R, (long long)M);
@@ -176,13 +187,13 @@ extern "C" int cn_train_loss(int32_t R, int32_t patch, int64_t M, const float* c
     const int na = loss_blocks(R, patch), nu = loss_units(R, patch);
     double* part_b = part_a + na;
     switch (patch) {
-        case 1: patch_loss_kernel<1><<<na, kLossThreads, 0, s>>>(nu, color, gt, depth, w_rgb, w_edge, w_smooth,
+        case 1: patch_loss_kernel<1><<<na, kLossThreads, 0, s>>>(nu, color, gt, depth, weights,
                                                                   gamma, R, dcolor, ddepth, part_a); break;
-        case 2: patch_loss_kernel<2><<<na, kLossThreads, 0, s>>>(nu, color, gt, depth, w_rgb, w_edge, w_smooth,
+        case 2: patch_loss_kernel<2><<<na, kLossThreads, 0, s>>>(nu, color, gt, depth, weights,
                                                                   gamma, R, dcolor, ddepth, part_a); break;
-        case 3: patch_loss_kernel<3><<<na, kLossThreads, 0, s>>>(nu, color, gt, depth, w_rgb, w_edge, w_smooth,
+        case 3: patch_loss_kernel<3><<<na, kLossThreads, 0, s>>>(nu, color, gt, depth, weights,
                                                                   gamma, R, dcolor, ddepth, part_a); break;
-        default: patch_loss_kernel<4><<<na, kLossThreads, 0, s>>>(nu, color, gt, depth, w_rgb, w_edge, w_smooth,
+        default: patch_loss_kernel<4><<<na, kLossThreads, 0, s>>>(nu, color, gt, depth, weights,
                                                                    gamma, R, dcolor, ddepth, part_a); break;
     }
     int rc = check_launch("cn_train_loss (patch terms)");
@@ -190,11 +201,10 @@ extern "C" int cn_train_loss(int32_t R, int32_t patch, int64_t M, const float* c
     int nb = 0;
     if (M > 0) {
         nb = (int)std::min<int64_t>(kEikonalBlocks, (M + kLossThreads - 1) / kLossThreads);
-        eikonal_kernel<<<nb, kLossThreads, 0, s>>>(M, normals, ld_n, w_eik / (float)M, dnormals, ld_dn, part_b);
+        eikonal_kernel<<<nb, kLossThreads, 0, s>>>(M, normals, ld_n, weights, dnormals, ld_dn, part_b);
         rc = check_launch("cn_train_loss (eikonal)");
         if (rc) return rc;
     }
-    loss_finalize_kernel<<<1, kLossThreads, 0, s>>>(part_a, na, part_b, nb, M > 0 ? (double)w_eik / (double)M : 0.0,
-                                                    loss);
+    loss_finalize_kernel<<<1, kLossThreads, 0, s>>>(part_a, na, part_b, nb, M, weights, loss, nonfinite);
     return check_launch("cn_train_loss (finalize)");
 }

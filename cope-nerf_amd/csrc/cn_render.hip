@@ -315,12 +315,14 @@ __global__ void __launch_bounds__(256) composite_fwd_kernel(int R, int S, const 
                                                             const float* __restrict__ rays_d,
                                                             const float* __restrict__ inv_s_p,
                                                             const float* __restrict__ near,
-                                                            const float* __restrict__ far, int n_coarse, float car,
+                                                            const float* __restrict__ far, int n_coarse,
+                                                            const float* __restrict__ car_p,
                                                             float* color, float* depth, float* weights, float* cdf) {
     const int lane = threadIdx.x & 63;
     const int r = blockIdx.x * kRaysPerBlock + (threadIdx.x >> 6);
     if (r >= R) return;
     const float inv_s = inv_s_p[0];
+    const float car = car_p[0];
     const float sample_dist = (far[0] - near[0]) / (float)n_coarse;
     const float d[3] = {rays_d[3 * r], rays_d[3 * r + 1], rays_d[3 * r + 2]};
     const int P = cdiv(S, 64);
@@ -368,13 +370,14 @@ __global__ void __launch_bounds__(256) composite_fwd_kernel(int R, int S, const 
 __global__ void __launch_bounds__(256) composite_bwd_kernel(
     int R, int S, const float* __restrict__ z, const float* __restrict__ sdf, const float* __restrict__ G, int64_t ld_g,
     const float* __restrict__ rgb, const float* __restrict__ rays_d, const float* __restrict__ inv_s_p,
-    const float* __restrict__ near, const float* __restrict__ far, int n_coarse, float car,
+    const float* __restrict__ near, const float* __restrict__ far, int n_coarse, const float* __restrict__ car_p,
     const float* __restrict__ dcolor, const float* __restrict__ ddepth, const float* __restrict__ dweights,
     const float* __restrict__ dcdf, float* dsdf, float* dG, float* drgb, float* dinv_part, float* drays_d) {
     const int lane = threadIdx.x & 63;
     const int r = blockIdx.x * kRaysPerBlock + (threadIdx.x >> 6);
     if (r >= R) return;
     const float inv_s = inv_s_p[0];
+    const float car = car_p[0];
     const float sample_dist = (far[0] - near[0]) / (float)n_coarse;
     const float d[3] = {rays_d[3 * r], rays_d[3 * r + 1], rays_d[3 * r + 2]};
     const float gc0 = dcolor ? dcolor[3 * r] : 0.0f;
@@ -535,9 +538,10 @@ extern "C" int cn_up_sample_merge(int32_t R, int32_t n, int32_t n_imp, float inv
 
 extern "C" int cn_composite_fwd(int32_t R, int32_t S, const float* z, const float* sdf, const float* G, int64_t ld_g,
                                 const float* rgb, const float* rays_d, const float* inv_s, const float* near,
-                                const float* far, int32_t n_coarse, float cos_anneal_ratio, float* color, float* depth,
+                                const float* far, int32_t n_coarse, const float* cos_anneal_ratio, float* color, float* depth,
                                 float* weights, float* cdf, cn_stream_t stream) {
-    CN_REQUIRE(z && sdf && G && rgb && rays_d && inv_s && near && far && color && depth && weights, CN_ERR_ARG,
+    CN_REQUIRE(z && sdf && G && rgb && rays_d && inv_s && near && far && cos_anneal_ratio && color && depth && weights,
+               CN_ERR_ARG,
                "cn_composite_fwd: null pointer");
     CN_REQUIRE(S >= 1 && S <= 64 * kMaxPerLane && n_coarse > 0 && ld_g >= 3, CN_ERR_UNSUPPORTED,
                "cn_composite_fwd: S=%d", S);
@@ -549,10 +553,11 @@ extern "C" int cn_composite_fwd(int32_t R, int32_t S, const float* z, const floa
 
 extern "C" int cn_composite_bwd(int32_t R, int32_t S, const float* z, const float* sdf, const float* G, int64_t ld_g,
                                 const float* rgb, const float* rays_d, const float* inv_s, const float* near,
-                                const float* far, int32_t n_coarse, float cos_anneal_ratio, const float* dcolor,
+                                const float* far, int32_t n_coarse, const float* cos_anneal_ratio, const float* dcolor,
                                 const float* ddepth, const float* dweights, const float* dcdf, float* dsdf, float* dG,
                                 float* drgb, float* dinv_s_part, float* drays_d, cn_stream_t stream) {
-    CN_REQUIRE(z && sdf && G && rgb && rays_d && inv_s && near && far && dsdf && dG && drgb && dinv_s_part,
+    CN_REQUIRE(z && sdf && G && rgb && rays_d && inv_s && near && far && cos_anneal_ratio && dsdf && dG && drgb &&
+                   dinv_s_part,
                CN_ERR_ARG, "cn_composite_bwd: null pointer");
     CN_REQUIRE(S >= 1 && S <= 64 * kMaxPerLane && n_coarse > 0 && ld_g >= 3, CN_ERR_UNSUPPORTED,
                "cn_composite_bwd: S=%d", S);

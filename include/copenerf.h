@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define CN_ABI_VERSION 3
+#define CN_ABI_VERSION 4
 
 typedef void* cn_stream_t; /* hipStream_t */
 
@@ -58,13 +58,20 @@ const char* cn_last_error(void);
  *         when tile == 1); rows >= N must be readable (zero-padded weights).
  *   Columns [0, N) of out0 get the epilogue value, columns [N, nzero) get 0.
  * ------------------------------------------------------------------------ */
+/* sg(x) = 1 - exp(-aux_beta * x): softplus'(z) recovered from a stored softplus
+ * output x = softplus_beta(z) / c (aux_beta = beta * c), since exp(beta a) = 1 +
+ * exp(beta z).  The derivative is never stored (ABI v4): the backward reads the
+ * activations it already keeps. */
 typedef enum cn_epilogue {
     CN_EPI_STORE = 0,        /* out0 = v + bias                                      */
-    CN_EPI_SOFTPLUS = 1,     /* z = v + bias; out0 = softplus_beta(z)/odiv; out1 = softplus'(z) */
+    CN_EPI_SOFTPLUS = 1,     /* z = v + bias; out0 = softplus_beta(z)/odiv           */
     CN_EPI_RELU = 2,         /* out0 = relu(v + bias)                                */
-    CN_EPI_MUL = 3,          /* out0 = v * aux0 (cols < nsplit); out_split = v (cols >= nsplit) */
-    CN_EPI_TANGENT = 4,      /* out0 = v*aux0/odiv (aux0 = sp'); out1 = beta*aux1*(1-aux0)*v (aux1 = s) */
-    CN_EPI_BWD_SOFTPLUS = 5, /* out0 = v*aux0 + aux1 (aux1 nullable)                 */
+    CN_EPI_MUL = 3,          /* out0 = v * sg(aux0) (cols < nsplit); out_split = v (cols >= nsplit) */
+    CN_EPI_TANGENT = 4,      /* out0 = v * sg(aux0) / odiv                           */
+    CN_EPI_BWD_SOFTPLUS = 5, /* out0 = v*sg(aux0) + aux1*aux2*aux2_scale*(1-sg)/sg (0 where sg = 0;
+                                aux1, aux2 both NULL or both set): with aux1 = s (the ∇-pass
+                                adjoint), aux2 = u' = sg*z'/c2 and aux2_scale = beta*c2 this is
+                                softplus' double-backward term beta*s*(1-sg)*z'  */
     CN_EPI_BWD_RELU = 6      /* out0 = aux0 > 0 ? v : 0                              */
 } cn_epilogue;
 
@@ -78,7 +85,7 @@ typedef struct cn_linear_desc {
     const float* aux0;
     const float* aux1;
     float* out0;
-    float* out1;
+    float* out1;         /* must be NULL (ABI v4: no epilogue writes a second output) */
     float* out_split;
     int64_t lda, lda2, ldb, ld_aux0, ld_aux1, ld_out0, ld_out1, ld_split;
     int32_t M, N, K, K1;
@@ -98,6 +105,10 @@ typedef struct cn_linear_desc {
                             B + ((k/16) ldb + n) 48 + 16 t + k%16, ldb = image rows >= the N
                             tiles; six term products accumulated in fp32 (error at the level
                             of fp32 accumulation; K, K1 multiples of 32) */
+    float aux_beta;      /* sg() scale of MUL / TANGENT / BWD_SOFTPLUS (> 0 for those) */
+    const float* aux2;   /* BWD_SOFTPLUS second-order input u' (or NULL) */
+    int64_t ld_aux2;
+    float aux2_scale;
     int32_t reserved_;
 } cn_linear_desc;
 
@@ -177,9 +188,10 @@ size_t cn_colsum_workspace_bytes(int32_t M, int32_t K);
 int cn_colsum(int32_t M, int32_t K, const float* w, const float* X, int64_t ldx, float wdiv, float* out,
               int32_t accumulate, float* workspace, int64_t workspace_bytes, cn_stream_t stream);
 
-/* out[m][n] = X[m][n] * w[n] for n < N (seed of the ∇ₓSDF pass, neus_fields.py:295-302) */
+/* out[m][n] = f(X[m][n]) * w[n] for n < N (seed of the ∇ₓSDF pass, neus_fields.py:295-302):
+ * f(x) = x when act_beta == 0, else softplus' from the softplus output, 1 - exp(-act_beta x). */
 int cn_scale_cols(int32_t M, int32_t N, const float* X, int64_t ldx, const float* w, float* out,
-                  int64_t ld_out, cn_stream_t stream);
+                  int64_t ld_out, float act_beta, cn_stream_t stream);
 
 /* ------------------------------------------------------------------------ *
  * Positional encoding of the SDF input (neus_embedder.py:6-51 with
@@ -268,10 +280,12 @@ int cn_up_sample_merge(int32_t R, int32_t n, int32_t n_imp, float inv_s, const f
  * Alpha compositing (neus_renderer.py:337-420, render_core).  One wavefront
  * per ray; transmittance as an exclusive product scan across the wave.
  * G holds ∇ₓSDF rows (normals = G[m][0..3)), sdf/G/rgb are indexed m = r*S+i.
+ * inv_s and cos_anneal_ratio are device scalars (training.py:120-124 ramps the
+ * ratio every iteration: a replayed hipGraph reads the current value). 
  * ------------------------------------------------------------------------ */
 int cn_composite_fwd(int32_t R, int32_t S, const float* z, const float* sdf, const float* G,
                      int64_t ld_g, const float* rgb, const float* rays_d, const float* inv_s,
-                     const float* near, const float* far, int32_t n_coarse, float cos_anneal_ratio,
+                     const float* near, const float* far, int32_t n_coarse, const float* cos_anneal_ratio,
                      float* color, float* depth, float* weights, float* cdf, cn_stream_t stream);
 
 /* Backward of cn_composite_fwd.  drays_d (nullable, [R][3]) receives the ray
@@ -280,7 +294,7 @@ int cn_composite_fwd(int32_t R, int32_t S, const float* z, const float* sdf, con
  * (neus_renderer.py:356), so no second-order term reaches the points. */
 int cn_composite_bwd(int32_t R, int32_t S, const float* z, const float* sdf, const float* G,
                      int64_t ld_g, const float* rgb, const float* rays_d, const float* inv_s,
-                     const float* near, const float* far, int32_t n_coarse, float cos_anneal_ratio,
+                     const float* near, const float* far, int32_t n_coarse, const float* cos_anneal_ratio,
                      const float* dcolor, const float* ddepth, const float* dweights,
                      const float* dcdf, float* dsdf, float* dG, float* drgb, float* dinv_s_part,
                      float* drays_d, cn_stream_t stream);
@@ -292,14 +306,18 @@ int cn_composite_bwd(int32_t R, int32_t S, const float* z, const float* sdf, con
  * ray patches, patch in 1..4; R rays, M samples):
  *   loss = w_rgb sum|color - gt| / R + w_eik mean_m (|n_m| - 1)^2
  *        + w_edge EdgePreservingSmoothness(depth, gt; gamma) + w_smooth Smoothness(depth)
+ *   weights: DEVICE [4] = (w_rgb, w_eik, w_edge, w_smooth), read by the kernels, so the
+ *   annealed weights of train.py:246-263, 401-405 change without re-capturing a graph;
+ *   nonfinite (nullable, device int32): set to 1 when the loss is not finite -- the
+ *   NaN assert of model/training.py:532-533 without a host sync;
  *   color, gt [R][3]; depth [R]; normals [M][ld_n] (columns 0..2); loss [1];
  *   dcolor [R][3], ddepth [R], dnormals [M][ld_dn] (columns 0..2) = d loss / d input.
  * Partial sums are reduced in double in a fixed order (bitwise reproducible).
  * ------------------------------------------------------------------------ */
 size_t cn_train_loss_workspace_bytes(int32_t R, int32_t patch);
 int cn_train_loss(int32_t R, int32_t patch, int64_t M, const float* color, const float* gt, const float* depth,
-                  const float* normals, int64_t ld_n, float w_rgb, float w_eik, float w_edge, float w_smooth,
-                  float gamma, float* loss, float* dcolor, float* ddepth, float* dnormals, int64_t ld_dn,
+                  const float* normals, int64_t ld_n, const float* weights, float gamma, float* loss,
+                  float* dcolor, float* ddepth, float* dnormals, int64_t ld_dn, int32_t* nonfinite,
                   void* workspace, int64_t workspace_bytes, cn_stream_t stream);
 
 #ifdef __cplusplus

@@ -65,9 +65,19 @@ def test_argument_validation_without_gpu():
     assert lib.cn_wgrad_workspace_bytes(524288, 256, 256) >= 4 * 256 * 256
     ws = lib.cn_train_loss_workspace_bytes(4096, 4)
     assert ws >= 8 * (4096 // 16 // 256)
-    assert lib.cn_train_loss(4096, 5, 0, 16, 16, 16, None, 0, 1.0, 0.1, 1.0, 1e-4, 0.1, 16, 16, 16, None, 0, 16, ws,
+    assert lib.cn_train_loss(4096, 5, 0, 16, 16, 16, None, 0, 16, 0.1, 16, 16, 16, None, 0, None, 16, ws,
                              None) == -5
     assert b"patch 5" in lib.cn_last_error()
+    # ABI v4: the softplus-derivative epilogues need aux_beta; no epilogue writes out1
+    d = _lib.LinearDesc()
+    d.A, d.B, d.out0, d.aux0 = 16, 16, 16, 16
+    d.M, d.N, d.K, d.lda, d.ldb, d.ld_out0, d.ld_aux0 = 8, 8, 32, 32, 32, 8, 8
+    d.epilogue = _lib.EPI_MUL
+    assert lib.cn_linear(ctypes.byref(d), None) == -1
+    assert b"aux_beta" in lib.cn_last_error()
+    d.aux_beta, d.out1 = 100.0, 16
+    assert lib.cn_linear(ctypes.byref(d), None) == -1
+    assert b"out1" in lib.cn_last_error()
 
 
 def test_product_path_refuses_cpu_tensors():

@@ -48,21 +48,21 @@ def test_linear_bf16_epilogues_and_concat():
     Bb = _rnd(N, K1 + K2, seed=6, scale=0.05).bfloat16().contiguous()
     bias = _rnd(N, seed=7, scale=0.3)
     v = (torch.cat([A, A2], 1).bfloat16().double() @ Bb.double().t())
-    a, s = torch.empty(M, N, device=DEV), torch.empty(M, N, device=DEV)
-    ops.linear(A, Bb, N, K1 + K2, a, ops.EPI_SOFTPLUS, A2=A2, K1=K1, bias=bias, out1=s)
+    a = torch.empty(M, N, device=DEV)
+    ops.linear(A, Bb, N, K1 + K2, a, ops.EPI_SOFTPLUS, A2=A2, K1=K1, bias=bias)
     z = (v + bias.double()).float()
     torch.testing.assert_close(a, torch.nn.functional.softplus(z, beta=100), rtol=1e-5, atol=2e-5)
-    torch.testing.assert_close(s, torch.where(z * 100 > 20, torch.ones_like(z), torch.sigmoid(100 * z)),
-                               rtol=1e-4, atol=1e-5)
-    aux0, aux1 = torch.rand(M, N, device=DEV), _rnd(M, N, seed=8)
-    o0, o1 = torch.empty(M, N, device=DEV), torch.empty(M, N, device=DEV)
-    ops.linear(A, Bb, N, K1 + K2, o0, ops.EPI_TANGENT, A2=A2, K1=K1, aux0=aux0, aux1=aux1, out1=o1)
-    vf = v.float()
-    torch.testing.assert_close(o0, vf * aux0, rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(o1, 100.0 * aux1 * (1 - aux0) * vf, rtol=1e-4, atol=1e-4)
+    aux0 = torch.nn.functional.softplus(_rnd(M, N, seed=9, scale=0.05), beta=100)
+    sg = -torch.expm1(-100.0 * aux0.double())
+    aux1, aux2 = _rnd(M, N, seed=8), _rnd(M, N, seed=10)
+    o0 = torch.empty(M, N, device=DEV)
+    ops.linear(A, Bb, N, K1 + K2, o0, ops.EPI_TANGENT, A2=A2, K1=K1, aux0=aux0, aux_beta=100.0)
+    torch.testing.assert_close(o0, (v * sg).float(), rtol=1e-5, atol=1e-5)
     o2 = torch.empty(M, N, device=DEV)
-    ops.linear(A, Bb, N, K1 + K2, o2, ops.EPI_BWD_SOFTPLUS, A2=A2, K1=K1, aux0=aux0, aux1=aux1)
-    torch.testing.assert_close(o2, vf * aux0 + aux1, rtol=1e-5, atol=1e-5)
+    ops.linear(A, Bb, N, K1 + K2, o2, ops.EPI_BWD_SOFTPLUS, A2=A2, K1=K1, aux0=aux0, aux_beta=100.0, aux1=aux1,
+               aux2=aux2, aux2_scale=100.0)
+    ref = v * sg + aux1.double() * aux2.double() * 100.0 * (1 - sg) / sg
+    torch.testing.assert_close(o2, ref.float(), rtol=1e-4, atol=1e-4)
 
 
 @pytest.mark.parametrize("M,N,K,pairs", [(70000, 256, 256, 2), (1000, 204, 64, 1), (5, 256, 256, 1),

@@ -59,12 +59,29 @@ def test_linear_softplus_and_derivative():
     A = _rnd(M, K, seed=9, scale=0.3)
     B = _rnd(N, K, seed=10, scale=0.05)
     bias = _rnd(N, seed=11, scale=0.3)
-    a, s = torch.empty(M, N, device=DEV), torch.empty(M, N, device=DEV)
-    ops.linear(A, B, N, K, a, ops.EPI_SOFTPLUS, bias=bias, out1=s, beta=100.0, threshold=20.0)
+    a = torch.empty(M, N, device=DEV)
+    ops.linear(A, B, N, K, a, ops.EPI_SOFTPLUS, bias=bias, beta=100.0, threshold=20.0)
     z = torch.nn.functional.linear(A, B, bias)
     torch.testing.assert_close(a, torch.nn.functional.softplus(z, beta=100), rtol=1e-5, atol=2e-5)
-    torch.testing.assert_close(s, torch.where(z * 100 > 20, torch.ones_like(z), torch.sigmoid(100 * z)),
-                               rtol=1e-4, atol=1e-5)
+    # the identity the backward epilogues rely on (ABI v4): softplus' = 1 - exp(-beta a)
+    # from the stored activation equals torch's derivative (1 on the linear branch) of the
+    # kernel's own pre-activation (the STORE epilogue: same accumulation, same z) to ~1e-7
+    zk = torch.empty(M, N, device=DEV)
+    ops.linear(A, B, N, K, zk, ops.EPI_STORE, bias=bias)
+    sg = -torch.expm1(-100.0 * a.double())
+    ref = torch.where(zk * 100 > 20, torch.ones_like(zk), torch.sigmoid(100 * zk)).double()
+    assert (sg - ref).abs().max().item() < 5e-7
+
+
+def _act(M, N, seed, c=1.0):
+    """Softplus(beta=100) activations / c of pre-activations in [-0.05, 0.05]
+    (softplus' in [0.007, 0.993]), as the SDF forward stores them."""
+    z = _rnd(M, N, seed=seed, scale=0.05)
+    return (torch.nn.functional.softplus(z, beta=100) / c).contiguous()
+
+
+def _sg(aux0, aux_beta):
+    return -torch.expm1(-aux_beta * aux0.double())
 
 
 def test_linear_mul_split_tangent_bwd_relu():
@@ -72,24 +89,35 @@ def test_linear_mul_split_tangent_bwd_relu():
     M, N, K = 300, 256, 224
     A = _rnd(M, K, seed=12)
     B = _rnd(N, K, seed=13, scale=0.1)
-    aux0 = torch.rand(M, N, device=DEV)
-    aux1 = _rnd(M, N, seed=14)
-    v = (A.double() @ B.double().t()).float()
+    aux0 = _act(M, N, 24, c=ops.SQRT2)
+    ab = 100.0 * ops.SQRT2
+    sg = _sg(aux0, ab)
+    aux1, aux2 = _rnd(M, N, seed=14), _rnd(M, N, seed=15)
+    v = A.double() @ B.double().t()
     out, split = torch.empty(M, 256, device=DEV), torch.empty(M, 64, device=DEV)
-    ops.linear(A, B, N, K, out, ops.EPI_MUL, aux0=aux0, nsplit=204, out_split=split, nzero=256, adiv=ops.SQRT2)
-    torch.testing.assert_close(out[:, :204], (v / ops.SQRT2 * aux0)[:, :204], rtol=1e-5, atol=1e-5)
+    ops.linear(A, B, N, K, out, ops.EPI_MUL, aux0=aux0, aux_beta=ab, nsplit=204, out_split=split, nzero=256,
+               adiv=ops.SQRT2)
+    torch.testing.assert_close(out[:, :204], (v / ops.SQRT2 * sg)[:, :204].float(), rtol=1e-5, atol=1e-5)
     assert torch.all(out[:, 204:] == 0)
-    torch.testing.assert_close(split[:, :52], (v / ops.SQRT2)[:, 204:], rtol=1e-5, atol=1e-5)
-    o0, o1 = torch.empty(M, N, device=DEV), torch.empty(M, N, device=DEV)
-    ops.linear(A, B, N, K, o0, ops.EPI_TANGENT, aux0=aux0, aux1=aux1, out1=o1, beta=100.0)
-    torch.testing.assert_close(o0, v * aux0, rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(o1, 100.0 * aux1 * (1 - aux0) * v, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(split[:, :52], (v / ops.SQRT2)[:, 204:].float(), rtol=1e-5, atol=1e-5)
+    o0 = torch.empty(M, N, device=DEV)
+    ops.linear(A, B, N, K, o0, ops.EPI_TANGENT, aux0=aux0, aux_beta=ab, odiv=ops.SQRT2, beta=100.0)
+    torch.testing.assert_close(o0, (v * sg / ops.SQRT2).float(), rtol=1e-5, atol=1e-5)
     o2 = torch.empty(M, N, device=DEV)
-    ops.linear(A, B, N, K, o2, ops.EPI_BWD_SOFTPLUS, aux0=aux0, aux1=aux1)
-    torch.testing.assert_close(o2, v * aux0 + aux1, rtol=1e-5, atol=1e-5)
+    ops.linear(A, B, N, K, o2, ops.EPI_BWD_SOFTPLUS, aux0=aux0, aux_beta=ab)
+    torch.testing.assert_close(o2, (v * sg).float(), rtol=1e-5, atol=1e-5)
+    # the second-order term beta s (1 - sg) z', z' = u' c / sg, rebuilt from s = aux1, u' = aux2
+    ops.linear(A, B, N, K, o2, ops.EPI_BWD_SOFTPLUS, aux0=aux0, aux_beta=ab, aux1=aux1, aux2=aux2,
+               aux2_scale=ab)
+    ref = v * sg + aux1.double() * aux2.double() * ab * (1 - sg) / sg
+    torch.testing.assert_close(o2, ref.float(), rtol=1e-4, atol=1e-4)
+    # sg = 0 (a zero activation) carries s = u' = 0: the term is 0, not 0 * inf
+    z0 = torch.zeros_like(aux0)
+    ops.linear(A, B, N, K, o2, ops.EPI_BWD_SOFTPLUS, aux0=z0, aux_beta=ab, aux1=z0, aux2=z0, aux2_scale=ab)
+    assert torch.all(o2 == 0)
     o3 = torch.empty(M, N, device=DEV)
     ops.linear(A, B, N, K, o3, ops.EPI_BWD_RELU, aux0=aux1)
-    torch.testing.assert_close(o3, torch.where(aux1 > 0, v, torch.zeros_like(v)), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(o3, torch.where(aux1 > 0, v, torch.zeros_like(v)).float(), rtol=1e-5, atol=1e-5)
 
 
 @pytest.mark.parametrize("M,N,K,pairs", [(70000, 256, 256, 2), (1000, 204, 64, 1), (5, 256, 256, 1),
@@ -130,6 +158,9 @@ def test_row_head_colsum_scale_cols():
     sc = torch.empty(M, K, device=DEV)
     ops.scale_cols(A, K, W[0].contiguous(), sc)
     torch.testing.assert_close(sc, A * W[0], rtol=0, atol=0)
+    act = _act(M, K, 25)
+    ops.scale_cols(act, K, W[0].contiguous(), sc, act_beta=100.0)
+    torch.testing.assert_close(sc, (_sg(act, 100.0) * W[0].double()).float(), rtol=1e-5, atol=1e-7)
 
 
 def test_c_abi_rejects_bad_arguments():

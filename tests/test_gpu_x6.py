@@ -63,21 +63,19 @@ def test_linear_x6_epilogues_and_concat():
     B = _rnd(N, K1 + K2, seed=7, scale=0.05)
     Bs = ops.split_bf16x3(B)
     bias = _rnd(N, seed=8, scale=0.3)
-    aux0, aux1 = torch.rand(M, N, device=DEV), _rnd(M, N, seed=9)
-    for epi, kw in ((ops.EPI_SOFTPLUS, dict(bias=bias, out1=True)), (ops.EPI_TANGENT, dict(aux0=aux0, aux1=aux1, out1=True)),
-                    (ops.EPI_BWD_SOFTPLUS, dict(aux0=aux0, aux1=aux1)), (ops.EPI_RELU, dict(bias=bias)),
-                    (ops.EPI_MUL, dict(aux0=aux0)), (ops.EPI_BWD_RELU, dict(aux0=aux1))):
+    aux0 = torch.nn.functional.softplus(_rnd(M, N, seed=9, scale=0.05), beta=100)
+    aux1, aux2 = _rnd(M, N, seed=10), _rnd(M, N, seed=11)
+    sg = dict(aux0=aux0, aux_beta=100.0)
+    for epi, kw in ((ops.EPI_SOFTPLUS, dict(bias=bias)), (ops.EPI_TANGENT, dict(sg)),
+                    (ops.EPI_BWD_SOFTPLUS, dict(sg, aux1=aux1, aux2=aux2, aux2_scale=100.0)),
+                    (ops.EPI_RELU, dict(bias=bias)), (ops.EPI_MUL, dict(sg)), (ops.EPI_BWD_RELU, dict(aux0=aux1))):
         outs = []
         for Bimg in (B, Bs):
             o0 = torch.empty(M, N, device=DEV)
-            o1 = torch.empty(M, N, device=DEV) if kw.get("out1") else None
-            args = {k: v for k, v in kw.items() if k != "out1"}
-            ops.linear(A, Bimg, N, K1 + K2, o0, epi, A2=A2, K1=K1, out1=o1, **args)
-            outs.append((o0, o1))
-        (a0, a1), (b0, b1) = outs
-        torch.testing.assert_close(b0, a0, rtol=2e-5, atol=2e-6 if epi != ops.EPI_TANGENT else 2e-5)
-        if a1 is not None:
-            torch.testing.assert_close(b1, a1, rtol=1e-4, atol=1e-5 if epi != ops.EPI_TANGENT else 1e-3)
+            ops.linear(A, Bimg, N, K1 + K2, o0, epi, A2=A2, K1=K1, **kw)
+            outs.append(o0)
+        a0, b0 = outs
+        torch.testing.assert_close(b0, a0, rtol=2e-5, atol=2e-6 if epi != ops.EPI_BWD_SOFTPLUS else 2e-4)
 
 
 def test_sdf_field_x6_gradients_match_fp32():

@@ -38,34 +38,37 @@ def main():
     A = torch.randn(M, K, device=dev) * 0.1
     B = torch.randn(N, K, device=dev) * 0.05
     bias = torch.randn(N, device=dev) * 0.1
-    aux0 = torch.rand(M, N, device=dev)
+    aux0 = torch.rand(M, N, device=dev) * 0.02  # softplus activations: sg = 1 - exp(-100 aux0)
     aux1 = torch.randn(M, N, device=dev)
+    aux2 = torch.randn(M, N, device=dev)
     o0 = torch.empty(M, N, device=dev)
-    o1 = torch.empty(M, N, device=dev)
+    sg = dict(aux0=aux0, aux_beta=100.0)
+    so = dict(sg, aux1=aux1, aux2=aux2, aux2_scale=100.0)
     fl = 2.0 * M * N * K
     res = {}
     bench(res, "torch.matmul (hipBLASLt)", lambda: torch.matmul(A, B.t(), out=o0))
     bench(res, "torch addmm+softplus", lambda: torch.nn.functional.softplus(torch.addmm(bias, A, B.t()), beta=100))
     for name, epi, kw in (("store", ops.EPI_STORE, dict(bias=bias)),
-                          ("softplus", ops.EPI_SOFTPLUS, dict(bias=bias, out1=o1)),
-                          ("softplus(no sig)", ops.EPI_SOFTPLUS, dict(bias=bias)),
-                          ("mul", ops.EPI_MUL, dict(aux0=aux0)),
-                          ("tangent", ops.EPI_TANGENT, dict(aux0=aux0, aux1=aux1, out1=o1)),
-                          ("bwd_softplus", ops.EPI_BWD_SOFTPLUS, dict(aux0=aux0, aux1=aux1)),
+                          ("softplus", ops.EPI_SOFTPLUS, dict(bias=bias)),
+                          ("mul", ops.EPI_MUL, sg),
+                          ("tangent", ops.EPI_TANGENT, sg),
+                          ("bwd_softplus", ops.EPI_BWD_SOFTPLUS, so),
                           ("relu", ops.EPI_RELU, dict(bias=bias)),
                           ("main loop only (bench)", 7, {})):
         bench(res, "cn_linear " + name, lambda: ops.linear(A, B, N, K, o0, epi, **kw))
     Bb = B.bfloat16().contiguous()
     for name, epi, kw in (("store", ops.EPI_STORE, dict(bias=bias)),
-                          ("softplus", ops.EPI_SOFTPLUS, dict(bias=bias, out1=o1)),
-                          ("tangent", ops.EPI_TANGENT, dict(aux0=aux0, aux1=aux1, out1=o1)),
+                          ("softplus", ops.EPI_SOFTPLUS, dict(bias=bias)),
+                          ("tangent", ops.EPI_TANGENT, sg),
                           ("main loop only (bench)", 7, {})):
         bench(res, "cn_linear bf16 " + name, lambda: ops.linear(A, Bb, N, K, o0, epi, **kw))
     Bs = ops.split_bf16x3(B)
     for name, epi, kw in (("store", ops.EPI_STORE, dict(bias=bias)),
-                          ("softplus", ops.EPI_SOFTPLUS, dict(bias=bias, out1=o1)),
-                          ("tangent", ops.EPI_TANGENT, dict(aux0=aux0, aux1=aux1, out1=o1)),
-                          ("bwd_softplus", ops.EPI_BWD_SOFTPLUS, dict(aux0=aux0, aux1=aux1)),
+                          ("softplus", ops.EPI_SOFTPLUS, dict(bias=bias)),
+                          ("relu", ops.EPI_RELU, dict(bias=bias)),
+                          ("mul", ops.EPI_MUL, sg),
+                          ("tangent", ops.EPI_TANGENT, sg),
+                          ("bwd_softplus", ops.EPI_BWD_SOFTPLUS, so),
                           ("main loop only (bench)", 7, {})):
         bench(res, "cn_linear x6 " + name, lambda: ops.linear(A, Bs, N, K, o0, epi, **kw))
     bench(res, "torch.matmul bf16 (hipBLASLt)", lambda: torch.matmul(A.bfloat16(), Bb.t()))

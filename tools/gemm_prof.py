@@ -26,8 +26,8 @@ def main():
         B = B.bfloat16().contiguous()
     elif mode == "x6":
         B = ops.split_bf16x3(B)
-    for epi, kw in ((ops.EPI_STORE, dict(bias=bias)), (ops.EPI_SOFTPLUS, dict(bias=bias, out1=o1)),
-                    (ops.EPI_TANGENT, dict(aux0=aux0, aux1=aux1, out1=o1)), (7, {})):
+    for epi, kw in ((ops.EPI_STORE, dict(bias=bias)), (ops.EPI_SOFTPLUS, dict(bias=bias)),
+                    (ops.EPI_TANGENT, dict(aux0=aux0, aux_beta=100.0)), (7, {})):
         for _ in range(int(os.environ.get("REPS", 5))):
             ops.linear(A, B, N, K, o0, epi, **kw)
     torch.cuda.synchronize()
