@@ -1,6 +1,6 @@
 """bench.py — train-step throughput of the MI355X NeuS hot path.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|...] [--graph]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 Metric (BASELINE.json): rays/sec of a full training step incl. backward at
@@ -8,17 +8,22 @@ Metric (BASELINE.json): rays/sec of a full training step incl. backward at
 poses, synthetic data): patch sampling + ray generation, the HIP renderer
 forward, L1 rgb + 0.1 eikonal + edge-aware / plain depth smoothness, the HIP
 backward (incl. the ∇ₓSDF double backward), the gradient all-reduce (N > 1)
-and Adam.  Weak scaling: every rank renders its own 4096 rays.
+and Adam.  Weak scaling: every rank renders its own 4096 rays.  The timed
+steps run uninstrumented.
 
 The JSON line also carries
-  roofline      the dominant kernel's algorithmic FLOPs / its average launch
-                time, measured with HIP events on the launching stream over the
-                timed steps, against the gfx950 fp32 MFMA peak; `traffic` is
-                the rocprofv3 PMC (FETCH_SIZE + WRITE_SIZE) per launch read from
-                profiles/ when a counter pass for this kernel is committed;
-  cpu_baseline  the CPU oracle (oracle/neus_oracle.py, a torch port of the
-                reference path) timed on this box's host cores on a bounded
-                sample (rank 0, N = 1 only).
+  roofline      the dominant kernel (the cn_linear launch class with the most
+                time), from a separate instrumented pass after the timed steps
+                (HIP events around each launch on the launching stream):
+                its algorithmic FLOPs and bytes per launch against the binding
+                ceiling, max(FLOPs / MFMA peak of the GEMM mode, bytes / HBM
+                peak); `traffic` is the rocprofv3 PMC (FETCH_SIZE + WRITE_SIZE)
+                per launch read from profiles/ when a counter pass for this
+                kernel is committed;
+  cpu_baseline  the CPU oracle (oracle/neus_oracle.py, a torch restatement of the
+                reference path pinned to the reference's outputs) timed on this
+                box's host cores: median of 5 steps at 1024 rays after a
+                warm-up (rank 0, N = 1 only).
 """
 from __future__ import annotations
 
@@ -37,6 +42,7 @@ sys.path[:0] = [os.path.join(ROOT, "cope-nerf_amd"), ROOT]
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, = fp32 vector peak
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 (v_mfma_f32_32x32x16_bf16, 32 cycles)
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E
 # fp32-GEMM FLOP/s ceiling of each operand mode: bf16x6 issues six bf16 MFMAs per fp32 product
 MODE_PEAK_TFLOPS = {"fp32": FP32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS,
                     "bf16x6": BF16_MFMA_PEAK_TFLOPS / 6.0}
@@ -49,20 +55,25 @@ SAMPLES = 128
 GFLOP_PER_RAY_REF = 1.4809  # reference GEMM FLOPs per ray per train step (64+4x16)
 
 
+# cn_linear's bf16x6 epilogues on the 256x128 tile (cn_gemm.hip g_wide_epis, default 0x1f)
+WIDE_EPIS = int(os.environ.get("COPENERF_WIDE_EPIS", "0x1f"), 0)
+EPI_ID = {"store": 0, "softplus": 1, "relu": 2, "mul": 3, "tangent": 4, "bwd_softplus": 5, "bwd_relu": 6}
+
+
 def kernel_symbol(key):
     """rocprofv3 name of the kernel a KernelTimer key times (cn_gemm.hip's
     cn_linear dispatch: waves, tiles, BK, workgroups/CU, prefetch depth,
     epilogue, row vector, operand mode).  fp32: BK 32 with the 2-deep prefetch
     (every K on the C2 path is a multiple of 64); bf16: BK 64, 1-deep; bf16x6
-    (split fp32): 256x128 tiles, BK 32, one workgroup per CU for STORE / SOFTPLUS
-    / RELU at K % 64 == 0 (every such K on C2), else 128x128, BK 16, 2-deep."""
+    (split fp32): 256x128 tiles, BK 32, one workgroup per CU for the epilogues in
+    WIDE_EPIS at K % 64 == 0 (every such K on C2), else 128x128, BK 16, 2-deep."""
     if key[0] == "linear":
-        wide = "x6" in key[3:] and key[1] == 0 and key[2] in ("store", "softplus", "relu")  # K % 64 == 0 on C2
+        epi = EPI_ID[key[2]]
+        wide = "x6" in key[3:] and key[1] == 0 and (WIDE_EPIS >> epi) & 1
         tiles = {0: "4, 2, 2, 2" if wide else "2, 2, 2, 2", 1: "4, 1, 1, 2"}
-        epi = {"store": 0, "softplus": 1, "relu": 2, "mul": 3, "tangent": 4, "bwd_softplus": 5, "bwd_relu": 6}
         mode = 1 if "bf16" in key[3:] else 2 if "x6" in key[3:] else 0
         mid = {0: "32, 2, 2", 1: "64, 2, 1", 2: "32, 1, 2" if wide else "16, 2, 2"}[mode]
-        return f"void cn::linear_kernel<{tiles[key[1]]}, {mid}, {epi[key[2]]}, false, {mode}>(cn::LinearArgs)"
+        return f"void cn::linear_kernel<{tiles[key[1]]}, {mid}, {epi}, false, {mode}>(cn::LinearArgs)"
     if "bf16" in key[2:]:
         return "void cn::wgrad_bf16_kernel<2, 2, 2, 2>(cn::WgradArgs) + cn::slab_reduce_kernel"
     if "x6" in key[2:]:
@@ -85,8 +96,22 @@ def pmc_traffic(symbol):
     return None, None
 
 
-def cpu_baseline(rays=256, steps=2):
-    """Time the CPU oracle (torch restatement of the reference path) on the host."""
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(rays=1024, steps=5):
+    """Time the CPU oracle (torch restatement of the reference path) on the host:
+    one warm-up step, then the median of `steps` steps at `rays` rays (BASELINE.md's
+    CPU-baseline plan)."""
+    import statistics
     from tests.helpers import build_modules, oracle_params
     from oracle import neus_oracle as O
     threads = int(os.environ.get("COPENERF_CPU_THREADS", min(16, os.cpu_count() or 1)))
@@ -99,20 +124,21 @@ def cpu_baseline(rays=256, steps=2):
         o = torch.zeros(R, 3)
         d = torch.cat([(torch.rand(R, 2, generator=g) - 0.5), -torch.ones(R, 1)], -1)
         nrm = d.norm(dim=-1, keepdim=True)
+        t0 = time.perf_counter()
         out = O.render(P, Pc, var, o, d / nrm, nrm, torch.zeros(1), torch.full((R, 1), 0.01), torch.full((R, 1), 5.0),
                        car=0.5, t_rand=torch.rand(R, 64, generator=g))
         loss = O.train_loss(out, torch.rand(R, 3, generator=g))
         torch.autograd.grad(loss, list(leaves.values()))
+        return time.perf_counter() - t0
 
-    one(16)  # warm the allocator / MKL
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        one(rays)
-    dt = time.perf_counter() - t0
-    return {"value": round(rays * steps / dt, 3), "unit": "rays/s", "cores": threads, "kind": "port",
+    one(rays)  # warm the allocator / MKL at the measured size
+    times = [one(rays) for _ in range(steps)]
+    med = statistics.median(times)
+    return {"value": round(rays / med, 3), "unit": "rays/s", "cores": threads, "kind": "port",
             "sample": f"oracle/neus_oracle.py train step (fwd + L1/eikonal/smoothness loss + backward, no optimiser), "
-                      f"{steps} steps x {rays} rays x 128 samples (64+4x16), full-width nets, fp32, "
-                      f"torch {torch.__version__} CPU, {threads} threads, {dt:.1f} s"}
+                      f"{rays} rays x 128 samples (64+4x16), full-width nets, fp32, torch {torch.__version__} CPU, "
+                      f"{threads} threads on '{_cpu_model()}'; median of {steps} steps after 1 warm-up "
+                      f"(min {min(times):.2f} s, max {max(times):.2f} s per step)"}
 
 
 CONFIGS = {
@@ -121,18 +147,19 @@ CONFIGS = {
            "C2: synthetic scene, 4096 rays x 128 samples (64 coarse + 4x16 importance) per GPU, fp32, "
            "fixed poses, full train step (fwd + losses + bwd + Adam)"),
     "c2fp32": (4096, {"mfma_dtype": "fp32"}, "C2 with the exact-product fp32 MFMA GEMMs"),
-    "c3": (4096, {"joint_pose": True, "stage1": True, "mfma_dtype": "bf16"},
-           "C3-style: synthetic scene, 4096 rays x 128 samples per GPU, bf16 MLP MFMA (fp32 accumulate), joint "
-           "pose optimisation (learnable SE(3) poses -> ray gradients) + stage-1 scene-flow and SDF-consistency "
-           "losses"),
-    "c3fp32": (4096, {"joint_pose": True, "stage1": True, "mfma_dtype": "bf16x6"},
+    "c3": (4096, {"joint_pose": True, "stage1": True, "mfma_dtype": "bf16", "start_it": 30000},
+           "C3-style: synthetic 10-frame scene, 4096 rays x 128 samples per GPU, bf16 MLP MFMA (fp32 accumulate), "
+           "joint pose optimisation (learnable SE(3) poses -> ray gradients) + the stage-1 losses (scene-flow SDF "
+           "loss, flow-RGB warp to the 3 next frames, SDF consistency at the world camera)"),
+    "c3fp32": (4096, {"joint_pose": True, "stage1": True, "mfma_dtype": "bf16x6", "start_it": 30000},
                "C3-style as c3 with fp32 GEMMs (bf16x6)"),
     "infer": (518400, {"infer": True, "mfma_dtype": "bf16x6"},
               "inference: full 540x960 image (518,400 rays x 128 samples, eval mode, no jitter), forward only "
               "(sampler + SDF + ∇SDF + colour + compositing), 65,536-ray chunks, fp32"),
     "c2bf16": (4096, {"mfma_dtype": "bf16"},
                "C2 workload (4096 rays x 128 samples, fixed poses) with bf16 MLP MFMA (fp32 accumulate)"),
-    "c4": (8192, {"mfma_dtype": "bf16x6"}, "C4: synthetic scene, 8192 rays x 128 samples per GPU, fp32, fixed poses, data-parallel"),
+    "c4": (8192, {"mfma_dtype": "bf16x6"}, "C4: synthetic scene, 8192 rays x 128 samples per GPU, fp32, fixed poses, "
+                                            "data-parallel"),
     "c5": (4096, {"ren_cfg": dict(n_samples=64, n_importance=128, n_outside=0, up_sample_steps=4, perturb=1.0,
                                   n_max_network_queries=64000, importance_sampling_start=0, naive_render=False),
                   "graph": True, "mfma_dtype": "bf16x6"},
@@ -149,6 +176,7 @@ def main():
     ap.add_argument("--rays", type=int, default=None, help="rays per GPU (default: the config's)")
     ap.add_argument("--graph", action="store_true", help="replay the step from a captured HIP graph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--timer-steps", type=int, default=3, help="instrumented steps after the timed ones (roofline)")
     args = ap.parse_args()
     rays_cfg, kw, workload = CONFIGS[args.config]
     kw = dict(kw)
@@ -165,8 +193,6 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank, world_size=world)
-    if graph and distributed:
-        raise SystemExit("--graph captures the single-GPU step; the data-parallel all-reduce stays eager")
 
     from copenerf import ops
     from copenerf.train_step import GraphedTrainer, SyntheticTrainer
@@ -182,7 +208,7 @@ def main():
         def step():
             out = render_image(tr.renderer, tr.K, tr.I, tr.I, (tr.H, tr.W), t_img, chunk=65536)
             return out["rgb"].sum()
-    if graph:
+    if graph:  # the captured step includes the data-parallel all-reduce (RCCL) when distributed
         g = GraphedTrainer(tr, warmup=max(1, args.warmup))
         step = g.step
 
@@ -191,12 +217,7 @@ def main():
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
-
-    timer = None if graph else ops.KernelTimer()
-    ops.set_kernel_timer(timer)
     torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
@@ -204,13 +225,20 @@ def main():
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ops.set_kernel_timer(None)
     if distributed:
         t = torch.tensor([elapsed], device=f"cuda:{local}", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     if not torch.isfinite(loss).item():
         raise RuntimeError("non-finite loss in the timed steps")
+    # the roofline pass: separate, instrumented (HIP events around every GEMM), eager
+    timer = ops.KernelTimer()
+    ops.set_kernel_timer(timer)
+    n_inst = max(1, args.timer_steps)
+    for _ in range(n_inst):
+        tr.step() if not infer else step()
+    torch.cuda.synchronize()
+    ops.set_kernel_timer(None)
 
     rays_total = rays * world * args.steps
     S = 192 if args.config == "c5" else SAMPLES
@@ -231,7 +259,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16 MFMA operands, fp32 accumulate/activations" if mode == "bf16" else "fp32",
-        "data": "synthetic (random 540x960 image, 4x4 patches, " +
+        "data": "synthetic (10 random 540x960 frames cycled one per step, 4x4 patches, " +
                 ("learnable SE(3) poses" if kw.get("joint_pose") else "fixed identity pose") +
                 ", geometric-init SDF, seed 678)",
         "config": {"workload": workload, "gemm": MODE_TEXT[mode], "rays_per_gpu": rays, "samples_per_ray": S,
@@ -240,8 +268,7 @@ def main():
         "roofline": None,
         "cpu_baseline": None,
     }
-    if timer is not None:
-        result.update(roofline_fields(timer, args.steps, rays_total / elapsed, mode))
+    result.update(roofline_fields(timer, n_inst, rays_total / elapsed, mode))
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
         result["cpu_baseline"] = cpu_baseline()
     if rank == 0:
@@ -256,25 +283,33 @@ def roofline_fields(timer, steps, rays_per_s, mode):
     # split-M MFMA kernel and its fixed-order slab reduction)
     dom_key = max((k for k in agg if k[0] == "linear"), key=lambda k: agg[k]["ms"])
     dom = agg[dom_key]
-    avg_ms = dom["ms"] / dom["launches"]
-    achieved = dom["flops"] / dom["launches"] / (avg_ms * 1e-3) / 1e12
+    avg_s = dom["ms"] / dom["launches"] * 1e-3
+    flops, nbytes = dom["flops"] / dom["launches"], dom["bytes"] / dom["launches"]
+    peak_tf = MODE_PEAK_TFLOPS[mode]
+    t_flop, t_byte = flops / (peak_tf * 1e12), nbytes / (HBM_PEAK_GBS * 1e9)
+    hbm = t_byte > t_flop  # the binding ceiling: the larger of the two times
     symbol = kernel_symbol(dom_key)
     traffic, traffic_src = pmc_traffic(symbol)
     kernels_ms = sum(a["ms"] for a in agg.values()) / steps
+    roof = {"bound": "hbm" if hbm else "mfma",
+            "achieved": round(nbytes / avg_s / 1e9, 1) if hbm else round(flops / avg_s / 1e12, 2),
+            "peak": HBM_PEAK_GBS if hbm else round(peak_tf, 1), "unit": "GB/s" if hbm else "TFLOP/s",
+            "frac": round(max(t_flop, t_byte) / avg_s, 4), "traffic": traffic, "traffic_source": traffic_src,
+            "kernel": symbol, "launches_per_step": dom["launches"] / steps, "avg_launch_ms": round(avg_s * 1e3, 4),
+            "algorithmic_gflop_per_launch": round(flops / 1e9, 3),
+            "algorithmic_mb_per_launch": round(nbytes / 1e6, 1),
+            "tflops": round(flops / avg_s / 1e12, 2), "gbs": round(nbytes / avg_s / 1e9, 1),
+            "frac_mfma": round(t_flop / avg_s, 4), "frac_hbm": round(t_byte / avg_s, 4),
+            "peak_basis": {"fp32": "fp32 MFMA dense", "bf16": "bf16 MFMA dense",
+                           "bf16x6": "bf16 MFMA dense / 6 products"}[mode] + "; HBM3E 8 TB/s"}
     return {
-        "roofline": {"bound": "mfma", "kernel": symbol, "achieved": round(achieved, 2),
-                     "peak": round(MODE_PEAK_TFLOPS[mode], 1), "unit": "TFLOP/s",
-                     "frac": round(achieved / MODE_PEAK_TFLOPS[mode], 4),
-                     "peak_basis": {"fp32": "fp32 MFMA dense", "bf16": "bf16 MFMA dense",
-                                    "bf16x6": "bf16 MFMA dense / 6 products"}[mode],
-                     "traffic": traffic, "traffic_source": traffic_src,
-                     "launches_per_step": dom["launches"] / steps, "avg_launch_ms": round(avg_ms, 4),
-                     "algorithmic_gflop_per_launch": round(dom["flops"] / dom["launches"] / 1e9, 3)},
+        "roofline": roof,
         "effective_ref_tflops": round(rays_per_s * GFLOP_PER_RAY_REF / 1e3, 2),
         "gemm_ms_per_step": round(kernels_ms, 3),
         "gemm_tflops_avg": round(sum(a["flops"] for a in agg.values()) / sum(a["ms"] for a in agg.values()) / 1e9, 2),
-        "roofline_by_class": {"/".join(map(str, k)): round(v["flops"] / v["ms"] / 1e9, 1) for k, v in
-                              sorted(agg.items(), key=lambda kv: -kv[1]["ms"])},
+        "roofline_by_class": {"/".join(map(str, k)): {"tflops": round(v["flops"] / v["ms"] / 1e9, 1),
+                                                       "gbs": round(v["bytes"] / v["ms"] / 1e6, 1)}
+                              for k, v in sorted(agg.items(), key=lambda kv: -kv[1]["ms"])},
         "kernel_breakdown_ms_per_step": {"/".join(map(str, k)): round(v["ms"] / steps, 3) for k, v in
                                          sorted(agg.items(), key=lambda kv: -kv[1]["ms"])},
     }

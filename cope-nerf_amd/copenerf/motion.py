@@ -145,11 +145,84 @@ class MotionNetwork(nn.Module):
             w2c.append(rel @ w2c[-1])
         return torch.stack(w2c)
 
+    # -- batched, device-resident form (graph-capturable) -------------------
+    def interval_time_grid(self, total_nb_images, nb_sample_timestep, n_intervals=None):
+        """The reference's per-interval time grids, built once on the host exactly as
+        compute_consecutive_relative_pose builds them (torch.linspace(t_k, t_k+1, n+1)[:-1],
+        Δt = grid[1] - grid[0]): ([K, n] steps, [K] Δt) for the intervals k -> k+1,
+        k < K (default K = total_nb_images - 1)."""
+        K = total_nb_images - 1 if n_intervals is None else n_intervals
+        steps, dts = [], []
+        for k in range(K):
+            t0 = k / (total_nb_images - 1) * 2 - 1
+            t1 = (k + 1.0) / (total_nb_images - 1) * 2 - 1
+            g = torch.linspace(t0, t1, nb_sample_timestep + 1)[:-1]
+            steps.append(g)
+            dts.append(g[1] - g[0])
+        dev = self._device()
+        return torch.stack(steps).to(dev), torch.stack(dts).to(dev)
 
-def scene_flow_loss(pts, normals, sdf_flows, weights, angular_velocity, velocity):
+    def batched_relative_poses(self, steps, dts):
+        """Every consecutive relative pose at once: one MotionNetwork forward over all
+        K*n time steps, then the reference's Euler recurrence (neus_fields.py:146-165)
+        T <- R_s T + V_s, R <- R R_s run for all K intervals together (n batched 3x3
+        steps instead of K*n host-launched ones).  steps [K, n], dts [K] -> [K, 4, 4]."""
+        K, n = steps.shape
+        omega, vel = self.forward(steps.reshape(-1, 1))
+        dt = dts.view(K, 1, 1)
+        Rs = euler_angles_to_matrix(omega.view(K, n, 3) * dt, "XYZ")  # [K, n, 3, 3]
+        Vs = vel.view(K, n, 3) * dt
+        R = torch.eye(3, device=steps.device).expand(K, 3, 3)
+        T = torch.zeros(K, 3, 1, device=steps.device)
+        for s in range(n):
+            T = Rs[:, s] @ T + Vs[:, s, :, None]
+            R = R @ Rs[:, s]
+        top = torch.cat([R, T], -1)  # [K, 3, 4]
+        row = torch.eye(4, device=steps.device)[3:4].expand(K, 1, 4)  # no host scalar copy: capturable
+        return torch.cat([top, row], 1)
+
+
+def masked_chain(P, lo, hi):
+    """w2c of the frames lo -> hi from consecutive relative poses P [K, 4, 4]:
+    P[hi-1] @ ... @ P[lo] (= compute_w2c_mappings(rel[lo:hi])[-1], neus_fields.py:174-186),
+    with lo / hi device integer tensors: every interval outside [lo, hi) enters as the
+    identity, so the shapes (and a captured graph) do not depend on the indices."""
+    K = P.shape[0]
+    k = torch.arange(K, device=P.device)
+    m = ((k >= lo) & (k < hi)).view(K, 1, 1)
+    eye = torch.eye(4, device=P.device)
+    Q = torch.where(m, P, eye)
+    out = eye
+    for j in range(K):
+        out = Q[j] @ out
+    return out
+
+
+def _allreduce_sum(x, group):
+    """Sum a detached scalar over the data-parallel ranks (the global normalisers of
+    SURVEY.md §8e); identity without a process group."""
+    if group is None:
+        return x
+    import torch.distributed as dist
+    x = x.clone()
+    dist.all_reduce(x, op=dist.ReduceOp.SUM, group=group)
+    return x
+
+
+def _world(group):
+    if group is None:
+        return 1
+    import torch.distributed as dist
+    return dist.get_world_size(group)
+
+
+def scene_flow_loss(pts, normals, sdf_flows, weights, angular_velocity, velocity, group=None):
     """SDF scene-flow consistency (train.py:467-477): the scene flow ω × p + v of
     every sample must satisfy the level-set equation ∇sdf · flow + ∂sdf/∂t = 0;
-    L1, weighted by the detached render weights over their global sum."""
+    L1, weighted by the detached render weights over their global sum.  With a
+    process group, Σw is all-reduced before the divide and the rank's term is
+    scaled by the world size, so the mean of the ranks' gradients is the gradient
+    of the single-GPU loss over all rays."""
     pts = pts.reshape(-1, 3)
     normals = normals.reshape(-1, 3)
     sdf_flows = sdf_flows.reshape(-1)
@@ -158,21 +231,29 @@ def scene_flow_loss(pts, normals, sdf_flows, weights, angular_velocity, velocity
     vel = velocity.reshape(1, 3).expand(pts.shape[0], 3)
     flow = torch.cross(omega, pts, dim=-1) + vel
     lhs = torch.sum(flow * normals, dim=-1)
-    return torch.sum(torch.abs(lhs + sdf_flows) * w) / (torch.sum(w) + 1e-10)
+    den = _allreduce_sum(torch.sum(w), group)
+    return _world(group) * torch.sum(torch.abs(lhs + sdf_flows) * w) / (den + 1e-10)
 
 
 def project_flow(pts, weights, w2c, ref_camera_mat, scale_mat, normalized_pixels, img_hw):
-    """Forward optical flow to a reference frame (train.py:478-496): the
+    """Forward optical flow to reference frames (train.py:484-495): the
     weight-averaged sample point of each ray, mapped by the relative pose w2c
-    [4,4] and projected with the reference camera; returns pixel offsets [R,2]."""
+    [T, 4, 4] (or [4, 4]) and projected with the reference cameras ref_camera_mat
+    [T, 4, 4] (or [1, 4, 4]); returns pixel offsets [T, R, 2] (or [R, 2])."""
+    single = w2c.dim() == 2
+    if single:
+        w2c, ref_camera_mat = w2c[None], ref_camera_mat.reshape(1, 4, 4)
     R = normalized_pixels.shape[0]
-    pts_map = (w2c[:3, :3] @ pts.reshape(-1, 3).T + w2c[:3, [-1]]).T
-    wp = torch.sum(weights.reshape(R, -1, 1) * pts_map.reshape(R, -1, 3), dim=1)
-    pix = (scale_mat[0, :3, :3] @ ref_camera_mat[0, :3, :3] @ wp.T).T
-    pix = pix[:, :2] / pix[:, [-1]]
+    P = pts.reshape(R, -1, 3)
+    pts_map = torch.einsum("tij,rsj->trsi", w2c[:, :3, :3], P) + w2c[:, None, None, :3, 3]
+    wp = torch.sum(weights.reshape(1, R, -1, 1) * pts_map, dim=2)  # [T, R, 3]
+    KS = scale_mat.reshape(-1, 4, 4)[0, :3, :3] @ ref_camera_mat[:, :3, :3]  # [T, 3, 3]
+    pix = torch.einsum("tij,trj->tri", KS, wp)
+    pix = pix[..., :2] / pix[..., 2:3]
     flow = pix - normalized_pixels
     h, w = img_hw
-    return torch.stack([flow[:, 0] * (w / 2), flow[:, 1] * (h / 2)], -1)
+    flow = torch.stack([flow[..., 0] * (w / 2), flow[..., 1] * (h / 2)], -1)
+    return flow[0] if single else flow
 
 
 def warp_pixel(src_frame, uv, normalize_pix=True):
@@ -187,15 +268,25 @@ def warp_pixel(src_frame, uv, normalize_pix=True):
                                            align_corners=True)
 
 
-def flow_rgb_loss(flow_fw, sampled_pixel, ref_img, rgb_gt):
+def flow_rgb_loss(flow_fw, sampled_pixel, ref_img, rgb_gt, group=None):
     """Photometric loss of the reference frame warped by the predicted flow
-    (train.py:506-515), masked to correspondences inside the image."""
-    corr = sampled_pixel + flow_fw
-    with torch.no_grad():
-        lim = torch.tensor([ref_img.shape[3], ref_img.shape[2]], dtype=torch.float32, device=corr.device)
-        valid = ((corr >= 0) & (corr < lim)).all(dim=1, keepdim=True)
-    warped = warp_pixel(ref_img, corr.T.unsqueeze(0).unsqueeze(-1)).squeeze().T
-    return torch.sum(torch.abs(warped - rgb_gt) * valid) / (torch.sum(valid) + 1e-10)
+    (train.py:506-515), masked to correspondences inside the image.  Batched over T
+    reference frames: flow_fw [T, R, 2], ref_img [T, 3, H, W] -> per-frame losses [T]
+    (or [R, 2] / [1, 3, H, W] -> a scalar).  Σvalid is all-reduced with a process group."""
+    single = flow_fw.dim() == 2
+    if single:
+        flow_fw = flow_fw[None]
+    T = flow_fw.shape[0]
+    corr = sampled_pixel[None] + flow_fw  # [T, R, 2]
+    with torch.no_grad():  # ((corr >= 0) & (corr < [W, H])).all(dim=1)
+        cx, cy = corr[..., 0], corr[..., 1]
+        valid = ((cx >= 0) & (cx < ref_img.shape[3]) & (cy >= 0) & (cy < ref_img.shape[2])).unsqueeze(-1)
+    # warp_pixel's uv: [T, 2, R, 1] -> grid [T, R, 1, 2] -> [T, 3, R, 1]
+    warped = warp_pixel(ref_img, corr.permute(0, 2, 1).unsqueeze(-1))[..., 0].permute(0, 2, 1)  # [T, R, 3]
+    num = torch.sum(torch.abs(warped - rgb_gt[None]) * valid, dim=(1, 2))
+    den = _allreduce_sum(torch.sum(valid, dim=(1, 2)).float(), group)
+    out = _world(group) * num / (den + 1e-10)
+    return out[0] if single else out
 
 
 def world_points(pts, cw2):

@@ -31,19 +31,20 @@ class KernelTimer:
         e.record()
         return e
 
-    def stop(self, key, e0, flops):
+    def stop(self, key, e0, flops, nbytes=0.0):
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
-        self.records.append((key, e0, e1, flops))
+        self.records.append((key, e0, e1, flops, nbytes))
 
     def summary(self):
         torch.cuda.synchronize()
         agg = {}
-        for key, e0, e1, fl in self.records:
-            a = agg.setdefault(key, {"launches": 0, "ms": 0.0, "flops": 0.0})
+        for key, e0, e1, fl, nb in self.records:
+            a = agg.setdefault(key, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
             a["launches"] += 1
             a["ms"] += e0.elapsed_time(e1)
             a["flops"] += fl
+            a["bytes"] += nb
         return agg
 
 
@@ -218,7 +219,12 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
         e0 = _timer.start()
         _lib.check(_lib.load().cn_linear(d, _stream()), "cn_linear")
         key = ("linear", tile, EPI_NAMES[epilogue]) + (("bf16",) if bf else ("x6",) if x6 else ())
-        _timer.stop(key + ((M, N, K),) if _timer.detail else key, e0, 2.0 * M * N * (kalg or K))
+        ka = kalg or K
+        # algorithmic HBM bytes: A (unpadded K) and every aux row read once, each output
+        # element written once, the weight image once (bf16x6: 3 bf16 terms per weight)
+        nb = 4.0 * M * ka + (6.0 if x6 else 2.0 if bf else 4.0) * N * ka + 4.0 * M * N
+        nb += 4.0 * M * N * sum(t is not None for t in (aux0, aux1, aux2)) + (4.0 * M if rowv is not None else 0.0)
+        _timer.stop(key + ((M, N, K),) if _timer.detail else key, e0, 2.0 * M * N * ka, nb)
     else:
         _lib.check(_lib.load().cn_linear(d, _stream()), "cn_linear")
     return out0
@@ -255,7 +261,7 @@ def wgrad(Y0, X0, N, K, dW, *, db=None, Y1=None, X1=None, accumulate=False, mode
         _lib.check(lib.cn_wgrad(d, _stream()), "cn_wgrad")
         key = ("wgrad", d.npairs) + (("bf16",) if mode == "bf16" else ("x6",) if mode == "bf16x6" else ())
         _timer.stop(key + ((M, d.n_out, d.k_out),) if _timer.detail else key, e0,
-                    2.0 * M * d.n_out * d.k_out * d.npairs)
+                    2.0 * M * d.n_out * d.k_out * d.npairs, 4.0 * d.npairs * M * (d.n_out + d.k_out))
     else:
         _lib.check(lib.cn_wgrad(d, _stream()), "cn_wgrad")
     return dW

@@ -72,18 +72,26 @@ _COF_DEV = {}
 
 def inv4x4(m):
     """Inverse of 4x4 matrices [..., 4, 4] by cofactors (adjugate / determinant):
-    one gather of the 96 minor-term triples, their products and signed sums,
-    a determinant and a division -- a handful of device ops, differentiable and
-    HIP-graph capturable (the LAPACK path behind torch.inverse is not); agrees
-    with torch.inverse to fp32 rounding on the well-conditioned camera / pose
-    matrices of this path."""
+    the 96 minor-term triples of the 16 entries are gathered by a one-hot matrix
+    product (exact: each output is 1.0 x one entry; and its backward is a matrix
+    product, where an index gather's backward is an accumulating index_put that
+    cannot be captured in a HIP graph), then their products (explicit multiplies:
+    prod()'s backward syncs) and signed sums, a
+    determinant and a division -- a handful of device ops, differentiable and
+    graph-capturable (the LAPACK path behind torch.inverse is neither); agrees with
+    torch.inverse to fp32 rounding on the well-conditioned camera / pose matrices
+    of this path."""
     key = (m.device, m.dtype)
     if key not in _COF_DEV:  # first use is outside any graph capture (warmup steps)
-        _COF_DEV[key] = (torch.as_tensor(_COF[0], device=m.device), torch.as_tensor(_COF[1], device=m.device,
-                                                                                    dtype=m.dtype))
-    idx, sgn = _COF_DEV[key]
-    a = m.reshape(*m.shape[:-2], 16)
-    cof = (a[..., idx].prod(-1) * sgn).sum(-1).reshape(*m.shape[:-2], 4, 4)  # C_ij
+        onehot = torch.zeros(16, _COF[0].size, dtype=m.dtype)
+        onehot[torch.as_tensor(_COF[0]).reshape(-1), torch.arange(_COF[0].size)] = 1.0
+        _COF_DEV[key] = (onehot.to(m.device), torch.as_tensor(_COF[1], device=m.device, dtype=m.dtype))
+    onehot, sgn = _COF_DEV[key]
+    a = m.reshape(-1, 16)
+    terms = (a @ onehot).reshape(*m.shape[:-2], 16, 6, 3)
+    # the triple products written out: prod()'s backward looks for zeros with nonzero(), a host sync
+    trip = terms[..., 0] * terms[..., 1] * terms[..., 2]
+    cof = (trip * sgn).sum(-1).reshape(*m.shape[:-2], 4, 4)  # C_ij
     det = (m[..., 0, :] * cof[..., 0, :]).sum(-1)
     return cof.transpose(-1, -2) / det[..., None, None]
 
@@ -129,12 +137,11 @@ def Exp(r):
 
 
 def convert3x4_4x4(m):
-    if torch.is_tensor(m):
+    if torch.is_tensor(m):  # the [0, 0, 0, 1] row from torch.eye: no host scalar copy (graph-capturable)
+        row = torch.eye(4, dtype=m.dtype, device=m.device)[3:4]
         if m.dim() == 3:
-            out = torch.cat([m, torch.zeros_like(m[:, 0:1])], 1)
-            out[:, 3, 3] = 1.0
-            return out
-        return torch.cat([m, torch.tensor([[0, 0, 0, 1]], dtype=m.dtype, device=m.device)], 0)
+            return torch.cat([m, row.expand(m.shape[0], 1, 4)], 1)
+        return torch.cat([m, row], 0)
     if m.ndim == 3:
         out = np.concatenate([m, np.zeros_like(m[:, 0:1])], 1)
         out[:, 3, 3] = 1.0
@@ -167,4 +174,12 @@ class PoseRetriever(nn.Module):
         c2w = make_c2w(self.r[cam_id], self.t[cam_id])
         if self.init_c2w is not None:
             c2w = c2w @ self.init_c2w[cam_id]
+        return c2w
+
+    def pose_at(self, idx):
+        """forward() for a device index tensor [1]: gathers instead of int(cam_id), so
+        no host sync (graph-capturable); same arithmetic."""
+        c2w = make_c2w(self.r.index_select(0, idx)[0], self.t.index_select(0, idx)[0])
+        if self.init_c2w is not None:
+            c2w = c2w @ self.init_c2w.index_select(0, idx)[0]
         return c2w

@@ -294,3 +294,111 @@ def scene_flow_loss(pts, normals, sdf_flows, weights, omega, vel):
     sf = torch.cross(omega.reshape(1, 3).repeat(pts.shape[0], 1), pts, dim=-1) + vel.reshape(1, 3).repeat(pts.shape[0], 1)
     lhs = torch.sum(sf * n, dim=-1)
     return torch.sum(torch.abs(lhs + sdf_flows.reshape(-1)) * w) / (torch.sum(w) + 1e-10)
+
+
+# ---------------------------------------------------------------------------
+# stage 1: motion network poses, flow-RGB and SDF consistency (train.py:467-517)
+def euler_xyz(angles):
+    """pytorch3d euler_angles_to_matrix(..., 'XYZ') (utils_poses/pose_pytorch3d.py)."""
+    def axis(a, ang):
+        c, s = torch.cos(ang), torch.sin(ang)
+        o, z = torch.ones_like(ang), torch.zeros_like(ang)
+        rows = {"X": (o, z, z, z, c, -s, z, s, c), "Y": (c, z, s, z, o, z, -s, z, c),
+                "Z": (c, -s, z, s, c, z, z, z, o)}[a]
+        return torch.stack(rows, -1).reshape(ang.shape + (3, 3))
+    x, y, zz = torch.unbind(angles, -1)
+    return (axis("X", x) @ axis("Y", y)) @ axis("Z", zz)
+
+
+def consecutive_relative_pose(motion, cam, n_images, nb_sample_timestep):
+    """neus_fields.py:142-161, one interval cam -> cam + 1 (sequential Euler steps)."""
+    ref = cam + 1.0
+    t0 = cam / (n_images - 1) * 2 - 1
+    t1 = ref / (n_images - 1) * 2 - 1
+    n = int(nb_sample_timestep * (ref - cam))
+    steps = torch.linspace(t0, t1, n + 1)[:-1]
+    dt = steps[1] - steps[0]
+    R = torch.eye(3)
+    T = torch.zeros(3)
+    omega, vel = motion(steps.view(-1, 1))
+    R_list = euler_xyz(omega * dt)
+    V_list = vel * dt
+    for k in range(len(steps)):
+        T = R_list[k] @ T.view(3, 1) + V_list[k].view(3, 1)
+        R = R @ R_list[k]
+    pose = torch.eye(4)
+    pose[:3, :3] = R
+    pose[:3, -1] = T.view(1, 3)
+    return dt, pose
+
+
+def relative_camera_pose(motion, lo, hi, n_images, nb_sample_timestep):
+    """neus_fields.py:163-168 + compute_w2c_mappings 174-186: the w2c chain lo -> hi."""
+    w2c = [torch.eye(4)]
+    for cam in range(int(lo), int(hi)):
+        _, p = consecutive_relative_pose(motion, cam, n_images, nb_sample_timestep)
+        w2c.append(p @ w2c[-1])
+    return torch.stack(w2c)
+
+
+def stage1_losses(out, motion, sdf_fn, *, image_idx, n_images, world_cam_idx, nb_sample_timestep, rgb_gt,
+                  sampled_pixel, normalized_pixel, camera_mats, ref_images, scale_mat, img_hw,
+                  ref_intervals=(1, 2, 3)):
+    """(sdf_loss, flow_rgb_loss, sdf_consistency_loss) of one stage-1 iteration,
+    train.py:467-517 (query_in_canonical_space False).  motion(t [N,1]) -> (ω, v);
+    sdf_fn(x [M,4]) -> sdf [M,1]; camera_mats [n_images, 4, 4]; ref_images
+    [n_images, 3, H, W]; ref frames image_idx + ref_intervals (dataset.py:231-250)."""
+    R = rgb_gt.shape[0]
+    pts = out["sampled_points"].reshape(-1, 3)
+    normals = out["normals"].reshape(-1, 3)
+    sdf_flows = out["sdf_flows"].reshape(-1)
+    weights = out["weights"].reshape(-1)
+    time_step = image_idx / (n_images - 1) * 2 - 1
+    world_time_step = world_cam_idx / (n_images - 1) * 2 - 1
+    omega, vel = motion(torch.tensor([time_step]).float().view(-1, 1))
+    omega = omega.repeat(pts.shape[0], 1)
+    vel = vel.repeat(pts.shape[0], 1)
+    scene_flow = torch.cross(omega, pts, dim=-1) + vel
+    lhs = torch.sum(scene_flow * normals, dim=-1)
+    sdf_loss = torch.sum(torch.abs(lhs + sdf_flows) * weights.detach()) / (torch.sum(weights.detach()) + 1e-10)
+
+    ref_idx = [image_idx + k for k in ref_intervals]
+    next_t = [(r / (n_images - 1) * 2 - 1) for r in ref_idx]
+    nb_valid = len([t for t in next_t if t <= 1.0])
+    flow_rgb = torch.tensor(0.0)
+    consistency = torch.tensor(0.0)
+    w2c = relative_camera_pose(motion, image_idx, ref_idx[nb_valid - 1], n_images, nb_sample_timestep)
+    w2c = w2c[[r - image_idx for r in ref_idx][:nb_valid]]
+    flows = []
+    for t in range(len(w2c)):
+        ref_K = camera_mats[ref_idx[t]][None]
+        pts_map = (w2c[t, :3, :3] @ pts.T + w2c[t, :3, [-1]]).T
+        wp = torch.sum(weights.view(R, -1, 1) * pts_map.view(R, -1, 3), dim=1)
+        pix = (scale_mat[0, :3, :3] @ ref_K[0, :3, :3] @ wp.T).T
+        pix = pix[:, :2] / pix[:, [-1]]
+        f = pix - normalized_pixel
+        f = torch.stack([f[:, 0] * (img_hw[1] / 2), f[:, 1] * (img_hw[0] / 2)], -1)
+        flows.append(f)
+    if image_idx != world_cam_idx:
+        with torch.no_grad():  # sdf_consistency_enable_pose_grad: False (default.yaml:62)
+            lo, hi = min(world_cam_idx, image_idx), max(world_cam_idx, image_idx)
+            c2c = relative_camera_pose(motion, lo, hi, n_images, nb_sample_timestep)[-1]
+            cw2 = torch.inverse(c2c) if world_cam_idx <= image_idx else c2c
+            pts_world = (cw2[:3, :3] @ pts.T + cw2[:3, [-1]]).T
+        sdf_w = sdf_fn(torch.cat([pts_world, torch.ones_like(pts_world[:, [0]]) * world_time_step], dim=1))
+        consistency = torch.mean(torch.abs(sdf_w - out["sdf"].reshape(-1, 1)))
+    for t in range(nb_valid):
+        ref_img = ref_images[ref_idx[t]][None]
+        corr = sampled_pixel + flows[t]
+        with torch.no_grad():
+            valid = ((corr >= 0) & (corr < torch.tensor([ref_img.shape[3], ref_img.shape[2]]).float())).all(
+                dim=1, keepdim=True)
+        H, W = ref_img.shape[2], ref_img.shape[3]
+        gx = corr[:, 0] / ((W - 1) / 2) - 1
+        gy = corr[:, 1] / ((H - 1) / 2) - 1
+        grid = torch.stack([gx, gy], -1).view(1, R, 1, 2)
+        warped = F.grid_sample(ref_img, grid, mode="bilinear", padding_mode="border", align_corners=True)
+        warped = warped.squeeze().T
+        flow_rgb = flow_rgb + torch.sum(torch.abs(warped - rgb_gt) * valid) / (torch.sum(valid) + 1e-10)
+    flow_rgb = flow_rgb / 3.0
+    return sdf_loss, flow_rgb, consistency

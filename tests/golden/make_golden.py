@@ -304,9 +304,109 @@ def motion_case(fields):
     print("wrote motion")
 
 
+def load_reference_trainer():
+    """model/common.py and model/poses_retriever.py loaded by path, and the methods of
+    model.training.Trainer that train.py calls per iteration (training.py:101-124,
+    377-558) executed from the reference's own source text: training.py itself cannot
+    be imported here (cv2 / imageio / torchvision are absent), so its
+    class body is parsed and only the listed methods are compiled, unmodified, in a
+    namespace holding the names they use (torch, np, F, the common.py functions)."""
+    import ast
+    load_reference()
+
+    def load(modname, rel):
+        spec = importlib.util.spec_from_file_location(modname, os.path.join(REF, rel))
+        mod = importlib.util.module_from_spec(spec)
+        sys.modules[modname] = mod
+        spec.loader.exec_module(mod)
+        return mod
+
+    common = load("model.common", "model/common.py")
+    poses = load("model.poses_retriever", "model/poses_retriever.py")
+    src = open(os.path.join(REF, "model", "training.py")).read()
+    tree = ast.parse(src)
+    cls = next(n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == "Trainer")
+    keep = {"__init__", "near_far_from_sphere", "get_cos_anneal_ratio", "get_patch_indices", "process_data_dict",
+            "process_data_reference", "process_data", "get_world_cameraOrigin_cameraRay", "compute_loss",
+            "backpropagation", "anneal"}
+    cls.body = [f for f in cls.body if isinstance(f, ast.FunctionDef) and f.name in keep]
+    mod = ast.Module(body=[cls], type_ignores=[])
+    ns = {"torch": torch, "np": np, "F": torch.nn.functional, "arange_pixels": common.arange_pixels,
+          "origin_to_world": common.origin_to_world, "image_points_to_world": common.image_points_to_world,
+          "transform_to_world": common.transform_to_world}
+    exec(compile(mod, os.path.join(REF, "model", "training.py"), "exec"), ns)
+    return common, poses, ns["Trainer"]
+
+
+def trainer_case():
+    """Rows a1-a5 of SURVEY.md §8 and the Trainer API from the reference's own code:
+    arange_pixels, Exp / make_c2w, PoseRetriever (forward + gradients), the patch ids of
+    a seeded get_patch_indices, process_data's rays for a posed camera, near / far,
+    cos_anneal_ratio and compute_loss."""
+    common, poses, RefTrainer = load_reference_trainer()
+    rec = {}
+    h, w = 12, 16
+    p, pn = common.arange_pixels((h, w), 1)
+    rec["arange_p"], rec["arange_pn"] = p, pn
+    g = torch.Generator().manual_seed(31)
+    rs = torch.cat([torch.zeros(1, 3), (torch.rand(4, 3, generator=g) - 0.5) * 0.6])
+    ts = (torch.rand(5, 3, generator=g) - 0.5)
+    rec["exp_r"], rec["exp_t"] = rs, ts
+    rec["exp_R"] = torch.stack([common.Exp(r) for r in rs])
+    rec["c2w"] = torch.stack([common.make_c2w(r, t) for r, t in zip(rs, ts)])
+    pr = poses.PoseRetriever(5)
+    with torch.no_grad():
+        pr.r.copy_(rs)
+        pr.t.copy_(ts)
+    mats = torch.stack([pr(i) for i in range(5)])
+    G = torch.randn(5, 4, 4, generator=g)
+    gr, gt = torch.autograd.grad((mats * G).sum(), [pr.r, pr.t])
+    rec.update({"pose_mats": mats.detach(), "pose_G": G, "pose_dr": gr, "pose_dt": gt})
+    # the Trainer: cfg as default.yaml's training section (n_training_points = 64 here)
+    cfg = dict(n_training_points=64, rgb_weight=[1.0, 1.0], eikonal_weight=[0.1, 0.1], sdf_weight=[0.1, 0.1],
+               flow_rgb_weight=[7.5, 7.5], sdf_consistency_weight=[0.0, 1.0],
+               edge_aware_smoothness_weight=[1.0, 0.0], smoothness_weight=[1e-4, 0.0])
+    cfg_all = {"rendering": {"depth_range": [0.01, 5.0]}}
+    tr = RefTrainer(None, None, None, cfg, device=torch.device("cpu"), total_nb_images=5, cfg_all=cfg_all,
+                    logger=None, gt_depths=None, world_cam_idx=2, train_dataset=None)
+    torch.manual_seed(5)
+    rec["patch_idx"] = tr.get_patch_indices(h, w, 4, 64)
+    rec["patch_seed"] = np.int32(5)
+    img = torch.rand(1, 3, h, w, generator=g)
+    fx = 0.9 * w
+    K = torch.tensor([[[2 * fx / w, 0, 0, 0], [0, -2 * fx / h, 0, 0], [0, 0, -1, 0], [0, 0, 0, 1]]])
+    scale = torch.eye(4)[None].clone()
+    scale[0, 0, 0] = scale[0, 1, 1] = scale[0, 2, 2] = 1.25  # a non-trivial scale_mat
+    data = {"img": img, "img.camera_mat": K, "img.scale_mat": scale, "img.idx": torch.tensor([3]),
+            "img.ref_imgs": img.clone(), "img.ref_idxs": [torch.tensor([4])]}
+    world_mat = pr(3).detach()
+    torch.manual_seed(6)
+    out = tr.process_data(data, world_mat, it=1, epoch=0, patch_size=4)
+    names = ("img", "ref_img", "p", "pn", "rays_o", "rays_d", "rays_d_norm", "rgb_gt", "camera_mat", "scale_mat")
+    for n, v in zip(names, out):
+        rec["pd_" + n] = v
+    rec["pd_seed"] = np.int32(6)
+    rec["pd_world_mat"] = world_mat
+    near, far = tr.near_far_from_sphere(out[4], out[5])
+    rec["near"], rec["far"] = near, far
+    rec["car_its"] = np.array([0, 1000, 25000, 50000, 80000], np.int64)
+    rec["car"] = np.array([tr.get_cos_anneal_ratio(i, 50000) for i in rec["car_its"]], np.float64)
+    # compute_loss on fixed terms
+    rr = torch.rand(64, 3, generator=g)
+    terms = torch.rand(6, generator=g)  # gradient, sdf, flow_rgb, sdf_consistency, edge-aware, smoothness
+    d = tr.compute_loss(data, rr, out[7], *terms.unbind(0))
+    rec["cl_rgb"], rec["cl_terms"] = rr, terms
+    for k in ("loss", "loss_rgb", "l2_mean"):
+        rec["cl_" + k] = d[k].detach()
+    np.savez_compressed(os.path.join(OUT, "trainer.npz"),
+                        **{k: (v.detach().numpy() if torch.is_tensor(v) else v) for k, v in rec.items()})
+    print("wrote trainer")
+
+
 def main():
     fields, rend = load_reference()
     motion_case(fields)
+    trainer_case()
     torch.set_num_threads(8)
     render_case(fields, rend, "render_small_train", seed=678, R=16, dh_sdf=64, dh_col=64, eval_mode=False,
                 car=0.5, full_grads=True)
@@ -330,7 +430,9 @@ def main_pretrained_only():
 
 
 if __name__ == "__main__":
-    if "--motion-only" in sys.argv:
+    if "--trainer-only" in sys.argv:
+        trainer_case()
+    elif "--motion-only" in sys.argv:
         main_motion_only()
     elif "--pretrained-only" in sys.argv:
         main_pretrained_only()

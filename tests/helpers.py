@@ -86,3 +86,18 @@ def load_pretrained_sdf(sdf, fx):
     sd = {k[5:]: v for k, v in fx.items() if k.startswith("sdfw.")}
     sdf.load_state_dict({k: v.to(next(sdf.parameters()).device) for k, v in sd.items()}, strict=True)
     return sdf
+
+
+def smooth_frames(n, H, W, device="cpu", seed=0):
+    """n smooth (low-frequency) RGB frames in (0.1, 0.9): bilinear warps of them have a
+    gradient that varies slowly across pixel boundaries, so the flow-RGB term
+    (train.py:506-515, grid_sample) is well conditioned for gradient parity; on
+    per-pixel noise a last-ulp change of a flow can cross a pixel edge and flip the
+    warp's gradient (the bilinear derivative jumps there)."""
+    g = torch.Generator().manual_seed(seed)
+    f = torch.rand(n, 3, 2, generator=g) * 2.0 + 0.5     # cycles per frame
+    ph = torch.rand(n, 3, generator=g) * 6.28
+    y = torch.linspace(0, 1, H).view(1, 1, H, 1)
+    x = torch.linspace(0, 1, W).view(1, 1, 1, W)
+    arg = 6.2831853 * (f[..., 0, None, None] * x + f[..., 1, None, None] * y) + ph[..., None, None]
+    return (0.5 + 0.4 * torch.sin(arg)).float().to(device)

@@ -1,0 +1,80 @@
+"""Data parallel on the HIP path: 2 processes, each running the HIP
+renderer on cuda:0 on its half of the patches of one batch, with joint pose and
+the stage-1 losses on -- their global normalisers (Σw of the scene-flow loss,
+Σvalid of flow-RGB) all-reduced before the divide -- and the HIP gradients
+exchanged by train_step.flat_allreduce_mean (gloo here; RCCL on the bench).
+Every rank must end with the single-process full-batch gradient."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+KW = dict(H=48, W=64, seed=21, joint_pose=True, stage1=True, n_images=6, start_it=30001, schedule="reference",
+          mfma_dtype="bf16x6", depth_range=(0.01, 3.0))
+R = 256  # 16 patches of 4x4
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _grads(tr):
+    return {n: p.grad.detach().cpu().numpy().copy() for n, p in
+            [("p%d" % i, p) for i, p in enumerate(tr.all_params)] if p.grad is not None}
+
+
+def _worker(rank, world, port, batch, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "cope-nerf_amd"), root, os.path.join(root, "tests")]
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    from copenerf.train_step import SyntheticTrainer
+    from helpers import smooth_frames
+    tr = SyntheticTrainer("cuda:0", rays=R // world, distributed=True, **KW)
+    tr.images = smooth_frames(KW["n_images"], KW["H"], KW["W"], "cuda:0")
+    tr.begin_iteration()
+    n = R // world
+    part = {k: torch.from_numpy(v[rank * n:(rank + 1) * n]).to("cuda:0") for k, v in batch.items()}
+    # this rank's rays from its own copy of the poses (their gradients are exchanged too)
+    loss = tr.iteration(tr.batch_from_pixels(part["pix"], part["pixn"], part["t_rand"]))
+    q.put((rank, _grads(tr), float(loss.item())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_hip_data_parallel_equals_full_batch(world):
+    from copenerf.train_step import SyntheticTrainer
+    from helpers import smooth_frames
+    ref = SyntheticTrainer("cuda:0", rays=R, **KW)
+    ref.images = smooth_frames(KW["n_images"], KW["H"], KW["W"], "cuda:0")
+    ref.begin_iteration()
+    batch = ref.make_batch()
+    batch_np = {k: batch[k].detach().cpu().numpy() for k in ("pix", "pixn", "t_rand")}
+    ref.iteration(batch)
+    gref = _grads(ref)
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, batch_np, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, g) for r, g, _ in (q.get(timeout=300) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert set(res[0]) == set(gref)
+    for name, g in gref.items():
+        scale = np.abs(g).max() + 1e-20
+        for r in range(world):
+            err = np.abs(res[r][name] - g).max()
+            assert err <= 1e-5 * scale, (name, r, err, scale)

@@ -184,15 +184,18 @@ def test_render_configs_c5_c1(n_samples, n_importance):
     assert (err > TOL_RGB_DEPTH).float().mean().item() <= 0.01
 
 
-def test_render_pretrained_sdf_matches_reference():
+@pytest.mark.parametrize("mode", FP32_MODES)
+def test_render_pretrained_sdf_matches_reference(mode):
     """The reference's trained SDF (pretrained_sdf/model.pt via the fixture): strict
-    |Δ rgb|, |Δ depth| <= 1e-4 on the reference's own sample positions, the
-    end-to-end path within the sampler-flip statistics, and the loss gradients."""
+    |Δ rgb|, |Δ depth| <= 1e-4 on the reference's own sample positions, the loss
+    gradients there within 2e-3 of each gradient's scale (the field-level bar:
+    identical samples leave no sampler flip to hide behind), and the end-to-end path
+    within the sampler-flip statistics."""
     from helpers import load_pretrained_sdf
     fx = fixture("render_pretrained")
     mods = build_modules(int(fx["seed"]), device=DEV)
     load_pretrained_sdf(mods[0], fx)
-    r = _renderer(mods)
+    r = _renderer(mods, mode)
     g = lambda k: fx[k].to(DEV)  # noqa: E731
     args = (g("rays_o"), g("rays_d"), g("rays_d_norm"), g("t"), g("near"), g("far"))
     out = r(*args, cos_anneal_ratio=float(fx["car"]), it=0, eval=False, z_vals=g("z_vals"))
@@ -204,7 +207,7 @@ def test_render_pretrained_sdf_matches_reference():
     params = named_params(*mods)
     grads = torch.autograd.grad(loss, [p for _, p in params])
     for (n, _), gr in zip(params, grads):
-        check_grad(n, gr, fx, rtol=2e-2, atol=2e-4 * (gr.abs().max().item() + 1e-3))
+        check_grad(n, gr, fx, rtol=2e-3, atol=2e-3 * (gr.abs().max().item() + 1e-6))
     out = r(*args, cos_anneal_ratio=float(fx["car"]), it=0, eval=False, t_rand=g("t_rand"))
     err = torch.maximum((out["depth_pred"].detach().cpu() - fx["out_depth_pred"]).abs().squeeze(1),
                         (out["color_fine"].detach().cpu() - fx["out_color_fine"]).abs().max(1)[0])
