@@ -206,11 +206,13 @@ def sdf_input_grad(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat):
     if dsdf is None and dfeat is None:
         return dx.zero_()
     dsdf_flat = None if dsdf is None else dsdf.reshape(M, 1).contiguous()
-    phi = dfeat if dfeat is not None else torch.zeros(M, lay.H_feat, device=dev)
     P = _empty(M, HL, dev)
-    ops.linear(phi, pk.Bt8, lay.out_dim[L8 - 1], rup(lay.H_feat, 32), P, EPI_BWD_SOFTPLUS,
-               rowv=dsdf_flat, colv=pk.w80p if dsdf_flat is not None else None, aux0=U[L8],
-               aux_beta=sig_beta(lay, L8 - 1), nzero=HL)
+    if dfeat is None:  # sdf only: P_7 = dsdf[m] w80[n] σ_7 -- elementwise, no GEMM over a zero operand
+        ops.scale_cols(U[L8], HL, pk.w80p, P, act_beta=sig_beta(lay, L8 - 1), rowv=dsdf_flat)
+    else:
+        ops.linear(dfeat, pk.Bt8, lay.out_dim[L8 - 1], rup(lay.H_feat, 32), P, EPI_BWD_SOFTPLUS,
+                   rowv=dsdf_flat, colv=pk.w80p if dsdf_flat is not None else None, aux0=U[L8],
+                   aux_beta=sig_beta(lay, L8 - 1), nzero=HL)
     PE = _empty(M, KE, dev) if sk >= 0 else None
     for l in range(L8 - 1, 0, -1):
         Kl = rup(lay.out_dim[l], 32)
@@ -295,11 +297,16 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG):
             return {}
         return dict(aux1=S[l], aux2=Ud[l + 1], aux2_scale=lay.beta * (SQRT2 if (l + 1) == sk else 1.0))
 
-    phi = dfeat if dfeat is not None else torch.zeros(M, lay.H_feat, device=dev)
     Z = _empty(M, HL, dev)
-    ops.linear(phi, pk.Bt8, lay.out_dim[L8 - 1], rup(lay.H_feat, 32), Z, EPI_BWD_SOFTPLUS,
-               rowv=dsdf_flat, colv=pk.w80p if dsdf_flat is not None else None, aux0=U[L8],
-               aux_beta=sig_beta(lay, L8 - 1), nzero=HL, **second_order(L8 - 1))
+    if dfeat is None and not second and dsdf_flat is not None:
+        # sdf only, first order (e.g. SDFNetwork.sdf at train.py:504): Z_7 = dsdf[m] w80[n] σ_7,
+        # elementwise -- no GEMM over a zero feature gradient
+        ops.scale_cols(U[L8], HL, pk.w80p, Z, act_beta=sig_beta(lay, L8 - 1), rowv=dsdf_flat)
+    else:
+        phi = dfeat if dfeat is not None else torch.zeros(M, lay.H_feat, device=dev)
+        ops.linear(phi, pk.Bt8, lay.out_dim[L8 - 1], rup(lay.H_feat, 32), Z, EPI_BWD_SOFTPLUS,
+                   rowv=dsdf_flat, colv=pk.w80p if dsdf_flat is not None else None, aux0=U[L8],
+                   aux_beta=sig_beta(lay, L8 - 1), nzero=HL, **second_order(L8 - 1))
     dWs, dbs = [None] * nl, [None] * nl
     dWs[L8], dbs[L8] = dW8, db8
     for l in range(L8 - 1, -1, -1):

@@ -239,21 +239,33 @@ def project_flow(pts, weights, w2c, ref_camera_mat, scale_mat, normalized_pixels
     """Forward optical flow to reference frames (train.py:484-495): the
     weight-averaged sample point of each ray, mapped by the relative pose w2c
     [T, 4, 4] (or [4, 4]) and projected with the reference cameras ref_camera_mat
-    [T, 4, 4] (or [1, 4, 4]); returns pixel offsets [T, R, 2] (or [R, 2])."""
+    [T, 4, 4] (or [1, 4, 4]); returns pixel offsets [T, R, 2] (or [R, 2]).
+    The reference maps every sample and then averages; by linearity
+    Σ_s w (R p + t) = R (Σ_s w p) + (Σ_s w) t, so the per-ray sums are formed once
+    and each frame costs O(R), not O(R·S) (no [T, R·S, 3] intermediate)."""
     single = w2c.dim() == 2
     if single:
         w2c, ref_camera_mat = w2c[None], ref_camera_mat.reshape(1, 4, 4)
     R = normalized_pixels.shape[0]
-    P = pts.reshape(R, -1, 3)
-    pts_map = torch.einsum("tij,rsj->trsi", w2c[:, :3, :3], P) + w2c[:, None, None, :3, 3]
-    wp = torch.sum(weights.reshape(1, R, -1, 1) * pts_map, dim=2)  # [T, R, 3]
+    w = weights.reshape(R, -1, 1)
+    pbar = torch.sum(w * pts.reshape(R, -1, 3), dim=1)   # [R, 3]
+    wbar = torch.sum(w, dim=1)                           # [R, 1]
+    wp = torch.einsum("tij,rj->tri", w2c[:, :3, :3], pbar) + wbar[None] * w2c[:, None, :3, 3]  # [T, R, 3]
     KS = scale_mat.reshape(-1, 4, 4)[0, :3, :3] @ ref_camera_mat[:, :3, :3]  # [T, 3, 3]
     pix = torch.einsum("tij,trj->tri", KS, wp)
     pix = pix[..., :2] / pix[..., 2:3]
     flow = pix - normalized_pixels
-    h, w = img_hw
-    flow = torch.stack([flow[..., 0] * (w / 2), flow[..., 1] * (h / 2)], -1)
+    h, w_ = img_hw
+    flow = torch.stack([flow[..., 0] * (w_ / 2), flow[..., 1] * (h / 2)], -1)
     return flow[0] if single else flow
+
+
+def affine_points(pts, m):
+    """(m[:3, :3] @ pts.T + m[:3, 3:]).T for pts [N, 3] as three fused multiply-adds over
+    the rows (a [3, 3] x [3, N] matrix product is a skinny GEMM; this is a stream)."""
+    out = torch.addcmul(m[:3, 3], pts[:, 0:1], m[:3, 0])
+    out = torch.addcmul(out, pts[:, 1:2], m[:3, 1])
+    return torch.addcmul(out, pts[:, 2:3], m[:3, 2])
 
 
 def warp_pixel(src_frame, uv, normalize_pix=True):
@@ -292,4 +304,4 @@ def flow_rgb_loss(flow_fw, sampled_pixel, ref_img, rgb_gt, group=None):
 def world_points(pts, cw2):
     """Sample points mapped into the world (canonical) frame for the SDF
     consistency re-query (train.py:497-505)."""
-    return (cw2[:3, :3] @ pts.reshape(-1, 3).T + cw2[:3, [-1]]).T
+    return affine_points(pts.reshape(-1, 3), cw2)

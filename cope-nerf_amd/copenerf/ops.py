@@ -280,12 +280,15 @@ def row_head(A, K, W, b, C, act, out, dst_index=None, ld_out=None):
     return out
 
 
-def scale_cols(X, N, w, out, act_beta=0.0):
-    """out = X * w (act_beta 0) or (1 - exp(-act_beta X)) * w: softplus' of stored activations."""
+def scale_cols(X, N, w, out, act_beta=0.0, rowv=None):
+    """out = f(X) * w (* rowv[m]); f(X) = X (act_beta 0) or 1 - exp(-act_beta X): softplus'
+    of stored activations."""
     _need(X, "X")
     _need(out, "out")
-    _lib.call("cn_scale_cols", X.shape[0], N, _ptr(X), _ld(X), _ptr(w), _ptr(out), _ld(out), float(act_beta),
-              _stream())
+    if rowv is not None and (not rowv.is_contiguous() or rowv.numel() != X.shape[0]):
+        raise RuntimeError("scale_cols: rowv must be a contiguous [M] tensor")
+    _lib.call("cn_scale_cols", X.shape[0], N, _ptr(X), _ld(X), _ptr(w), _ptr(rowv), _ptr(out), _ld(out),
+              float(act_beta), _stream())
     return out
 
 

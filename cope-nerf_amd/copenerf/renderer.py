@@ -108,6 +108,11 @@ class NeuSRenderer(nn.Module):
             raise NotImplementedError("n_outside > 0 (NeRF++ background) is out of scope; every config uses 0")
         if naive_render:
             raise NotImplementedError("naive_render (logistic up-sampler) is out of scope; every config uses False")
+        # opt-in: keep forward()'s SDF weight images (effective weights + packed GEMM images)
+        # in last_sdf_pack for a second SDF query of the same step; the caller must clear it
+        # (it holds the step's autograd graph)
+        self.expose_sdf_pack = False
+        self.last_sdf_pack = None
 
     def set_mfma_dtype(self, dtype: str):
         """"fp32" (default: exact fp32 MFMA products, the |Δ| <= 1e-4 parity path),
@@ -179,6 +184,7 @@ class NeuSRenderer(nn.Module):
 
         sdf_packed = self.sdf_network.params_and_pack()
         col_packed = self.color_network.params_and_pack()
+        self.last_sdf_pack = sdf_packed if self.expose_sdf_pack else None
         if z_vals is None:
             z = self.sample_z(rays_o, rays_d, time_step, near, far, n_samples, n_importance, t_rand, sdf_packed)
         else:

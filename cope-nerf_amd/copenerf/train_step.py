@@ -41,7 +41,7 @@ import torch.distributed as dist
 
 from .fields import RenderingNetwork, SDFNetwork, SingleVarianceNetwork
 from .losses import EdgePreservingSmoothnessLoss, SmoothnessLoss, eikonal_loss, rgb_l1, train_losses
-from .motion import MotionNetwork, flow_rgb_loss, masked_chain, project_flow, scene_flow_loss
+from .motion import MotionNetwork, affine_points, flow_rgb_loss, masked_chain, project_flow, scene_flow_loss
 from .rays import PoseRetriever, get_patch_indices, intrinsics_ndc, inv4x4, pixels_from_indices, world_rays
 from .renderer import NeuSRenderer
 
@@ -166,6 +166,7 @@ class SyntheticTrainer:
         self.var = SingleVarianceNetwork(0.3).to(self.device)
         self.renderer = NeuSRenderer(None, self.sdf, self.var, self.col, None, **(ren_cfg or REN_CFG)).to(self.device)
         self.renderer.set_mfma_dtype(mfma_dtype)
+        self.renderer.expose_sdf_pack = stage1  # the stage-1 SDF re-query reuses the step's weight images
         self.params = list(self.sdf.parameters()) + list(self.var.parameters()) + list(self.col.parameters())
         self.joint_pose, self.stage1 = joint_pose, stage1
         self.n_images = n_images
@@ -317,10 +318,11 @@ class SyntheticTrainer:
             lo, hi = torch.clamp(img, max=w), torch.clamp(img, min=w)
             c2c = masked_chain(P.detach(), lo, hi)
             cw2 = torch.where(img.view(1, 1) >= w, inv4x4(c2c), c2c)
-            pts = out["sampled_points"].detach().reshape(-1, 3)
-            pw = (cw2[:3, :3] @ pts.T + cw2[:3, 3:]).T
+            pw = affine_points(out["sampled_points"].detach().reshape(-1, 3), cw2)
             x = torch.cat([pw, torch.full_like(pw[:, :1], self.world_time_step)], 1)
-        sdf_w = self.sdf.sdf(x)
+        # SDFNetwork.sdf (train.py:504) on the weights the renderer packed for this step
+        pack, self.renderer.last_sdf_pack = self.renderer.last_sdf_pack, None
+        sdf_w = self.sdf.field(x, want_feat=False, want_grad=False, packed=pack)[0]
         cons = torch.mean(torch.abs(sdf_w - out["sdf"].reshape(-1, 1))) * (img != w).float().view(())
         return sdf_loss, flow_rgb, cons
 

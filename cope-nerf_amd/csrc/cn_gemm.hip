@@ -43,6 +43,7 @@ struct LinearArgs {
     float inv_adiv, inv_odiv, beta, threshold;
     float aux_c;       // -aux_beta * log2(e): sigma = 1 - 2^(aux_c * aux0)
     float aux2_scale;  // BWD_SOFTPLUS second-order term scale
+    int stagger;       // odd workgroups start this many s_sleep(127) later (epilogue / main-loop desync)
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -171,6 +172,9 @@ __device__ __forceinline__ void tile_coords(int vt, int T, int& tm, int& tn) {
 // The accumulator layout of the two MFMAs is the same, so the epilogue is shared.
 #ifndef X6_EXP
 #define X6_EXP 0  // benchmark-only ablations of the bf16x6 main loop (tools/x6_ablation.sh)
+#endif
+#ifndef LSTORE_ALWAYS
+#define LSTORE_ALWAYS 0  // 1: branch-free staging (measured: main loop -1.5 %, epilogue variants +2-3 %)
 #endif
 template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int EPI, bool ROWV, int MODE>
 __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel(LinearArgs p) {
@@ -343,6 +347,10 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 
     int vt = next_valid(blockIdx.x);
     if (vt >= ntiles) return;
+    // stagger: with 2 workgroups per CU, the second resident one (block ids past the first
+    // gridDim / 2 fill the CUs' second slots) starts later; with 1 per CU, the odd ones
+    if (OCC >= 2 ? (blockIdx.x >= gridDim.x / 2) : (blockIdx.x & 1))
+        for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
     int tm, tn;
     tile_coords(vt, T, tm, tn);
     gload(0, 0, tm * BM, tn * BN, true);
@@ -454,7 +462,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 const bool more = kc + 1 < nk;
                 gload(0, more ? kc + 1 : 0, more ? m0 : m_next, more ? n0 : n_next, more || has_next);
                 compute(cur);
-                if (more) lstore(0, cur ^ 1);
+                if (LSTORE_ALWAYS || more) lstore(0, cur ^ 1);
                 __syncthreads();
             }
         } else {
@@ -469,7 +477,12 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                     const bool here = cn < nk;
                     gload(j, here ? cn : 0, here ? m0 : m_next, here ? n0 : n_next, here || (cn == nk && has_next));
                     compute(j & 1);
-                    if (kc + j + 1 < nk) lstore((j + 1) % DEPTH, (j + 1) & 1);
+                    // unconditional (branch-free: compute and the next stage's staging share a
+                    // basic block, so the scheduler can interleave the split VALU / LDS writes
+                    // with the MFMAs).  After the last chunk this stages the next tile's first
+                    // chunk (or zeros) into the free buffer: harmless, the epilogue parks over it
+                    // and the next tile stages it again.
+                    if (LSTORE_ALWAYS || kc + j + 1 < nk) lstore((j + 1) % DEPTH, (j + 1) & 1);
                     __syncthreads();
                 }
             }
@@ -1217,8 +1230,8 @@ __global__ void __launch_bounds__(256) row_head_kernel(int M, int K, const float
 // out[m][n] = X[m][n] * w[n], float4-vectorized (N, the leading dimensions and
 // the pointers are multiples of 4 floats / 16-byte aligned: checked by the host).
 __global__ void __launch_bounds__(256) scale_cols_kernel(int M, int N4, const float* __restrict__ X, int64_t ldx,
-                                                         const float* __restrict__ w, float* out, int64_t ldo,
-                                                         float aux_c) {
+                                                         const float* __restrict__ w, const float* __restrict__ rowv,
+                                                         float* out, int64_t ldo, float aux_c) {
     const int64_t tot = (int64_t)M * N4;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += stride) {
@@ -1228,7 +1241,9 @@ __global__ void __launch_bounds__(256) scale_cols_kernel(int M, int N4, const fl
         const floatx4 s = *reinterpret_cast<const floatx4*>(w + n);
         if (aux_c != 0.0f)  // X holds softplus outputs: scale softplus' = 1 - exp(-beta X)
             for (int e = 0; e < 4; ++e) x[e] = sigma_from_act(x[e], aux_c);
-        *reinterpret_cast<floatx4*>(out + m * ldo + n) = x * s;
+        floatx4 y = x * s;
+        if (rowv) y = y * rowv[m];
+        *reinterpret_cast<floatx4*>(out + m * ldo + n) = y;
     }
 }
 
@@ -1390,6 +1405,10 @@ static int g_linear_variant = [] {
 // bf16x6 epilogues that run on the 256x128 one-workgroup-per-CU tile (bit e = cn_epilogue e;
 // benchmarking aid: COPENERF_WIDE_EPIS).  Default: the epilogues that read at most one aux
 // stream (STORE, SOFTPLUS, RELU, MUL, TANGENT).
+static int g_stagger = [] {  // benchmarking aid: COPENERF_STAGGER (units of s_sleep 127 = 8128 cycles)
+    const char* e = getenv("COPENERF_STAGGER");
+    return e ? atoi(e) : 0;
+}();
 static int g_wide_epis = [] {
     const char* e = getenv("COPENERF_WIDE_EPIS");
     return e ? (int)strtol(e, nullptr, 0) : 0x1f;
@@ -1494,6 +1513,7 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     a.ld_aux0 = (int)d->ld_aux0; a.ld_aux1 = (int)d->ld_aux1; a.ld_aux2 = (int)d->ld_aux2;
     a.aux_c = -d->aux_beta * 1.44269504088896341f;
     a.aux2_scale = d->aux2_scale;
+    a.stagger = g_stagger;
     a.ld_out0 = (int)d->ld_out0; a.ld_out1 = (int)d->ld_out1; a.ld_split = (int)d->ld_split;
     a.M = d->M; a.N = d->N; a.K = d->K; a.K1 = K1; a.nzero = nzero;
     a.nsplit = (e == CN_EPI_MUL && d->out_split) ? d->nsplit : d->N;
@@ -1617,8 +1637,8 @@ extern "C" int cn_row_head(int32_t M, int32_t K, const float* A, int64_t lda, co
     return check_launch("cn_row_head");
 }
 
-extern "C" int cn_scale_cols(int32_t M, int32_t N, const float* X, int64_t ldx, const float* w, float* out,
-                             int64_t ld_out, float act_beta, cn_stream_t stream) {
+extern "C" int cn_scale_cols(int32_t M, int32_t N, const float* X, int64_t ldx, const float* w, const float* rowv,
+                             float* out, int64_t ld_out, float act_beta, cn_stream_t stream) {
     CN_REQUIRE(act_beta >= 0.0f, CN_ERR_ARG, "cn_scale_cols: act_beta must be >= 0");
     CN_REQUIRE(X && w && out, CN_ERR_ARG, "cn_scale_cols: null pointer");
     CN_REQUIRE(N % 4 == 0 && ldx % 4 == 0 && ld_out % 4 == 0 && al16(X) && al16(w) && al16(out), CN_ERR_ALIGN,
@@ -1626,7 +1646,7 @@ extern "C" int cn_scale_cols(int32_t M, int32_t N, const float* X, int64_t ldx, 
     if ((int64_t)M * N == 0) return CN_OK;
     const int64_t tot = (int64_t)M * (N / 4);
     const int blocks = (int)std::min<int64_t>((tot + 255) / 256, 8192);
-    scale_cols_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(M, N / 4, X, ldx, w, out, ld_out,
+    scale_cols_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(M, N / 4, X, ldx, w, rowv, out, ld_out,
                                                                -act_beta * 1.44269504088896341f);
     return check_launch("cn_scale_cols");
 }

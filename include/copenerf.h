@@ -188,10 +188,12 @@ size_t cn_colsum_workspace_bytes(int32_t M, int32_t K);
 int cn_colsum(int32_t M, int32_t K, const float* w, const float* X, int64_t ldx, float wdiv, float* out,
               int32_t accumulate, float* workspace, int64_t workspace_bytes, cn_stream_t stream);
 
-/* out[m][n] = f(X[m][n]) * w[n] for n < N (seed of the ∇ₓSDF pass, neus_fields.py:295-302):
+/* out[m][n] = f(X[m][n]) * w[n] (* rowv[m] when rowv != NULL) for n < N: the seed of the
+ * ∇ₓSDF pass (neus_fields.py:295-302), and the sdf-only adjoint of the last hidden layer
+ * (d sdf / d z_7 = dsdf[m] w80[n] softplus'(z_7), no feature gradient: no GEMM needed);
  * f(x) = x when act_beta == 0, else softplus' from the softplus output, 1 - exp(-act_beta x). */
-int cn_scale_cols(int32_t M, int32_t N, const float* X, int64_t ldx, const float* w, float* out,
-                  int64_t ld_out, float act_beta, cn_stream_t stream);
+int cn_scale_cols(int32_t M, int32_t N, const float* X, int64_t ldx, const float* w, const float* rowv,
+                  float* out, int64_t ld_out, float act_beta, cn_stream_t stream);
 
 /* ------------------------------------------------------------------------ *
  * Positional encoding of the SDF input (neus_embedder.py:6-51 with

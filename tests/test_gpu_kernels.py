@@ -161,6 +161,9 @@ def test_row_head_colsum_scale_cols():
     act = _act(M, K, 25)
     ops.scale_cols(act, K, W[0].contiguous(), sc, act_beta=100.0)
     torch.testing.assert_close(sc, (_sg(act, 100.0) * W[0].double()).float(), rtol=1e-5, atol=1e-7)
+    ops.scale_cols(act, K, W[0].contiguous(), sc, act_beta=100.0, rowv=w)
+    torch.testing.assert_close(sc, (_sg(act, 100.0) * W[0].double() * w.double()[:, None]).float(), rtol=1e-5,
+                               atol=1e-7)
 
 
 def test_c_abi_rejects_bad_arguments():
