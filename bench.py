@@ -55,7 +55,9 @@ SAMPLES = 128
 GFLOP_PER_RAY_REF = 1.4809  # reference GEMM FLOPs per ray per train step (64+4x16)
 
 
-# cn_linear's bf16x6 epilogues on the 256x128 tile (cn_gemm.hip g_wide_epis, default 0x1f)
+# cn_linear's bf16x6 epilogues on the 128x256 tile (cn_gemm.hip g_x6_tall, default 0x18) and on
+# the 256x128 tile (g_wide_epis, default 0x1f); the rest on 128x128
+TALL_EPIS = int(os.environ.get("COPENERF_X6_TALL", "0x18"), 0)
 WIDE_EPIS = int(os.environ.get("COPENERF_WIDE_EPIS", "0x1f"), 0)
 EPI_ID = {"store": 0, "softplus": 1, "relu": 2, "mul": 3, "tangent": 4, "bwd_softplus": 5, "bwd_relu": 6}
 
@@ -69,10 +71,12 @@ def kernel_symbol(key):
     WIDE_EPIS at K % 64 == 0 (every such K on C2), else 128x128, BK 16, 2-deep."""
     if key[0] == "linear":
         epi = EPI_ID[key[2]]
-        wide = "x6" in key[3:] and key[1] == 0 and (WIDE_EPIS >> epi) & 1
-        tiles = {0: "4, 2, 2, 2" if wide else "2, 2, 2, 2", 1: "4, 1, 1, 2"}
+        x6 = "x6" in key[3:] and key[1] == 0
+        tall = x6 and (TALL_EPIS >> epi) & 1  # N = 256 on every C2 call of these epilogues
+        wide = x6 and not tall and (WIDE_EPIS >> epi) & 1
+        tiles = {0: "4, 2, 1, 4" if tall else "4, 2, 2, 2" if wide else "2, 2, 2, 2", 1: "4, 1, 1, 2"}
         mode = 1 if "bf16" in key[3:] else 2 if "x6" in key[3:] else 0
-        mid = {0: "32, 2, 2", 1: "64, 2, 1", 2: "32, 1, 2" if wide else "16, 2, 2"}[mode]
+        mid = {0: "32, 2, 2", 1: "64, 2, 1", 2: "32, 1, 2" if (wide or tall) else "16, 2, 2"}[mode]
         return f"void cn::linear_kernel<{tiles[key[1]]}, {mid}, {epi}, false, {mode}>(cn::LinearArgs)"
     if "bf16" in key[2:]:
         return "void cn::wgrad_bf16_kernel<2, 2, 2, 2>(cn::WgradArgs) + cn::slab_reduce_kernel"

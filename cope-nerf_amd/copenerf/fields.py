@@ -140,6 +140,9 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
     Returns a dict of device buffers; with keep=True everything the backward
     needs (layer inputs U_l and the ∇ pass adjoints S_l) is retained.  softplus'
     σ_l is never stored: its consumers recover it from U[l+1] (sig_beta).
+    want_feat="hidden": no feature head -- the caller consumes the last hidden
+    activation U[L8] directly (the renderer folds the feature head into the
+    colour network's first layer, NeuSRenderer._folded_color_pack).
     """
     M, dev = x.shape[0], x.device
     nl, sk, HL, KE = lay.n_lin, lay.skip, lay.HL, lay.KE
@@ -166,7 +169,7 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
     sdf = sdf_out if sdf_out is not None else _empty(M, 1, dev)
     ops.row_head(U[L8], lay.in_dim[L8], pk.w80, pk.b80, 1, 0, sdf, dst_index=dst)
     feat = None
-    if want_feat:
+    if want_feat is True:
         feat = _empty(M, rup(lay.H_feat, 128), dev)
         ops.linear(U[L8], pk.Bf8, lay.H_feat, rup(lay.in_dim[L8], 32), feat, EPI_STORE, bias=pk.bf8,
                    nzero=feat.shape[1])
@@ -192,7 +195,7 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
     return {"U": U, "S": S, "sdf": sdf, "feat": feat, "G": G}
 
 
-def sdf_input_grad(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat):
+def sdf_input_grad(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dh=None):
     """dL/dx of the sdf / feature outputs (the non-detached SDF forward of
     neus_renderer.py:352; the ∇ₓSDF pass runs on detached points,
     neus_renderer.py:356, so it contributes nothing here).  Primal adjoint chain
@@ -203,11 +206,14 @@ def sdf_input_grad(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat):
     nl, sk, HL, KE = lay.n_lin, lay.skip, lay.HL, lay.KE
     L8 = nl - 1
     dx = _empty(M, 4, dev)
-    if dsdf is None and dfeat is None:
+    if dsdf is None and dfeat is None and dh is None:
         return dx.zero_()
     dsdf_flat = None if dsdf is None else dsdf.reshape(M, 1).contiguous()
     P = _empty(M, HL, dev)
-    if dfeat is None:  # sdf only: P_7 = dsdf[m] w80[n] σ_7 -- elementwise, no GEMM over a zero operand
+    if dh is not None:  # gradient of the last hidden activation given (folded feature head): no GEMM
+        ops.softplus_adjoint(U[L8], HL, P, act_beta=sig_beta(lay, L8 - 1), D=dh, rowv=dsdf_flat,
+                             colv=pk.w80p if dsdf_flat is not None else None)
+    elif dfeat is None:  # sdf only: P_7 = dsdf[m] w80[n] σ_7 -- elementwise, no GEMM over a zero operand
         ops.scale_cols(U[L8], HL, pk.w80p, P, act_beta=sig_beta(lay, L8 - 1), rowv=dsdf_flat)
     else:
         ops.linear(dfeat, pk.Bt8, lay.out_dim[L8 - 1], rup(lay.H_feat, 32), P, EPI_BWD_SOFTPLUS,
@@ -230,7 +236,7 @@ def sdf_input_grad(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat):
     return dx
 
 
-def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG):
+def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None):
     """Parameter gradients of SDFNetwork for upstream (dL/dsdf, dL/dfeature,
     dL/d∇ₓSDF).  The ∇ₓSDF term (the create_graph double backward of
     neus_fields.py:296) is computed forward-over-reverse:
@@ -239,7 +245,10 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG):
       adjoint   Z_l = (W_{l+1}ᵀ Z_{l+1}) ⊙ σ_l + β s_l ⊙ (1-σ_l) ⊙ ż_l
       weights   dW_l = Σ_m Z_l u_lᵀ + s_l u̇_lᵀ,   db_l = Σ_m Z_l
 
-    where s_l are the ∇ pass adjoints kept from the forward.  Six GEMMs per
+    where s_l are the ∇ pass adjoints kept from the forward; dh (instead of
+    dfeat): the gradient of the last hidden activation itself (folded feature
+    head), so Z_7 is elementwise and the feature rows of lin8 get no gradient
+    here (autograd routes theirs through the fold).  Six GEMMs per
     layer instead of autograd's nine.  σ_l is recovered from
     U[l+1] inside every epilogue (sig_beta), and the second-order term is rebuilt
     by the adjoint's epilogue from s_l and u̇_{l+1} (ż_l = u̇_{l+1} c / σ_l), so the
@@ -275,7 +284,7 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG):
     i8, o8 = lay.in_dim[L8], lay.out_dim[L8]
     dW8 = torch.empty(o8, i8, device=dev)
     db8 = torch.empty(o8, device=dev)
-    if dfeat is not None:
+    if dfeat is not None and dh is None:
         ops.wgrad(dfeat, U[L8], lay.H_feat, i8, dW8[1:], db=db8[1:], mode=wmode)
     else:
         dW8[1:].zero_()
@@ -298,7 +307,12 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG):
         return dict(aux1=S[l], aux2=Ud[l + 1], aux2_scale=lay.beta * (SQRT2 if (l + 1) == sk else 1.0))
 
     Z = _empty(M, HL, dev)
-    if dfeat is None and not second and dsdf_flat is not None:
+    if dh is not None:  # Z_7 = (dh + dsdf w80) σ_7 + the second-order term: elementwise
+        so = second_order(L8 - 1)
+        ops.softplus_adjoint(U[L8], HL, Z, act_beta=sig_beta(lay, L8 - 1), D=dh, rowv=dsdf_flat,
+                             colv=pk.w80p if dsdf_flat is not None else None, aux1=so.get("aux1"),
+                             aux2=so.get("aux2"), aux2_scale=so.get("aux2_scale", 0.0))
+    elif dfeat is None and not second and dsdf_flat is not None:
         # sdf only, first order (e.g. SDFNetwork.sdf at train.py:504): Z_7 = dsdf[m] w80[n] σ_7,
         # elementwise -- no GEMM over a zero feature gradient
         ops.scale_cols(U[L8], HL, pk.w80p, Z, act_beta=sig_beta(lay, L8 - 1), rowv=dsdf_flat)
@@ -334,8 +348,12 @@ class _SDFFieldFn(torch.autograd.Function):
         st = sdf_forward(lay, pk, x, want_feat=want_feat, want_grad=want_grad, keep=keep)
         ctx.lay, ctx.pk, ctx.st = lay, pk, (st if keep else None)
         ctx.nparams = len(params)
+        ctx.hidden = want_feat == "hidden"
         empty = x.new_empty(0)
-        feat = st["feat"][:, :lay.H_feat] if want_feat else empty
+        if ctx.hidden:  # the last hidden activation in place of the feature (folded feature head)
+            feat = st["U"][lay.n_lin - 1][:, :lay.in_dim[lay.n_lin - 1]]
+        else:
+            feat = st["feat"][:, :lay.H_feat] if want_feat else empty
         G = st["G"] if want_grad else x.new_empty(0)
         if not want_feat:
             ctx.mark_non_differentiable(feat)
@@ -352,10 +370,13 @@ class _SDFFieldFn(torch.autograd.Function):
             dfeat = dfeat.contiguous()
         if dG is not None:
             dG = dG.contiguous()
-        dx = sdf_input_grad(ctx.lay, ctx.pk, ctx.st, dsdf, dfeat) if ctx.needs_input_grad[0] else None
+        dh = None
+        if ctx.hidden:
+            dh, dfeat = dfeat, None
+        dx = sdf_input_grad(ctx.lay, ctx.pk, ctx.st, dsdf, dfeat, dh=dh) if ctx.needs_input_grad[0] else None
         grads = [None] * ctx.nparams
         if any(ctx.needs_input_grad[5:]):
-            dWs, dbs = sdf_backward(ctx.lay, ctx.pk, ctx.st, dsdf, dfeat, dG)
+            dWs, dbs = sdf_backward(ctx.lay, ctx.pk, ctx.st, dsdf, dfeat, dG, dh=dh)
             grads = []
             for w, b in zip(dWs, dbs):
                 grads += [w, b]
@@ -445,7 +466,8 @@ class SDFNetwork(nn.Module):
         return Ws, bs, pack_sdf(lay, Ws, bs, self.mfma_dtype)
 
     def field(self, x, *, want_feat=True, want_grad=True, packed=None):
-        """Fused (sdf, feature, ∇ₓsdf) of the points x [M, 4] in one launch sequence."""
+        """Fused (sdf, feature, ∇ₓsdf) of the points x [M, 4] in one launch sequence
+        (want_feat="hidden": the last hidden activation instead of the feature)."""
         Ws, bs, pk = packed if packed is not None else self.params_and_pack()
         params = []
         for w, b in zip(Ws, bs):
@@ -668,13 +690,26 @@ class RenderingNetwork(nn.Module):
                                        in_dim=in_dim, out_dim=out_dim, multires_view=self.multires_view)
         return self._layout
 
-    def params_and_pack(self):
+    def params_and_pack(self, fold_feature=None):
+        """Effective weights and their kernel images.  fold_feature=(W8, b8), the SDF's
+        last Linear (row 0 sdf, rows 1: the feature head): lin0's feature columns W0f are
+        replaced by W0f @ W8[1:] and its bias by b0 + W0f @ b8[1:], so the first layer
+        reads the SDF's last hidden activation h directly:
+            W0f (W8[1:] h + b8[1:]) + b0  =  (W0f W8[1:]) h + (b0 + W0f b8[1:]).
+        The products are torch ops on the effective weights: autograd takes the
+        gradient of the folded weight back to both networks' parameters."""
         lay = self.layout()
         Ws, bs = [], []
         for l in range(lay.n_lin):
             lin = getattr(self, "lin" + str(l))
             Ws.append(effective_weight(lin))
             bs.append(lin.bias)
+        if fold_feature is not None:
+            W8, b8 = fold_feature
+            c = lay.P + lay.V + lay.Gd
+            W0f = Ws[0][:, c:]
+            Ws[0] = torch.cat([Ws[0][:, :c], W0f @ W8[1:]], 1)
+            bs[0] = bs[0] + W0f @ b8[1:]
         return Ws, bs, pack_color(lay, Ws, bs, self.mfma_dtype)
 
     def color(self, points, normals, dirs, dir_div, feature_vectors, packed=None):

@@ -292,6 +292,18 @@ def scale_cols(X, N, w, out, act_beta=0.0, rowv=None):
     return out
 
 
+def softplus_adjoint(act, N, out, *, act_beta, D=None, rowv=None, colv=None, aux1=None, aux2=None, aux2_scale=0.0):
+    """out = (D + rowv (x) colv) * sg(act) + aux1 * aux2 * aux2_scale * (1 - sg) / sg -- cn_softplus_adjoint."""
+    for t, n in ((act, "act"), (out, "out"), (D, "D"), (aux1, "aux1"), (aux2, "aux2")):
+        _need(t, n)
+    if rowv is not None and (not rowv.is_contiguous() or rowv.numel() != act.shape[0]):
+        raise RuntimeError("softplus_adjoint: rowv must be a contiguous [M] tensor")
+    _lib.call("cn_softplus_adjoint", act.shape[0], N, _ptr(D), _ld(D), _ptr(act), _ld(act), float(act_beta),
+              _ptr(rowv), _ptr(colv), _ptr(aux1), _ld(aux1), _ptr(aux2), _ld(aux2), float(aux2_scale), _ptr(out),
+              _ld(out), _stream())
+    return out
+
+
 def colsum(X, K, out, *, w=None, wdiv=1.0, accumulate=False):
     _need(X, "X")
     M = X.shape[0]

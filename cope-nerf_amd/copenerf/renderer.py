@@ -127,6 +127,16 @@ class NeuSRenderer(nn.Module):
         self.color_network.mfma_dtype = dtype
         return self
 
+    def _can_fold(self):
+        """The feature head folds into the colour network when the colour network reads
+        the SDF feature as its last input block and the SDF's hidden width equals the
+        feature width (every shipped config; set fold_feature=False to disable)."""
+        if not getattr(self, "fold_feature", True):
+            return False
+        lay, cl = self.sdf_network.layout(), self.color_network.layout()
+        L8 = lay.n_lin - 1
+        return lay.in_dim[L8] == lay.HL == cl.F and lay.out_dim[L8] == 1 + cl.F
+
     # -- sampling ------------------------------------------------------------
     @torch.no_grad()
     def sample_z(self, rays_o, rays_d, time_step, near, far, n_samples, n_importance, t_rand, sdf_packed):
@@ -183,7 +193,12 @@ class NeuSRenderer(nn.Module):
             t_rand = None
 
         sdf_packed = self.sdf_network.params_and_pack()
-        col_packed = self.color_network.params_and_pack()
+        fold = self._can_fold()
+        # the SDF feature head folded into the colour network's first layer (both linear,
+        # neus_renderer.py:352-358): no feature GEMM forward, the SDF's last adjoint is
+        # elementwise backward, one weight gradient fewer (RenderingNetwork.params_and_pack)
+        col_packed = self.color_network.params_and_pack(
+            fold_feature=(sdf_packed[0][-1], sdf_packed[1][-1]) if fold else None)
         self.last_sdf_pack = sdf_packed if self.expose_sdf_pack else None
         if z_vals is None:
             z = self.sample_z(rays_o, rays_d, time_step, near, far, n_samples, n_importance, t_rand, sdf_packed)
@@ -197,7 +212,8 @@ class NeuSRenderer(nn.Module):
         else:
             pts_time = torch.empty(R * S, 4, device=dev)
             ops.points(rays_o, rays_d, z, time_step, pts_time, mid=True, near=near, far=far, n_coarse=n_samples)
-        sdf, feat, G = self.sdf_network.field(pts_time, want_feat=True, want_grad=True, packed=sdf_packed)
+        sdf, feat, G = self.sdf_network.field(pts_time, want_feat="hidden" if fold else True, want_grad=True,
+                                              packed=sdf_packed)
         rgb = self.color_network.color(pts_time, G, rays_d, S, feat, packed=col_packed)
         inv_s = self.deviation_network(torch.zeros([1, 3], device=dev))[:, :1].clip(1 / 1e3, 1 / 1e-3)
         car = ops.device_scalar(cos_anneal_ratio, dev)  # a device scalar: graph replays read the current ratio

@@ -1247,6 +1247,41 @@ __global__ void __launch_bounds__(256) scale_cols_kernel(int M, int N4, const fl
     }
 }
 
+// Adjoint of a softplus layer without a GEMM, when the upstream gradient of its output
+// is already at hand (the SDF's last hidden layer once the feature head is folded into
+// the colour network):  out = (D + rowv (x) colv) * sg + aux1 * aux2 * c2 * (1 - sg) / sg,
+// sg = softplus' recovered from the activation (sigma_from_act); absent terms are 0.
+__global__ void __launch_bounds__(256) softplus_adjoint_kernel(int M, int N4, const float* __restrict__ D, int64_t ldd,
+                                                               const float* __restrict__ act, int64_t lda, float aux_c,
+                                                               const float* __restrict__ rowv,
+                                                               const float* __restrict__ colv,
+                                                               const float* __restrict__ aux1, int64_t ld1,
+                                                               const float* __restrict__ aux2, int64_t ld2, float c2,
+                                                               float* out, int64_t ldo) {
+    const int64_t tot = (int64_t)M * N4;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += stride) {
+        const int64_t m = idx / N4;
+        const int n = (int)(idx - m * N4) * 4;
+        const floatx4 a = *reinterpret_cast<const floatx4*>(act + m * lda + n);
+        floatx4 g = D ? *reinterpret_cast<const floatx4*>(D + m * ldd + n) : floatx4{0.f, 0.f, 0.f, 0.f};
+        if (rowv) g = g + rowv[m] * *reinterpret_cast<const floatx4*>(colv + n);
+        floatx4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
+        if (aux1) {
+            s1 = *reinterpret_cast<const floatx4*>(aux1 + m * ld1 + n);
+            s2 = *reinterpret_cast<const floatx4*>(aux2 + m * ld2 + n);
+        }
+        floatx4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float sg = sigma_from_act(a[e], aux_c);
+            const float rr = sg > 0.0f ? (1.0f - sg) * __builtin_amdgcn_rcpf(sg) : 0.0f;
+            o[e] = g[e] * sg + s1[e] * s2[e] * (c2 * rr);
+        }
+        *reinterpret_cast<floatx4*>(out + m * ldo + n) = o;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Colour head backward: sigmoid + Linear(256 -> 3) (neus_fields.py:367-373).
 // Block = 256 threads = one column each, over a slice of rows.
@@ -1409,6 +1444,13 @@ static int g_stagger = [] {  // benchmarking aid: COPENERF_STAGGER (units of s_s
     const char* e = getenv("COPENERF_STAGGER");
     return e ? atoi(e) : 0;
 }();
+// bf16x6 epilogues on the 128x256 tile (bit e = cn_epilogue e; benchmarking aid: COPENERF_X6_TALL).
+// Default MUL and TANGENT (one aux stream: -6 / -10 us per C2 layer launch); BWD_SOFTPLUS measured
+// +10-20 us on it, the light epilogues equal.
+static int g_x6_tall = [] {
+    const char* e = getenv("COPENERF_X6_TALL");
+    return e ? (int)strtol(e, nullptr, 0) : 0x18;
+}();
 static int g_wide_epis = [] {
     const char* e = getenv("COPENERF_WIDE_EPIS");
     return e ? (int)strtol(e, nullptr, 0) : 0x1f;
@@ -1537,8 +1579,13 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
             // (the wide tile only for the light epilogues: with one workgroup per CU an aux-reading
             // epilogue no longer overlaps a partner workgroup's main loop, measured slower)
             const bool light = (g_wide_epis >> d->epilogue) & 1;
+            // 128x256 ("tall-N") tiles: one workgroup owns whole 256-wide output rows, so A is
+            // read from HBM once (the two N-tiles of the 256x128 tiling re-fetch 30-50 % of it,
+            // PMC) and split once per row
+            const bool tall = (g_x6_tall >> d->epilogue) & 1;
+            if (d->K % 64 == 0 && tall && d->N > 128 && d->ldb >= 256 && g_linear_variant == 0)
+                return launch_linear_tile<4, 2, 1, 4, 32, 1, 2, 2>(d, a, s);
             if (d->K % 64 == 0 && g_linear_variant == 0 && light) return launch_linear_tile<4, 2, 2, 2, 32, 1, 2, 2>(d, a, s);
-            if (d->K % 64 == 0 && g_linear_variant == 4) return launch_linear_tile<2, 2, 2, 2, 16, 2, 4, 2>(d, a, s);
             return launch_linear_tile<2, 2, 2, 2, 16, 2, 2, 2>(d, a, s);
         }
         return launch_linear_tile<4, 1, 1, 2, 16, 2, 2, 2>(d, a, s);
@@ -1649,6 +1696,26 @@ extern "C" int cn_scale_cols(int32_t M, int32_t N, const float* X, int64_t ldx, 
     scale_cols_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(M, N / 4, X, ldx, w, rowv, out, ld_out,
                                                                -act_beta * 1.44269504088896341f);
     return check_launch("cn_scale_cols");
+}
+
+extern "C" int cn_softplus_adjoint(int32_t M, int32_t N, const float* D, int64_t ldd, const float* act, int64_t lda,
+                                   float act_beta, const float* rowv, const float* colv, const float* aux1,
+                                   int64_t ld1, const float* aux2, int64_t ld2, float aux2_scale, float* out,
+                                   int64_t ld_out, cn_stream_t stream) {
+    CN_REQUIRE(act && out && act_beta > 0.0f, CN_ERR_ARG, "cn_softplus_adjoint: act, out and act_beta > 0 required");
+    CN_REQUIRE((rowv == nullptr) == (colv == nullptr) && (aux1 == nullptr) == (aux2 == nullptr), CN_ERR_ARG,
+               "cn_softplus_adjoint: rowv/colv and aux1/aux2 go together");
+    CN_REQUIRE(N % 4 == 0 && lda % 4 == 0 && ld_out % 4 == 0 && al16(act) && al16(out) &&
+                   (!D || (ldd % 4 == 0 && al16(D))) && (!colv || al16(colv)) &&
+                   (!aux1 || (ld1 % 4 == 0 && ld2 % 4 == 0 && al16(aux1) && al16(aux2))),
+               CN_ERR_ALIGN, "cn_softplus_adjoint: N, leading dimensions and pointers must be multiples of 4 floats");
+    if ((int64_t)M * N == 0) return CN_OK;
+    const int64_t tot = (int64_t)M * (N / 4);
+    const int blocks = (int)std::min<int64_t>((tot + 255) / 256, 8192);
+    softplus_adjoint_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(M, N / 4, D, ldd, act, lda,
+                                                                     -act_beta * 1.44269504088896341f, rowv, colv,
+                                                                     aux1, ld1, aux2, ld2, aux2_scale, out, ld_out);
+    return check_launch("cn_softplus_adjoint");
 }
 
 extern "C" size_t cn_rgb_head_bwd_workspace_bytes(int32_t M, int32_t K) {

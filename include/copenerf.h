@@ -195,6 +195,17 @@ int cn_colsum(int32_t M, int32_t K, const float* w, const float* X, int64_t ldx,
 int cn_scale_cols(int32_t M, int32_t N, const float* X, int64_t ldx, const float* w, const float* rowv,
                   float* out, int64_t ld_out, float act_beta, cn_stream_t stream);
 
+/* Adjoint of a softplus layer from the gradient of its output, without a GEMM (the
+ * SDF's last hidden layer when the feature head is folded into the colour network's
+ * first layer: the colour backward already yields d/d(hidden)):
+ *   out[m][n] = ((D ? D[m][n] : 0) + (rowv ? rowv[m] colv[n] : 0)) * sg
+ *             + (aux1 ? aux1[m][n] aux2[m][n] aux2_scale (1 - sg) / sg : 0),   0 where sg = 0,
+ *   sg = 1 - exp(-act_beta act[m][n]) (softplus' from the activation, as cn_linear's epilogues). */
+int cn_softplus_adjoint(int32_t M, int32_t N, const float* D, int64_t ldd, const float* act, int64_t lda,
+                        float act_beta, const float* rowv, const float* colv, const float* aux1, int64_t ld1,
+                        const float* aux2, int64_t ld2, float aux2_scale, float* out, int64_t ld_out,
+                        cn_stream_t stream);
+
 /* ------------------------------------------------------------------------ *
  * Positional encoding of the SDF input (neus_embedder.py:6-51 with
  * include_input, log-sampled bands 2^0..2^(multires-1), [sin, cos]; applied at
