@@ -21,6 +21,7 @@
 #include "cn_common.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 namespace cn {
@@ -176,6 +177,8 @@ __device__ __forceinline__ void tile_coords(int vt, int T, int& tm, int& tn) {
 #ifndef LSTORE_ALWAYS
 #define LSTORE_ALWAYS 0  // 1: branch-free staging (measured: main loop -1.5 %, epilogue variants +2-3 %)
 #endif
+constexpr int kTblCols = 512;  // widest N with a bias / colv (the LDS column table)
+
 template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int EPI, bool ROWV, int MODE>
 __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel(LinearArgs p) {
     constexpr int NT = 64 * WM * WN;
@@ -204,9 +207,18 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     static_assert((BM / NPART) * CS <= LDS_FLOATS, "C tile slab must fit in the staging LDS");
     constexpr int PROWS = BM / NPART;
 
-    __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
+    // bias / colv of every column (N <= kTblCols, host-checked) live in LDS past the staging
+    // buffers, filled once per workgroup: the epilogue issues no vector-memory load for them,
+    // so its only VMEM waits are for the aux rows it reads (the compiler's vmcnt for a
+    // per-tile bias load, under the divergent region branch, was a full drain before every
+    // pass -- each pass waited for the previous pass's stores)
+    constexpr bool kBias = EPI == CN_EPI_STORE || EPI == CN_EPI_SOFTPLUS || EPI == CN_EPI_RELU;
+    constexpr int TBL = (kBias ? kTblCols : 0) + (ROWV ? kTblCols : 0);
+    __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS + TBL];
     float* sA = smem;
     float* sB = smem + 2 * BM * LS;
+    float* sBias = smem + LDS_FLOATS;
+    float* sColv = smem + LDS_FLOATS + (kBias ? kTblCols : 0);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -330,7 +342,6 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     constexpr bool kAux0 = EPI == CN_EPI_MUL || EPI == CN_EPI_TANGENT || EPI == CN_EPI_BWD_SOFTPLUS ||
                            EPI == CN_EPI_BWD_RELU;
     constexpr bool kAux1 = EPI == CN_EPI_BWD_SOFTPLUS;  // aux1 = s, aux2 = u' (second-order term)
-    constexpr bool kOut1 = false;
 
     // epilogue thread geometry: row rr + k*RPP of the slab, columns 4*c4 .. 4*c4+3
     const int c4 = tid % C4;
@@ -347,6 +358,14 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 
     int vt = next_valid(blockIdx.x);
     if (vt >= ntiles) return;
+    if constexpr (TBL > 0) {  // visible after the first tile's staging barrier
+        const rsrc_t rbias = make_view(p.bias, kBias && p.bias ? p.N * 4 : 0);
+        const rsrc_t rcolv = make_view(p.colv, ROWV ? p.N * 4 : 0);
+        for (int i = tid; i < kTblCols / 4; i += NT) {
+            if (kBias) *reinterpret_cast<floatx4*>(sBias + 4 * i) = bload4(rbias, 16 * i, 0);
+            if (ROWV) *reinterpret_cast<floatx4*>(sColv + 4 * i) = bload4(rcolv, 16 * i, 0);
+        }
+    }
     // stagger: with 2 workgroups per CU, the second resident one (block ids past the first
     // gridDim / 2 fill the CUs' second slots) starts later; with 1 per CU, the odd ones
     if (OCC >= 2 ? (blockIdx.x >= gridDim.x / 2) : (blockIdx.x & 1))
@@ -354,6 +373,11 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     int tm, tn;
     tile_coords(vt, T, tm, tn);
     gload(0, 0, tm * BM, tn * BN, true);
+    // (see the end of the tile loop: set 0 enters the loop as an asm-defined value on both paths)
+#pragma unroll
+    for (int q = 0; q < ALD; ++q) asm volatile("" : "+v"(ra[0][q]));
+#pragma unroll
+    for (int q = 0; q < BLD; ++q) asm volatile("" : "+v"(rb[0][q]));
 
     while (vt < ntiles) {
         const int m0 = tm * BM, n0 = tn * BN;
@@ -488,6 +512,17 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             }
         }
 
+        // Every staging load is complete by here (the epilogue's registers reuse the idle
+        // set's, so the compiler drains them first).  Re-defining the register sets through
+        // an empty asm tells it so: the next tile's staging of its prefetched first chunk then
+        // waits for nothing, instead of for the epilogue's stores (one vmcnt, in issue order).
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+#pragma unroll
+            for (int q = 0; q < ALD; ++q) asm volatile("" : "+v"(ra[d][q]));
+#pragma unroll
+            for (int q = 0; q < BLD; ++q) asm volatile("" : "+v"(rb[d][q]));
+        }
         if constexpr (EPI == 7) {  // benchmark only: main loop alone, keep every accumulator live
             float sum = 0.0f;
 #pragma unroll
@@ -522,107 +557,134 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         const bool tile_main = n0 + BN <= Nmain;
         const int col = n0 + 4 * c4;
         const int region = col < Nmain ? 0 : (col < p.N ? 1 : (col < p.nzero ? 2 : 3));
+        // (columns >= N read zeros from the table: their lanes are not region 0 anyway)
+        const int tcol = min(col, kTblCols - 4);
         floatx4 bias = {0.f, 0.f, 0.f, 0.f}, colv = {0.f, 0.f, 0.f, 0.f};
-        if (region == 0) {
-            if (p.bias) bias = *reinterpret_cast<const floatx4*>(p.bias + col);
-            if (ROWV) colv = *reinterpret_cast<const floatx4*>(p.colv + col);
-        }
+        if (kBias) bias = *reinterpret_cast<const floatx4*>(sBias + tcol);
+        if (ROWV) colv = *reinterpret_cast<const floatx4*>(sColv + tcol);
         float* sC = smem;
+        // aux rows of an epilogue group, double-buffered: group g+1's loads are issued
+        // before group g's stores, so waiting for them never waits for those stores
+        // (gfx9's one vmcnt counts loads and stores in issue order); group 0's are
+        // issued before the accumulators are parked
+        constexpr int NG = PROWS / RPP / GROUP;
+        floatx4 x0[2][GROUP], x1[2][GROUP], x2[2][GROUP];
+        float rv[2][GROUP];
+        auto aux_load = [&](int part, int g, int slot) {
 #pragma unroll
-        for (int part = 0; part < NPART; ++part) {
-            if (part > 0) __syncthreads();  // previous slab consumed
+            for (int q = 0; q < GROUP; ++q) {
+                const int lrow = part * PROWS + (g * GROUP + q) * RPP;  // wave-uniform slab row of the pass
+                // unconditional: the views make reads past a row (columns >= N) or
+                // past the last row harmless, and only region-0 lanes use the values
+                if (kAux0) x0[slot][q] = bload4(view_at(tX0, lrow), voX0, 0);
+                if (kAux1) x1[slot][q] = bload4(view_at(tX1, lrow), voX1, 0);
+                if (kAux1) x2[slot][q] = bload4(view_at(tX2, lrow), voX2, 0);
+                if (ROWV) rv[slot][q] = bload1(view_at(tR, lrow), rr * 4, 0);
+            }
+        };
+        constexpr bool kAnyAux = kAux0 || kAux1 || ROWV;
+        // main-region values of pass q of a group (the EPI's math on 4 columns)
+        auto main_vals = [&](const floatx4& v, int slot, int q, floatx4& o0) {
 #pragma unroll
-            for (int i = 0; i < TM; ++i)
+            for (int e = 0; e < 4; ++e) {
+                // scaling by 1/adiv, 1/odiv is a multiply by exactly 1.0 when absent:
+                // no per-element select for a uniform flag
+                float u = v[e] * p.inv_adiv;
+                if (ROWV) u = u + rv[slot][q] * colv[e];
+                if constexpr (EPI == CN_EPI_STORE) {
+                    o0[e] = u + bias[e];
+                } else if constexpr (EPI == CN_EPI_SOFTPLUS) {
+                    o0[e] = softplus_hw(u + bias[e], c_exp, c_thr, c_log) * p.inv_odiv;
+                } else if constexpr (EPI == CN_EPI_RELU) {
+                    const float z = u + bias[e];
+                    o0[e] = z > 0.0f ? z : 0.0f;
+                } else if constexpr (EPI == CN_EPI_MUL) {
+                    o0[e] = u * sigma_from_act(x0[slot][q][e], p.aux_c);
+                } else if constexpr (EPI == CN_EPI_TANGENT) {
+                    o0[e] = u * sigma_from_act(x0[slot][q][e], p.aux_c) * p.inv_odiv;
+                } else if constexpr (EPI == CN_EPI_BWD_SOFTPLUS) {
+                    // Z = v sigma + beta s (1 - sigma) z', with z' = u' / sigma from the
+                    // stored tangent u' = sigma z' (aux2_scale = beta * its divisor):
+                    // the second-order term of softplus is rebuilt here instead of
+                    // being written by the tangent pass and read back.  sigma = 0
+                    // implies s = u' = 0 (both carry the factor sigma): term 0.
+                    // aux1 / aux2 absent: zero-record views read 0.
+                    const float sg = sigma_from_act(x0[slot][q][e], p.aux_c);
+                    const float rr = sg > 0.0f ? (1.0f - sg) * __builtin_amdgcn_rcpf(sg) : 0.0f;
+                    o0[e] = u * sg + x1[slot][q][e] * x2[slot][q][e] * (p.aux2_scale * rr);
+                } else if constexpr (EPI == CN_EPI_BWD_RELU) {
+                    o0[e] = x0[slot][q][e] > 0.0f ? u : 0.0f;
+                }
+            }
+        };
+        // Two specialisations of the slab passes: MAIN (wave-uniform: every column of the
+        // tile is in the main region) stores every pass unconditionally, so each wait for
+        // a group's aux rows counts exactly the stores issued after them; the general one
+        // (edge tiles: split / zero-fill / untouched columns) branches per lane and ends
+        // with the aux registers consumed, so no path carries a pending load into the next
+        // tile (where the compiler would drain the vmcnt, epilogue stores included).
+        auto consume_aux = [&]() {
 #pragma unroll
-                for (int j = 0; j < TN; ++j)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int row = wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                        if (NPART == 1 || row / PROWS == part)
-                            sC[(row - part * PROWS) * CS + wn * TN * 32 + j * 32 + (lane & 31)] = acc[i][j][r];
-                    }
-            __syncthreads();
-            if (region == 3) continue;
-#pragma unroll
-            for (int pb = 0; pb < PROWS / RPP; pb += GROUP) {
-                floatx4 v[GROUP], x0[GROUP], x1[GROUP], x2[GROUP];
-                float rv[GROUP];
+            for (int sl = 0; sl < 2; ++sl)
 #pragma unroll
                 for (int q = 0; q < GROUP; ++q) {
-                    const int lrow = part * PROWS + (pb + q) * RPP;  // slab row offset of this pass (wave-uniform)
-                    v[q] = *reinterpret_cast<const floatx4*>(sC + (rr + (pb + q) * RPP) * CS + 4 * c4);
-                    // unconditional: the views make reads past a row (columns >= N) or
-                    // past the last row harmless, and only region-0 lanes use the values
-                    if (kAux0) x0[q] = bload4(view_at(tX0, lrow), voX0, 0);
-                    if (kAux1) x1[q] = bload4(view_at(tX1, lrow), voX1, 0);
-                    if (kAux1) x2[q] = bload4(view_at(tX2, lrow), voX2, 0);
-                    if (ROWV) rv[q] = bload1(view_at(tR, lrow), rr * 4, 0);
+                    if (kAux0) asm volatile("" ::"v"(x0[sl][q]));
+                    if (kAux1) asm volatile("" ::"v"(x1[sl][q]));
+                    if (kAux1) asm volatile("" ::"v"(x2[sl][q]));
+                    if (ROWV) asm volatile("" ::"v"(rv[sl][q]));
                 }
-                // main-region values of pass q (the EPI's math on 4 columns)
-                auto main_vals = [&](int q, floatx4& o0, floatx4& o1) {
+        };
+        auto passes = [&](auto main_tag) {
+            constexpr bool MAIN = decltype(main_tag)::value;
+            if (kAnyAux) aux_load(0, 0, 0);
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        // scaling by 1/adiv, 1/odiv is a multiply by exactly 1.0 when absent:
-                        // no per-element select for a uniform flag
-                        float u = v[q][e] * p.inv_adiv;
-                        if (ROWV) u = u + rv[q] * colv[e];
-                        if constexpr (EPI == CN_EPI_STORE) {
-                            o0[e] = u + bias[e];
-                        } else if constexpr (EPI == CN_EPI_SOFTPLUS) {
-                            o0[e] = softplus_hw(u + bias[e], c_exp, c_thr, c_log) * p.inv_odiv;
-                        } else if constexpr (EPI == CN_EPI_RELU) {
-                            const float z = u + bias[e];
-                            o0[e] = z > 0.0f ? z : 0.0f;
-                        } else if constexpr (EPI == CN_EPI_MUL) {
-                            o0[e] = u * sigma_from_act(x0[q][e], p.aux_c);
-                        } else if constexpr (EPI == CN_EPI_TANGENT) {
-                            o0[e] = u * sigma_from_act(x0[q][e], p.aux_c) * p.inv_odiv;
-                        } else if constexpr (EPI == CN_EPI_BWD_SOFTPLUS) {
-                            // Z = v sigma + beta s (1 - sigma) z', with z' = u' / sigma from the
-                            // stored tangent u' = sigma z' (aux2_scale = beta * its divisor):
-                            // the second-order term of softplus is rebuilt here instead of
-                            // being written by the tangent pass and read back.  sigma = 0
-                            // implies s = u' = 0 (both carry the factor sigma): term 0.
-                            // aux1 / aux2 absent: zero-record views read 0.
-                            const float sg = sigma_from_act(x0[q][e], p.aux_c);
-                            const float rr = sg > 0.0f ? (1.0f - sg) * __builtin_amdgcn_rcpf(sg) : 0.0f;
-                            o0[e] = u * sg + x1[q][e] * x2[q][e] * (p.aux2_scale * rr);
-                        } else if constexpr (EPI == CN_EPI_BWD_RELU) {
-                            o0[e] = x0[q][e] > 0.0f ? u : 0.0f;
+            for (int part = 0; part < NPART; ++part) {
+                if (part > 0) __syncthreads();  // previous slab consumed
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int row = wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                            if (NPART == 1 || row / PROWS == part)
+                                sC[(row - part * PROWS) * CS + wn * TN * 32 + j * 32 + (lane & 31)] = acc[i][j][r];
                         }
+                __syncthreads();
+#pragma unroll
+                for (int g = 0; g < NG; ++g) {
+                    const int slot = (part * NG + g) & 1;
+                    const int pb = g * GROUP;
+                    if (kAnyAux) {  // prefetch the next group (or the next part's first)
+                        if (g + 1 < NG) aux_load(part, g + 1, slot ^ 1);
+                        else if (part + 1 < NPART) aux_load(part + 1, 0, slot ^ 1);
                     }
-                };
-                if (tile_main) {  // wave-uniform: every column of the tile is in the main region
 #pragma unroll
                     for (int q = 0; q < GROUP; ++q) {
                         const int lrow = part * PROWS + (pb + q) * RPP;
-                        floatx4 o0, o1;
-                        main_vals(q, o0, o1);
-                        bstore4(view_at(tO0, lrow), voO0, 0, o0);
-                        if (kOut1) bstore4(view_at(tO1, lrow), voO1, 0, o1);  // absent out1: empty view
-                    }
-                } else {
-#pragma unroll
-                    for (int q = 0; q < GROUP; ++q) {
-                        const int lrow = part * PROWS + (pb + q) * RPP;
-                        floatx4 o0, o1;
-                        if (region == 0) {
-                            main_vals(q, o0, o1);
+                        const floatx4 v = *reinterpret_cast<const floatx4*>(sC + (rr + (pb + q) * RPP) * CS + 4 * c4);
+                        floatx4 o0;
+                        if constexpr (MAIN) {
+                            main_vals(v, slot, q, o0);
                             bstore4(view_at(tO0, lrow), voO0, 0, o0);
-                            if (kOut1) bstore4(view_at(tO1, lrow), voO1, 0, o1);
+                        } else if (region == 0) {
+                            main_vals(v, slot, q, o0);
+                            bstore4(view_at(tO0, lrow), voO0, 0, o0);
                         } else if (region == 1) {  // EPI_MUL split columns: raw (A·Bᵀ)/adiv
 #pragma unroll
-                            for (int e = 0; e < 4; ++e) o0[e] = v[q][e] * p.inv_adiv;
+                            for (int e = 0; e < 4; ++e) o0[e] = v[e] * p.inv_adiv;
                             bstore4(view_at(tS, lrow), voS, 0, o0);
                             if (col < p.nzero) bstore4(view_at(tO0, lrow), voO0, 0, floatx4{0.f, 0.f, 0.f, 0.f});
-                        } else {  // region 2: zero fill
+                        } else if (region == 2) {  // zero fill (region 3: past nzero, untouched)
                             bstore4(view_at(tO0, lrow), voO0, 0, floatx4{0.f, 0.f, 0.f, 0.f});
-                            if (kOut1) bstore4(view_at(tO1, lrow), voO1, 0, floatx4{0.f, 0.f, 0.f, 0.f});
                         }
                     }
                 }
             }
-        }
+            if constexpr (!MAIN && kAnyAux) consume_aux();
+        };
+        if (tile_main) passes(std::true_type{});
+        else passes(std::false_type{});
         __syncthreads();  // sC is the next tile's staging buffer
         vt = vt_next;
         tm = tm_next;
@@ -1532,6 +1594,8 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
                    "cn_linear: split output required");
     CN_REQUIRE((d->rowv == nullptr) == (d->colv == nullptr), CN_ERR_ARG, "cn_linear: rowv/colv go together");
     CN_REQUIRE(al16(d->bias) && al16(d->colv), CN_ERR_ALIGN, "cn_linear: bias / colv must be 16-byte aligned");
+    CN_REQUIRE((!d->bias && !d->colv) || d->N <= kTblCols, CN_ERR_UNSUPPORTED,
+               "cn_linear: N=%d > %d with a bias / colv", d->N, kTblCols);
     // the epilogue moves 4 columns per 16-byte access
     CN_REQUIRE(d->N % 4 == 0 && nzero % 4 == 0 && (e != CN_EPI_MUL || d->nsplit % 4 == 0), CN_ERR_SHAPE,
                "cn_linear: N, nzero and nsplit must be multiples of 4");

@@ -79,7 +79,7 @@ typedef struct cn_linear_desc {
     const float* A;
     const float* A2;
     const float* B;
-    const float* bias;   /* [N] or NULL */
+    const float* bias;   /* [N] or NULL (N <= 512 with a bias or colv) */
     const float* rowv;   /* [M] or NULL : rank-1 term rowv[m]*colv[n] added to v */
     const float* colv;   /* [N] or NULL */
     const float* aux0;

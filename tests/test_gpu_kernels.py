@@ -166,6 +166,27 @@ def test_row_head_colsum_scale_cols():
                                atol=1e-7)
 
 
+def test_softplus_adjoint():
+    """cn_softplus_adjoint: the adjoint of the last SDF hidden layer when the feature
+    head is folded into the colour network -- (D + rowv colv) σ + c2 s1 s2 (1-σ)/σ,
+    σ recovered from the stored activation (0 where σ = 0)."""
+    ops = _ops()
+    M, K = 3000, 256
+    act = _act(M, K, 31)
+    D = _rnd(M, K, seed=32)
+    rv, cv = _rnd(M, seed=33), _rnd(K, seed=34)
+    s1, s2 = _rnd(M, K, seed=35), _rnd(M, K, seed=36)
+    out = torch.empty(M, K, device=DEV)
+    sg = _sg(act, 100.0)
+    rr = torch.where(sg > 0, (1 - sg) / sg.clamp_min(1e-300), torch.zeros_like(sg))
+    ops.softplus_adjoint(act, K, out, act_beta=100.0, D=D)
+    torch.testing.assert_close(out, (D.double() * sg).float(), rtol=1e-5, atol=1e-7)
+    ops.softplus_adjoint(act, K, out, act_beta=100.0, D=D, rowv=rv, colv=cv, aux1=s1, aux2=s2, aux2_scale=0.7)
+    ref = (D.double() + rv.double()[:, None] * cv.double()) * sg + 0.7 * s1.double() * s2.double() * rr
+    torch.testing.assert_close(out, ref.float(), rtol=1e-4, atol=1e-5)
+    assert torch.isfinite(out).all()
+
+
 def test_c_abi_rejects_bad_arguments():
     ops = _ops()
     A = torch.zeros(10, 30, device=DEV)
