@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libcopenerf.so"
 LIB_PATH = os.environ.get("COPENERF_LIB", os.path.join(_HERE, LIB_NAME))
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 c_f32p = ctypes.c_void_p  # device pointers are passed as integers
 c_i32 = ctypes.c_int32
@@ -32,6 +32,7 @@ EPI_MUL = 3
 EPI_TANGENT = 4
 EPI_BWD_SOFTPLUS = 5
 EPI_BWD_RELU = 6
+EPI_SOFTPLUS_HEAD = 8
 
 
 class LinearDesc(ctypes.Structure):
@@ -45,6 +46,7 @@ class LinearDesc(ctypes.Structure):
         ("adiv", c_f32), ("odiv", c_f32), ("beta", c_f32), ("threshold", c_f32),
         ("mfma_dtype", c_i32), ("aux_beta", c_f32), ("aux2", c_ptr), ("ld_aux2", c_i64),
         ("aux2_scale", c_f32), ("reserved_", c_i32),
+        ("head_w", c_ptr), ("head_b", c_ptr), ("head_out", c_ptr), ("head_idx", c_ptr),
     ]
 
 

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import dataclasses
 import math
+import os
 from typing import List, Optional
 
 import numpy as np
@@ -29,8 +30,8 @@ import torch.nn.functional as F
 
 from . import ops
 from .embedder import embed_dim
-from .ops import (EPI_BWD_RELU, EPI_BWD_SOFTPLUS, EPI_MUL, EPI_RELU, EPI_SOFTPLUS, EPI_STORE, EPI_TANGENT,
-                  SQRT2, rup)
+from .ops import (EPI_BWD_RELU, EPI_BWD_SOFTPLUS, EPI_MUL, EPI_RELU, EPI_SOFTPLUS, EPI_SOFTPLUS_HEAD, EPI_STORE,
+                  EPI_TANGENT, SQRT2, rup)
 
 
 def effective_weight(lin: nn.Linear) -> torch.Tensor:
@@ -125,6 +126,22 @@ def pack_sdf(lay: SDFLayout, Ws, bs, mfma_dtype: str = "fp32") -> SDFPack:
         return SDFPack(Bf, Bt, b, w80.contiguous()[None], b80.contiguous(), w80p, Bf8, Bt8, b8[1:].contiguous())
 
 
+FUSE_HEAD = os.environ.get("COPENERF_FUSE_HEAD", "1") != "0"
+
+
+def _fuse_head(lay: SDFLayout, pk: SDFPack) -> bool:
+    """The last hidden layer computes the sdf head in its epilogue (EPI_SOFTPLUS_HEAD)
+    when one GEMM tile spans its whole output row: N <= 128 in every mode, N <= 256
+    with the bf16x6 128x256 tile."""
+    L8 = lay.n_lin - 1
+    N = lay.out_dim[L8 - 1]
+    if not FUSE_HEAD or lay.in_dim[L8] != N or N % 4 or L8 == lay.skip or L8 - 1 == 0:
+        return False
+    B = pk.Bf[L8 - 1]
+    x6 = B.dim() == 3
+    return N <= 128 or (x6 and N <= 256 and B.shape[1] >= 256 and rup(lay.in_dim[L8 - 1], 32) % 64 == 0)
+
+
 def sig_beta(lay: SDFLayout, l: int) -> float:
     """aux_beta of softplus' σ_l read from the stored activation U[l+1] = a_l / c
     (c = √2 for the layer feeding the skip concat, neus_fields.py:276-277):
@@ -155,19 +172,32 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
         o = lay.out_dim[sk - 1]
         e_view = Usk[:, o:o + lay.E]
     ops.sdf_embed(x, lay.multires, lay.scale, U[0], e_view, SQRT2)
+    L8 = nl - 1
+    sdf = sdf_out if sdf_out is not None else _empty(M, 1, dev)
+    fuse = _fuse_head(lay, pk)
+    S7 = None
     for l in range(nl - 1):
         into = (l + 1) == sk
-        out = Usk if into else _empty(M, HL, dev)
         K = KE if l == 0 else rup(lay.in_dim[l], 32)
-        ops.linear(U[l], pk.Bf[l], lay.out_dim[l], K, out, EPI_SOFTPLUS, bias=pk.b[l],
-                   nzero=lay.out_dim[l] if into else HL, odiv=SQRT2 if into else 1.0, beta=lay.beta,
-                   threshold=lay.threshold, kalg=lay.in_dim[l])
+        if l == L8 - 1 and fuse:
+            # the sdf head (and the ∇-pass seed s_7 = w80 ⊙ softplus'_7) in the layer's epilogue;
+            # the activation itself is stored only when a consumer needs it (not on the sampler path)
+            out = _empty(M, HL, dev) if (keep_u or want_feat is not False) else None
+            S7 = _empty(M, HL, dev) if want_grad else None
+            ops.linear(U[l], pk.Bf[l], lay.out_dim[l], K, out, EPI_SOFTPLUS_HEAD, bias=pk.b[l], nzero=HL, beta=lay.beta,
+                       threshold=lay.threshold, kalg=lay.in_dim[l], out1=S7, colv=pk.w80p if want_grad else None,
+                       aux_beta=sig_beta(lay, l) if want_grad else 0.0, head_w=pk.w80[0], head_b=pk.b80, head_out=sdf,
+                       head_idx=dst, M=M)
+        else:
+            out = Usk if into else _empty(M, HL, dev)
+            ops.linear(U[l], pk.Bf[l], lay.out_dim[l], K, out, EPI_SOFTPLUS, bias=pk.b[l],
+                       nzero=lay.out_dim[l] if into else HL, odiv=SQRT2 if into else 1.0, beta=lay.beta,
+                       threshold=lay.threshold, kalg=lay.in_dim[l])
         U[l + 1] = out
         if not keep_u and l >= 1 and (l != sk):
             U[l] = None  # free as we go on the no-grad sampler path
-    L8 = nl - 1
-    sdf = sdf_out if sdf_out is not None else _empty(M, 1, dev)
-    ops.row_head(U[L8], lay.in_dim[L8], pk.w80, pk.b80, 1, 0, sdf, dst_index=dst)
+    if not fuse:
+        ops.row_head(U[L8], lay.in_dim[L8], pk.w80, pk.b80, 1, 0, sdf, dst_index=dst)
     feat = None
     if want_feat is True:
         feat = _empty(M, rup(lay.H_feat, 128), dev)
@@ -176,8 +206,10 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
     G, S = None, None
     if want_grad:
         S = [None] * (nl - 1)
-        S[L8 - 1] = _empty(M, HL, dev)
-        ops.scale_cols(U[L8], HL, pk.w80p, S[L8 - 1], act_beta=sig_beta(lay, L8 - 1))
+        S[L8 - 1] = S7
+        if S7 is None:
+            S[L8 - 1] = _empty(M, HL, dev)
+            ops.scale_cols(U[L8], HL, pk.w80p, S[L8 - 1], act_beta=sig_beta(lay, L8 - 1))
         QE = _empty(M, KE, dev) if sk >= 0 else None
         for l in range(L8 - 1, 0, -1):
             Kl = rup(lay.out_dim[l], 32)
@@ -708,8 +740,9 @@ class RenderingNetwork(nn.Module):
             W8, b8 = fold_feature
             c = lay.P + lay.V + lay.Gd
             W0f = Ws[0][:, c:]
-            Ws[0] = torch.cat([Ws[0][:, :c], W0f @ W8[1:]], 1)
-            bs[0] = bs[0] + W0f @ b8[1:]
+            # in float64: exact to fp32 rounding, and faster than hipBLASLt's fp32 kernel for 256^3
+            Ws[0] = torch.cat([Ws[0][:, :c], (W0f.double() @ W8[1:].double()).float()], 1)
+            bs[0] = bs[0] + (W0f.double() @ b8[1:].double()).float()
         return Ws, bs, pack_color(lay, Ws, bs, self.mfma_dtype)
 
     def color(self, points, normals, dirs, dir_div, feature_vectors, packed=None):

@@ -12,8 +12,8 @@ import math
 import torch
 
 from . import _lib
-from ._lib import (EPI_BWD_RELU, EPI_BWD_SOFTPLUS, EPI_MUL, EPI_RELU, EPI_SOFTPLUS, EPI_STORE,  # noqa: F401
-                   EPI_TANGENT)
+from ._lib import (EPI_BWD_RELU, EPI_BWD_SOFTPLUS, EPI_MUL, EPI_RELU, EPI_SOFTPLUS, EPI_SOFTPLUS_HEAD,  # noqa: F401
+                   EPI_STORE, EPI_TANGENT)
 
 SQRT2 = float(math.sqrt(2.0))  # torch's x / np.sqrt(2) divides by the fp32 rounding of this
 
@@ -50,7 +50,7 @@ class KernelTimer:
 
 _timer = None
 EPI_NAMES = {0: "store", 1: "softplus", 2: "relu", 3: "mul", 4: "tangent", 5: "bwd_softplus", 6: "bwd_relu",
-             7: "bench_mainloop"}
+             7: "bench_mainloop", 8: "softplus_head"}
 
 
 def set_kernel_timer(t):
@@ -164,7 +164,8 @@ class ImagePacker:
 
 def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None, colv=None, aux0=None,
            aux1=None, aux2=None, out_split=None, nsplit=None, nzero=None, adiv=1.0, odiv=1.0, beta=100.0,
-           threshold=20.0, aux_beta=0.0, aux2_scale=0.0, tile=None, M=None, kalg=None):
+           threshold=20.0, aux_beta=0.0, aux2_scale=0.0, tile=None, M=None, kalg=None, out1=None, head_w=None,
+           head_b=None, head_out=None, head_idx=None):
     """out = epilogue((A|A2) @ B[:N].T / adiv) -- cn_linear.  MUL / TANGENT /
     BWD_SOFTPLUS read softplus' as sg = 1 - exp(-aux_beta * aux0) from the stored
     softplus output aux0 (include/copenerf.h).  kalg: the unpadded
@@ -172,13 +173,18 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     selects the bf16 MFMA path (A rounded to bf16 on load, fp32 accumulate); K is
     then rounded up to 64, so A's columns up to that must exist (zero padding).
     A [K/16, N, 48] bfloat16 B (split_bf16x3) selects CN_MFMA_F32_BF16X6: the fp32
-    GEMM computed from three bf16 terms per operand on the bf16 MFMA."""
+    GEMM computed from three bf16 terms per operand on the bf16 MFMA.
+    EPI_SOFTPLUS_HEAD (the last SDF hidden layer): out0 = softplus activation (or
+    None: not stored), out1 = colv * softplus' (or None), head_out[head_idx[m] or m]
+    = out0[m] · head_w + head_b."""
     x6 = B.dim() == 3
     if x6 and (B.dtype != torch.bfloat16 or B.shape[2] != 48 or not B.is_contiguous()):
         raise RuntimeError(f"cn_linear: a 3-D B must be split_bf16x3's [K/16, N, 48] bfloat16 image (got "
                            f"{tuple(B.shape)}, {B.dtype}, strides {B.stride()})")
+    if out0 is None and epilogue != EPI_SOFTPLUS_HEAD:
+        raise RuntimeError("cn_linear: out0 is required")
     for t, n in ((A, "A"), (A2, "A2"), (B, "B"), (out0, "out0"), (aux0, "aux0"), (aux1, "aux1"), (aux2, "aux2"),
-                 (out_split, "out_split")):
+                 (out_split, "out_split"), (out1, "out1")):
         _need(t, n, ndim=3 if (x6 and t is B) else 2)
         if t is not None and t is not B and t.dtype == torch.bfloat16:
             raise RuntimeError(f"cn_linear: {n} must be float32 (only B may be bfloat16)")
@@ -198,16 +204,30 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     b_rows, b_k = (B.shape[1], 16 * B.shape[0]) if x6 else (B.shape[0], B.shape[1])
     if b_rows < rup(N, bn) or b_k < K:
         raise RuntimeError(f"cn_linear: B {tuple(B.shape)} too small for N={N}, K={K} (tile {tile})")
-    if out0.shape[0] < M:
-        raise RuntimeError("cn_linear: out0 has fewer rows than A")
+    if (out0 is not None and out0.shape[0] < M) or (out1 is not None and out1.shape[0] < M):
+        raise RuntimeError("cn_linear: out0 / out1 has fewer rows than A")
+    if epilogue == EPI_SOFTPLUS_HEAD:
+        _need(head_w, "head_w", ndim=1)
+        _need(head_b, "head_b", ndim=1)
+        _need(head_out, "head_out", ndim=1)
+        if not head_out.is_contiguous():
+            raise RuntimeError("cn_linear: head_out must be contiguous")
+        if head_w.numel() < N or head_w.stride(0) != 1:
+            raise RuntimeError("cn_linear: head_w must be a contiguous [N] vector")
+        if head_idx is None and head_out.numel() < M:
+            raise RuntimeError("cn_linear: head_out has fewer than M elements")
+        if head_idx is not None and (head_idx.dtype != torch.int32 or head_idx.numel() < M):
+            raise RuntimeError("cn_linear: head_idx must be int32 with M elements")
+        head_w = head_w if head_w.data_ptr() % 16 == 0 else head_w.clone()
     d = _lib.LinearDesc()
     d.A, d.A2, d.B, d.bias = _ptr(A), _ptr(A2), _ptr(B), _ptr(bias)
     d.rowv, d.colv, d.aux0, d.aux1 = _ptr(rowv), _ptr(colv), _ptr(aux0), _ptr(aux1)
-    d.out0, d.out1, d.out_split = _ptr(out0), None, _ptr(out_split)
+    d.out0, d.out1, d.out_split = _ptr(out0), _ptr(out1), _ptr(out_split)
+    d.head_w, d.head_b, d.head_out, d.head_idx = _ptr(head_w), _ptr(head_b), _ptr(head_out), _ptr(head_idx)
     d.aux2, d.ld_aux2 = _ptr(aux2), _ld(aux2)
     d.aux_beta, d.aux2_scale = aux_beta, aux2_scale
     d.lda, d.lda2, d.ldb = _ld(A), _ld(A2), (B.shape[1] if x6 else _ld(B))
-    d.ld_aux0, d.ld_aux1, d.ld_out0, d.ld_out1, d.ld_split = _ld(aux0), _ld(aux1), _ld(out0), 0, _ld(out_split)
+    d.ld_aux0, d.ld_aux1, d.ld_out0, d.ld_out1, d.ld_split = _ld(aux0), _ld(aux1), _ld(out0), _ld(out1), _ld(out_split)
     d.M, d.N, d.K = M, N, K
     d.K1 = K1 if K1 is not None else K
     d.nzero = nzero if nzero is not None else N
@@ -222,8 +242,9 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
         ka = kalg or K
         # algorithmic HBM bytes: A (unpadded K) and every aux row read once, each output
         # element written once, the weight image once (bf16x6: 3 bf16 terms per weight)
-        nb = 4.0 * M * ka + (6.0 if x6 else 2.0 if bf else 4.0) * N * ka + 4.0 * M * N
-        nb += 4.0 * M * N * sum(t is not None for t in (aux0, aux1, aux2)) + (4.0 * M if rowv is not None else 0.0)
+        nb = 4.0 * M * ka + (6.0 if x6 else 2.0 if bf else 4.0) * N * ka
+        nb += 4.0 * M * N * sum(t is not None for t in (out0, out1, aux0, aux1, aux2))
+        nb += 4.0 * M * ((rowv is not None) + (head_out is not None) + (head_idx is not None))
         _timer.stop(key + ((M, N, K),) if _timer.detail else key, e0, 2.0 * M * N * ka, nb)
     else:
         _lib.check(_lib.load().cn_linear(d, _stream()), "cn_linear")

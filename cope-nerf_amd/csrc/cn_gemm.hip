@@ -45,6 +45,10 @@ struct LinearArgs {
     float aux_c;       // -aux_beta * log2(e): sigma = 1 - 2^(aux_c * aux0)
     float aux2_scale;  // BWD_SOFTPLUS second-order term scale
     int stagger;       // odd workgroups start this many s_sleep(127) later (epilogue / main-loop desync)
+    const float* head_w;  // SOFTPLUS_HEAD: row-dot weights [N], bias [1], output, destination rows
+    const float* head_b;
+    float* head_out;
+    const int* head_idx;
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -174,6 +178,12 @@ __device__ __forceinline__ void tile_coords(int vt, int T, int& tm, int& tn) {
 #ifndef X6_EXP
 #define X6_EXP 0  // benchmark-only ablations of the bf16x6 main loop (tools/x6_ablation.sh)
 #endif
+#ifndef DIRECT_EPI
+#define DIRECT_EPI 1  // aux-free epilogues of main tiles store from the MFMA layout (no LDS park)
+#endif
+#ifndef EPI_EXP
+#define EPI_EXP 0  // benchmark-only: 1 = epilogue without its global stores (tools/ab_libs.sh)
+#endif
 #ifndef LSTORE_ALWAYS
 #define LSTORE_ALWAYS 0  // 1: branch-free staging (measured: main loop -1.5 %, epilogue variants +2-3 %)
 #endif
@@ -212,13 +222,18 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     // so its only VMEM waits are for the aux rows it reads (the compiler's vmcnt for a
     // per-tile bias load, under the divergent region branch, was a full drain before every
     // pass -- each pass waited for the previous pass's stores)
-    constexpr bool kBias = EPI == CN_EPI_STORE || EPI == CN_EPI_SOFTPLUS || EPI == CN_EPI_RELU;
-    constexpr int TBL = (kBias ? kTblCols : 0) + (ROWV ? kTblCols : 0);
+    // (SOFTPLUS_HEAD: + the head weights and bias; its rows fit one tile, N <= 256)
+    constexpr bool kHead = EPI == CN_EPI_SOFTPLUS_HEAD;
+    constexpr bool kBias = EPI == CN_EPI_STORE || EPI == CN_EPI_SOFTPLUS || EPI == CN_EPI_RELU || kHead;
+    constexpr bool kColv = ROWV || kHead;
+    constexpr int TBLC = kHead ? 256 : kTblCols;
+    constexpr int TBL = (kBias ? TBLC : 0) + (kColv ? TBLC : 0) + (kHead ? TBLC + 4 : 0);
     __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS + TBL];
     float* sA = smem;
     float* sB = smem + 2 * BM * LS;
     float* sBias = smem + LDS_FLOATS;
-    float* sColv = smem + LDS_FLOATS + (kBias ? kTblCols : 0);
+    float* sColv = sBias + (kBias ? TBLC : 0);
+    float* sHeadW = sColv + (kColv ? TBLC : 0);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -360,11 +375,14 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     if (vt >= ntiles) return;
     if constexpr (TBL > 0) {  // visible after the first tile's staging barrier
         const rsrc_t rbias = make_view(p.bias, kBias && p.bias ? p.N * 4 : 0);
-        const rsrc_t rcolv = make_view(p.colv, ROWV ? p.N * 4 : 0);
-        for (int i = tid; i < kTblCols / 4; i += NT) {
+        const rsrc_t rcolv = make_view(p.colv, kColv && p.colv ? p.N * 4 : 0);
+        const rsrc_t rhw = make_view(p.head_w, kHead ? p.N * 4 : 0);
+        for (int i = tid; i < TBLC / 4; i += NT) {
             if (kBias) *reinterpret_cast<floatx4*>(sBias + 4 * i) = bload4(rbias, 16 * i, 0);
-            if (ROWV) *reinterpret_cast<floatx4*>(sColv + 4 * i) = bload4(rcolv, 16 * i, 0);
+            if (kColv) *reinterpret_cast<floatx4*>(sColv + 4 * i) = bload4(rcolv, 16 * i, 0);
+            if (kHead) *reinterpret_cast<floatx4*>(sHeadW + 4 * i) = bload4(rhw, 16 * i, 0);
         }
+        if (kHead && tid == 0) sHeadW[TBLC] = p.head_b[0];
     }
     // stagger: with 2 workgroups per CU, the second resident one (block ids past the first
     // gridDim / 2 fill the CUs' second slots) starts later; with 1 per CU, the odd ones
@@ -372,12 +390,18 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
     int tm, tn;
     tile_coords(vt, T, tm, tn);
-    gload(0, 0, tm * BM, tn * BN, true);
-    // (see the end of the tile loop: set 0 enters the loop as an asm-defined value on both paths)
+    // the first DEPTH chunks of a tile are in the register sets when its loop starts (the next
+    // tile's are fetched during the current tile's last DEPTH chunks); see the end of the tile
+    // loop for the asm re-definition (the sets enter the loop as asm-defined values on both paths)
 #pragma unroll
-    for (int q = 0; q < ALD; ++q) asm volatile("" : "+v"(ra[0][q]));
+    for (int d = 0; d < DEPTH; ++d) gload(d, d, tm * BM, tn * BN, true);
 #pragma unroll
-    for (int q = 0; q < BLD; ++q) asm volatile("" : "+v"(rb[0][q]));
+    for (int d = 0; d < DEPTH; ++d) {
+#pragma unroll
+        for (int q = 0; q < ALD; ++q) asm volatile("" : "+v"(ra[d][q]));
+#pragma unroll
+        for (int q = 0; q < BLD; ++q) asm volatile("" : "+v"(rb[d][q]));
+    }
 
     while (vt < ntiles) {
         const int m0 = tm * BM, n0 = tn * BN;
@@ -387,8 +411,6 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 
         lstore(0, 0);
         __syncthreads();
-#pragma unroll
-        for (int d = 1; d < DEPTH; ++d) gload(d, d, m0, n0, true);  // nk is a multiple of DEPTH
 
         floatx16 acc[TM][TN];
 #pragma unroll
@@ -492,14 +514,16 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         } else {
             // DEPTH register sets: chunks c+1 .. c+DEPTH-1 are in flight while chunk c
             // is computed from LDS buffer c&1; set c%DEPTH (already in LDS) then takes
-            // chunk c+DEPTH, or the next tile's first chunk when c+DEPTH == nk.
+            // chunk c+DEPTH, or the next tile's chunk c+DEPTH-nk past the end.
             static_assert(DEPTH % 2 == 0, "LDS buffer of chunk kc+j is j&1");
             for (int kc = 0; kc < nk; kc += DEPTH) {
 #pragma unroll
                 for (int j = 0; j < DEPTH; ++j) {
                     const int cn = kc + j + DEPTH;
                     const bool here = cn < nk;
-                    gload(j, here ? cn : 0, here ? m0 : m_next, here ? n0 : n_next, here || (cn == nk && has_next));
+                    // past this tile: chunk cn - nk of the next one, issued before this tile's
+                    // epilogue stores, so the next tile's first DEPTH stagings never wait for them
+                    gload(j, here ? cn : cn - nk, here ? m0 : m_next, here ? n0 : n_next, here || has_next);
                     compute(j & 1);
                     // unconditional (branch-free: compute and the next stage's staging share a
                     // basic block, so the scheduler can interleave the split VALU / LDS writes
@@ -544,7 +568,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         // row = (r&3) + 8*(r>>2) + 4*(lane>>5).
         const int rows = min(BM, p.M - m0);
         // per-tile views, re-based on the pass's first row by SALU arithmetic (view_at)
-        const TileView tO0 = {p.out0 + (int64_t)m0 * p.ld_out0 + n0, p.ld_out0, (rows * p.ld_out0 - n0) * 4};
+        const TileView tO0 = {p.out0 + (int64_t)m0 * p.ld_out0 + n0, p.ld_out0, p.out0 ? (rows * p.ld_out0 - n0) * 4 : 0};
         const TileView tO1 = {p.out1 + (int64_t)m0 * p.ld_out1 + n0, p.ld_out1, p.out1 ? (rows * p.ld_out1 - n0) * 4 : 0};
         const TileView tX0 = {p.aux0 + (int64_t)m0 * p.ld_aux0 + n0, p.ld_aux0, p.aux0 ? (rows * p.ld_aux0 - n0) * 4 : 0};
         const TileView tX1 = {p.aux1 + (int64_t)m0 * p.ld_aux1 + n0, p.ld_aux1, p.aux1 ? (rows * p.ld_aux1 - n0) * 4 : 0};
@@ -558,10 +582,13 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         const int col = n0 + 4 * c4;
         const int region = col < Nmain ? 0 : (col < p.N ? 1 : (col < p.nzero ? 2 : 3));
         // (columns >= N read zeros from the table: their lanes are not region 0 anyway)
-        const int tcol = min(col, kTblCols - 4);
-        floatx4 bias = {0.f, 0.f, 0.f, 0.f}, colv = {0.f, 0.f, 0.f, 0.f};
+        const int tcol = min(col, TBLC - 4);
+        floatx4 bias = {0.f, 0.f, 0.f, 0.f}, colv = {0.f, 0.f, 0.f, 0.f}, hw = {0.f, 0.f, 0.f, 0.f};
         if (kBias) bias = *reinterpret_cast<const floatx4*>(sBias + tcol);
-        if (ROWV) colv = *reinterpret_cast<const floatx4*>(sColv + tcol);
+        if (kColv) colv = *reinterpret_cast<const floatx4*>(sColv + tcol);
+        if (kHead) hw = *reinterpret_cast<const floatx4*>(sHeadW + tcol);
+        const float hb = kHead ? sHeadW[TBLC] : 0.0f;
+        const TileView tI = {reinterpret_cast<const float*>(p.head_idx) + m0, 1, kHead && p.head_idx ? rows * 4 : 0};
         float* sC = smem;
         // aux rows of an epilogue group, double-buffered: group g+1's loads are issued
         // before group g's stores, so waiting for them never waits for those stores
@@ -570,6 +597,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         constexpr int NG = PROWS / RPP / GROUP;
         floatx4 x0[2][GROUP], x1[2][GROUP], x2[2][GROUP];
         float rv[2][GROUP];
+        int hidx[2][GROUP];
         auto aux_load = [&](int part, int g, int slot) {
 #pragma unroll
             for (int q = 0; q < GROUP; ++q) {
@@ -580,9 +608,10 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 if (kAux1) x1[slot][q] = bload4(view_at(tX1, lrow), voX1, 0);
                 if (kAux1) x2[slot][q] = bload4(view_at(tX2, lrow), voX2, 0);
                 if (ROWV) rv[slot][q] = bload1(view_at(tR, lrow), rr * 4, 0);
+                if (kHead) hidx[slot][q] = __builtin_bit_cast(int, bload1(view_at(tI, lrow), rr * 4, 0));
             }
         };
-        constexpr bool kAnyAux = kAux0 || kAux1 || ROWV;
+        constexpr bool kAnyAux = kAux0 || kAux1 || ROWV || kHead;
         // main-region values of pass q of a group (the EPI's math on 4 columns)
         auto main_vals = [&](const floatx4& v, int slot, int q, floatx4& o0) {
 #pragma unroll
@@ -593,7 +622,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 if (ROWV) u = u + rv[slot][q] * colv[e];
                 if constexpr (EPI == CN_EPI_STORE) {
                     o0[e] = u + bias[e];
-                } else if constexpr (EPI == CN_EPI_SOFTPLUS) {
+                } else if constexpr (EPI == CN_EPI_SOFTPLUS || kHead) {
                     o0[e] = softplus_hw(u + bias[e], c_exp, c_thr, c_log) * p.inv_odiv;
                 } else if constexpr (EPI == CN_EPI_RELU) {
                     const float z = u + bias[e];
@@ -632,6 +661,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                     if (kAux1) asm volatile("" ::"v"(x1[sl][q]));
                     if (kAux1) asm volatile("" ::"v"(x2[sl][q]));
                     if (ROWV) asm volatile("" ::"v"(rv[sl][q]));
+                    if (kHead) asm volatile("" ::"v"(hidx[sl][q]));
                 }
         };
         auto passes = [&](auto main_tag) {
@@ -664,8 +694,38 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         const int lrow = part * PROWS + (pb + q) * RPP;
                         const floatx4 v = *reinterpret_cast<const floatx4*>(sC + (rr + (pb + q) * RPP) * CS + 4 * c4);
                         floatx4 o0;
+                        if constexpr (kHead) {  // the row's activation, the ∇-pass seed, the head row-dot
+                            float part = 0.0f;
+                            if (MAIN || region == 0) {
+                                main_vals(v, slot, q, o0);
+                                bstore4(view_at(tO0, lrow), voO0, 0, o0);  // (out0 NULL: empty view)
+                                floatx4 s1;
+#pragma unroll
+                                for (int e = 0; e < 4; ++e) {
+                                    part += o0[e] * hw[e];
+                                    s1[e] = colv[e] * sigma_from_act(o0[e], p.aux_c);
+                                }
+                                bstore4(view_at(tO1, lrow), voO1, 0, s1);  // (out1 NULL: empty view)
+                            } else if (region == 2) {
+                                bstore4(view_at(tO0, lrow), voO0, 0, floatx4{0.f, 0.f, 0.f, 0.f});
+                                bstore4(view_at(tO1, lrow), voO1, 0, floatx4{0.f, 0.f, 0.f, 0.f});
+                            }
+                            // row sum over the C4 lanes holding the row (fixed butterfly order)
+#pragma unroll
+                            for (int off = C4 / 2; off > 0; off >>= 1) part += __shfl_xor(part, off, 64);
+                            const int row = m0 + lrow + rr;
+                            if (c4 == 0 && row < p.M) {
+                                const int dst = p.head_idx ? hidx[slot][q] : row;
+                                p.head_out[dst] = part + hb;
+                            }
+                            continue;
+                        }
                         if constexpr (MAIN) {
                             main_vals(v, slot, q, o0);
+                            if (EPI_EXP == 1) {  // keep the values live without a global store
+                                asm volatile("" ::"v"(o0));
+                                continue;
+                            }
                             bstore4(view_at(tO0, lrow), voO0, 0, o0);
                         } else if (region == 0) {
                             main_vals(v, slot, q, o0);
@@ -683,9 +743,38 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             }
             if constexpr (!MAIN && kAnyAux) consume_aux();
         };
-        if (tile_main) passes(std::true_type{});
-        else passes(std::false_type{});
-        __syncthreads();  // sC is the next tile's staging buffer
+        // Direct epilogue (main tiles of the aux-free epilogues): every accumulator element
+        // goes out from the MFMA layout itself -- lane l holds column l&31 of rows (r&3) +
+        // 8(r>>2) + 4(l>>5), so one dword store per (i, j, r) writes two full 128-byte row
+        // segments -- with no LDS park, no barrier and no readback.
+        constexpr bool kDirect = DIRECT_EPI && !kAnyAux && EPI != 7;
+        if (kDirect && tile_main) {
+            const int lrow = wm * TM * 32 + 4 * (lane >> 5);
+            const int lcol = wn * TN * 32 + (lane & 31);
+            const int vo = (lrow * p.ld_out0 + lcol) * 4;
+            float bj[TN];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bj[j] = kBias ? sBias[min(n0 + lcol + 32 * j, kTblCols - 1)] : 0.0f;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const rsrc_t vw = view_at(tO0, i * 32 + (r & 3) + 8 * (r >> 2));
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        const float z = acc[i][j][r] * p.inv_adiv + bj[j];
+                        float o;
+                        if constexpr (EPI == CN_EPI_SOFTPLUS) o = softplus_hw(z, c_exp, c_thr, c_log) * p.inv_odiv;
+                        else if constexpr (EPI == CN_EPI_RELU) o = z > 0.0f ? z : 0.0f;
+                        else o = z;
+                        bstore1(vw, vo, 128 * j, o);
+                    }
+                }
+        } else {
+            if (tile_main) passes(std::true_type{});
+            else passes(std::false_type{});
+            __syncthreads();  // sC is the next tile's staging buffer
+        }
         vt = vt_next;
         tm = tm_next;
         tn = tn_next;
@@ -1521,6 +1610,10 @@ static int g_wide_epis = [] {
 template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int MODE = 0>
 static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_t s) {
     constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
+    if (d->epilogue == CN_EPI_SOFTPLUS_HEAD && d->N > BN) {
+        set_error("cn_linear: SOFTPLUS_HEAD with N=%d needs a tile of >= N columns (this mode / tile: %d)", d->N, BN);
+        return CN_ERR_UNSUPPORTED;
+    }
     a.n_tiles_m = cdiv(d->M, BM);
     a.n_tiles_n = cdiv(d->N, BN);
     const int ntiles = cdiv(a.n_tiles_m, 8) * 8 * a.n_tiles_n;
@@ -1544,6 +1637,7 @@ static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_
         CN_EPI_CASE(CN_EPI_TANGENT)
         CN_EPI_CASE(CN_EPI_BWD_SOFTPLUS)
         CN_EPI_CASE(CN_EPI_BWD_RELU)
+        CN_EPI_CASE(CN_EPI_SOFTPLUS_HEAD)
 #undef CN_EPI_CASE
         case 7: linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, 7, false, MODE><<<grid, block, 0, s>>>(a); break;
         default: set_error("cn_linear: bad epilogue %d", d->epilogue); return CN_ERR_ARG;
@@ -1555,7 +1649,8 @@ static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     CN_REQUIRE(d, CN_ERR_ARG, "cn_linear: null desc");
-    CN_REQUIRE(d->A && d->B && d->out0, CN_ERR_ARG, "cn_linear: A, B and out0 are required");
+    const bool head = d->epilogue == CN_EPI_SOFTPLUS_HEAD;
+    CN_REQUIRE(d->A && d->B && (d->out0 || head), CN_ERR_ARG, "cn_linear: A, B and out0 are required");
     CN_REQUIRE(d->M >= 0 && d->N > 0 && d->K > 0, CN_ERR_SHAPE, "cn_linear: bad M/N/K %d/%d/%d", d->M, d->N, d->K);
     CN_REQUIRE(d->mfma_dtype == CN_MFMA_F32 || d->mfma_dtype == CN_MFMA_BF16 || d->mfma_dtype == CN_MFMA_F32_BF16X6,
                CN_ERR_ARG, "cn_linear: bad mfma_dtype %d", d->mfma_dtype);
@@ -1576,13 +1671,25 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     const int bn = d->tile == 0 ? 128 : 64;
     CN_REQUIRE(nzero <= cdiv(d->N, bn) * bn, CN_ERR_SHAPE,
                "cn_linear: nzero=%d beyond the column tiles covering N=%d (tile width %d)", nzero, d->N, bn);
-    CN_REQUIRE(d->ld_out0 >= nzero, CN_ERR_SHAPE, "cn_linear: ld_out0=%lld < nzero=%d", (long long)d->ld_out0, nzero);
+    CN_REQUIRE(!d->out0 || d->ld_out0 >= nzero, CN_ERR_SHAPE, "cn_linear: ld_out0=%lld < nzero=%d",
+               (long long)d->ld_out0, nzero);
     const int e = d->epilogue;
     if (e == CN_EPI_MUL || e == CN_EPI_TANGENT || e == CN_EPI_BWD_SOFTPLUS || e == CN_EPI_BWD_RELU)
         CN_REQUIRE(d->aux0 && d->ld_aux0 >= d->N, CN_ERR_ARG, "cn_linear: epilogue %d needs aux0", e);
     if (e == CN_EPI_MUL || e == CN_EPI_TANGENT || e == CN_EPI_BWD_SOFTPLUS)
         CN_REQUIRE(d->aux_beta > 0.0f, CN_ERR_ARG, "cn_linear: epilogue %d needs aux_beta > 0 (sigma from aux0)", e);
-    CN_REQUIRE(d->out1 == nullptr, CN_ERR_ARG, "cn_linear: out1 is not produced by any epilogue (ABI v4)");
+    CN_REQUIRE(d->out1 == nullptr || head, CN_ERR_ARG, "cn_linear: out1 is produced by SOFTPLUS_HEAD only");
+    if (head) {
+        CN_REQUIRE(d->head_w && d->head_b && d->head_out && !d->rowv && al16(d->head_w), CN_ERR_ARG,
+                   "cn_linear: SOFTPLUS_HEAD needs head_w (16B aligned), head_b, head_out and no rowv");
+        CN_REQUIRE(d->N <= 256 && (d->odiv == 0.0f || d->odiv == 1.0f), CN_ERR_UNSUPPORTED,
+                   "cn_linear: SOFTPLUS_HEAD needs N <= 256 (N=%d) and odiv 1", d->N);
+        if (d->out1)
+            CN_REQUIRE(d->colv && d->aux_beta > 0.0f && d->ld_out1 >= nzero && al16(d->out1) && d->ld_out1 % 4 == 0,
+                       CN_ERR_ARG, "cn_linear: SOFTPLUS_HEAD out1 needs colv, aux_beta > 0 and ld_out1 >= nzero");
+    } else {
+        CN_REQUIRE(!d->head_out && !d->head_w && !d->head_idx, CN_ERR_ARG, "cn_linear: head_* only for SOFTPLUS_HEAD");
+    }
     if (e == CN_EPI_BWD_SOFTPLUS)
         CN_REQUIRE((d->aux1 == nullptr) == (d->aux2 == nullptr) &&
                        (!d->aux1 || (d->ld_aux1 >= d->N && d->ld_aux2 >= d->N)),
@@ -1592,7 +1699,7 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     if (e == CN_EPI_MUL && d->nsplit < d->N)
         CN_REQUIRE(d->out_split && d->nsplit >= 0 && d->ld_split >= d->N - d->nsplit, CN_ERR_ARG,
                    "cn_linear: split output required");
-    CN_REQUIRE((d->rowv == nullptr) == (d->colv == nullptr), CN_ERR_ARG, "cn_linear: rowv/colv go together");
+    CN_REQUIRE((d->rowv == nullptr) == (d->colv == nullptr) || head, CN_ERR_ARG, "cn_linear: rowv/colv go together");
     CN_REQUIRE(al16(d->bias) && al16(d->colv), CN_ERR_ALIGN, "cn_linear: bias / colv must be 16-byte aligned");
     CN_REQUIRE((!d->bias && !d->colv) || d->N <= kTblCols, CN_ERR_UNSUPPORTED,
                "cn_linear: N=%d > %d with a bias / colv", d->N, kTblCols);
@@ -1620,6 +1727,7 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     a.aux_c = -d->aux_beta * 1.44269504088896341f;
     a.aux2_scale = d->aux2_scale;
     a.stagger = g_stagger;
+    a.head_w = d->head_w; a.head_b = d->head_b; a.head_out = d->head_out; a.head_idx = d->head_idx;
     a.ld_out0 = (int)d->ld_out0; a.ld_out1 = (int)d->ld_out1; a.ld_split = (int)d->ld_split;
     a.M = d->M; a.N = d->N; a.K = d->K; a.K1 = K1; a.nzero = nzero;
     a.nsplit = (e == CN_EPI_MUL && d->out_split) ? d->nsplit : d->N;
@@ -1646,7 +1754,7 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
             // 128x256 ("tall-N") tiles: one workgroup owns whole 256-wide output rows, so A is
             // read from HBM once (the two N-tiles of the 256x128 tiling re-fetch 30-50 % of it,
             // PMC) and split once per row
-            const bool tall = (g_x6_tall >> d->epilogue) & 1;
+            const bool tall = ((g_x6_tall >> d->epilogue) & 1) || (head && d->N > 128);
             if (d->K % 64 == 0 && tall && d->N > 128 && d->ldb >= 256 && g_linear_variant == 0)
                 return launch_linear_tile<4, 2, 1, 4, 32, 1, 2, 2>(d, a, s);
             if (d->K % 64 == 0 && g_linear_variant == 0 && light) return launch_linear_tile<4, 2, 2, 2, 32, 1, 2, 2>(d, a, s);

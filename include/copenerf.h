@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define CN_ABI_VERSION 4
+#define CN_ABI_VERSION 5
 
 typedef void* cn_stream_t; /* hipStream_t */
 
@@ -72,7 +72,14 @@ typedef enum cn_epilogue {
                                 aux1, aux2 both NULL or both set): with aux1 = s (the ∇-pass
                                 adjoint), aux2 = u' = sg*z'/c2 and aux2_scale = beta*c2 this is
                                 softplus' double-backward term beta*s*(1-sg)*z'  */
-    CN_EPI_BWD_RELU = 6      /* out0 = aux0 > 0 ? v : 0                              */
+    CN_EPI_BWD_RELU = 6,     /* out0 = aux0 > 0 ? v : 0                              */
+    CN_EPI_SOFTPLUS_HEAD = 8 /* the last SDF hidden layer with the sdf head fused (ABI v5):
+                                a = softplus_beta(v + bias) (odiv 1); out0 = a (or NULL: not
+                                stored); out1 = colv * sg(a) (or NULL: the ∇-pass seed
+                                s = w80 ⊙ softplus', aux_beta > 0); head_out[head_idx ?
+                                head_idx[m] : m] = Σ_n a[m][n] head_w[n] + head_b[0]
+                                (neus_fields.py:279-283, the sdf column of lin8); needs the
+                                whole row in one tile: N <= 256 (bf16x6) or N <= 128 */
 } cn_epilogue;
 
 typedef struct cn_linear_desc {
@@ -85,7 +92,7 @@ typedef struct cn_linear_desc {
     const float* aux0;
     const float* aux1;
     float* out0;
-    float* out1;         /* must be NULL (ABI v4: no epilogue writes a second output) */
+    float* out1;         /* SOFTPLUS_HEAD only (else NULL) */
     float* out_split;
     int64_t lda, lda2, ldb, ld_aux0, ld_aux1, ld_out0, ld_out1, ld_split;
     int32_t M, N, K, K1;
@@ -110,6 +117,10 @@ typedef struct cn_linear_desc {
     int64_t ld_aux2;
     float aux2_scale;
     int32_t reserved_;
+    const float* head_w;       /* SOFTPLUS_HEAD: [N] row-dot weights, head_b: [1] */
+    const float* head_b;
+    float* head_out;           /* [M] (or indexed by head_idx) */
+    const int32_t* head_idx;   /* [M] destination rows or NULL */
 } cn_linear_desc;
 
 enum cn_mfma_dtype { CN_MFMA_F32 = 0, CN_MFMA_BF16 = 1, CN_MFMA_F32_BF16X6 = 2 };

@@ -166,6 +166,41 @@ def test_row_head_colsum_scale_cols():
                                atol=1e-7)
 
 
+@pytest.mark.parametrize("N,x6", [(128, False), (256, True), (64, False), (256, False)])
+def test_softplus_head(N, x6):
+    """EPI_SOFTPLUS_HEAD: the last SDF hidden layer with the sdf head and the ∇-pass seed
+    in its epilogue -- a = softplus_100(A Bᵀ + b), out1 = colv ⊙ sg(a), head[idx[m]] =
+    a[m]·w + c -- against torch in float64; out0 may be absent; N = 256 needs the
+    bf16x6 128x256 tile (the fp32 mode's 128-wide tile is rejected)."""
+    ops = _ops()
+    M, K = 3000, 256
+    A = _rnd(M, K, seed=41, scale=0.1)
+    W = _rnd(N, K, seed=42, scale=0.05)
+    b = _rnd(N, seed=43, scale=0.05)
+    hw, hb, cv = _rnd(N, seed=44), _rnd(1, seed=45), _rnd(N, seed=46)
+    B = ops.split_bf16x3(W) if x6 else W
+    z = A.double() @ W.double().t() + b.double()
+    a_ref = torch.nn.functional.softplus(z, beta=100)
+    out0, out1 = torch.empty(M, N, device=DEV), torch.empty(M, N, device=DEV)
+    head = torch.empty(M, device=DEV)
+    kw = dict(bias=b, beta=100.0, threshold=20.0, head_w=hw, head_b=hb, head_out=head)
+    if N > 128 and not x6:
+        with pytest.raises(RuntimeError, match="SOFTPLUS_HEAD"):
+            ops.linear(A, B, N, K, out0, ops.EPI_SOFTPLUS_HEAD, **kw)
+        return
+    ops.linear(A, B, N, K, out0, ops.EPI_SOFTPLUS_HEAD, out1=out1, colv=cv, aux_beta=100.0, **kw)
+    torch.testing.assert_close(out0, a_ref.float(), rtol=1e-5, atol=2e-6)
+    sg = _sg(out0, 100.0)
+    torch.testing.assert_close(out1, (cv.double() * sg).float(), rtol=1e-5, atol=1e-7)
+    h_ref = out0.double() @ hw.double() + hb.double()
+    torch.testing.assert_close(head, h_ref.float(), rtol=1e-5, atol=1e-5)
+    # scattered, no stored activation: the same head values at the destination rows
+    perm = torch.randperm(M, generator=torch.Generator().manual_seed(7)).to(DEV).int()
+    head2 = torch.full((M,), float("nan"), device=DEV)
+    ops.linear(A, B, N, K, None, ops.EPI_SOFTPLUS_HEAD, **dict(kw, head_out=head2), head_idx=perm)
+    assert torch.equal(head2[perm.long()], head)
+
+
 def test_softplus_adjoint():
     """cn_softplus_adjoint: the adjoint of the last SDF hidden layer when the feature
     head is folded into the colour network -- (D + rowv colv) σ + c2 s1 s2 (1-σ)/σ,
