@@ -322,15 +322,19 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None):
         dW8[1:].zero_()
         db8[1:].zero_()
     dsdf_flat = None
+    # dW8[0] = Σ_m dsdf U8 (+ Ud8) / scale: fused into the adjoint kernel on the folded-head path
+    fused_cs = dh is not None and (dsdf is not None or second) and i8 == HL
     if dsdf is not None:
         dsdf = dsdf.reshape(M, 1).contiguous()
         dsdf_flat = dsdf
-        ops.colsum(U[L8], i8, dW8[0], w=dsdf, wdiv=lay.scale)
+        if not fused_cs:
+            ops.colsum(U[L8], i8, dW8[0], w=dsdf, wdiv=lay.scale)
         ops.colsum(dsdf, 1, db8[0:1], wdiv=lay.scale)
     else:
-        dW8[0].zero_()
+        if not fused_cs:
+            dW8[0].zero_()
         db8[0].zero_()
-    if second:
+    if second and not fused_cs:
         ops.colsum(Ud[L8], i8, dW8[0], wdiv=lay.scale, accumulate=True)
 
     def second_order(l):  # BWD_SOFTPLUS inputs of β s_l (1-σ_l) ż_l, ż_l = u̇_{l+1} c_l / σ_l
@@ -343,7 +347,8 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None):
         so = second_order(L8 - 1)
         ops.softplus_adjoint(U[L8], HL, Z, act_beta=sig_beta(lay, L8 - 1), D=dh, rowv=dsdf_flat,
                              colv=pk.w80p if dsdf_flat is not None else None, aux1=so.get("aux1"),
-                             aux2=so.get("aux2"), aux2_scale=so.get("aux2_scale", 0.0))
+                             aux2=so.get("aux2"), aux2_scale=so.get("aux2_scale", 0.0),
+                             cs_out=dW8[0] if fused_cs else None, cs_div=lay.scale)
     elif dfeat is None and not second and dsdf_flat is not None:
         # sdf only, first order (e.g. SDFNetwork.sdf at train.py:504): Z_7 = dsdf[m] w80[n] σ_7,
         # elementwise -- no GEMM over a zero feature gradient

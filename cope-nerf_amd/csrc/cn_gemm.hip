@@ -1433,6 +1433,58 @@ __global__ void __launch_bounds__(256) softplus_adjoint_kernel(int M, int N4, co
     }
 }
 
+// The same with the column sums of the sdf row of lin8's weight gradient: a block owns a
+// contiguous slab of rows and all N columns (256 threads = 256/(N/4) row lanes x N/4 float4
+// columns), accumulates Σ_m rowv[m] act[m][n] + aux2[m][n] per thread in fp32, combines its
+// row lanes in a fixed order through LDS and writes one partial row per block.
+constexpr int kSaRows = 512;  // rows per block of the column-sum form
+__global__ void __launch_bounds__(256) softplus_adjoint_cs_kernel(int M, int N4, const float* __restrict__ D,
+                                                                  int64_t ldd, const float* __restrict__ act,
+                                                                  int64_t lda, float aux_c,
+                                                                  const float* __restrict__ rowv,
+                                                                  const float* __restrict__ colv,
+                                                                  const float* __restrict__ aux1, int64_t ld1,
+                                                                  const float* __restrict__ aux2, int64_t ld2,
+                                                                  float c2, float* out, int64_t ldo, float* part) {
+    __shared__ floatx4 red[256];
+    const int c = threadIdx.x % N4;
+    const int rl = threadIdx.x / N4;
+    const int nrl = 256 / N4;
+    const int n = 4 * c;
+    const int m0 = blockIdx.x * kSaRows, m1 = min(M, m0 + kSaRows);
+    const floatx4 cv = colv ? *reinterpret_cast<const floatx4*>(colv + n) : floatx4{0.f, 0.f, 0.f, 0.f};
+    floatx4 cs = {0.f, 0.f, 0.f, 0.f};
+    if (rl < nrl) {
+        for (int m = m0 + rl; m < m1; m += nrl) {
+            const floatx4 a = *reinterpret_cast<const floatx4*>(act + (int64_t)m * lda + n);
+            floatx4 g = D ? *reinterpret_cast<const floatx4*>(D + (int64_t)m * ldd + n) : floatx4{0.f, 0.f, 0.f, 0.f};
+            const float rv = rowv ? rowv[m] : 0.0f;
+            g = g + rv * cv;
+            floatx4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
+            if (aux1) {
+                s1 = *reinterpret_cast<const floatx4*>(aux1 + (int64_t)m * ld1 + n);
+                s2 = *reinterpret_cast<const floatx4*>(aux2 + (int64_t)m * ld2 + n);
+            }
+            floatx4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float sg = sigma_from_act(a[e], aux_c);
+                const float rr = sg > 0.0f ? (1.0f - sg) * __builtin_amdgcn_rcpf(sg) : 0.0f;
+                o[e] = g[e] * sg + s1[e] * s2[e] * (c2 * rr);
+            }
+            *reinterpret_cast<floatx4*>(out + (int64_t)m * ldo + n) = o;
+            cs = cs + rv * a + s2;
+        }
+    }
+    red[threadIdx.x] = cs;
+    __syncthreads();
+    if (rl == 0) {
+        floatx4 t = red[c];
+        for (int r = 1; r < nrl; ++r) t = t + red[r * N4 + c];
+        *reinterpret_cast<floatx4*>(part + (int64_t)blockIdx.x * N4 * 4 + n) = t;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Colour head backward: sigmoid + Linear(256 -> 3) (neus_fields.py:367-373).
 // Block = 256 threads = one column each, over a slice of rows.
@@ -1551,16 +1603,26 @@ static bool wgrad_wide_on() {
     }();
     return on;
 }
-static bool wgrad_wide(const cn_wgrad_desc* d) {
+// 3 (bf16x6, K <= 64, Y rows 256-padded; COPENERF_WGRAD_NARROW=1): 256x64 tiles of 512-thread
+// workgroups.  Measured slower than the 128x64 tiles on the C2 first-layer shapes (0.418 vs
+// 0.388 ms, 0.207 vs 0.187 ms), so off by default.
+// Returns the wide mode: 0 none, 1 = 256x256, 2 = 256x64.
+static int wgrad_wide(const cn_wgrad_desc* d) {
+    static const bool narrow = [] {
+        const char* e = getenv("COPENERF_WGRAD_NARROW");
+        return e && atoi(e) != 0;
+    }();
     const int64_t np = (int64_t)cdiv(d->N, 256) * 256, kp = (int64_t)cdiv(d->K, 256) * 256;
-    return wgrad_wide_on() && d->mfma_dtype == CN_MFMA_F32_BF16X6 && d->ldy0 >= np && d->ldx0 >= kp &&
-           (d->npairs == 1 || (d->ldy1 >= np && d->ldx1 >= kp));
+    if (!wgrad_wide_on() || d->mfma_dtype != CN_MFMA_F32_BF16X6 || d->ldy0 < np || (d->npairs == 2 && d->ldy1 < np))
+        return 0;
+    if (d->ldx0 >= kp && (d->npairs == 1 || d->ldx1 >= kp)) return 1;
+    return narrow && d->K <= 64 ? 2 : 0;
 }
 
-static void wgrad_geometry(int M, int N, int K, bool wide, int* tile, int* Npad, int* Kpad, int* nslices,
+static void wgrad_geometry(int M, int N, int K, int wide, int* tile, int* Npad, int* Kpad, int* nslices,
                            int* rows_per_slice) {
-    const int t = wide ? 2 : (K % 128 == 0) ? 0 : 1;
-    const int BNo = t == 2 ? 256 : 128, BKo = t == 2 ? 256 : t == 0 ? 128 : 64;
+    const int t = wide == 1 ? 2 : wide == 2 ? 3 : (K % 128 == 0) ? 0 : 1;
+    const int BNo = t >= 2 ? 256 : 128, BKo = t == 2 ? 256 : t == 0 ? 128 : 64;
     *tile = t;
     *Npad = cdiv(N, BNo) * BNo;
     *Kpad = cdiv(K, BKo) * BKo;
@@ -1569,7 +1631,7 @@ static void wgrad_geometry(int M, int N, int K, bool wide, int* tile, int* Npad,
         const char* e = getenv("COPENERF_WGRAD_BLOCKS");
         return e ? atoi(e) : 512;
     }();
-    int ns = std::max(1, (t == 2 ? kTarget / 2 : kTarget) / tiles);
+    int ns = std::max(1, (t == 2 ? kTarget / 2 : kTarget) / tiles);  // (t 3: 2 workgroups per CU)
     ns = std::min(ns, std::max(1, cdiv(M, 512)));
     int rps = cdiv(cdiv(M, ns), 64) * 64;  // whole 32-row (fp32) / 64-row (bf16) chunks
     ns = std::max(1, cdiv(M, rps));
@@ -1774,9 +1836,9 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
 
 extern "C" size_t cn_wgrad_workspace_bytes(int32_t M, int32_t N, int32_t K) {
     size_t need = 0;  // the larger of the two tilings (the call's mfma_dtype picks one)
-    for (int w = 0; w < 2; ++w) {
+    for (int w = 0; w < 3; ++w) {
         int tile, Npad, Kpad, ns, rps;
-        wgrad_geometry(std::max(M, 1), N, K, w && wgrad_wide_on(), &tile, &Npad, &Kpad, &ns, &rps);
+        wgrad_geometry(std::max(M, 1), N, K, wgrad_wide_on() ? w : 0, &tile, &Npad, &Kpad, &ns, &rps);
         need = std::max(need, sizeof(float) * ((size_t)ns * Npad * Kpad + (size_t)ns * Npad));
     }
     return need;
@@ -1807,7 +1869,7 @@ extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
     a.bpart = d->db ? d->workspace + (size_t)ns * Npad * Kpad : nullptr;
     a.ldy0 = (int)d->ldy0; a.ldx0 = (int)d->ldx0; a.ldy1 = (int)d->ldy1; a.ldx1 = (int)d->ldx1;
     a.M = d->M; a.Npad = Npad; a.Kpad = Kpad; a.npairs = d->npairs; a.rows_per_slice = rps;
-    const int BNo = tile == 2 ? 256 : 128, BKo = tile == 2 ? 256 : tile == 0 ? 128 : 64;
+    const int BNo = tile >= 2 ? 256 : 128, BKo = tile == 2 ? 256 : tile == 0 ? 128 : 64;
     a.n_tiles_k = Kpad / BKo;
     a.n_tiles_n = Npad / BNo;
     a.nslices = ns;
@@ -1817,6 +1879,8 @@ extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
     if (d->mfma_dtype == CN_MFMA_F32_BF16X6) {
         if (tile == 2)
             wgrad_x6_kernel<4, 4><<<grid, 512, 0, s>>>(a);
+        else if (tile == 3)
+            wgrad_x6_kernel<4, 1><<<grid, 512, 0, s>>>(a);
         else if (tile == 0)
             wgrad_x6_kernel<2, 2><<<grid, 256, 0, s>>>(a);
         else
@@ -1870,10 +1934,15 @@ extern "C" int cn_scale_cols(int32_t M, int32_t N, const float* X, int64_t ldx, 
     return check_launch("cn_scale_cols");
 }
 
+extern "C" size_t cn_softplus_adjoint_workspace_bytes(int32_t M, int32_t N) {
+    return sizeof(float) * (size_t)std::max(1, cdiv(M, kSaRows)) * std::max(N, 4);
+}
+
 extern "C" int cn_softplus_adjoint(int32_t M, int32_t N, const float* D, int64_t ldd, const float* act, int64_t lda,
                                    float act_beta, const float* rowv, const float* colv, const float* aux1,
                                    int64_t ld1, const float* aux2, int64_t ld2, float aux2_scale, float* out,
-                                   int64_t ld_out, cn_stream_t stream) {
+                                   int64_t ld_out, float* cs_out, float cs_div, float* workspace,
+                                   int64_t workspace_bytes, cn_stream_t stream) {
     CN_REQUIRE(act && out && act_beta > 0.0f, CN_ERR_ARG, "cn_softplus_adjoint: act, out and act_beta > 0 required");
     CN_REQUIRE((rowv == nullptr) == (colv == nullptr) && (aux1 == nullptr) == (aux2 == nullptr), CN_ERR_ARG,
                "cn_softplus_adjoint: rowv/colv and aux1/aux2 go together");
@@ -1881,6 +1950,20 @@ extern "C" int cn_softplus_adjoint(int32_t M, int32_t N, const float* D, int64_t
                    (!D || (ldd % 4 == 0 && al16(D))) && (!colv || al16(colv)) &&
                    (!aux1 || (ld1 % 4 == 0 && ld2 % 4 == 0 && al16(aux1) && al16(aux2))),
                CN_ERR_ALIGN, "cn_softplus_adjoint: N, leading dimensions and pointers must be multiples of 4 floats");
+    if (cs_out) {
+        CN_REQUIRE(N >= 4 && N <= 1024 && workspace &&
+                       (size_t)workspace_bytes >= cn_softplus_adjoint_workspace_bytes(M, N),
+                   CN_ERR_SHAPE, "cn_softplus_adjoint: column sums need N <= 1024 and the workspace");
+        if (M == 0) return launch_slab_reduce(workspace, 0, N, 1, N, N, cs_out, N, 1.0f, 0, (hipStream_t)stream);
+        const int nblk = cdiv(M, kSaRows);
+        hipStream_t s = (hipStream_t)stream;
+        softplus_adjoint_cs_kernel<<<nblk, 256, 0, s>>>(M, N / 4, D, ldd, act, lda, -act_beta * 1.44269504088896341f,
+                                                        rowv, colv, aux1, ld1, aux2, ld2, aux2_scale, out, ld_out,
+                                                        workspace);
+        const int rc = check_launch("cn_softplus_adjoint");
+        if (rc) return rc;
+        return launch_slab_reduce(workspace, nblk, N, 1, N, N, cs_out, N, cs_div == 0.f ? 1.f : cs_div, 0, s);
+    }
     if ((int64_t)M * N == 0) return CN_OK;
     const int64_t tot = (int64_t)M * (N / 4);
     const int blocks = (int)std::min<int64_t>((tot + 255) / 256, 8192);

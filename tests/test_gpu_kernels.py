@@ -220,6 +220,17 @@ def test_softplus_adjoint():
     ref = (D.double() + rv.double()[:, None] * cv.double()) * sg + 0.7 * s1.double() * s2.double() * rr
     torch.testing.assert_close(out, ref.float(), rtol=1e-4, atol=1e-5)
     assert torch.isfinite(out).all()
+    # the column-sum form: same out, plus lin8's sdf-row gradient Σ_m rv act + s2, over a ragged M
+    for m in (M, 1537, 1):
+        out2, cs = torch.full((m, K), float("nan"), device=DEV), torch.empty(K, device=DEV)
+        ops.softplus_adjoint(act[:m], K, out2, act_beta=100.0, D=D[:m], rowv=rv[:m].contiguous(), colv=cv,
+                             aux1=s1[:m], aux2=s2[:m], aux2_scale=0.7, cs_out=cs, cs_div=2.0)
+        assert torch.equal(out2, out[:m])
+        cs_ref = (rv[:m].double()[:, None] * act[:m].double() + s2[:m].double()).sum(0) / 2.0
+        torch.testing.assert_close(cs, cs_ref.float(), rtol=1e-5, atol=1e-4)
+    cs2 = torch.empty(K, device=DEV)
+    ops.softplus_adjoint(act, K, out, act_beta=100.0, D=D, cs_out=cs2)  # no rowv / aux2: zero sums
+    assert torch.all(cs2 == 0)
 
 
 def test_c_abi_rejects_bad_arguments():

@@ -102,7 +102,7 @@ def test_sdf_field_x6_gradients_match_fp32():
 
 @pytest.mark.parametrize("M,N,K,pairs", [(70000, 256, 256, 2), (1000, 204, 64, 1), (5, 256, 256, 1),
                                          (4097, 256, 320, 1), (300, 52, 192, 2), (33, 128, 128, 2),
-                                         (2000, 256, 512, 2), (3000, 204, 256, 2)])
+                                         (2000, 256, 512, 2), (3000, 204, 256, 2), (70001, 256, 64, 2)])
 def test_wgrad_x6_matches_fp32_accuracy(M, N, K, pairs):
     """cn_wgrad in bf16x6 mode: dW's error against float64 within a small factor
     of the exact fp32 MFMA kernel's on the same inputs; db (summed from the fp32

@@ -12,7 +12,7 @@ from copenerf.train_step import SyntheticTrainer  # noqa: E402
 
 def main():
     steps = int(os.environ.get("STEPS", 5))
-    tr = SyntheticTrainer("cuda:0", rays=int(os.environ.get("RAYS", 4096)))
+    tr = SyntheticTrainer("cuda:0", rays=int(os.environ.get("RAYS", 4096)), mfma_dtype=os.environ.get("MODE", "bf16x6"))
     for _ in range(3):
         tr.step()
     torch.cuda.synchronize()
