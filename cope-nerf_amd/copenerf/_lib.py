@@ -45,7 +45,7 @@ class LinearDesc(ctypes.Structure):
         ("nzero", c_i32), ("nsplit", c_i32), ("epilogue", c_i32), ("tile", c_i32),
         ("adiv", c_f32), ("odiv", c_f32), ("beta", c_f32), ("threshold", c_f32),
         ("mfma_dtype", c_i32), ("aux_beta", c_f32), ("aux2", c_ptr), ("ld_aux2", c_i64),
-        ("aux2_scale", c_f32), ("reserved_", c_i32),
+        ("aux2_scale", c_f32), ("flags", c_i32),
         ("head_w", c_ptr), ("head_b", c_ptr), ("head_out", c_ptr), ("head_idx", c_ptr),
     ]
 

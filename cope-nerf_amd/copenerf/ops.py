@@ -49,6 +49,10 @@ class KernelTimer:
 
 
 _timer = None
+# cn_linear_desc.flags bit 0 alternated launch to launch (the memory-side cache holds the last
+# rows a layer wrote when the next one starts; see include/copenerf.h)
+ALTERNATE_TILE_ORDER = __import__("os").environ.get("COPENERF_ALT_ORDER", "1") != "0"
+_flip = 0
 EPI_NAMES = {0: "store", 1: "softplus", 2: "relu", 3: "mul", 4: "tangent", 5: "bwd_softplus", 6: "bwd_relu",
              7: "bench_mainloop", 8: "softplus_head"}
 
@@ -235,6 +239,10 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     d.epilogue, d.tile = epilogue, tile
     d.adiv, d.odiv, d.beta, d.threshold = adiv, odiv, beta, threshold
     d.mfma_dtype = 2 if x6 else (1 if bf else 0)
+    global _flip
+    if ALTERNATE_TILE_ORDER:  # consecutive launches walk the rows in opposite directions
+        _flip ^= 1
+        d.flags = _flip
     if _timer is not None:
         e0 = _timer.start()
         _lib.check(_lib.load().cn_linear(d, _stream()), "cn_linear")

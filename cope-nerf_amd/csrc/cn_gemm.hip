@@ -49,6 +49,7 @@ struct LinearArgs {
     const float* head_b;
     float* head_out;
     const int* head_idx;
+    int flags;
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -282,7 +283,12 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         const int k0 = kc * BK;
         const int rows = valid ? min(BM, p.M - m0) : 0;
         const bool second = k0 >= p.K1;  // wave-uniform: A2 half of a virtual concat
-        const float* abase = second ? p.A2 + (int64_t)m0 * p.lda2 : p.A + (int64_t)m0 * p.lda;
+#if X6_EXP == 6  // benchmark only: every tile reads A rows [0, 4096) (L2-resident: no HBM A traffic)
+        const int ma = m0 & 4095;
+#else
+        const int ma = m0;
+#endif
+        const float* abase = second ? p.A2 + (int64_t)ma * p.lda2 : p.A + (int64_t)ma * p.lda;
         const int ald = second ? p.lda2 : p.lda;
         const int ak = second ? k0 - p.K1 : k0;
         const rsrc_t rA = make_view(abase, rows * ald * 4);
@@ -336,10 +342,17 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             }
         }
     };
+    // flags bit 0: walk the M-tiles last to first (consecutive layers of a chain alternate, so
+    // a layer reads first the rows its producer wrote last, still in the memory-side cache)
+    const int ntm8 = ((p.n_tiles_m + 7) / 8) * 8;
+    auto coords = [&](int vt, int& tm, int& tn) {
+        tile_coords(vt, T, tm, tn);
+        if (p.flags & 1) tm = ntm8 - 1 - tm;
+    };
     auto next_valid = [&](int vt) {
         for (; vt < ntiles; vt += gridDim.x) {
             int tm, tn;
-            tile_coords(vt, T, tm, tn);
+            coords(vt, tm, tn);
             if (tm * BM < p.M) return vt;
         }
         return ntiles;
@@ -389,7 +402,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     if (OCC >= 2 ? (blockIdx.x >= gridDim.x / 2) : (blockIdx.x & 1))
         for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
     int tm, tn;
-    tile_coords(vt, T, tm, tn);
+    coords(vt, tm, tn);
     // the first DEPTH chunks of a tile are in the register sets when its loop starts (the next
     // tile's are fetched during the current tile's last DEPTH chunks); see the end of the tile
     // loop for the asm re-definition (the sets enter the loop as asm-defined values on both paths)
@@ -407,7 +420,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         const int m0 = tm * BM, n0 = tn * BN;
         const int vt_next = next_valid(vt + gridDim.x);
         int tm_next = 0, tn_next = 0;
-        if (vt_next < ntiles) tile_coords(vt_next, T, tm_next, tn_next);
+        if (vt_next < ntiles) coords(vt_next, tm_next, tn_next);
 
         lstore(0, 0);
         __syncthreads();
@@ -1790,6 +1803,7 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     a.aux2_scale = d->aux2_scale;
     a.stagger = g_stagger;
     a.head_w = d->head_w; a.head_b = d->head_b; a.head_out = d->head_out; a.head_idx = d->head_idx;
+    a.flags = d->flags;
     a.ld_out0 = (int)d->ld_out0; a.ld_out1 = (int)d->ld_out1; a.ld_split = (int)d->ld_split;
     a.M = d->M; a.N = d->N; a.K = d->K; a.K1 = K1; a.nzero = nzero;
     a.nsplit = (e == CN_EPI_MUL && d->out_split) ? d->nsplit : d->N;

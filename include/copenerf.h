@@ -116,7 +116,9 @@ typedef struct cn_linear_desc {
     const float* aux2;   /* BWD_SOFTPLUS second-order input u' (or NULL) */
     int64_t ld_aux2;
     float aux2_scale;
-    int32_t reserved_;
+    int32_t flags;       /* bit 0: visit the M-tiles last to first (a chain's consecutive launches
+                            alternate it so a layer first reads the rows its producer wrote last,
+                            still in the memory-side cache); results do not depend on it */
     const float* head_w;       /* SOFTPLUS_HEAD: [N] row-dot weights, head_b: [1] */
     const float* head_b;
     float* head_out;           /* [M] (or indexed by head_idx) */

@@ -41,6 +41,24 @@ def test_linear_store_matches_torch(M, N, K, tile):
     assert torch.all(out[:, N:] == 0)
 
 
+def test_linear_tile_order_does_not_change_results():
+    """cn_linear_desc.flags bit 0 (reverse M-tile walk, alternated launch to launch by
+    ops.linear): both walks give bitwise identical outputs, edge tiles included."""
+    ops = _ops()
+    if not ops.ALTERNATE_TILE_ORDER:
+        pytest.skip("COPENERF_ALT_ORDER=0")
+    M, N, K = 70001, 256, 256
+    A = _rnd(M, K, seed=51)
+    W = _rnd(N, K, seed=52, scale=0.05)
+    for B in (W, ops.split_bf16x3(W)):
+        outs = []
+        for _ in range(2):  # consecutive launches: opposite walks
+            o = torch.empty(M, N, device=DEV)
+            ops.linear(A, B, N, K, o, ops.EPI_SOFTPLUS, bias=W[0].contiguous(), beta=100.0)
+            outs.append(o)
+        assert torch.equal(outs[0], outs[1])
+
+
 def test_linear_virtual_concat_rank1_and_divisor():
     ops = _ops()
     M, K1, K2, N = 333, 256, 64, 256
