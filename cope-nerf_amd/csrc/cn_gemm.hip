@@ -1262,13 +1262,19 @@ __global__ void __launch_bounds__(128 * WM, 2) wgrad_x6_kernel(WgradArgs p) {
 // for r < rows, c < cols.  A workgroup owns 64 float4 column groups x 4 slab
 // groups; each thread sums its slab group in double with 4 loads in flight, the 4
 // groups combine through LDS in a fixed order (bitwise reproducible).
+// 256 threads = kSlabGroups slab groups x (256 / kSlabGroups) float4 column groups: slab
+// group sg sums slabs sg, sg + SG, ... in double, the groups meet in a fixed order in LDS.
+// (16 x 16: a 256-slab weight gradient is 16 loads per thread, 4x the blocks of a 4 x 64 split.)
+constexpr int kSlabGroups = 16;
 __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ part, int nslab, int64_t stride,
                                                           int rows, int cols, int64_t ldp, float* out, int64_t ldo,
                                                           float div, int accumulate) {
-    __shared__ double red[4][64][4];
+    constexpr int SG = kSlabGroups, CG = 256 / SG;
+    __shared__ double red[SG][CG][4];
     const int c4n = cdiv(cols, 4);
-    const int64_t g = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);  // float4 group over rows x c4n
-    const int sg = threadIdx.x >> 6;
+    const int t = threadIdx.x % CG;
+    const int sg = threadIdx.x / CG;
+    const int64_t g = (int64_t)blockIdx.x * CG + t;  // float4 group over rows x c4n
     const bool valid = g < (int64_t)rows * c4n;
     const int r = valid ? (int)(g / c4n) : 0;
     const int c = valid ? (int)(g % c4n) * 4 : 0;
@@ -1277,11 +1283,11 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restric
     if (valid) {
         const float* base = part + (int64_t)r * ldp + c;
         int sl = sg;
-        for (; sl + 12 < nslab; sl += 16) {
+        for (; sl + 3 * SG < nslab; sl += 4 * SG) {
             floatx4 v[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const float* q = base + (int64_t)(sl + 4 * u) * stride;
+                const float* q = base + (int64_t)(sl + SG * u) * stride;
                 if (vec) {
                     v[u] = *reinterpret_cast<const floatx4*>(q);
                 } else {
@@ -1293,17 +1299,17 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restric
 #pragma unroll
                 for (int e = 0; e < 4; ++e) a[e] += (double)v[u][e];
         }
-        for (; sl < nslab; sl += 4) {
+        for (; sl < nslab; sl += SG) {
             const float* q = base + (int64_t)sl * stride;
             for (int e = 0; e < 4; ++e) a[e] += (c + e < cols) ? (double)q[e] : 0.0;
         }
     }
-    for (int e = 0; e < 4; ++e) red[sg][threadIdx.x & 63][e] = a[e];
+    for (int e = 0; e < 4; ++e) red[sg][t][e] = a[e];
     __syncthreads();
     if (sg == 0 && valid) {
-        const int t = threadIdx.x & 63;
         for (int e = 0; e < 4 && c + e < cols; ++e) {
-            const double tot = ((red[0][t][e] + red[1][t][e]) + red[2][t][e]) + red[3][t][e];
+            double tot = red[0][t][e];
+            for (int q = 1; q < SG; ++q) tot += red[q][t][e];
             float v = (float)tot;
             if (div != 1.0f) v = v / div;
             float* o = out + (int64_t)r * ldo + c + e;
@@ -1317,8 +1323,9 @@ static int launch_slab_reduce(const float* part, int nslab, int64_t stride, int 
                               int64_t ldo, float div, int accumulate, hipStream_t s) {
     const int64_t groups = (int64_t)rows * cdiv(cols, 4);
     if (groups == 0) return CN_OK;
-    slab_reduce_kernel<<<(int)((groups + 63) / 64), 256, 0, s>>>(part, nslab, stride, rows, cols, ldp, out, ldo, div,
-                                                                 accumulate);
+    constexpr int CG = 256 / kSlabGroups;
+    slab_reduce_kernel<<<(int)((groups + CG - 1) / CG), 256, 0, s>>>(part, nslab, stride, rows, cols, ldp, out, ldo,
+                                                                     div, accumulate);
     return check_launch("slab_reduce");
 }
 
