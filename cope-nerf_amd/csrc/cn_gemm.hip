@@ -1507,62 +1507,76 @@ __global__ void __launch_bounds__(256) softplus_adjoint_cs_kernel(int M, int N4,
 
 // ---------------------------------------------------------------------------
 // Colour head backward: sigmoid + Linear(256 -> 3) (neus_fields.py:367-373).
-// Block = 256 threads = one column each, over a slice of rows.
+// Block = 256 threads = 4 row lanes x 64 float4 column groups (K <= 256) over a slice of
+// rows; the per-row sigmoid' factors are staged in LDS once, the row lanes' partial dW3 /
+// db3 sums meet in a fixed order.
 constexpr int kHeadRowsPerBlock = 256;
 
-__global__ void rgb_head_bwd_kernel(int M, int K, const float* __restrict__ drgb, const float* __restrict__ rgb,
-                                    const float* __restrict__ H3, int64_t ld_h, const float* __restrict__ W3,
-                                    float* dZ2, int64_t ld_dz, float* part /*[nblk][4][K]*/) {
-    const int k = threadIdx.x;
+__global__ void __launch_bounds__(256) rgb_head_bwd_kernel(int M, int K, const float* __restrict__ drgb,
+                                                           const float* __restrict__ rgb,
+                                                           const float* __restrict__ H3, int64_t ld_h,
+                                                           const float* __restrict__ W3, float* dZ2, int64_t ld_dz,
+                                                           float* part /*[nblk][4][K]*/) {
+    __shared__ float sd[kHeadRowsPerBlock][3];
+    __shared__ floatx4 red[4][64][3];
+    __shared__ float redb[4][3];
+    const int tid = threadIdx.x;
     const int m0 = blockIdx.x * kHeadRowsPerBlock;
     const int m1 = min(M, m0 + kHeadRowsPerBlock);
+    for (int i = tid; i < (m1 - m0) * 3; i += 256) {
+        const int64_t q = 3 * (int64_t)m0 + i;
+        const float y = rgb[q];
+        sd[i / 3][i % 3] = drgb[q] * (1.0f - y) * y;  // torch sigmoid_backward: grad * (1 - y) * y
+    }
+    __syncthreads();
+    const int c4 = tid & 63, rl = tid >> 6;
+    const int k = 4 * c4;
     const bool kv = k < K;
-    float w0 = 0.f, w1 = 0.f, w2 = 0.f;
+    floatx4 w0 = {0.f, 0.f, 0.f, 0.f}, w1 = w0, w2 = w0;
     if (kv) {
-        w0 = W3[k];
-        w1 = W3[K + k];
-        w2 = W3[2 * K + k];
+        w0 = *reinterpret_cast<const floatx4*>(W3 + k);
+        w1 = *reinterpret_cast<const floatx4*>(W3 + K + k);
+        w2 = *reinterpret_cast<const floatx4*>(W3 + 2 * K + k);
     }
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, ab = 0.f;
-    // 4 rows per iteration: their H3 loads are issued together (the sums keep row order)
-    constexpr int U = 4;
-    for (int mb = m0; mb < m1; mb += U) {
-        float hv[U], g[U][3], y[U][3];
+    floatx4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0;
+    float b0 = 0.f, b1 = 0.f, b2 = 0.f;
+    for (int m = m0 + rl; m < m1; m += 4) {
+        const float d0 = sd[m - m0][0], d1 = sd[m - m0][1], d2 = sd[m - m0][2];
+        if (kv) {
+            const floatx4 h = *reinterpret_cast<const floatx4*>(H3 + (int64_t)m * ld_h + k);
+            floatx4 dz;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int m = mb + u < m1 ? mb + u : m1 - 1;  // clamped: rows past m1 are loaded, not used
-            hv[u] = kv ? H3[(int64_t)m * ld_h + k] : 0.0f;
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                g[u][c] = drgb[3 * (int64_t)m + c];
-                y[u][c] = rgb[3 * (int64_t)m + c];
+            for (int e = 0; e < 4; ++e) {
+                const float dh = d0 * w0[e] + d1 * w1[e] + d2 * w2[e];
+                dz[e] = h[e] > 0.0f ? dh : 0.0f;
             }
+            *reinterpret_cast<floatx4*>(dZ2 + (int64_t)m * ld_dz + k) = dz;
+            a0 = a0 + d0 * h;
+            a1 = a1 + d1 * h;
+            a2 = a2 + d2 * h;
         }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (mb + u >= m1) break;
-            const int m = mb + u;
-            // torch sigmoid_backward: grad * (1 - y) * y
-            const float d0 = g[u][0] * (1.0f - y[u][0]) * y[u][0];
-            const float d1 = g[u][1] * (1.0f - y[u][1]) * y[u][1];
-            const float d2 = g[u][2] * (1.0f - y[u][2]) * y[u][2];
-            if (kv) {
-                const float dh = d0 * w0 + d1 * w1 + d2 * w2;
-                dZ2[(int64_t)m * ld_dz + k] = hv[u] > 0.0f ? dh : 0.0f;
-                a0 += d0 * hv[u];
-                a1 += d1 * hv[u];
-                a2 += d2 * hv[u];
-            }
-            if (k < 3) ab += (k == 0 ? d0 : (k == 1 ? d1 : d2));
-        }
+        b0 += d0;
+        b1 += d1;
+        b2 += d2;
     }
+    red[rl][c4][0] = a0;
+    red[rl][c4][1] = a1;
+    red[rl][c4][2] = a2;
+    if (c4 == 0) {
+        redb[rl][0] = b0;
+        redb[rl][1] = b1;
+        redb[rl][2] = b2;
+    }
+    __syncthreads();
     float* pb = part + (int64_t)blockIdx.x * 4 * K;
-    if (kv) {
-        pb[k] = a0;
-        pb[K + k] = a1;
-        pb[2 * K + k] = a2;
+    if (rl == 0 && kv) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const floatx4 t = ((red[0][c4][c] + red[1][c4][c]) + red[2][c4][c]) + red[3][c4][c];
+            *reinterpret_cast<floatx4*>(pb + c * K + k) = t;
+        }
     }
-    if (k < 3) pb[3 * K + k] = ab;
+    if (tid < 3) pb[3 * K + tid] = ((redb[0][tid] + redb[1][tid]) + redb[2][tid]) + redb[3][tid];
 }
 
 
@@ -2003,6 +2017,8 @@ extern "C" int cn_rgb_head_bwd(int32_t M, int32_t K, const float* drgb, const fl
                                float* workspace, int64_t workspace_bytes, cn_stream_t stream) {
     CN_REQUIRE(drgb && rgb && H3 && W3 && dZ2 && dW3 && db3 && workspace, CN_ERR_ARG, "cn_rgb_head_bwd: null pointer");
     CN_REQUIRE(K > 0 && K <= 256, CN_ERR_UNSUPPORTED, "cn_rgb_head_bwd: K=%d", K);
+    CN_REQUIRE(K % 4 == 0 && ld_h % 4 == 0 && ld_dz % 4 == 0 && al16(H3) && al16(dZ2) && al16(W3), CN_ERR_ALIGN,
+               "cn_rgb_head_bwd: K, leading dimensions and H3 / dZ2 / W3 must be multiples of 4 floats");
     CN_REQUIRE((size_t)workspace_bytes >= cn_rgb_head_bwd_workspace_bytes(M, K), CN_ERR_SHAPE, "cn_rgb_head_bwd: workspace");
     const int nblk = std::max(1, cdiv(M, kHeadRowsPerBlock));
     hipStream_t s = (hipStream_t)stream;
