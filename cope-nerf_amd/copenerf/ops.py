@@ -390,6 +390,18 @@ def rgb_head_bwd(drgb, rgb, H3, K, W3, dZ2, dW3, db3):
               _ptr(dW3), _ptr(db3), _ptr(ws), ws.numel() * 4, _stream())
 
 
+def patch_indices(h, w, ps, n_patches, key, out=None):
+    """Flat pixel ids [n_patches * ps * ps] (int64) of distinct random patches -- cn_patch_indices;
+    key: int32 [4] device tensor."""
+    _need(key, "key", ndim=1)
+    if key.dtype != torch.int32 or key.numel() < 4:
+        raise RuntimeError("patch_indices: key must be an int32 tensor of 4 values")
+    if out is None:
+        out = torch.empty(n_patches * ps * ps, dtype=torch.int64, device=key.device)
+    _lib.call("cn_patch_indices", h, w, ps, n_patches, _ptr(key), _ptr(out), _stream())
+    return out
+
+
 def coarse_z(near, far, n, t_rand, z):
     _lib.call("cn_coarse_z", z.shape[0], n, _ptr(near), _ptr(far), _ptr(t_rand), _ptr(z), _stream())
     return z

@@ -23,8 +23,13 @@ def get_patch_indices(h, w, patch_size, n_points, generator=None, device="cpu"):
     n_patches = n_points // (patch_size ** 2)
     h_adj, w_adj = h - patch_size + 1, w - patch_size + 1
     n_patches = min(n_patches, h_adj * w_adj)
-    # a uniformly random n_patches-subset of the corners, as randperm(...)[:n_patches]
-    # (training.py:422), by the top-k of random keys instead of a full device sort
+    if torch.device(device).type == "cuda":
+        # the first n_patches of a keyed pseudo-random permutation of the corners, as
+        # randperm(...)[:n_patches] (training.py:422), in one launch (cn_patch_indices)
+        from . import ops
+        key = torch.randint(-2 ** 31, 2 ** 31 - 1, (4,), generator=generator, device=device, dtype=torch.int32)
+        return ops.patch_indices(h, w, patch_size, n_patches, key)
+    # CPU tensors: a uniformly random n_patches-subset by the top-k of random keys
     keys = torch.rand(h_adj * w_adj, generator=generator, device=device)
     corners = torch.topk(keys, n_patches, sorted=False).indices
     rows, cols = corners // w_adj, corners % w_adj

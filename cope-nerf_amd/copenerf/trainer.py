@@ -13,7 +13,8 @@ torch.inverse) and the renderer they feed is the HIP NeuSRenderer.
 Differences, by design:
   * get_patch_indices draws the patch corners with torch.randperm on the CPU
     exactly as training.py:422 (so a seeded run samples the reference's patches)
-    unless `patch_rng="device"` (a top-k of device random keys: no host sync).
+    unless `patch_rng="device"` (cn_patch_indices: the first corners of a keyed
+    pseudo-random permutation, one launch, no host sync).
   * compute_loss checks for NaN like training.py:532-533 (`nan_check="sync"`,
     the default: AssertionError at once) or sets a device flag without a host
     sync (`nan_check="deferred"`, for captured steps; `check_finite()` raises).

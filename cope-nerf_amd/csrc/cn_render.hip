@@ -486,9 +486,64 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// Keyed pseudo-random permutation of [0, n): a balanced 4-round Feistel network on 2*hb
+// bits (2^(2 hb) >= n) with cycle walking (values >= n are permuted again; starting below
+// n the walk returns below n, expected < 4 steps).  Round function: a 32-bit avalanche hash.
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+__device__ __forceinline__ uint32_t feistel(uint32_t x, int hb, const uint32_t k[4]) {
+    const uint32_t mask = (1u << hb) - 1u;
+    uint32_t L = x >> hb, R = x & mask;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t t = L ^ (mix32(R ^ k[r]) & mask);
+        L = R;
+        R = t;
+    }
+    return (L << hb) | R;
+}
+
+// One thread per patch: its corner and its ps x ps pixel ids.
+__global__ void patch_indices_kernel(int h, int w, int ps, int np, int hb, const int* __restrict__ key, int64_t* idx) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= np) return;
+    const int wa = w - ps + 1;
+    const uint32_t n = (uint32_t)(h - ps + 1) * (uint32_t)wa;
+    const uint32_t k[4] = {(uint32_t)key[0], (uint32_t)key[1], (uint32_t)key[2], (uint32_t)key[3]};
+    uint32_t x = (uint32_t)p;
+    do {
+        x = feistel(x, hb, k);
+    } while (x >= n);
+    const int row = (int)(x / (uint32_t)wa), col = (int)(x % (uint32_t)wa);
+    int64_t* o = idx + (int64_t)p * ps * ps;
+    for (int a = 0; a < ps; ++a)
+        for (int b = 0; b < ps; ++b) o[a * ps + b] = (int64_t)(row + a) * w + col + b;
+}
+
 }  // namespace cn
 
 using namespace cn;
+
+extern "C" int cn_patch_indices(int32_t h, int32_t w, int32_t ps, int32_t n_patches, const int32_t* key, int64_t* idx,
+                                cn_stream_t stream) {
+    CN_REQUIRE(key && idx, CN_ERR_ARG, "cn_patch_indices: null pointer");
+    CN_REQUIRE(ps >= 1 && h >= ps && w >= ps && n_patches >= 0, CN_ERR_SHAPE, "cn_patch_indices: h=%d w=%d ps=%d",
+               h, w, ps);
+    const int64_t n = (int64_t)(h - ps + 1) * (w - ps + 1);
+    CN_REQUIRE(n_patches <= n && n < (1LL << 30), CN_ERR_SHAPE, "cn_patch_indices: %d patches of %lld corners",
+               n_patches, (long long)n);
+    if (n_patches == 0) return CN_OK;
+    int hb = 1;
+    while ((1LL << (2 * hb)) < n) ++hb;
+    patch_indices_kernel<<<(n_patches + 255) / 256, 256, 0, (hipStream_t)stream>>>(h, w, ps, n_patches, hb, key, idx);
+    return check_launch("cn_patch_indices");
+}
 
 extern "C" int cn_coarse_z(int32_t R, int32_t n, const float* near, const float* far, const float* t_rand, float* z,
                            cn_stream_t stream) {

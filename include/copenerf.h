@@ -275,6 +275,17 @@ int cn_rgb_head_bwd(int32_t M, int32_t K, const float* drgb, const float* rgb, c
                     float* workspace, int64_t workspace_bytes, cn_stream_t stream);
 
 /* ------------------------------------------------------------------------ *
+ * Patch sampling (model/training.py:413-436 on the device): idx[p*ps*ps + a*ps + b] =
+ * (row_p + a) * w + col_p + b for n_patches distinct corners (row_p, col_p) of the
+ * (h-ps+1) x (w-ps+1) grid -- the first n_patches values of a keyed pseudo-random
+ * permutation of the corner ids (4-round Feistel network with cycle walking; key:
+ * 4 int32 on the device, e.g. from torch.randint), the device counterpart of
+ * randperm(n)[:n_patches] without a sort.
+ * ------------------------------------------------------------------------ */
+int cn_patch_indices(int32_t h, int32_t w, int32_t ps, int32_t n_patches, const int32_t* key, int64_t* idx,
+                     cn_stream_t stream);
+
+/* ------------------------------------------------------------------------ *
  * Sampling along rays (neus_renderer.py:453-525).
  * ------------------------------------------------------------------------ */
 /* z[r][i] = near*(1-lin_i) + far*lin_i, lin = linspace(0,1,n); stratified

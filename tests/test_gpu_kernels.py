@@ -438,3 +438,31 @@ def test_train_loss_matches_reference_losses(patch):
     assert abs(got.item() - ref.item()) <= 1e-6 * abs(ref.item()), (got.item(), ref.item())
     for a, b, n in zip(g_grads, r_grads, ("color", "depth", "G")):
         torch.testing.assert_close(a, 2.0 * b, rtol=1e-5, atol=1e-9, msg=lambda m: f"{n}: {m}")
+
+
+def test_patch_indices_distinct_whole_patches():
+    """cn_patch_indices (device patch sampling, training.py:413-436): whole ps x ps
+    patches at distinct corners inside the image, deterministic per key, and the
+    corners of many keys spread uniformly over the corner grid."""
+    ops = _ops()
+    from copenerf.rays import get_patch_indices
+    h, w, ps, n_pts = 540, 960, 4, 4096
+    n = (h - ps + 1) * (w - ps + 1)
+    key = torch.tensor([1, -2, 3, 12345], dtype=torch.int32, device=DEV)
+    a = ops.patch_indices(h, w, ps, n_pts // 16, key)
+    assert torch.equal(a, ops.patch_indices(h, w, ps, n_pts // 16, key))
+    idx = a.view(-1, 16).cpu()
+    corners = idx[:, 0]
+    assert corners.unique().numel() == corners.numel()
+    offs = torch.tensor([r * w + c for r in range(ps) for c in range(ps)])
+    assert torch.equal(idx - corners[:, None], offs.expand_as(idx))
+    assert int(idx.max()) < h * w and int((corners % w).max()) <= w - ps and int((corners // w).max()) <= h - ps
+    # every corner of a tiny grid is reachable: all n corners when n_patches == n
+    full = ops.patch_indices(6, 7, 2, 30, key).view(-1, 4)[:, 0].cpu()
+    assert sorted(((full // 7) * 6 + full % 7).tolist()) == list(range(30))
+    # uniformity over keys: mean corner id ~ n/2, both halves of the grid drawn equally
+    g = torch.Generator(device=DEV).manual_seed(3)
+    cs = torch.cat([get_patch_indices(h, w, ps, n_pts, generator=g, device=DEV).view(-1, 16)[:, 0] for _ in range(64)])
+    cid = (cs // w) * (w - ps + 1) + cs % w
+    frac_low = (cid < n // 2).float().mean().item()
+    assert abs(frac_low - 0.5) < 0.02, frac_low

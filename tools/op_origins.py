@@ -39,7 +39,10 @@ class Origins(TorchDispatchMode):
 
 
 def main():
-    tr = SyntheticTrainer("cuda:0", rays=4096, mfma_dtype=os.environ.get("MODE", "bf16x6"))
+    kw = dict(mfma_dtype=os.environ.get("MODE", "bf16x6"))
+    if os.environ.get("C3"):  # the c3fp32 bench config: joint pose + stage 1
+        kw.update(joint_pose=True, stage1=True, start_it=30000)
+    tr = SyntheticTrainer("cuda:0", rays=4096, **kw)
     for _ in range(2):
         tr.step()
     torch.cuda.synchronize()
@@ -51,7 +54,7 @@ def main():
     for (op, site), n in m.count.items():
         by_site[site] += n
     print("total aten ops", sum(m.count.values()))
-    for site, n in by_site.most_common(40):
+    for site, n in by_site.most_common(60):
         ops = collections.Counter({op: c for (op, s), c in m.count.items() if s == site})
         top = ", ".join(f"{o.split('.')[1]}x{c}" for o, c in ops.most_common(4))
         print(f"{n:5d} {site:60s} {top}")
