@@ -323,13 +323,15 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None):
         db8[1:].zero_()
     dsdf_flat = None
     # dW8[0] = Σ_m dsdf U8 (+ Ud8) / scale: fused into the adjoint kernel on the folded-head path
-    fused_cs = dh is not None and (dsdf is not None or second) and i8 == HL
+    # (also on the sdf-only first-order path, e.g. the consistency re-query: Z_7 = dsdf w80 σ_7)
+    sdf_only = dh is None and dfeat is None and not second and dsdf is not None
+    fused_cs = i8 == HL and ((dh is not None and (dsdf is not None or second)) or sdf_only)
     if dsdf is not None:
         dsdf = dsdf.reshape(M, 1).contiguous()
         dsdf_flat = dsdf
         if not fused_cs:
             ops.colsum(U[L8], i8, dW8[0], w=dsdf, wdiv=lay.scale)
-        ops.colsum(dsdf, 1, db8[0:1], wdiv=lay.scale)
+            ops.colsum(dsdf, 1, db8[0:1], wdiv=lay.scale)
     else:
         if not fused_cs:
             dW8[0].zero_()
@@ -348,11 +350,17 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None):
         ops.softplus_adjoint(U[L8], HL, Z, act_beta=sig_beta(lay, L8 - 1), D=dh, rowv=dsdf_flat,
                              colv=pk.w80p if dsdf_flat is not None else None, aux1=so.get("aux1"),
                              aux2=so.get("aux2"), aux2_scale=so.get("aux2_scale", 0.0),
-                             cs_out=dW8[0] if fused_cs else None, cs_div=lay.scale)
-    elif dfeat is None and not second and dsdf_flat is not None:
+                             cs_out=dW8[0] if fused_cs else None,
+                             rs_out=db8[0:1] if (fused_cs and dsdf_flat is not None) else None, cs_div=lay.scale)
+    elif sdf_only:
         # sdf only, first order (e.g. SDFNetwork.sdf at train.py:504): Z_7 = dsdf[m] w80[n] σ_7,
-        # elementwise -- no GEMM over a zero feature gradient
-        ops.scale_cols(U[L8], HL, pk.w80p, Z, act_beta=sig_beta(lay, L8 - 1), rowv=dsdf_flat)
+        # elementwise -- no GEMM over a zero feature gradient; lin8's sdf row / bias gradients
+        # from the same pass when fused_cs
+        if fused_cs:
+            ops.softplus_adjoint(U[L8], HL, Z, act_beta=sig_beta(lay, L8 - 1), rowv=dsdf_flat, colv=pk.w80p,
+                                 cs_out=dW8[0], rs_out=db8[0:1], cs_div=lay.scale)
+        else:
+            ops.scale_cols(U[L8], HL, pk.w80p, Z, act_beta=sig_beta(lay, L8 - 1), rowv=dsdf_flat)
     else:
         phi = dfeat if dfeat is not None else torch.zeros(M, lay.H_feat, device=dev)
         ops.linear(phi, pk.Bt8, lay.out_dim[L8 - 1], rup(lay.H_feat, 32), Z, EPI_BWD_SOFTPLUS,

@@ -322,9 +322,10 @@ def scale_cols(X, N, w, out, act_beta=0.0, rowv=None):
 
 
 def softplus_adjoint(act, N, out, *, act_beta, D=None, rowv=None, colv=None, aux1=None, aux2=None, aux2_scale=0.0,
-                     cs_out=None, cs_div=1.0):
+                     cs_out=None, rs_out=None, cs_div=1.0):
     """out = (D + rowv (x) colv) * sg(act) + aux1 * aux2 * aux2_scale * (1 - sg) / sg -- cn_softplus_adjoint;
-    cs_out[n] = Σ_m (rowv[m] act[m][n] + aux2[m][n]) / cs_div when given (lin8's sdf-row gradient)."""
+    cs_out[n] = Σ_m (rowv[m] act[m][n] + aux2[m][n]) / cs_div when given (lin8's sdf-row gradient),
+    rs_out[0] = Σ_m rowv[m] / cs_div (its bias gradient)."""
     for t, n in ((act, "act"), (out, "out"), (D, "D"), (aux1, "aux1"), (aux2, "aux2")):
         _need(t, n)
     if rowv is not None and (not rowv.is_contiguous() or rowv.numel() != act.shape[0]):
@@ -339,7 +340,8 @@ def softplus_adjoint(act, N, out, *, act_beta, D=None, rowv=None, colv=None, aux
         ws = torch.empty(lib.cn_softplus_adjoint_workspace_bytes(M, N) // 4 + 1, device=act.device, dtype=torch.float32)
     _lib.call("cn_softplus_adjoint", M, N, _ptr(D), _ld(D), _ptr(act), _ld(act), float(act_beta),
               _ptr(rowv), _ptr(colv), _ptr(aux1), _ld(aux1), _ptr(aux2), _ld(aux2), float(aux2_scale), _ptr(out),
-              _ld(out), _ptr(cs_out), float(cs_div), _ptr(ws), 0 if ws is None else ws.numel() * 4, _stream())
+              _ld(out), _ptr(cs_out), _ptr(rs_out if cs_out is not None else None), float(cs_div), _ptr(ws),
+              0 if ws is None else ws.numel() * 4, _stream())
     return out
 
 

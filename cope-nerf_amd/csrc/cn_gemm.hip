@@ -1465,8 +1465,10 @@ __global__ void __launch_bounds__(256) softplus_adjoint_cs_kernel(int M, int N4,
                                                                   const float* __restrict__ colv,
                                                                   const float* __restrict__ aux1, int64_t ld1,
                                                                   const float* __restrict__ aux2, int64_t ld2,
-                                                                  float c2, float* out, int64_t ldo, float* part) {
+                                                                  float c2, float* out, int64_t ldo, float* part,
+                                                                  float* rpart) {
     __shared__ floatx4 red[256];
+    __shared__ float redr[256];
     const int c = threadIdx.x % N4;
     const int rl = threadIdx.x / N4;
     const int nrl = 256 / N4;
@@ -1474,34 +1476,48 @@ __global__ void __launch_bounds__(256) softplus_adjoint_cs_kernel(int M, int N4,
     const int m0 = blockIdx.x * kSaRows, m1 = min(M, m0 + kSaRows);
     const floatx4 cv = colv ? *reinterpret_cast<const floatx4*>(colv + n) : floatx4{0.f, 0.f, 0.f, 0.f};
     floatx4 cs = {0.f, 0.f, 0.f, 0.f};
-    if (rl < nrl) {
-        for (int m = m0 + rl; m < m1; m += nrl) {
-            const floatx4 a = *reinterpret_cast<const floatx4*>(act + (int64_t)m * lda + n);
-            floatx4 g = D ? *reinterpret_cast<const floatx4*>(D + (int64_t)m * ldd + n) : floatx4{0.f, 0.f, 0.f, 0.f};
-            const float rv = rowv ? rowv[m] : 0.0f;
-            g = g + rv * cv;
-            floatx4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
-            if (aux1) {
-                s1 = *reinterpret_cast<const floatx4*>(aux1 + (int64_t)m * ld1 + n);
-                s2 = *reinterpret_cast<const floatx4*>(aux2 + (int64_t)m * ld2 + n);
-            }
-            floatx4 o;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float sg = sigma_from_act(a[e], aux_c);
-                const float rr = sg > 0.0f ? (1.0f - sg) * __builtin_amdgcn_rcpf(sg) : 0.0f;
-                o[e] = g[e] * sg + s1[e] * s2[e] * (c2 * rr);
-            }
-            *reinterpret_cast<floatx4*>(out + (int64_t)m * ldo + n) = o;
-            cs = cs + rv * a + s2;
+    float rs = 0.0f;  // Σ rowv over the rows of this lane (the head bias gradient), column-0 lanes
+    auto row = [&](int m) {
+        const floatx4 a = *reinterpret_cast<const floatx4*>(act + (int64_t)m * lda + n);
+        floatx4 g = D ? *reinterpret_cast<const floatx4*>(D + (int64_t)m * ldd + n) : floatx4{0.f, 0.f, 0.f, 0.f};
+        const float rv = rowv ? rowv[m] : 0.0f;
+        g = g + rv * cv;
+        floatx4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
+        if (aux1) {
+            s1 = *reinterpret_cast<const floatx4*>(aux1 + (int64_t)m * ld1 + n);
+            s2 = *reinterpret_cast<const floatx4*>(aux2 + (int64_t)m * ld2 + n);
         }
+        floatx4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float sg = sigma_from_act(a[e], aux_c);
+            const float rr = sg > 0.0f ? (1.0f - sg) * __builtin_amdgcn_rcpf(sg) : 0.0f;
+            o[e] = g[e] * sg + s1[e] * s2[e] * (c2 * rr);
+        }
+        *reinterpret_cast<floatx4*>(out + (int64_t)m * ldo + n) = o;
+        cs = cs + rv * a + s2;
+        rs += rv;
+    };
+    if (rl < nrl) {
+        int m = m0 + rl;
+        for (; m + nrl < m1; m += 2 * nrl) {  // two rows in flight per lane (row order of the sums kept)
+            row(m);
+            row(m + nrl);
+        }
+        if (m < m1) row(m);
     }
     red[threadIdx.x] = cs;
+    redr[threadIdx.x] = rs;
     __syncthreads();
     if (rl == 0) {
         floatx4 t = red[c];
-        for (int r = 1; r < nrl; ++r) t = t + red[r * N4 + c];
+        float tr = redr[c];
+        for (int r = 1; r < nrl; ++r) {
+            t = t + red[r * N4 + c];
+            tr += redr[r * N4 + c];
+        }
         *reinterpret_cast<floatx4*>(part + (int64_t)blockIdx.x * N4 * 4 + n) = t;
+        if (c == 0 && rpart) rpart[blockIdx.x] = tr;
     }
 }
 
@@ -1970,13 +1986,13 @@ extern "C" int cn_scale_cols(int32_t M, int32_t N, const float* X, int64_t ldx, 
 }
 
 extern "C" size_t cn_softplus_adjoint_workspace_bytes(int32_t M, int32_t N) {
-    return sizeof(float) * (size_t)std::max(1, cdiv(M, kSaRows)) * std::max(N, 4);
+    return sizeof(float) * (size_t)std::max(1, cdiv(M, kSaRows)) * (std::max(N, 4) + 1);
 }
 
 extern "C" int cn_softplus_adjoint(int32_t M, int32_t N, const float* D, int64_t ldd, const float* act, int64_t lda,
                                    float act_beta, const float* rowv, const float* colv, const float* aux1,
                                    int64_t ld1, const float* aux2, int64_t ld2, float aux2_scale, float* out,
-                                   int64_t ld_out, float* cs_out, float cs_div, float* workspace,
+                                   int64_t ld_out, float* cs_out, float* rs_out, float cs_div, float* workspace,
                                    int64_t workspace_bytes, cn_stream_t stream) {
     CN_REQUIRE(act && out && act_beta > 0.0f, CN_ERR_ARG, "cn_softplus_adjoint: act, out and act_beta > 0 required");
     CN_REQUIRE((rowv == nullptr) == (colv == nullptr) && (aux1 == nullptr) == (aux2 == nullptr), CN_ERR_ARG,
@@ -1989,15 +2005,22 @@ extern "C" int cn_softplus_adjoint(int32_t M, int32_t N, const float* D, int64_t
         CN_REQUIRE(N >= 4 && N <= 1024 && workspace &&
                        (size_t)workspace_bytes >= cn_softplus_adjoint_workspace_bytes(M, N),
                    CN_ERR_SHAPE, "cn_softplus_adjoint: column sums need N <= 1024 and the workspace");
-        if (M == 0) return launch_slab_reduce(workspace, 0, N, 1, N, N, cs_out, N, 1.0f, 0, (hipStream_t)stream);
+        if (M == 0) {
+            const int rc = launch_slab_reduce(workspace, 0, N, 1, N, N, cs_out, N, 1.0f, 0, (hipStream_t)stream);
+            return (rc || !rs_out) ? rc : launch_slab_reduce(workspace, 0, 1, 1, 1, 1, rs_out, 1, 1.0f, 0, (hipStream_t)stream);
+        }
         const int nblk = cdiv(M, kSaRows);
         hipStream_t s = (hipStream_t)stream;
+        float* rpart = rs_out ? workspace + (size_t)nblk * N : nullptr;
         softplus_adjoint_cs_kernel<<<nblk, 256, 0, s>>>(M, N / 4, D, ldd, act, lda, -act_beta * 1.44269504088896341f,
                                                         rowv, colv, aux1, ld1, aux2, ld2, aux2_scale, out, ld_out,
-                                                        workspace);
-        const int rc = check_launch("cn_softplus_adjoint");
+                                                        workspace, rpart);
+        int rc = check_launch("cn_softplus_adjoint");
         if (rc) return rc;
-        return launch_slab_reduce(workspace, nblk, N, 1, N, N, cs_out, N, cs_div == 0.f ? 1.f : cs_div, 0, s);
+        const float dv = cs_div == 0.f ? 1.f : cs_div;
+        rc = launch_slab_reduce(workspace, nblk, N, 1, N, N, cs_out, N, dv, 0, s);
+        if (rc || !rs_out) return rc;
+        return launch_slab_reduce(rpart, nblk, 1, 1, 1, 1, rs_out, 1, dv, 0, s);
     }
     if ((int64_t)M * N == 0) return CN_OK;
     const int64_t tot = (int64_t)M * (N / 4);

@@ -215,14 +215,15 @@ int cn_scale_cols(int32_t M, int32_t N, const float* X, int64_t ldx, const float
  *             + (aux1 ? aux1[m][n] aux2[m][n] aux2_scale (1 - sg) / sg : 0),   0 where sg = 0,
  *   sg = 1 - exp(-act_beta act[m][n]) (softplus' from the activation, as cn_linear's epilogues). */
 /* With cs_out != NULL it also produces the sdf row of lin8's weight gradient from the
- * operands it already streams (the fused form of cn_colsum's two calls):
+ * operands it already streams (the fused form of cn_colsum's calls):
  *   cs_out[n] = (sum_m (rowv ? rowv[m] act[m][n] : 0) + (aux2 ? aux2[m][n] : 0)) / cs_div,
- * fixed-order slab reduction through workspace (cn_softplus_adjoint_workspace_bytes). */
+ *   rs_out[0] = (sum_m rowv[m]) / cs_div (the sdf head's bias gradient; rs_out may be NULL),
+ * fixed-order slab reductions through workspace (cn_softplus_adjoint_workspace_bytes). */
 size_t cn_softplus_adjoint_workspace_bytes(int32_t M, int32_t N);
 int cn_softplus_adjoint(int32_t M, int32_t N, const float* D, int64_t ldd, const float* act, int64_t lda,
                         float act_beta, const float* rowv, const float* colv, const float* aux1, int64_t ld1,
                         const float* aux2, int64_t ld2, float aux2_scale, float* out, int64_t ld_out,
-                        float* cs_out, float cs_div, float* workspace, int64_t workspace_bytes,
+                        float* cs_out, float* rs_out, float cs_div, float* workspace, int64_t workspace_bytes,
                         cn_stream_t stream);
 
 /* ------------------------------------------------------------------------ *

@@ -240,12 +240,13 @@ def test_softplus_adjoint():
     assert torch.isfinite(out).all()
     # the column-sum form: same out, plus lin8's sdf-row gradient Σ_m rv act + s2, over a ragged M
     for m in (M, 1537, 1):
-        out2, cs = torch.full((m, K), float("nan"), device=DEV), torch.empty(K, device=DEV)
+        out2, cs, rs = torch.full((m, K), float("nan"), device=DEV), torch.empty(K, device=DEV), torch.empty(1, device=DEV)
         ops.softplus_adjoint(act[:m], K, out2, act_beta=100.0, D=D[:m], rowv=rv[:m].contiguous(), colv=cv,
-                             aux1=s1[:m], aux2=s2[:m], aux2_scale=0.7, cs_out=cs, cs_div=2.0)
+                             aux1=s1[:m], aux2=s2[:m], aux2_scale=0.7, cs_out=cs, rs_out=rs, cs_div=2.0)
         assert torch.equal(out2, out[:m])
         cs_ref = (rv[:m].double()[:, None] * act[:m].double() + s2[:m].double()).sum(0) / 2.0
         torch.testing.assert_close(cs, cs_ref.float(), rtol=1e-5, atol=1e-4)
+        torch.testing.assert_close(rs, (rv[:m].double().sum() / 2.0).float().view(1), rtol=1e-5, atol=1e-5)
     cs2 = torch.empty(K, device=DEV)
     ops.softplus_adjoint(act, K, out, act_beta=100.0, D=D, cs_out=cs2)  # no rowv / aux2: zero sums
     assert torch.all(cs2 == 0)
