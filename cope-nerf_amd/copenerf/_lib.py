@@ -35,6 +35,11 @@ EPI_BWD_RELU = 6
 EPI_SOFTPLUS_HEAD = 8
 
 
+class WnJob(ctypes.Structure):
+    _fields_ = [("v", c_ptr), ("g", c_ptr), ("w", c_ptr), ("dw", c_ptr), ("dv", c_ptr), ("dg", c_ptr),
+                ("rows", c_i32), ("cols", c_i32)]
+
+
 class LinearDesc(ctypes.Structure):
     _fields_ = [
         ("A", c_ptr), ("A2", c_ptr), ("B", c_ptr), ("bias", c_ptr), ("rowv", c_ptr), ("colv", c_ptr),
@@ -74,6 +79,7 @@ SIGNATURES = {
     "cn_abi_version": (c_i32, []),
     "cn_last_error": (ctypes.c_char_p, []),
     "cn_linear": (c_i32, [ctypes.POINTER(LinearDesc), c_ptr]),
+    "cn_weight_norm": (c_i32, [ctypes.POINTER(WnJob), c_i32, c_i32, c_ptr]),
     "cn_wgrad_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32]),
     "cn_wgrad": (c_i32, [ctypes.POINTER(WgradDesc), c_ptr]),
     "cn_pack_weights": (c_i32, [ctypes.POINTER(PackJob), c_i32, c_ptr]),

@@ -116,6 +116,32 @@ def unsplit_bf16x3(B: torch.Tensor) -> torch.Tensor:
 FORMATS = {"fp32": 0, "bf16": 1, "bf16x6": 2}
 
 
+def weight_norm_batch(vs, gs, *, dws=None):
+    """cn_weight_norm over lists of (v [rows, cols], g [rows, 1] or [rows]) in one launch:
+    forward -> [W]; with dws (the gradients of the W) -> ([dv], [dg])."""
+    jobs = (_lib.WnJob * max(1, len(vs)))()
+    outs = []
+    for i, (v, g) in enumerate(zip(vs, gs)):
+        _need(v, "v")
+        if not v.is_contiguous() or not g.is_contiguous() or g.numel() != v.shape[0]:
+            raise RuntimeError("weight_norm_batch: v [rows, cols] and g [rows] must be contiguous")
+        j = jobs[i]
+        j.v, j.g, j.rows, j.cols = v.data_ptr(), g.data_ptr(), v.shape[0], v.shape[1]
+        if dws is None:
+            w = torch.empty_like(v)
+            j.w = w.data_ptr()
+            outs.append(w)
+        else:
+            dw = dws[i].contiguous()
+            dv, dg = torch.empty_like(v), torch.empty_like(g)
+            j.dw, j.dv, j.dg = dw.data_ptr(), dv.data_ptr(), dg.data_ptr()
+            outs.append((dv, dg, dw))
+    _lib.check(_lib.load().cn_weight_norm(jobs, len(vs), 0 if dws is None else 1, _stream()), "cn_weight_norm")
+    if dws is None:
+        return outs
+    return [o[0] for o in outs], [o[1] for o in outs]
+
+
 class ImagePacker:
     """Collects cn_pack_job regions of weight images and builds them in one
     cn_pack_weights launch (the per-call weight packing of fields.py)."""

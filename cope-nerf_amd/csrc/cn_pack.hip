@@ -58,9 +58,72 @@ __global__ void __launch_bounds__(256) pack_kernel(PackBatch b) {
     }
 }
 
+constexpr int kWnJobsPerLaunch = 16;
+struct WnBatch {
+    cn_wn_job job[kWnJobsPerLaunch];
+};
+
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    return x;
+}
+
+// grid (row blocks, jobs), 256 threads = 4 waves = 4 rows per block.
+__global__ void __launch_bounds__(256) weight_norm_kernel(WnBatch b, int backward) {
+    const cn_wn_job& j = b.job[blockIdx.y];
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= j.rows) return;
+    const float* v = j.v + (int64_t)row * j.cols;
+    float ss = 0.0f;
+    for (int c = lane; c < j.cols; c += 64) ss += v[c] * v[c];
+    const float nrm = sqrtf(wave_sum(ss));
+    const float g = j.g[row];
+    if (!backward) {
+        const float s = g / nrm;
+        float* w = j.w + (int64_t)row * j.cols;
+        for (int c = lane; c < j.cols; c += 64) w[c] = v[c] * s;
+        return;
+    }
+    const float* dw = j.dw + (int64_t)row * j.cols;
+    float dot = 0.0f;
+    for (int c = lane; c < j.cols; c += 64) dot += dw[c] * v[c];
+    dot = wave_sum(dot);
+    const float dg = dot / nrm;
+    if (lane == 0) j.dg[row] = dg;
+    const float s = g / nrm, t = dg / nrm;
+    float* dv = j.dv + (int64_t)row * j.cols;
+    for (int c = lane; c < j.cols; c += 64) dv[c] = s * (dw[c] - v[c] * t);
+}
+
 }  // namespace cn
 
 using namespace cn;
+
+extern "C" int cn_weight_norm(const cn_wn_job* jobs, int32_t njobs, int32_t backward, cn_stream_t stream) {
+    CN_REQUIRE(njobs >= 0 && (jobs || njobs == 0), CN_ERR_ARG, "cn_weight_norm: bad job list");
+    for (int i = 0; i < njobs; ++i) {
+        const cn_wn_job& j = jobs[i];
+        CN_REQUIRE(j.v && j.g && (backward ? (j.dw && j.dv && j.dg) : (j.w != nullptr)), CN_ERR_ARG,
+                   "cn_weight_norm: job %d null pointer", i);
+        CN_REQUIRE(j.rows >= 0 && j.cols >= 0, CN_ERR_SHAPE, "cn_weight_norm: job %d shape", i);
+    }
+    for (int i0 = 0; i0 < njobs; i0 += kWnJobsPerLaunch) {
+        const int n = njobs - i0 < kWnJobsPerLaunch ? njobs - i0 : kWnJobsPerLaunch;
+        WnBatch b{};
+        int most = 0;
+        for (int i = 0; i < n; ++i) {
+            b.job[i] = jobs[i0 + i];
+            most = std::max(most, b.job[i].rows);
+        }
+        if (most == 0) continue;
+        weight_norm_kernel<<<dim3((most + 3) / 4, n), 256, 0, (hipStream_t)stream>>>(b, backward ? 1 : 0);
+        const int rc = check_launch("cn_weight_norm");
+        if (rc) return rc;
+    }
+    return CN_OK;
+}
 
 extern "C" int cn_pack_weights(const cn_pack_job* jobs, int32_t njobs, cn_stream_t stream) {
     CN_REQUIRE(njobs >= 0 && (jobs || njobs == 0), CN_ERR_ARG, "cn_pack_weights: bad job list");

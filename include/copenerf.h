@@ -154,6 +154,27 @@ typedef struct cn_pack_job {
 int cn_pack_weights(const cn_pack_job* jobs, int32_t njobs, cn_stream_t stream);
 
 /* ------------------------------------------------------------------------ *
+ * Weight normalisation of every Linear of a network in one launch
+ * (torch.nn.utils.weight_norm, dim 0, as the reference wraps every layer:
+ * model/neus_fields.py:84-140, 336-360): per output row i,
+ *   forward   W_i = v_i (g_i / |v_i|)
+ *   backward  dg_i = (dW_i . v_i) / |v_i|,  dv_i = (g_i / |v_i|) (dW_i - v_i dg_i / |v_i|)
+ * v, w, dw, dv row-major contiguous [rows][cols]; g, dg [rows].  One wavefront per
+ * row (fixed-order reductions).
+ * ------------------------------------------------------------------------ */
+typedef struct cn_wn_job {
+    const float* v;
+    const float* g;
+    float* w;            /* forward output */
+    const float* dw;     /* backward input */
+    float* dv;           /* backward outputs */
+    float* dg;
+    int32_t rows, cols;
+} cn_wn_job;
+
+int cn_weight_norm(const cn_wn_job* jobs, int32_t njobs, int32_t backward, cn_stream_t stream);
+
+/* ------------------------------------------------------------------------ *
  * Weight gradient: dW[n][k] = sum_m ( Y0[m][n]*X0[m][k] + Y1[m][n]*X1[m][k] ),
  * db[n] = sum_m Y0[m][n].  Reduction over the M = R*S sample rows is split
  * over workgroups into fp32 slabs (workspace) and summed in a fixed order, so

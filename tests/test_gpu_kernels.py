@@ -467,3 +467,21 @@ def test_patch_indices_distinct_whole_patches():
     cid = (cs // w) * (w - ps + 1) + cs % w
     frac_low = (cid < n // 2).float().mean().item()
     assert abs(frac_low - 0.5) < 0.02, frac_low
+
+
+def test_weight_norm_batch_matches_torch():
+    """cn_weight_norm (every weight-normed Linear of a network in one launch, forward and
+    backward) against torch._weight_norm and its autograd, dim 0."""
+    from copenerf.fields import _WeightNormFn
+    shapes = [(256, 39), (256, 256), (204, 256), (257, 256), (3, 256), (6, 13)]
+    vs = [_rnd(o, i, seed=60 + k).requires_grad_(True) for k, (o, i) in enumerate(shapes)]
+    gs = [(_rnd(o, 1, seed=70 + k) + 2.0).requires_grad_(True) for k, (o, i) in enumerate(shapes)]
+    ref = [torch._weight_norm(v, g, 0) for v, g in zip(vs, gs)]
+    got = _WeightNormFn.apply(len(vs), *vs, *gs)
+    for a, b in zip(got, ref):
+        torch.testing.assert_close(a, b, rtol=2e-6, atol=1e-7)
+    dWs = [_rnd(*w.shape, seed=80 + k) for k, w in enumerate(ref)]
+    gr = torch.autograd.grad(ref, vs + gs, dWs)
+    gg = torch.autograd.grad(got, vs + gs, dWs)
+    for a, b in zip(gg, gr):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
