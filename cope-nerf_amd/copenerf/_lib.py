@@ -103,6 +103,8 @@ SIGNATURES = {
     "cn_colsum_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32]),
     "cn_colsum": (c_i32, [c_i32, c_i32, c_ptr, c_ptr, c_i64, c_f32, c_ptr, c_i32, c_ptr, c_i64, c_ptr]),
     "cn_patch_indices": (c_i32, [c_i32, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_ptr]),
+    "cn_euler_chain": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr]),
+    "cn_euler_chain_bwd": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr]),
     "cn_coarse_z": (c_i32, [c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr]),
     "cn_points": (c_i32, [c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_i32, c_ptr, c_ptr, c_i32, c_ptr, c_ptr]),
     "cn_up_sample_merge": (c_i32, [c_i32, c_i32, c_i32, c_f32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,

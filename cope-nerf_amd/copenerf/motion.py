@@ -169,6 +169,8 @@ class MotionNetwork(nn.Module):
         steps instead of K*n host-launched ones).  steps [K, n], dts [K] -> [K, 4, 4]."""
         K, n = steps.shape
         omega, vel = self.forward(steps.reshape(-1, 1))
+        if omega.is_cuda:  # the recurrence forward and backward in one launch each (cn_euler_chain)
+            return _EulerChainFn.apply(omega, vel, dts.reshape(K).contiguous(), K, n)
         dt = dts.view(K, 1, 1)
         Rs = euler_angles_to_matrix(omega.view(K, n, 3) * dt, "XYZ")  # [K, n, 3, 3]
         Vs = vel.view(K, n, 3) * dt
@@ -180,6 +182,38 @@ class MotionNetwork(nn.Module):
         top = torch.cat([R, T], -1)  # [K, 3, 4]
         row = torch.eye(4, device=steps.device)[3:4].expand(K, 1, 4)  # no host scalar copy: capturable
         return torch.cat([top, row], 1)
+
+
+class _EulerChainFn(torch.autograd.Function):
+    """All K consecutive relative poses from the motion network's velocities: the
+    reference's Euler recurrence (neus_fields.py:146-165) as one HIP thread per interval
+    (cn_euler_chain), and its reverse recurrence for d omega, d vel (cn_euler_chain_bwd)
+    -- instead of ~150 tiny 3x3 launches forward and backward."""
+
+    @staticmethod
+    def forward(ctx, omega, vel, dts, K, n):
+        from . import ops  # noqa: F401  (the library is loaded by ops)
+        from . import _lib
+        P = torch.empty(K, 4, 4, device=omega.device, dtype=torch.float32)
+        stream = torch.cuda.current_stream().cuda_stream
+        _lib.call("cn_euler_chain", K, n, omega.data_ptr(), omega.stride(0), vel.data_ptr(), vel.stride(0),
+                  dts.data_ptr(), P.data_ptr(), stream)
+        ctx.save_for_backward(omega, vel, dts)
+        ctx.Kn = (K, n)
+        return P
+
+    @staticmethod
+    def backward(ctx, dP):
+        from . import _lib
+        omega, vel, dts = ctx.saved_tensors
+        K, n = ctx.Kn
+        dP = dP.contiguous()
+        domega = torch.empty(K * n, 3, device=omega.device, dtype=torch.float32)
+        dvel = torch.empty(K * n, 3, device=omega.device, dtype=torch.float32)
+        stream = torch.cuda.current_stream().cuda_stream
+        _lib.call("cn_euler_chain_bwd", K, n, omega.data_ptr(), omega.stride(0), vel.data_ptr(), vel.stride(0),
+                  dts.data_ptr(), dP.data_ptr(), domega.data_ptr(), dvel.data_ptr(), stream)
+        return domega, dvel, None, None, None
 
 
 def masked_chain(P, lo, hi):

@@ -526,9 +526,156 @@ __global__ void patch_indices_kernel(int h, int w, int ps, int np, int hb, const
         for (int b = 0; b < ps; ++b) o[a * ps + b] = (int64_t)(row + a) * w + col + b;
 }
 
+// 3x3 helpers for the Euler chain (row-major, sums in k order as a small torch matmul)
+struct M3 {
+    float m[9];
+};
+__device__ __forceinline__ M3 mul3(const M3& a, const M3& b) {
+    M3 c;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) c.m[3 * i + j] = a.m[3 * i] * b.m[j] + a.m[3 * i + 1] * b.m[3 + j] + a.m[3 * i + 2] * b.m[6 + j];
+    return c;
+}
+__device__ __forceinline__ M3 mul3_tb(const M3& a, const M3& b) {  // a bᵀ
+    M3 c;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) c.m[3 * i + j] = a.m[3 * i] * b.m[3 * j] + a.m[3 * i + 1] * b.m[3 * j + 1] + a.m[3 * i + 2] * b.m[3 * j + 2];
+    return c;
+}
+__device__ __forceinline__ M3 mul3_ta(const M3& a, const M3& b) {  // aᵀ b
+    M3 c;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) c.m[3 * i + j] = a.m[i] * b.m[j] + a.m[3 + i] * b.m[3 + j] + a.m[6 + i] * b.m[6 + j];
+    return c;
+}
+__device__ __forceinline__ M3 rot_x(float a, bool d) {  // Rx(a) or dRx/da
+    const float c = cosf(a), s = sinf(a);
+    return d ? M3{{0, 0, 0, 0, -s, -c, 0, c, -s}} : M3{{1, 0, 0, 0, c, -s, 0, s, c}};
+}
+__device__ __forceinline__ M3 rot_y(float a, bool d) {
+    const float c = cosf(a), s = sinf(a);
+    return d ? M3{{-s, 0, c, 0, 0, 0, -c, 0, -s}} : M3{{c, 0, s, 0, 1, 0, -s, 0, c}};
+}
+__device__ __forceinline__ M3 rot_z(float a, bool d) {
+    const float c = cosf(a), s = sinf(a);
+    return d ? M3{{-s, -c, 0, c, -s, 0, 0, 0, 0}} : M3{{c, -s, 0, s, c, 0, 0, 0, 1}};
+}
+
+constexpr int kEulerMaxSteps = 64;
+
+__global__ void euler_chain_kernel(int K, int n, const float* __restrict__ omega, int64_t ld_o,
+                                   const float* __restrict__ vel, int64_t ld_v, const float* __restrict__ dt,
+                                   float* P) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= K) return;
+    const float h = dt[k];
+    M3 Q = {{1, 0, 0, 0, 1, 0, 0, 0, 1}};
+    float T[3] = {0.f, 0.f, 0.f};
+    for (int s = 0; s < n; ++s) {
+        const float* o = omega + (int64_t)(k * n + s) * ld_o;
+        const float* v = vel + (int64_t)(k * n + s) * ld_v;
+        const M3 A = mul3(mul3(rot_x(o[0] * h, false), rot_y(o[1] * h, false)), rot_z(o[2] * h, false));
+        float Tn[3];
+        for (int i = 0; i < 3; ++i) Tn[i] = (A.m[3 * i] * T[0] + A.m[3 * i + 1] * T[1] + A.m[3 * i + 2] * T[2]) + v[i] * h;
+        for (int i = 0; i < 3; ++i) T[i] = Tn[i];
+        Q = mul3(Q, A);
+    }
+    float* p = P + 16 * (int64_t)k;
+    for (int i = 0; i < 3; ++i) {
+        p[4 * i] = Q.m[3 * i];
+        p[4 * i + 1] = Q.m[3 * i + 1];
+        p[4 * i + 2] = Q.m[3 * i + 2];
+        p[4 * i + 3] = T[i];
+    }
+    p[12] = 0.f;
+    p[13] = 0.f;
+    p[14] = 0.f;
+    p[15] = 1.f;
+}
+
+// Reverse recurrence: with Q_{s+1} = Q_s A_s and T_{s+1} = A_s T_s + V_s,
+//   gA_s = gT_{s+1} T_sᵀ + Q_sᵀ gQ_{s+1},  gV_s = gT_{s+1},  gT_s = A_sᵀ gT_{s+1},  gQ_s = gQ_{s+1} A_sᵀ,
+// and the angles through A = Rx Ry Rz.
+__global__ void euler_chain_bwd_kernel(int K, int n, const float* __restrict__ omega, int64_t ld_o,
+                                       const float* __restrict__ vel, int64_t ld_v, const float* __restrict__ dt,
+                                       const float* __restrict__ dP, float* domega, float* dvel) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= K) return;
+    const float h = dt[k];
+    M3 Qs[kEulerMaxSteps];
+    float Ts[kEulerMaxSteps][3];
+    M3 Q = {{1, 0, 0, 0, 1, 0, 0, 0, 1}};
+    float T[3] = {0.f, 0.f, 0.f};
+    for (int s = 0; s < n; ++s) {  // forward again, keeping Q_s, T_s
+        Qs[s] = Q;
+        for (int i = 0; i < 3; ++i) Ts[s][i] = T[i];
+        const float* o = omega + (int64_t)(k * n + s) * ld_o;
+        const float* v = vel + (int64_t)(k * n + s) * ld_v;
+        const M3 A = mul3(mul3(rot_x(o[0] * h, false), rot_y(o[1] * h, false)), rot_z(o[2] * h, false));
+        float Tn[3];
+        for (int i = 0; i < 3; ++i) Tn[i] = (A.m[3 * i] * T[0] + A.m[3 * i + 1] * T[1] + A.m[3 * i + 2] * T[2]) + v[i] * h;
+        for (int i = 0; i < 3; ++i) T[i] = Tn[i];
+        Q = mul3(Q, A);
+    }
+    const float* g = dP + 16 * (int64_t)k;
+    M3 gQ = {{g[0], g[1], g[2], g[4], g[5], g[6], g[8], g[9], g[10]}};
+    float gT[3] = {g[3], g[7], g[11]};
+    for (int s = n - 1; s >= 0; --s) {
+        const float* o = omega + (int64_t)(k * n + s) * ld_o;
+        const float a = o[0] * h, b = o[1] * h, c = o[2] * h;
+        const M3 X = rot_x(a, false), Y = rot_y(b, false), Z = rot_z(c, false);
+        const M3 A = mul3(mul3(X, Y), Z);
+        M3 gA = mul3_ta(Qs[s], gQ);
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) gA.m[3 * i + j] += gT[i] * Ts[s][j];
+        float* dv = dvel + 3 * (int64_t)(k * n + s);
+        for (int i = 0; i < 3; ++i) dv[i] = gT[i] * h;
+        float gTn[3];
+        for (int j = 0; j < 3; ++j) gTn[j] = A.m[j] * gT[0] + A.m[3 + j] * gT[1] + A.m[6 + j] * gT[2];
+        for (int j = 0; j < 3; ++j) gT[j] = gTn[j];
+        gQ = mul3_tb(gQ, A);
+        const M3 dA[3] = {mul3(mul3(rot_x(a, true), Y), Z), mul3(mul3(X, rot_y(b, true)), Z),
+                          mul3(mul3(X, Y), rot_z(c, true))};
+        float* dw = domega + 3 * (int64_t)(k * n + s);
+        for (int q = 0; q < 3; ++q) {
+            float acc = 0.f;
+            for (int e = 0; e < 9; ++e) acc += gA.m[e] * dA[q].m[e];
+            dw[q] = acc * h;
+        }
+    }
+}
+
 }  // namespace cn
 
 using namespace cn;
+
+extern "C" int cn_euler_chain(int32_t K, int32_t n, const float* omega, int64_t ld_o, const float* vel, int64_t ld_v,
+                              const float* dt, float* P, cn_stream_t stream) {
+    CN_REQUIRE(omega && vel && dt && P, CN_ERR_ARG, "cn_euler_chain: null pointer");
+    CN_REQUIRE(K >= 0 && n >= 1 && n <= kEulerMaxSteps && ld_o >= 3 && ld_v >= 3, CN_ERR_SHAPE,
+               "cn_euler_chain: K=%d n=%d (n <= %d)", K, n, kEulerMaxSteps);
+    if (K == 0) return CN_OK;
+    euler_chain_kernel<<<(K + 63) / 64, 64, 0, (hipStream_t)stream>>>(K, n, omega, ld_o, vel, ld_v, dt, P);
+    return check_launch("cn_euler_chain");
+}
+
+extern "C" int cn_euler_chain_bwd(int32_t K, int32_t n, const float* omega, int64_t ld_o, const float* vel,
+                                  int64_t ld_v, const float* dt, const float* dP, float* domega, float* dvel,
+                                  cn_stream_t stream) {
+    CN_REQUIRE(omega && vel && dt && dP && domega && dvel, CN_ERR_ARG, "cn_euler_chain_bwd: null pointer");
+    CN_REQUIRE(K >= 0 && n >= 1 && n <= kEulerMaxSteps && ld_o >= 3 && ld_v >= 3, CN_ERR_SHAPE,
+               "cn_euler_chain_bwd: K=%d n=%d (n <= %d)", K, n, kEulerMaxSteps);
+    if (K == 0) return CN_OK;
+    euler_chain_bwd_kernel<<<(K + 63) / 64, 64, 0, (hipStream_t)stream>>>(K, n, omega, ld_o, vel, ld_v, dt, dP,
+                                                                          domega, dvel);
+    return check_launch("cn_euler_chain_bwd");
+}
 
 extern "C" int cn_patch_indices(int32_t h, int32_t w, int32_t ps, int32_t n_patches, const int32_t* key, int64_t* idx,
                                 cn_stream_t stream) {

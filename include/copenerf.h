@@ -308,6 +308,20 @@ int cn_patch_indices(int32_t h, int32_t w, int32_t ps, int32_t n_patches, const 
                      cn_stream_t stream);
 
 /* ------------------------------------------------------------------------ *
+ * Stage-1 relative poses (neus_fields.py:142-161, every interval at once): for
+ * interval k < K with its n time steps, A_s = EulerXYZ(omega_s dt_k) (pytorch3d
+ * convention, Rx Ry Rz), V_s = vel_s dt_k, T <- A_s T + V_s, Q <- Q A_s from
+ * Q = I, T = 0; P[k] = [Q T; 0 0 0 1] (row-major 4x4).  omega / vel rows
+ * k*n + s with leading dimensions ld_o / ld_v (floats).  The backward maps dP
+ * [K][4][4] to domega, dvel ([K*n][3] contiguous) by the reverse recurrence.
+ * One thread per interval (n <= 64).
+ * ------------------------------------------------------------------------ */
+int cn_euler_chain(int32_t K, int32_t n, const float* omega, int64_t ld_o, const float* vel, int64_t ld_v,
+                   const float* dt, float* P, cn_stream_t stream);
+int cn_euler_chain_bwd(int32_t K, int32_t n, const float* omega, int64_t ld_o, const float* vel, int64_t ld_v,
+                       const float* dt, const float* dP, float* domega, float* dvel, cn_stream_t stream);
+
+/* ------------------------------------------------------------------------ *
  * Sampling along rays (neus_renderer.py:453-525).
  * ------------------------------------------------------------------------ */
 /* z[r][i] = near*(1-lin_i) + far*lin_i, lin = linspace(0,1,n); stratified

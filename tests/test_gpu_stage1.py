@@ -146,3 +146,27 @@ def test_synthetic_trainer_modes_step(joint_pose, stage1):
         assert not torch.equal(tr.motion.lin0.bias.detach(), m0)
     for p in tr.all_params:
         assert torch.isfinite(p).all()
+
+
+def test_euler_chain_kernel_matches_torch_recurrence():
+    """cn_euler_chain / _bwd (all K relative poses, neus_fields.py:146-165) against the
+    torch recurrence of MotionNetwork.batched_relative_poses on the CPU: poses and the
+    motion network's parameter gradients."""
+    from copenerf.motion import MotionNetwork
+    from copenerf.train_step import MOTION_CFG
+    torch.manual_seed(5)
+    m = MotionNetwork(**MOTION_CFG)
+    with torch.no_grad():  # non-trivial velocities
+        for p in m.parameters():
+            p.add_(0.05 * torch.randn_like(p))
+    mc = MotionNetwork(**MOTION_CFG).to(DEV)
+    mc.load_state_dict({k: v.to(DEV) for k, v in m.state_dict().items()})
+    steps, dts = m.interval_time_grid(10, 10)
+    P_ref = m.batched_relative_poses(steps, dts)
+    P = mc.batched_relative_poses(steps.to(DEV), dts.to(DEV))
+    torch.testing.assert_close(P.cpu(), P_ref, rtol=1e-5, atol=2e-6)
+    G = torch.randn(P_ref.shape, generator=torch.Generator().manual_seed(6))
+    g_ref = torch.autograd.grad((P_ref * G).sum(), list(m.parameters()))
+    g = torch.autograd.grad((P * G.to(DEV)).sum(), list(mc.parameters()))
+    for a, b in zip(g, g_ref):
+        _close(a, b, "motion grad", 1e-4)
