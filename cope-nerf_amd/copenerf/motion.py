@@ -162,15 +162,21 @@ class MotionNetwork(nn.Module):
         dev = self._device()
         return torch.stack(steps).to(dev), torch.stack(dts).to(dev)
 
-    def batched_relative_poses(self, steps, dts):
+    def batched_relative_poses(self, steps, dts, extra_t=None):
         """Every consecutive relative pose at once: one MotionNetwork forward over all
         K*n time steps, then the reference's Euler recurrence (neus_fields.py:146-165)
         T <- R_s T + V_s, R <- R R_s run for all K intervals together (n batched 3x3
         steps instead of K*n host-launched ones).  steps [K, n], dts [K] -> [K, 4, 4]."""
         K, n = steps.shape
-        omega, vel = self.forward(steps.reshape(-1, 1))
+        t = steps.reshape(-1, 1)
+        if extra_t is not None:  # more time queries in the same network evaluation (returned as well)
+            t = torch.cat([t, extra_t.reshape(-1, 1).to(t.dtype)])
+        omega, vel = self.forward(t)
+        extra = (omega[K * n:], vel[K * n:]) if extra_t is not None else None
+        omega, vel = omega[:K * n], vel[:K * n]
         if omega.is_cuda:  # the recurrence forward and backward in one launch each (cn_euler_chain)
-            return _EulerChainFn.apply(omega, vel, dts.reshape(K).contiguous(), K, n)
+            P = _EulerChainFn.apply(omega, vel, dts.reshape(K).contiguous(), K, n)
+            return P if extra is None else (P, extra)
         dt = dts.view(K, 1, 1)
         Rs = euler_angles_to_matrix(omega.view(K, n, 3) * dt, "XYZ")  # [K, n, 3, 3]
         Vs = vel.view(K, n, 3) * dt
@@ -181,7 +187,8 @@ class MotionNetwork(nn.Module):
             R = R @ Rs[:, s]
         top = torch.cat([R, T], -1)  # [K, 3, 4]
         row = torch.eye(4, device=steps.device)[3:4].expand(K, 1, 4)  # no host scalar copy: capturable
-        return torch.cat([top, row], 1)
+        P = torch.cat([top, row], 1)
+        return P if extra is None else (P, extra)
 
 
 class _EulerChainFn(torch.autograd.Function):

@@ -292,10 +292,10 @@ class SyntheticTrainer:
         n = self.n_images
         img = self.sched.img
         R = batch["rgb_gt"].shape[0]
-        omega, vel = self.motion(self.sched.t.view(1, 1))
+        # one motion-network evaluation: the K*n Euler time steps and the frame's own time
+        P, (omega, vel) = self.motion.batched_relative_poses(self.steps_grid, self.dts, extra_t=self.sched.t)
         sdf_loss = scene_flow_loss(out["sampled_points"], out["normals"], out["sdf_flows"], out["weights"], omega,
                                    vel, group=grp)
-        P = self.motion.batched_relative_poses(self.steps_grid, self.dts)  # [K, 4, 4]
         K = P.shape[0]
         # flow-RGB: w2c_j = P[i+j-1] @ ... @ P[i] for the reference frames j = 1..3
         js = self.ref_intervals
