@@ -1703,6 +1703,10 @@ static int g_linear_variant = [] {
 // bf16x6 epilogues that run on the 256x128 one-workgroup-per-CU tile (bit e = cn_epilogue e;
 // benchmarking aid: COPENERF_WIDE_EPIS).  Default: the epilogues that read at most one aux
 // stream (STORE, SOFTPLUS, RELU, MUL, TANGENT).
+static int g_wide_min_k = [] {  // measured: K = 64 launches 3-7 % faster on the 2-per-CU tile
+    const char* e = getenv("COPENERF_WIDE_MINK");
+    return e ? atoi(e) : 128;
+}();
 static int g_stagger = [] {  // benchmarking aid: COPENERF_STAGGER (units of s_sleep 127 = 8128 cycles)
     const char* e = getenv("COPENERF_STAGGER");
     return e ? atoi(e) : 0;
@@ -1868,9 +1872,14 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
             // read from HBM once (the two N-tiles of the 256x128 tiling re-fetch 30-50 % of it,
             // PMC) and split once per row
             const bool tall = ((g_x6_tall >> d->epilogue) & 1) || (head && d->N > 128);
-            if (d->K % 64 == 0 && tall && d->N > 128 && d->ldb >= 256 && g_linear_variant == 0)
+            // short K (a first layer): the main loop is two chunks, so the one-workgroup-per-CU tiles
+            // cannot hide their epilogue; the 2-per-CU 128x128 tile overlaps it with the partner's
+            // (COPENERF_WIDE_MINK: the smallest K for the 1-per-CU tiles)
+            const bool longk = d->K >= g_wide_min_k;
+            if (d->K % 64 == 0 && tall && d->N > 128 && d->ldb >= 256 && g_linear_variant == 0 && (longk || head))
                 return launch_linear_tile<4, 2, 1, 4, 32, 1, 2, 2>(d, a, s);
-            if (d->K % 64 == 0 && g_linear_variant == 0 && light) return launch_linear_tile<4, 2, 2, 2, 32, 1, 2, 2>(d, a, s);
+            if (d->K % 64 == 0 && g_linear_variant == 0 && light && longk)
+                return launch_linear_tile<4, 2, 2, 2, 32, 1, 2, 2>(d, a, s);
             return launch_linear_tile<2, 2, 2, 2, 16, 2, 2, 2>(d, a, s);
         }
         return launch_linear_tile<4, 1, 1, 2, 16, 2, 2, 2>(d, a, s);
