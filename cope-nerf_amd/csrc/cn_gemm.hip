@@ -437,6 +437,35 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             if constexpr (MODE == 2) {
                 const float* a_base = sA + cur * BM * LS + arow * LS + 4 * (lane >> 5);
                 const float* b_base = sB + cur * BN * LS + brow * LS + 4 * (lane >> 5);
+                if constexpr (TM * TN >= 8) {
+                    // 64x128 wave tiles: the B fragments of one column block at a time (12 VGPRs
+                    // instead of 48 live); a single accumulation chain issues back to back
+#pragma unroll
+                    for (int ks = 0; ks < BK / 16; ++ks) {
+                        bf16x8 af[3][TM];
+#pragma unroll
+                        for (int t = 0; t < 3; ++t)
+#pragma unroll
+                            for (int i = 0; i < TM; ++i)
+                                af[t][i] = *reinterpret_cast<const bf16x8*>(a_base + i * 32 * LS + t * (BK / 2) + ks * 8);
+#pragma unroll
+                        for (int j = 0; j < TN; ++j) {
+                            bf16x8 bj[3];
+#pragma unroll
+                            for (int t = 0; t < 3; ++t)
+                                bj[t] = *reinterpret_cast<const bf16x8*>(b_base + j * 32 * LS + t * (BK / 2) + ks * 8);
+                            constexpr int TA[6] = {0, 1, 0, 2, 1, 0};
+                            constexpr int TB[6] = {0, 0, 1, 0, 1, 2};
+#pragma unroll
+                            for (int u = 0; u < 6; ++u)
+#pragma unroll
+                                for (int i = 0; i < TM; ++i)
+                                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[TA[u]][i], bj[TB[u]], acc[i][j],
+                                                                                         0, 0, 0);
+                        }
+                    }
+                    return;
+                }
 #pragma unroll
                 for (int ks = 0; ks < BK / 16; ++ks) {
                     bf16x8 af[3][TM], bf[3][TN];
@@ -760,8 +789,64 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         // goes out from the MFMA layout itself -- lane l holds column l&31 of rows (r&3) +
         // 8(r>>2) + 4(l>>5), so one dword store per (i, j, r) writes two full 128-byte row
         // segments -- with no LDS park, no barrier and no readback.
-        constexpr bool kDirect = DIRECT_EPI && !kAnyAux && EPI != 7;
-        if (kDirect && tile_main) {
+        // On the 64x128 wave tiles the elementwise aux epilogues (MUL, TANGENT, BWD_SOFTPLUS) go
+        // the same way: their aux rows are read in the MFMA layout too (dword loads, two 128-byte
+        // row segments per instruction), RG accumulator rows at a time, double-buffered (group
+        // g+1's loads issued before group g's stores, so each wait skips those stores)
+        constexpr bool kDirectAux = DIRECT_EPI && TM * TN >= 8 && !ROWV &&
+                                    (EPI == CN_EPI_MUL || EPI == CN_EPI_TANGENT || EPI == CN_EPI_BWD_SOFTPLUS);
+        constexpr bool kDirect = DIRECT_EPI && ((!kAnyAux && EPI != 7) || kDirectAux);
+        if (kDirect && tile_main && kDirectAux) {
+            const int lrow = wm * TM * 32 + 4 * (lane >> 5);
+            const int lcol = wn * TN * 32 + (lane & 31);
+            const int vo = (lrow * p.ld_out0 + lcol) * 4;
+            const int v0 = (lrow * p.ld_aux0 + lcol) * 4;
+            const int v1 = (lrow * p.ld_aux1 + lcol) * 4;
+            const int v2 = (lrow * p.ld_aux2 + lcol) * 4;
+            constexpr int RG = kAux1 ? 2 : 4;          // accumulator rows r per group
+            constexpr int NGD = TM * 16 / RG;          // groups per tile
+            float xa[2][RG][TN], xb[2][RG][TN], xc[2][RG][TN];
+            auto dload = [&](int g, int sl) {
+                const int i = g / (16 / RG), r0 = (g % (16 / RG)) * RG;
+#pragma unroll
+                for (int q = 0; q < RG; ++q) {
+                    const int r = r0 + q, row = i * 32 + (r & 3) + 8 * (r >> 2);
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        xa[sl][q][j] = bload1(view_at(tX0, row), v0, 128 * j);
+                        if (kAux1) xb[sl][q][j] = bload1(view_at(tX1, row), v1, 128 * j);
+                        if (kAux1) xc[sl][q][j] = bload1(view_at(tX2, row), v2, 128 * j);
+                    }
+                }
+            };
+            dload(0, 0);
+#pragma unroll
+            for (int g = 0; g < NGD; ++g) {
+                const int sl = g & 1;
+                if (g + 1 < NGD) dload(g + 1, sl ^ 1);
+                const int i = g / (16 / RG), r0 = (g % (16 / RG)) * RG;
+#pragma unroll
+                for (int q = 0; q < RG; ++q) {
+                    const int r = r0 + q;
+                    const rsrc_t vw = view_at(tO0, i * 32 + (r & 3) + 8 * (r >> 2));
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        const float u = acc[i][j][r] * p.inv_adiv;
+                        const float sg = sigma_from_act(xa[sl][q][j], p.aux_c);
+                        float o;
+                        if constexpr (EPI == CN_EPI_MUL) {
+                            o = u * sg;
+                        } else if constexpr (EPI == CN_EPI_TANGENT) {
+                            o = u * sg * p.inv_odiv;
+                        } else {  // BWD_SOFTPLUS, as main_vals
+                            const float rr2 = sg > 0.0f ? (1.0f - sg) * __builtin_amdgcn_rcpf(sg) : 0.0f;
+                            o = u * sg + xb[sl][q][j] * xc[sl][q][j] * (p.aux2_scale * rr2);
+                        }
+                        bstore1(vw, vo, 128 * j, o);
+                    }
+                }
+            }
+        } else if (kDirect && tile_main) {
             const int lrow = wm * TM * 32 + 4 * (lane >> 5);
             const int lcol = wn * TN * 32 + (lane & 31);
             const int vo = (lrow * p.ld_out0 + lcol) * 4;
@@ -1718,6 +1803,17 @@ static int g_x6_tall = [] {
     const char* e = getenv("COPENERF_X6_TALL");
     return e ? (int)strtol(e, nullptr, 0) : 0x18;
 }();
+// bf16x6 epilogues on the 256x256 tile (bit e = cn_epilogue e; COPENERF_X6_SQ): 8 waves of 64x128,
+// 16-deep stages; a workgroup owns whole 256-wide rows (A read and split once) and every staged
+// fragment feeds more MFMAs (0.375 vs 0.5 KiB of LDS reads per MFMA on the 256x128 tile).  Main
+// loop 316-320 vs 374 us at C2's layer shape; with the epilogue (tools/sq_check.py, bitwise equal
+// outputs): SOFTPLUS 445 vs 480-509, STORE 467 vs 491, RELU 385 vs 408-420, MUL / TANGENT 443-451 vs
+// 470 (their aux rows read in the MFMA layout); BWD_SOFTPLUS 667 vs 614 (stays on 128x128).  Only
+// for N == 256 without a split output: every tile then takes the direct (MFMA-layout) epilogue.
+static int g_x6_sq = [] {
+    const char* e = getenv("COPENERF_X6_SQ");
+    return e ? (int)strtol(e, nullptr, 0) : 0x1f;
+}();
 static int g_wide_epis = [] {
     const char* e = getenv("COPENERF_WIDE_EPIS");
     return e ? (int)strtol(e, nullptr, 0) : 0x1f;
@@ -1876,6 +1972,10 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
             // cannot hide their epilogue; the 2-per-CU 128x128 tile overlaps it with the partner's
             // (COPENERF_WIDE_MINK: the smallest K for the 1-per-CU tiles)
             const bool longk = d->K >= g_wide_min_k;
+            const bool sq = ((g_x6_sq >> d->epilogue) & 1) && d->N == 256 && !d->rowv &&
+                            !(d->epilogue == CN_EPI_MUL && d->out_split && d->nsplit < d->N);
+            if (d->K % 32 == 0 && sq && d->N > 128 && d->ldb >= 256 && g_linear_variant == 0 && (longk || head))
+                return launch_linear_tile<4, 2, 2, 4, 16, 1, 2, 2>(d, a, s);
             if (d->K % 64 == 0 && tall && d->N > 128 && d->ldb >= 256 && g_linear_variant == 0 && (longk || head))
                 return launch_linear_tile<4, 2, 1, 4, 32, 1, 2, 2>(d, a, s);
             if (d->K % 64 == 0 && g_linear_variant == 0 && light && longk)
