@@ -405,7 +405,10 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None):
         Zl = Z
         if l > 0:
             Z = _empty(M, HL, dev)
-            ops.linear(Zl, pk.Bt[l], lay.out_dim[l - 1], rup(lay.out_dim[l], 32), Z, EPI_BWD_SOFTPLUS,
+            # first order only (no second-order term): Z = (W̃ᵀZ)σ is the MUL epilogue, which runs on
+            # the 256x256 tile (BWD_SOFTPLUS would add an all-zero term on the 128x128 tile)
+            ops.linear(Zl, pk.Bt[l], lay.out_dim[l - 1], rup(lay.out_dim[l], 32), Z,
+                       EPI_BWD_SOFTPLUS if second else EPI_MUL,
                        aux0=U[l], aux_beta=sig_beta(lay, l - 1), nzero=HL, adiv=SQRT2 if l == sk else 1.0,
                        kalg=lay.out_dim[l], **second_order(l - 1))
         dW = torch.empty(lay.out_dim[l], lay.in_dim[l], device=dev)

@@ -796,7 +796,10 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         constexpr bool kDirectAux = DIRECT_EPI && TM * TN >= 8 && !ROWV &&
                                     (EPI == CN_EPI_MUL || EPI == CN_EPI_TANGENT || EPI == CN_EPI_BWD_SOFTPLUS);
         constexpr bool kDirect = DIRECT_EPI && ((!kAnyAux && EPI != 7) || kDirectAux);
-        if (kDirect && tile_main && kDirectAux) {
+        // 64x128 wave tiles are dispatched only where every tile is a main tile (N == 256, no split,
+        // no rowv: host-checked), so their kernels carry no LDS-park path (and its registers)
+        constexpr bool kDirectOnly = kDirect && TM * TN >= 8;
+        auto direct_aux = [&]() {
             const int lrow = wm * TM * 32 + 4 * (lane >> 5);
             const int lcol = wn * TN * 32 + (lane & 31);
             const int vo = (lrow * p.ld_out0 + lcol) * 4;
@@ -846,7 +849,8 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                     }
                 }
             }
-        } else if (kDirect && tile_main) {
+        };
+        auto direct_plain = [&]() {
             const int lrow = wm * TM * 32 + 4 * (lane >> 5);
             const int lcol = wn * TN * 32 + (lane & 31);
             const int vo = (lrow * p.ld_out0 + lcol) * 4;
@@ -868,10 +872,20 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         bstore1(vw, vo, 128 * j, o);
                     }
                 }
+        };
+        if constexpr (kDirectOnly) {
+            if constexpr (kDirectAux) direct_aux();
+            else direct_plain();
         } else {
-            if (tile_main) passes(std::true_type{});
-            else passes(std::false_type{});
-            __syncthreads();  // sC is the next tile's staging buffer
+            if (kDirectAux && tile_main) {
+                direct_aux();
+            } else if (kDirect && tile_main) {
+                direct_plain();
+            } else {
+                if (tile_main) passes(std::true_type{});
+                else passes(std::false_type{});
+                __syncthreads();  // sC is the next tile's staging buffer
+            }
         }
         vt = vt_next;
         tm = tm_next;
@@ -1972,7 +1986,8 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
             // cannot hide their epilogue; the 2-per-CU 128x128 tile overlaps it with the partner's
             // (COPENERF_WIDE_MINK: the smallest K for the 1-per-CU tiles)
             const bool longk = d->K >= g_wide_min_k;
-            const bool sq = ((g_x6_sq >> d->epilogue) & 1) && d->N == 256 && !d->rowv &&
+            // (the epilogues with a direct form: STORE, SOFTPLUS, RELU, MUL, TANGENT, BWD_SOFTPLUS)
+            const bool sq = ((g_x6_sq & 0xbf) >> d->epilogue & 1) && d->N == 256 && !d->rowv &&
                             !(d->epilogue == CN_EPI_MUL && d->out_split && d->nsplit < d->N);
             if (d->K % 32 == 0 && sq && d->N > 128 && d->ldb >= 256 && g_linear_variant == 0 && (longk || head))
                 return launch_linear_tile<4, 2, 2, 4, 16, 1, 2, 2>(d, a, s);
