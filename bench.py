@@ -55,29 +55,13 @@ SAMPLES = 128
 GFLOP_PER_RAY_REF = 1.4809  # reference GEMM FLOPs per ray per train step (64+4x16)
 
 
-# cn_linear's bf16x6 epilogues on the 128x256 tile (cn_gemm.hip g_x6_tall, default 0x18) and on
-# the 256x128 tile (g_wide_epis, default 0x1f); the rest on 128x128
-TALL_EPIS = int(os.environ.get("COPENERF_X6_TALL", "0x18"), 0)
-WIDE_EPIS = int(os.environ.get("COPENERF_WIDE_EPIS", "0x1f"), 0)
-EPI_ID = {"store": 0, "softplus": 1, "relu": 2, "mul": 3, "tangent": 4, "bwd_softplus": 5, "bwd_relu": 6}
-
-
 def kernel_symbol(key):
-    """rocprofv3 name of the kernel a KernelTimer key times (cn_gemm.hip's
-    cn_linear dispatch: waves, tiles, BK, workgroups/CU, prefetch depth,
-    epilogue, row vector, operand mode).  fp32: BK 32 with the 2-deep prefetch
-    (every K on the C2 path is a multiple of 64); bf16: BK 64, 1-deep; bf16x6
-    (split fp32): 256x128 tiles, BK 32, one workgroup per CU for the epilogues in
-    WIDE_EPIS at K % 64 == 0 (every such K on C2), else 128x128, BK 16, 2-deep."""
+    """rocprofv3 name of the kernel a KernelTimer key times: cn_linear's tile choice is
+    mirrored in copenerf.ops (the key's second field names the bf16x6 tile); a cn_wgrad
+    call is its split-M MFMA kernel plus the fixed-order slab reduction."""
     if key[0] == "linear":
-        epi = EPI_ID[key[2]]
-        x6 = "x6" in key[3:] and key[1] == 0
-        tall = x6 and (TALL_EPIS >> epi) & 1  # N = 256 on every C2 call of these epilogues
-        wide = x6 and not tall and (WIDE_EPIS >> epi) & 1
-        tiles = {0: "4, 2, 1, 4" if tall else "4, 2, 2, 2" if wide else "2, 2, 2, 2", 1: "4, 1, 1, 2"}
-        mode = 1 if "bf16" in key[3:] else 2 if "x6" in key[3:] else 0
-        mid = {0: "32, 2, 2", 1: "64, 2, 1", 2: "32, 1, 2" if (wide or tall) else "16, 2, 2"}[mode]
-        return f"void cn::linear_kernel<{tiles[key[1]]}, {mid}, {epi}, false, {mode}>(cn::LinearArgs)"
+        from copenerf import ops
+        return ops.linear_kernel_symbol(key)
     if "bf16" in key[2:]:
         return "void cn::wgrad_bf16_kernel<2, 2, 2, 2>(cn::WgradArgs) + cn::slab_reduce_kernel"
     if "x6" in key[2:]:

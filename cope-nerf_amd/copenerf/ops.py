@@ -8,6 +8,7 @@ leading dimension (stride(0)) is passed explicitly, so column views such as
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -51,7 +52,7 @@ class KernelTimer:
 _timer = None
 # cn_linear_desc.flags bit 0 alternated launch to launch (the memory-side cache holds the last
 # rows a layer wrote when the next one starts; see include/copenerf.h)
-ALTERNATE_TILE_ORDER = __import__("os").environ.get("COPENERF_ALT_ORDER", "1") != "0"
+ALTERNATE_TILE_ORDER = os.environ.get("COPENERF_ALT_ORDER", "1") != "0"
 _flip = 0
 EPI_NAMES = {0: "store", 1: "softplus", 2: "relu", 3: "mul", 4: "tangent", 5: "bwd_softplus", 6: "bwd_relu",
              7: "bench_mainloop", 8: "softplus_head"}
@@ -192,6 +193,46 @@ class ImagePacker:
         self.jobs, self.keep = [], []
 
 
+# cn_linear's bf16x6 tile choice (cn_gemm.hip, cn_linear; the same env knobs), for the kernel
+# timer's launch classes and the rocprofv3 names of their kernels
+_X6_SQ = int(os.environ.get("COPENERF_X6_SQ", "0x1f"), 0) & 0xbf
+_X6_TALL = int(os.environ.get("COPENERF_X6_TALL", "0x18"), 0)
+_WIDE_EPIS = int(os.environ.get("COPENERF_WIDE_EPIS", "0x1f"), 0)
+_WIDE_MINK = int(os.environ.get("COPENERF_WIDE_MINK", "128"))
+_LINEAR_TILES = {  # tag -> linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH> (bf16x6); tile 1 / other modes below
+    "sq": "4, 2, 2, 4, 16, 1, 2", "tall": "4, 2, 1, 4, 32, 1, 2", "wide": "4, 2, 2, 2, 32, 1, 2",
+    "t128": "2, 2, 2, 2, 16, 2, 2"}
+
+
+def _x6_tile(epi, N, K, ldb, rowv, split):
+    head = epi == EPI_SOFTPLUS_HEAD
+    longk = K >= _WIDE_MINK
+    if (_X6_SQ >> epi) & 1 and N == 256 and not rowv and not (epi == EPI_MUL and split) and K % 32 == 0 \
+            and ldb >= 256 and (longk or head):
+        return "sq"
+    tall = (_X6_TALL >> epi) & 1 or (head and N > 128)
+    if K % 64 == 0 and tall and N > 128 and ldb >= 256 and (longk or head):
+        return "tall"
+    if K % 64 == 0 and (_WIDE_EPIS >> epi) & 1 and longk:
+        return "wide"
+    return "t128"
+
+
+def linear_kernel_symbol(key):
+    """rocprofv3 name of the kernel behind a kernel-timer cn_linear key."""
+    _, tag, epi = key[:3]
+    rowv = epi.endswith("+rowv")
+    eid = {v: k for k, v in EPI_NAMES.items()}[epi.split("+")[0]]
+    mode = 1 if "bf16" in key[3:] else 2 if "x6" in key[3:] else 0
+    if mode == 2:
+        tiles = _LINEAR_TILES.get(tag, "4, 1, 1, 2, 16, 2, 2")
+    elif mode == 1:
+        tiles = "2, 2, 2, 2, 64, 2, 1" if tag == 0 else "4, 1, 1, 2, 64, 2, 1"
+    else:
+        tiles = "2, 2, 2, 2, 32, 2, 2" if tag == 0 else "4, 1, 1, 2, 32, 2, 2"
+    return f"void cn::linear_kernel<{tiles}, {eid}, {str(rowv).lower()}, {mode}>(cn::LinearArgs)"
+
+
 def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None, colv=None, aux0=None,
            aux1=None, aux2=None, out_split=None, nsplit=None, nzero=None, adiv=1.0, odiv=1.0, beta=100.0,
            threshold=20.0, aux_beta=0.0, aux2_scale=0.0, tile=None, M=None, kalg=None, out1=None, head_w=None,
@@ -272,7 +313,10 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     if _timer is not None:
         e0 = _timer.start()
         _lib.check(_lib.load().cn_linear(d, _stream()), "cn_linear")
-        key = ("linear", tile, EPI_NAMES[epilogue]) + (("bf16",) if bf else ("x6",) if x6 else ())
+        tag = _x6_tile(epilogue, N, K, d.ldb, rowv is not None,
+                       out_split is not None and d.nsplit < N) if x6 and tile == 0 else tile
+        key = ("linear", tag, EPI_NAMES[epilogue] + ("+rowv" if rowv is not None else "")) + \
+            (("bf16",) if bf else ("x6",) if x6 else ())
         ka = kalg or K
         # algorithmic HBM bytes: A (unpadded K) and every aux row read once, each output
         # element written once, the weight image once (bf16x6: 3 bf16 terms per weight)
