@@ -301,9 +301,13 @@ def sdf_input_grad(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dh=None):
     return dx
 
 
-def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None):
+def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want_dx=False):
     """Parameter gradients of SDFNetwork for upstream (dL/dsdf, dL/dfeature,
-    dL/d∇ₓSDF).  The ∇ₓSDF term (the create_graph double backward of
+    dL/d∇ₓSDF); with want_dx also dL/dx, returned third.  First order (dG None) the
+    parameter adjoint chain Z_l is the input adjoint chain P_l of sdf_input_grad
+    (same seed, same recurrence), so dx comes from the same GEMMs: the skip layer's
+    adjoint also writes its embedding columns, then W_0ᵀ Z_0 and the assembly (the
+    consistency re-query of train.py:504 with pose gradients: 7 GEMM passes fewer).  The ∇ₓSDF term (the create_graph double backward of
     neus_fields.py:296) is computed forward-over-reverse:
 
       tangent   u̇_0 = J_emb(x)·v,  ż_l = W_l u̇_l,  u̇_{l+1} = σ_l ⊙ ż_l
@@ -401,22 +405,37 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None):
                    aux_beta=sig_beta(lay, L8 - 1), nzero=HL, **second_order(L8 - 1))
     dWs, dbs = [None] * nl, [None] * nl
     dWs[L8], dbs[L8] = dW8, db8
+    share = want_dx and not second  # Z_l == P_l: dx from the parameter adjoint chain
+    PE = _empty(M, KE, dev) if (share and sk >= 0) else None
     for l in range(L8 - 1, -1, -1):
         Zl = Z
         if l > 0:
             Z = _empty(M, HL, dev)
-            # first order only (no second-order term): Z = (W̃ᵀZ)σ is the MUL epilogue, which runs on
-            # the 256x256 tile (BWD_SOFTPLUS would add an all-zero term on the 128x128 tile)
-            ops.linear(Zl, pk.Bt[l], lay.out_dim[l - 1], rup(lay.out_dim[l], 32), Z,
-                       EPI_BWD_SOFTPLUS if second else EPI_MUL,
-                       aux0=U[l], aux_beta=sig_beta(lay, l - 1), nzero=HL, adiv=SQRT2 if l == sk else 1.0,
-                       kalg=lay.out_dim[l], **second_order(l - 1))
+            if share and l == sk:  # + the embedding columns of the skip input (sdf_input_grad's PE)
+                ops.linear(Zl, pk.Bt[l], lay.in_dim[l], rup(lay.out_dim[l], 32), Z, EPI_MUL, aux0=U[l],
+                           aux_beta=sig_beta(lay, l - 1), nsplit=lay.out_dim[l - 1], out_split=PE, nzero=HL,
+                           adiv=SQRT2, kalg=lay.out_dim[l])
+            else:
+                # first order only (no second-order term): Z = (W̃ᵀZ)σ is the MUL epilogue, which runs on
+                # the 256x256 tile (BWD_SOFTPLUS would add an all-zero term on the 128x128 tile)
+                ops.linear(Zl, pk.Bt[l], lay.out_dim[l - 1], rup(lay.out_dim[l], 32), Z,
+                           EPI_BWD_SOFTPLUS if second else EPI_MUL,
+                           aux0=U[l], aux_beta=sig_beta(lay, l - 1), nzero=HL, adiv=SQRT2 if l == sk else 1.0,
+                           kalg=lay.out_dim[l], **second_order(l - 1))
         dW = torch.empty(lay.out_dim[l], lay.in_dim[l], device=dev)
         db = torch.empty(lay.out_dim[l], device=dev)
         ops.wgrad(Zl, U[l], lay.out_dim[l], lay.in_dim[l], dW, db=db,
                   Y1=S[l] if second else None, X1=Ud[l] if second else None, mode=wmode)
         dWs[l], dbs[l] = dW, db
-    return dWs, dbs
+    if not want_dx:
+        return dWs, dbs
+    if not share:
+        return dWs, dbs, sdf_input_grad(lay, pk, st, dsdf, dfeat, dh=dh)
+    P0 = _empty(M, KE, dev)  # Zl is Z_0 here
+    ops.linear(Zl, pk.Bt[0], lay.E, rup(lay.out_dim[0], 32), P0, EPI_STORE, nzero=KE, kalg=lay.out_dim[0])
+    dx = _empty(M, 4, dev)
+    ops.sdf_grad_assemble(lay.multires, lay.scale, U[0], P0, PE, dx)
+    return dWs, dbs, dx
 
 
 class _SDFFieldFn(torch.autograd.Function):
@@ -454,13 +473,19 @@ class _SDFFieldFn(torch.autograd.Function):
         dh = None
         if ctx.hidden:
             dh, dfeat = dfeat, None
-        dx = sdf_input_grad(ctx.lay, ctx.pk, ctx.st, dsdf, dfeat, dh=dh) if ctx.needs_input_grad[0] else None
+        want_dx = ctx.needs_input_grad[0]
+        dx = None
         grads = [None] * ctx.nparams
         if any(ctx.needs_input_grad[5:]):
-            dWs, dbs = sdf_backward(ctx.lay, ctx.pk, ctx.st, dsdf, dfeat, dG, dh=dh)
+            res = sdf_backward(ctx.lay, ctx.pk, ctx.st, dsdf, dfeat, dG, dh=dh, want_dx=want_dx)
+            dWs, dbs = res[0], res[1]
+            if want_dx:
+                dx = res[2]
             grads = []
             for w, b in zip(dWs, dbs):
                 grads += [w, b]
+        elif want_dx:
+            dx = sdf_input_grad(ctx.lay, ctx.pk, ctx.st, dsdf, dfeat, dh=dh)
         ctx.st = None
         return (dx,) + none4 + tuple(grads)
 

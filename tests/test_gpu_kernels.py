@@ -296,6 +296,35 @@ def test_sdf_field_forward_gradient_and_double_backward(dh):
         torch.testing.assert_close(gg.cpu(), r, rtol=2e-3, atol=2e-4 * scale, msg=lambda m: f"{n}: {m}")
 
 
+@pytest.mark.parametrize("want_feat", [False, True])
+def test_sdf_first_order_input_and_parameter_gradients(want_feat):
+    """First order with dL/dx and the parameter gradients together (e.g. train.py:504's
+    SDFNetwork.sdf on pose-dependent points): the input gradient comes out of the
+    parameter adjoint chain (fields.sdf_backward want_dx) -- against oracle autograd."""
+    sdf, col, dev = build_modules(33)
+    P, Pc, var, leaves = oracle_params(sdf, col, dev)
+    M = 2500
+    x = _sdf_points(M, 7)
+    g = torch.Generator().manual_seed(8)
+    a, Bm = torch.randn(M, 1, generator=g), torch.randn(M, 256, generator=g) * 0.01
+    xr = x.clone().requires_grad_(True)
+    out = O.sdf_mlp(P, xr)
+    L = (a * out[:, :1]).sum() + ((Bm * out[:, 1:]).sum() if want_feat else 0.0)
+    names = [n for n in leaves if n.startswith("sdf.")]
+    ref = torch.autograd.grad(L, [xr] + [leaves[n] for n in names])
+    sdf_g = sdf.to(DEV)
+    xg = x.to(DEV).requires_grad_(True)
+    s, f, _ = sdf_g.field(xg, want_feat=want_feat, want_grad=False)
+    Lg = (a.to(DEV) * s).sum() + ((Bm.to(DEV) * f).sum() if want_feat else 0.0)
+    params = dict(sdf_g.named_parameters())
+    got = torch.autograd.grad(Lg, [xg] + [params[n[4:]] for n in names])
+    sc = ref[0].abs().max().item() + 1e-6  # dL/d(x, y, z, t): all four embedded inputs
+    torch.testing.assert_close(got[0].cpu(), ref[0], rtol=2e-3, atol=2e-4 * sc)
+    for n, r, gg in zip(names, ref[1:], got[1:]):
+        scale = r.abs().max().item() + 1e-6
+        torch.testing.assert_close(gg.cpu(), r, rtol=2e-3, atol=2e-4 * scale, msg=lambda m: f"{n}: {m}")
+
+
 def test_color_field_forward_backward():
     sdf, col, dev = build_modules(32)
     P, Pc, var, leaves = oracle_params(sdf, col, dev)
