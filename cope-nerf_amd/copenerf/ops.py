@@ -195,7 +195,7 @@ class ImagePacker:
 
 # cn_linear's bf16x6 tile choice (cn_gemm.hip, cn_linear; the same env knobs), for the kernel
 # timer's launch classes and the rocprofv3 names of their kernels
-_X6_SQ = int(os.environ.get("COPENERF_X6_SQ", "0x1f"), 0) & 0xbf
+_X6_SQ = int(os.environ.get("COPENERF_X6_SQ", "0x5f"), 0)
 _X6_TALL = int(os.environ.get("COPENERF_X6_TALL", "0x18"), 0)
 _WIDE_EPIS = int(os.environ.get("COPENERF_WIDE_EPIS", "0x1f"), 0)
 _WIDE_MINK = int(os.environ.get("COPENERF_WIDE_MINK", "128"))

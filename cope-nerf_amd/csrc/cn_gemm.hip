@@ -794,7 +794,8 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         // row segments per instruction), RG accumulator rows at a time, double-buffered (group
         // g+1's loads issued before group g's stores, so each wait skips those stores)
         constexpr bool kDirectAux = DIRECT_EPI && TM * TN >= 8 && !ROWV &&
-                                    (EPI == CN_EPI_MUL || EPI == CN_EPI_TANGENT || EPI == CN_EPI_BWD_SOFTPLUS);
+                                    (EPI == CN_EPI_MUL || EPI == CN_EPI_TANGENT || EPI == CN_EPI_BWD_SOFTPLUS ||
+                                     EPI == CN_EPI_BWD_RELU);
         constexpr bool kDirect = DIRECT_EPI && ((!kAnyAux && EPI != 7) || kDirectAux);
         // 64x128 wave tiles are dispatched only where every tile is a main tile (N == 256, no split,
         // no rowv: host-checked), so their kernels carry no LDS-park path (and its registers)
@@ -835,9 +836,11 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 #pragma unroll
                     for (int j = 0; j < TN; ++j) {
                         const float u = acc[i][j][r] * p.inv_adiv;
-                        const float sg = sigma_from_act(xa[sl][q][j], p.aux_c);
+                        const float sg = EPI == CN_EPI_BWD_RELU ? 0.0f : sigma_from_act(xa[sl][q][j], p.aux_c);
                         float o;
-                        if constexpr (EPI == CN_EPI_MUL) {
+                        if constexpr (EPI == CN_EPI_BWD_RELU) {
+                            o = xa[sl][q][j] > 0.0f ? u : 0.0f;
+                        } else if constexpr (EPI == CN_EPI_MUL) {
                             o = u * sg;
                         } else if constexpr (EPI == CN_EPI_TANGENT) {
                             o = u * sg * p.inv_odiv;
@@ -1822,11 +1825,12 @@ static int g_x6_tall = [] {
 // fragment feeds more MFMAs (0.375 vs 0.5 KiB of LDS reads per MFMA on the 256x128 tile).  Main
 // loop 316-320 vs 374 us at C2's layer shape; with the epilogue (tools/sq_check.py, bitwise equal
 // outputs): SOFTPLUS 445 vs 480-509, STORE 467 vs 491, RELU 385 vs 408-420, MUL / TANGENT 443-451 vs
-// 470 (their aux rows read in the MFMA layout); BWD_SOFTPLUS 667 vs 614 (stays on 128x128).  Only
-// for N == 256 without a split output: every tile then takes the direct (MFMA-layout) epilogue.
+// 470 (their aux rows read in the MFMA layout); BWD_RELU 455-463 vs 477-479; BWD_SOFTPLUS 667 vs 614
+// (stays on 128x128).  Only for N == 256 without a split output: every tile then takes the direct
+// (MFMA-layout) epilogue.
 static int g_x6_sq = [] {
     const char* e = getenv("COPENERF_X6_SQ");
-    return e ? (int)strtol(e, nullptr, 0) : 0x1f;
+    return e ? (int)strtol(e, nullptr, 0) : 0x5f;
 }();
 static int g_wide_epis = [] {
     const char* e = getenv("COPENERF_WIDE_EPIS");
@@ -1986,8 +1990,8 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
             // cannot hide their epilogue; the 2-per-CU 128x128 tile overlaps it with the partner's
             // (COPENERF_WIDE_MINK: the smallest K for the 1-per-CU tiles)
             const bool longk = d->K >= g_wide_min_k;
-            // (the epilogues with a direct form: STORE, SOFTPLUS, RELU, MUL, TANGENT, BWD_SOFTPLUS)
-            const bool sq = ((g_x6_sq & 0xbf) >> d->epilogue & 1) && d->N == 256 && !d->rowv &&
+            // (the epilogues with a direct form: STORE, SOFTPLUS, RELU, MUL, TANGENT, BWD_SOFTPLUS, BWD_RELU)
+            const bool sq = (g_x6_sq >> d->epilogue & 1) && d->N == 256 && !d->rowv &&
                             !(d->epilogue == CN_EPI_MUL && d->out_split && d->nsplit < d->N);
             if (d->K % 32 == 0 && sq && d->N > 128 && d->ldb >= 256 && g_linear_variant == 0 && (longk || head))
                 return launch_linear_tile<4, 2, 2, 4, 16, 1, 2, 2>(d, a, s);

@@ -27,6 +27,7 @@ def child():
     for name, epi, kw in (("store", ops.EPI_STORE, dict(bias=bias)), ("softplus", ops.EPI_SOFTPLUS, dict(bias=bias)),
                           ("relu", ops.EPI_RELU, dict(bias=bias)), ("mul", ops.EPI_MUL, sg),
                           ("tangent", ops.EPI_TANGENT, sg), ("bwd_softplus", ops.EPI_BWD_SOFTPLUS, so),
+                          ("bwd_relu", ops.EPI_BWD_RELU, dict(aux0=aux1)),
                           ("main", 7, {})):
         o0 = torch.zeros(M, N, device="cuda")
         fn = lambda: ops.linear(A, Bs, N, K, o0, epi, **kw)  # noqa: E731
