@@ -207,7 +207,7 @@ _LINEAR_TILES = {  # tag -> linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH> (bf16x
 def _x6_tile(epi, N, K, ldb, rowv, split):
     head = epi == EPI_SOFTPLUS_HEAD
     longk = K >= _WIDE_MINK
-    if (_X6_SQ >> epi) & 1 and N == 256 and not rowv and not (epi == EPI_MUL and split) and K % 32 == 0 \
+    if (_X6_SQ >> epi) & 1 and 128 < N <= 256 and not rowv and not (epi == EPI_MUL and split) and K % 32 == 0 \
             and ldb >= 256 and (longk or head):
         return "sq"
     tall = (_X6_TALL >> epi) & 1 or (head and N > 128)

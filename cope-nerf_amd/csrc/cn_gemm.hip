@@ -797,9 +797,22 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                                     (EPI == CN_EPI_MUL || EPI == CN_EPI_TANGENT || EPI == CN_EPI_BWD_SOFTPLUS ||
                                      EPI == CN_EPI_BWD_RELU);
         constexpr bool kDirect = DIRECT_EPI && ((!kAnyAux && EPI != 7) || kDirectAux);
-        // 64x128 wave tiles are dispatched only where every tile is a main tile (N == 256, no split,
-        // no rowv: host-checked), so their kernels carry no LDS-park path (and its registers)
+        // 64x128 wave tiles are dispatched only where one tile spans all columns (128 < N <= 256, no
+        // split, no rowv: host-checked), so their kernels carry no LDS-park path (and its registers)
         constexpr bool kDirectOnly = kDirect && TM * TN >= 8;
+        // per column block j of this lane: the store offset, or one past any view (the buffer
+        // drops the store) for columns >= nzero; live = column < N (else the zero fill of
+        // [N, nzero)).  On main tiles every column is live; the 256x256 tile also takes
+        // 128 < N < 256 (e.g. the 204-wide layer before the skip, whose row tail holds the
+        // embedding: nzero = N there, so those columns are never written)
+        auto direct_cols = [&](int vo, int lcol, int* voj, bool* live) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int col = n0 + lcol + 32 * j;
+                voj[j] = col < p.nzero ? vo + 128 * j : (1 << 30);
+                live[j] = col < p.N;
+            }
+        };
         auto direct_aux = [&]() {
             const int lrow = wm * TM * 32 + 4 * (lane >> 5);
             const int lcol = wn * TN * 32 + (lane & 31);
@@ -807,6 +820,9 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             const int v0 = (lrow * p.ld_aux0 + lcol) * 4;
             const int v1 = (lrow * p.ld_aux1 + lcol) * 4;
             const int v2 = (lrow * p.ld_aux2 + lcol) * 4;
+            int voj[TN];
+            bool live[TN];
+            direct_cols(vo, lcol, voj, live);
             constexpr int RG = kAux1 ? 2 : 4;          // accumulator rows r per group
             constexpr int NGD = TM * 16 / RG;          // groups per tile
             float xa[2][RG][TN], xb[2][RG][TN], xc[2][RG][TN];
@@ -848,7 +864,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                             const float rr2 = sg > 0.0f ? (1.0f - sg) * __builtin_amdgcn_rcpf(sg) : 0.0f;
                             o = u * sg + xb[sl][q][j] * xc[sl][q][j] * (p.aux2_scale * rr2);
                         }
-                        bstore1(vw, vo, 128 * j, o);
+                        bstore1(vw, voj[j], 0, live[j] ? o : 0.0f);
                     }
                 }
             }
@@ -857,6 +873,9 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             const int lrow = wm * TM * 32 + 4 * (lane >> 5);
             const int lcol = wn * TN * 32 + (lane & 31);
             const int vo = (lrow * p.ld_out0 + lcol) * 4;
+            int voj[TN];
+            bool live[TN];
+            direct_cols(vo, lcol, voj, live);
             float bj[TN];
 #pragma unroll
             for (int j = 0; j < TN; ++j) bj[j] = kBias ? sBias[min(n0 + lcol + 32 * j, kTblCols - 1)] : 0.0f;
@@ -872,7 +891,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         if constexpr (EPI == CN_EPI_SOFTPLUS) o = softplus_hw(z, c_exp, c_thr, c_log) * p.inv_odiv;
                         else if constexpr (EPI == CN_EPI_RELU) o = z > 0.0f ? z : 0.0f;
                         else o = z;
-                        bstore1(vw, vo, 128 * j, o);
+                        bstore1(vw, voj[j], 0, live[j] ? o : 0.0f);
                     }
                 }
         };
@@ -1826,8 +1845,8 @@ static int g_x6_tall = [] {
 // loop 316-320 vs 374 us at C2's layer shape; with the epilogue (tools/sq_check.py, bitwise equal
 // outputs): SOFTPLUS 445 vs 480-509, STORE 467 vs 491, RELU 385 vs 408-420, MUL / TANGENT 443-451 vs
 // 470 (their aux rows read in the MFMA layout); BWD_RELU 455-463 vs 477-479; BWD_SOFTPLUS 667 vs 614
-// (stays on 128x128).  Only for N == 256 without a split output: every tile then takes the direct
-// (MFMA-layout) epilogue.
+// (stays on 128x128).  Only for 128 < N <= 256 without a split output: one tile spans every column
+// and takes the direct (MFMA-layout) epilogue, columns >= N masked (zero fill up to nzero).
 static int g_x6_sq = [] {
     const char* e = getenv("COPENERF_X6_SQ");
     return e ? (int)strtol(e, nullptr, 0) : 0x5f;
@@ -1991,7 +2010,7 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
             // (COPENERF_WIDE_MINK: the smallest K for the 1-per-CU tiles)
             const bool longk = d->K >= g_wide_min_k;
             // (the epilogues with a direct form: STORE, SOFTPLUS, RELU, MUL, TANGENT, BWD_SOFTPLUS, BWD_RELU)
-            const bool sq = (g_x6_sq >> d->epilogue & 1) && d->N == 256 && !d->rowv &&
+            const bool sq = (g_x6_sq >> d->epilogue & 1) && d->N > 128 && d->N <= 256 && !d->rowv &&
                             !(d->epilogue == CN_EPI_MUL && d->out_split && d->nsplit < d->N);
             if (d->K % 32 == 0 && sq && d->N > 128 && d->ldb >= 256 && g_linear_variant == 0 && (longk || head))
                 return launch_linear_tile<4, 2, 2, 4, 16, 1, 2, 2>(d, a, s);

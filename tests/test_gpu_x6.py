@@ -133,3 +133,31 @@ def test_wgrad_x6_matches_fp32_accuracy(M, N, K, pairs):
     dW2 = torch.empty_like(res["bf16x6"][0])
     ops.wgrad(Y0, X0, N, K, dW2, Y1=Y1, X1=X1, mode="bf16x6")
     assert torch.equal(dW2, res["bf16x6"][0])
+
+
+@pytest.mark.parametrize("nzero", [204, 256])
+def test_linear_x6_narrow_n_on_the_wide_tile(nzero):
+    """128 < N < 256 (the 204-wide layer before the skip) on the 256x256 tile: columns < N
+    equal the exact-fp32 mode's, [N, nzero) are zero-filled and columns >= nzero (the
+    skip input's embedding in the real layout) are never written."""
+    from copenerf import ops
+    M, N, K = 1537, 204, 256
+    A = _rnd(M, K, seed=21, scale=0.3)
+    B = torch.zeros(256, K, device=DEV)
+    B[:N] = _rnd(N, K, seed=22, scale=0.05)
+    Bs = ops.split_bf16x3(B)
+    bias = _rnd(N, seed=23, scale=0.3)
+    aux0 = torch.nn.functional.softplus(_rnd(M, 256, seed=24, scale=0.05), beta=100)
+    sg = dict(aux0=aux0, aux_beta=100.0)
+    for epi, kw in ((ops.EPI_SOFTPLUS, dict(bias=bias, odiv=ops.SQRT2)), (ops.EPI_STORE, dict(bias=bias)),
+                    (ops.EPI_RELU, dict(bias=bias)), (ops.EPI_TANGENT, dict(sg, odiv=ops.SQRT2)),
+                    (ops.EPI_MUL, dict(sg)), (ops.EPI_BWD_RELU, dict(aux0=aux0 - 0.005))):
+        outs = []
+        for Bimg in (B, Bs):
+            o = torch.full((M, 256), 7.0, device=DEV)
+            ops.linear(A, Bimg, N, K, o, epi, nzero=nzero, **kw)
+            outs.append(o)
+        ref, got = outs
+        torch.testing.assert_close(got[:, :N], ref[:, :N], rtol=2e-5, atol=2e-6, msg=lambda m: f"epi {epi}: {m}")
+        assert torch.all(got[:, N:nzero] == 0), epi
+        assert torch.all(got[:, nzero:] == 7.0), epi
