@@ -199,15 +199,16 @@ _X6_SQ = int(os.environ.get("COPENERF_X6_SQ", "0x5f"), 0)
 _X6_TALL = int(os.environ.get("COPENERF_X6_TALL", "0x18"), 0)
 _WIDE_EPIS = int(os.environ.get("COPENERF_WIDE_EPIS", "0x1f"), 0)
 _WIDE_MINK = int(os.environ.get("COPENERF_WIDE_MINK", "128"))
+_X6_SQ_MINM = int(os.environ.get("COPENERF_X6_SQ_MINM", "0"))
 _LINEAR_TILES = {  # tag -> linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH> (bf16x6); tile 1 / other modes below
     "sq": "4, 2, 2, 4, 16, 1, 2", "tall": "4, 2, 1, 4, 32, 1, 2", "wide": "4, 2, 2, 2, 32, 1, 2",
     "t128": "2, 2, 2, 2, 16, 2, 2"}
 
 
-def _x6_tile(epi, N, K, ldb, rowv, split):
+def _x6_tile(epi, N, K, ldb, rowv, split, M=None):
     head = epi == EPI_SOFTPLUS_HEAD
     longk = K >= _WIDE_MINK
-    if (_X6_SQ >> epi) & 1 and 128 < N <= 256 and not rowv and not (epi == EPI_MUL and split) and K % 32 == 0 \
+    if (_X6_SQ >> epi) & 1 and 128 < N <= 256 and (M is None or M >= _X6_SQ_MINM) and not rowv and not (epi == EPI_MUL and split) and K % 32 == 0 \
             and ldb >= 256 and (longk or head):
         return "sq"
     tall = (_X6_TALL >> epi) & 1 or (head and N > 128)
@@ -314,7 +315,7 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
         e0 = _timer.start()
         _lib.check(_lib.load().cn_linear(d, _stream()), "cn_linear")
         tag = _x6_tile(epilogue, N, K, d.ldb, rowv is not None,
-                       out_split is not None and d.nsplit < N) if x6 and tile == 0 else tile
+                       out_split is not None and d.nsplit < N, M=d.M) if x6 and tile == 0 else tile
         key = ("linear", tag, EPI_NAMES[epilogue] + ("+rowv" if rowv is not None else "")) + \
             (("bf16",) if bf else ("x6",) if x6 else ())
         ka = kalg or K

@@ -1851,6 +1851,10 @@ static int g_x6_sq = [] {
     const char* e = getenv("COPENERF_X6_SQ");
     return e ? (int)strtol(e, nullptr, 0) : 0x5f;
 }();
+static int g_x6_sq_min_m = [] {  // smallest M for the 256x256 tile (COPENERF_X6_SQ_MINM)
+    const char* e = getenv("COPENERF_X6_SQ_MINM");
+    return e ? atoi(e) : 0;
+}();
 static int g_wide_epis = [] {
     const char* e = getenv("COPENERF_WIDE_EPIS");
     return e ? (int)strtol(e, nullptr, 0) : 0x1f;
@@ -2010,7 +2014,7 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
             // (COPENERF_WIDE_MINK: the smallest K for the 1-per-CU tiles)
             const bool longk = d->K >= g_wide_min_k;
             // (the epilogues with a direct form: STORE, SOFTPLUS, RELU, MUL, TANGENT, BWD_SOFTPLUS, BWD_RELU)
-            const bool sq = (g_x6_sq >> d->epilogue & 1) && d->N > 128 && d->N <= 256 && !d->rowv &&
+            const bool sq = (g_x6_sq >> d->epilogue & 1) && d->N > 128 && d->N <= 256 && !d->rowv && d->M >= g_x6_sq_min_m &&
                             !(d->epilogue == CN_EPI_MUL && d->out_split && d->nsplit < d->N);
             if (d->K % 32 == 0 && sq && d->N > 128 && d->ldb >= 256 && g_linear_variant == 0 && (longk || head))
                 return launch_linear_tile<4, 2, 2, 4, 16, 1, 2, 2>(d, a, s);
