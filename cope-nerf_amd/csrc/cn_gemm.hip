@@ -15,10 +15,8 @@
 // step s, so each lane reads 4 consecutive k with one ds_read_b128.
 // Tile 1 is 128x64 (4x1 waves of 1x2 tiles) for N or K = 64 shapes.
 //
-// `wgrad_kernel` computes dW = Σ_m Y[m]ᵀ X[m] (the reduction over the M sample
-// rows) with the same MFMA, splitting M over workgroups into fp32 slabs that
-// `wgrad_reduce` sums in a fixed order (bitwise reproducible, no atomics).
-#include "cn_common.h"
+// The weight gradients dW = Σ_m Y[m]ᵀ X[m] are in cn_wgrad.hip.
+#include "cn_mfma.h"
 
 #include <algorithm>
 #include <type_traits>
@@ -52,106 +50,6 @@ struct LinearArgs {
     int flags;
 };
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-
-// Buffer views: every global access of the GEMM goes through a buffer resource
-// whose base is a tile row and whose record count ends at the last valid row,
-// so (a) per-access addressing is a per-lane 32-bit voffset fixed for the whole
-// kernel plus a wave-uniform soffset (column offset) and SALU-built descriptors,
-// no 64-bit VALU address math, and (b) rows >= M read as zero and their stores
-// are dropped by the range check, with no per-row compare.  The range check
-// covers voffset only (not soffset), so the row part of every offset is either
-// in voffset or in the descriptor base.  On gfx950 the f32 MFMA and VALU instructions of the
-// waves of one SIMD issue strictly one after the other (tools/probes), so every
-// VALU instruction removed here is matrix-pipe time won back.
-// bytes: a tile's extent, < 2^31 by the host's leading-dimension limit; <= 0 = empty view
-__device__ __forceinline__ rsrc_t make_view(const float* base, int bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, bytes < 0 ? 0 : bytes, 0x00020000);
-}
-// A tile's rows of one tensor: base = its first row, bytes = extent up to the last valid row.
-struct TileView {
-    const float* base;
-    int ld;
-    int bytes;
-};
-__device__ __forceinline__ rsrc_t view_at(const TileView& t, int lrow) {
-    return make_view(t.base + (int64_t)lrow * t.ld, t.bytes - lrow * t.ld * 4);
-}
-__device__ __forceinline__ floatx4 bload4(rsrc_t r, int voff, int soff) {
-    return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
-}
-__device__ __forceinline__ float bload1(rsrc_t r, int voff, int soff) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
-}
-// the value goes through a by-value parameter: __builtin_bit_cast applied directly
-// to a vector element (acc[i][j][r]) miscompiles in ROCm 7.2 clang (every store
-// of an unrolled loop gets element 0)
-__device__ __forceinline__ void bstore1(rsrc_t r, int voff, int soff, float v) {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, soff, 0);
-}
-__device__ __forceinline__ void bstore4(rsrc_t r, int voff, int soff, floatx4 v) {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, soff, 0);
-}
-
-// torch.nn.Softplus(beta, threshold) on the hardware transcendentals: e = 2^(z beta
-// log2 e), a = log2(1 + e) ln2 / beta; the linear branch (beta z > threshold) exactly
-// as torch.  Absolute error of a is ~1e-9 (log2 of the rounded 1 + e; v_exp/v_log
-// are 1 ulp), far below the fp32 GEMM rounding of the layer that produced z.
-__device__ __forceinline__ float softplus_hw(float z, float c_exp, float c_thr, float c_log) {
-    const float y = z * c_exp;  // beta z log2(e)
-    const float e = __builtin_amdgcn_exp2f(y);
-    const bool lin = y > c_thr;  // beta z > threshold (boundary moved by <= 1 ulp; the branches agree to 1e-10 there)
-    return lin ? z : __builtin_amdgcn_logf(1.0f + e) * c_log;
-}
-
-// softplus'(z) = sigmoid(beta z) recovered from the softplus output a = softplus(z):
-// exp(beta a) = 1 + exp(beta z), so sigma = 1 - exp(-beta a) (= 1 exactly in fp32 on
-// torch's linear branch, beta z > 20).  aux_c = -beta * log2(e) (times the divisor the
-// stored activation carries).  Absolute error <= ~1e-7: the backward never stores
-// sigma, every consumer reads the activation it already has.
-__device__ __forceinline__ float sigma_from_act(float a, float aux_c) {
-    return 1.0f - __builtin_amdgcn_exp2f(a * aux_c);
-}
-
-// Three-term bf16 split of 4 fp32 values (CN_MFMA_F32_BF16X6): v = t0 + t1 + t2
-// with every term the RNE bf16 of the remainder.  Written on packed pairs: the
-// bf16 -> fp32 widening of a v_cvt_pk_bf16_f32 result is a shift (low half) and
-// a mask (high half), the remainders are v_pk_add_f32: 18 VALU per 4 values
-// (the per-element convertvector round trip compiles to 30).
-typedef float floatx2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ floatx2 widen_bf16x2(unsigned p) {
-    return floatx2{__builtin_bit_cast(float, p << 16), __builtin_bit_cast(float, p & 0xffff0000u)};
-}
-__device__ __forceinline__ void split3(floatx4 v, bf16x4& t0, bf16x4& t1, bf16x4& t2) {
-    unsigned p0[2], p1[2], p2[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const floatx2 x = {v[2 * h], v[2 * h + 1]};
-        p0[h] = __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf16x2));
-        const floatx2 r = x - widen_bf16x2(p0[h]);
-        p1[h] = __builtin_bit_cast(unsigned, __builtin_convertvector(r, bf16x2));
-        const floatx2 q = r - widen_bf16x2(p1[h]);
-        p2[h] = __builtin_bit_cast(unsigned, __builtin_convertvector(q, bf16x2));
-    }
-    t0 = __builtin_bit_cast(bf16x4, (u32x2){p0[0], p0[1]});
-    t1 = __builtin_bit_cast(bf16x4, (u32x2){p1[0], p1[1]});
-    t2 = __builtin_bit_cast(bf16x4, (u32x2){p2[0], p2[1]});
-}
-
-// Virtual tile vt -> (tm, tn).  XCD-aware: blocks b and b+8 are dispatched to
-// the same XCD, so the T N-tiles of one M-tile are placed 8 apart and share that
-// XCD's L2 copy of the A rows.  Tiles are padded to a multiple of 8 M-tiles.
-__device__ __forceinline__ void tile_coords(int vt, int T, int& tm, int& tn) {
-    const int grp = vt / (8 * T);
-    const int w = vt % (8 * T);
-    tm = grp * 8 + (w & 7);
-    tn = w >> 3;
-}
 
 // Persistent over output tiles: gridDim.x workgroups (OCC per CU) walk the
 // virtual tiles; the first K-chunk of the next tile is fetched into registers
@@ -915,540 +813,6 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     }
 }
 
-// ---------------------------------------------------------------------------
-// Weight gradient.
-struct WgradArgs {
-    const float* Y0;
-    const float* X0;
-    const float* Y1;
-    const float* X1;
-    float* part;   // [nslices][Npad][Kpad]
-    float* bpart;  // [nslices][Npad]
-    int ldy0, ldx0, ldy1, ldx1;
-    int M, Npad, Kpad, npairs, rows_per_slice, n_tiles_n, n_tiles_k, nslices;
-};
-
-template <int WM, int WN, int TM, int TN>
-__global__ void __launch_bounds__(64 * WM * WN, 2) wgrad_kernel(WgradArgs p) {
-    constexpr int NT = 64 * WM * WN;
-    constexpr int BNo = 32 * TM * WM;  // output rows (n) per tile
-    constexpr int BKo = 32 * TN * WN;  // output cols (k) per tile
-    constexpr int MC = 32;             // sample rows per chunk
-    constexpr int YF4 = MC * BNo / 4;
-    constexpr int XF4 = MC * BKo / 4;
-    static_assert(YF4 % NT == 0 && XF4 % NT == 0, "tile/thread mismatch");
-    constexpr int YLD = YF4 / NT;
-    constexpr int XLD = XF4 / NT;
-
-    __shared__ __attribute__((aligned(16))) float smem[2 * MC * (BNo + BKo)];
-    float* sY = smem;
-    float* sX = smem + 2 * MC * BNo;
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int wm = wave / WN;
-    const int wn = wave % WN;
-
-    // XCD-aware: blocks b and b+8 share an XCD (and its L2), so the T output tiles
-    // of one M-slice, which read the same Y / X rows, are placed 8 blocks apart
-    const int T = p.n_tiles_n * p.n_tiles_k;
-    const int b = blockIdx.x;
-    const int tile = (b >> 3) % T;
-    const int slice = (b & 7) + 8 * ((b >> 3) / T);
-    if (slice >= p.nslices) return;
-    const int tn = tile / p.n_tiles_k;
-    const int tk = tile % p.n_tiles_k;
-    const int n0 = tn * BNo;
-    const int k0 = tk * BKo;
-    const int mbeg = slice * p.rows_per_slice;
-    const int mend = min(p.M, mbeg + p.rows_per_slice);
-    const int nch = mend > mbeg ? cdiv(mend - mbeg, MC) : 0;
-    const int total = nch * p.npairs;
-    const bool do_bias = (tk == 0) && (p.bpart != nullptr);
-
-    // buffer views (see linear_kernel): the chunk's first row is the descriptor
-    // base (SALU), rows past mend read as zero through the range check
-    constexpr int YRS = NT / (BNo / 4);  // staged rows per Y load instruction
-    constexpr int XRS = NT / (BKo / 4);
-    const int yrow = tid / (BNo / 4), yc4 = tid % (BNo / 4);
-    const int xrow = tid / (BKo / 4), xc4 = tid % (BKo / 4);
-    floatx4 ry[YLD], rx[XLD];
-    auto gload = [&](int c) {
-        const int pair = c >= nch;
-        const int mrow = mbeg + (c - pair * nch) * MC;
-        const float* Y = pair ? p.Y1 : p.Y0;
-        const float* X = pair ? p.X1 : p.X0;
-        const int ly = pair ? p.ldy1 : p.ldy0;
-        const int lx = pair ? p.ldx1 : p.ldx0;
-        const int nrows = min(MC, mend - mrow);
-        const rsrc_t vY = make_view(Y + (int64_t)mrow * ly + n0, (nrows * ly - n0) * 4);
-        const rsrc_t vX = make_view(X + (int64_t)mrow * lx + k0, (nrows * lx - k0) * 4);
-#pragma unroll
-        for (int q = 0; q < YLD; ++q) ry[q] = bload4(vY, ((yrow + q * YRS) * ly + yc4 * 4) * 4, 0);
-#pragma unroll
-        for (int q = 0; q < XLD; ++q) rx[q] = bload4(vX, ((xrow + q * XRS) * lx + xc4 * 4) * 4, 0);
-    };
-    auto lstore = [&](int buf) {
-#pragma unroll
-        for (int q = 0; q < YLD; ++q) {
-            const int f = tid + q * NT;
-            *reinterpret_cast<floatx4*>(sY + buf * MC * BNo + f * 4) = ry[q];
-        }
-#pragma unroll
-        for (int q = 0; q < XLD; ++q) {
-            const int f = tid + q * NT;
-            *reinterpret_cast<floatx4*>(sX + buf * MC * BKo + f * 4) = rx[q];
-        }
-    };
-
-    floatx16 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-    float bacc = 0.0f;
-
-    if (total > 0) {
-        gload(0);
-        lstore(0);
-    }
-    __syncthreads();
-    const int h = lane >> 5;
-    const int ycol = wm * TM * 32 + (lane & 31);
-    const int xcol = wn * TN * 32 + (lane & 31);
-    for (int c = 0; c < total; ++c) {
-        const int cur = c & 1;
-        if (c + 1 < total) gload(c + 1);
-        const float* yb = sY + cur * MC * BNo;
-        const float* xb = sX + cur * MC * BKo;
-        if (do_bias && c < nch && tid < BNo) {
-#pragma unroll 8
-            for (int r = 0; r < MC; ++r) bacc += yb[r * BNo + tid];
-        }
-#pragma unroll
-        for (int s = 0; s < MC / 2; ++s) {
-            float af[TM], bf[TN];
-#pragma unroll
-            for (int i = 0; i < TM; ++i) af[i] = yb[(2 * s + h) * BNo + ycol + i * 32];
-#pragma unroll
-            for (int j = 0; j < TN; ++j) bf[j] = xb[(2 * s + h) * BKo + xcol + j * 32];
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
-        }
-        if (c + 1 < total) lstore(cur ^ 1);
-        __syncthreads();
-    }
-
-    // slab stores: lane offset in voffset, the accumulator row step in soffset
-    const rsrc_t vP = make_view(p.part + (int64_t)slice * p.Npad * p.Kpad, p.Npad * p.Kpad * 4);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int col = k0 + wn * TN * 32 + j * 32 + (lane & 31);
-            const int rbase = n0 + wm * TM * 32 + i * 32 + 4 * (lane >> 5);
-            const int vo = (rbase * p.Kpad + col) * 4;
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                bstore1(vP, vo, ((r & 3) + 8 * (r >> 2)) * p.Kpad * 4, acc[i][j][r]);
-        }
-    }
-    if (do_bias && tid < BNo) p.bpart[(int64_t)slice * p.Npad + n0 + tid] = bacc;
-}
-
-// bf16-operand weight gradient (config C3): the same tiles and slabs as
-// wgrad_kernel, with Y and X rounded to bf16 while staging and written
-// TRANSPOSED into LDS ([n][m] and [k][m], 64 m per row + 8 pad = 36 dwords), so
-// one ds_read_b128 gives a lane the 8 consecutive m of its
-// v_mfma_f32_32x32x16_bf16 fragment.  A thread stages 4 rows x 4 columns per
-// pass and packs each column's 4 m into one ds_write_b64; the 16-byte blocks of
-// a row are XOR-swizzled so those writes do not collide on banks.  db is summed from the
-// fp32 values in registers (partials reduced through LDS at the end).
-template <int WM, int WN, int TM, int TN>
-__global__ void __launch_bounds__(64 * WM * WN, 2) wgrad_bf16_kernel(WgradArgs p) {
-    constexpr int NT = 64 * WM * WN;
-    constexpr int BNo = 32 * TM * WM;
-    constexpr int BKo = 32 * TN * WN;
-    constexpr int MC = 64;
-    constexpr int LSB = MC / 2 + 4;  // dwords per LDS row
-    constexpr int YC = BNo / 4, XC = BKo / 4;        // float4 column groups per staged row
-    constexpr int YMQ = NT / YC, XMQ = NT / XC;      // m-quads per pass
-    constexpr int YP = (MC / 4) / YMQ, XP = (MC / 4) / XMQ;
-    static_assert(YP >= 1 && XP >= 1 && YMQ * YC == NT && XMQ * XC == NT, "staging geometry");
-    static_assert(2 * BNo <= (BNo + BKo) * LSB, "bias partials fit in LDS");
-
-    __shared__ __attribute__((aligned(16))) float smem[2 * (BNo + BKo) * LSB];
-    float* sY = smem;
-    float* sX = smem + 2 * BNo * LSB;
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int wm = wave / WN;
-    const int wn = wave % WN;
-    const int T = p.n_tiles_n * p.n_tiles_k;
-    const int b = blockIdx.x;
-    const int tile = (b >> 3) % T;
-    const int slice = (b & 7) + 8 * ((b >> 3) / T);
-    if (slice >= p.nslices) return;
-    const int tn = tile / p.n_tiles_k;
-    const int tk = tile % p.n_tiles_k;
-    const int n0 = tn * BNo;
-    const int k0 = tk * BKo;
-    const int mbeg = slice * p.rows_per_slice;
-    const int mend = min(p.M, mbeg + p.rows_per_slice);
-    const int nch = mend > mbeg ? cdiv(mend - mbeg, MC) : 0;
-    const int total = nch * p.npairs;
-    const bool do_bias = (tk == 0) && (p.bpart != nullptr);
-
-    const int yc = tid % YC, ymq = tid / YC;
-    const int xc = tid % XC, xmq = tid / XC;
-    floatx4 ry[YP][4], rx[XP][4];
-    float bsum[4] = {0.f, 0.f, 0.f, 0.f};
-    auto gload = [&](int c) {
-        const int pair = c >= nch;
-        const int mrow = mbeg + (c - pair * nch) * MC;
-        const float* Y = pair ? p.Y1 : p.Y0;
-        const float* X = pair ? p.X1 : p.X0;
-        const int ly = pair ? p.ldy1 : p.ldy0;
-        const int lx = pair ? p.ldx1 : p.ldx0;
-        const int nrows = min(MC, mend - mrow);
-        const rsrc_t vY = make_view(Y + (int64_t)mrow * ly + n0, (nrows * ly - n0) * 4);
-        const rsrc_t vX = make_view(X + (int64_t)mrow * lx + k0, (nrows * lx - k0) * 4);
-#pragma unroll
-        for (int pp = 0; pp < YP; ++pp)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                ry[pp][r] = bload4(vY, (((ymq + pp * YMQ) * 4 + r) * ly + yc * 4) * 4, 0);
-#pragma unroll
-        for (int pp = 0; pp < XP; ++pp)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                rx[pp][r] = bload4(vX, (((xmq + pp * XMQ) * 4 + r) * lx + xc * 4) * 4, 0);
-    };
-    // XOR swizzle of the 16-byte blocks of a row by (row >> 2) & 7: the staging
-    // writes (threads on rows 4 apart) spread over all banks; reads undo it
-    auto swz = [&](int row, int mq) { return row * LSB + (((mq >> 1) ^ ((row >> 2) & 7)) << 2) + ((mq & 1) << 1); };
-    auto lstore = [&](int buf, bool bias) {
-        float* y = sY + buf * BNo * LSB;
-        float* x = sX + buf * BKo * LSB;
-#pragma unroll
-        for (int pp = 0; pp < YP; ++pp)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const floatx4 col = {ry[pp][0][e], ry[pp][1][e], ry[pp][2][e], ry[pp][3][e]};
-                if (bias) bsum[e] += (col[0] + col[1]) + (col[2] + col[3]);
-                *reinterpret_cast<bf16x4*>(y + swz(yc * 4 + e, ymq + pp * YMQ)) = __builtin_convertvector(col, bf16x4);
-            }
-#pragma unroll
-        for (int pp = 0; pp < XP; ++pp)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const floatx4 col = {rx[pp][0][e], rx[pp][1][e], rx[pp][2][e], rx[pp][3][e]};
-                *reinterpret_cast<bf16x4*>(x + swz(xc * 4 + e, xmq + pp * XMQ)) = __builtin_convertvector(col, bf16x4);
-            }
-    };
-
-    floatx16 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-
-    if (total > 0) {
-        gload(0);
-        lstore(0, do_bias && nch > 0);
-    }
-    __syncthreads();
-    const int h = lane >> 5;
-    const int ycol = wm * TM * 32 + (lane & 31);
-    const int xcol = wn * TN * 32 + (lane & 31);
-    for (int c = 0; c < total; ++c) {
-        const int cur = c & 1;
-        const bool more = c + 1 < total;
-        if (more) gload(c + 1);
-        const float* yb = sY + cur * BNo * LSB + ycol * LSB;
-        const float* xb = sX + cur * BKo * LSB + xcol * LSB;
-        const int sw = ((lane & 31) >> 2) & 7;  // (row >> 2) & 7 of this lane's rows
-#pragma unroll
-        for (int ks = 0; ks < MC / 16; ++ks) {
-            const int blk = ((2 * ks + h) ^ sw) << 2;
-            bf16x8 af[TM], bf[TN];
-#pragma unroll
-            for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(yb + i * 32 * LSB + blk);
-#pragma unroll
-            for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const bf16x8*>(xb + j * 32 * LSB + blk);
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
-        }
-        if (more) lstore(cur ^ 1, do_bias && c + 1 < nch);
-        __syncthreads();
-    }
-
-    const rsrc_t vP = make_view(p.part + (int64_t)slice * p.Npad * p.Kpad, p.Npad * p.Kpad * 4);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int col = k0 + wn * TN * 32 + j * 32 + (lane & 31);
-            const int rbase = n0 + wm * TM * 32 + i * 32 + 4 * (lane >> 5);
-            const int vo = (rbase * p.Kpad + col) * 4;
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                bstore1(vP, vo, ((r & 3) + 8 * (r >> 2)) * p.Kpad * 4, acc[i][j][r]);
-        }
-    }
-    if (do_bias) {  // reduce the per-thread column partials over the m-quads (fixed order)
-        float* red = smem;  // [YMQ][BNo]
-#pragma unroll
-        for (int e = 0; e < 4; ++e) red[ymq * BNo + yc * 4 + e] = bsum[e];
-        __syncthreads();
-        if (tid < BNo) {
-            float t = 0.0f;
-            for (int q = 0; q < YMQ; ++q) t += red[q * BNo + tid];
-            p.bpart[(int64_t)slice * p.Npad + n0 + tid] = t;
-        }
-    }
-}
-
-// fp32 weight gradient on the bf16 MFMA (CN_MFMA_F32_BF16X6), 128x128 output
-// tiles: Y and X are split into three bf16 terms while staging (split3) and the
-// six term products with i + j <= 2 accumulate in fp32, as in linear_kernel
-// MODE 2.  Staging is transposed like wgrad_bf16_kernel's, 32 sample rows per
-// chunk: thread t holds m-quad t % 8 of column group t / 8 (4 m x 4 columns of
-// Y and of X), so 16 contiguous lanes write two LDS rows 4 apart whose 64-byte
-// segments fall on the two halves of the 32 write banks; an LDS row is the three
-// 16-dword term planes + 4 pad (52 dwords: the ds_read_b128 fragment reads of 16
-// consecutive rows hit 16 distinct bank quads).  One LDS buffer (53 KB, two
-// workgroups per CU): the next chunk's loads fly during the MFMAs.  TN = 1: 64
-// output columns, X staged by the first two waves.  WM = 4, TN = 4: a whole
-// 256x256 layer per workgroup of 8 waves (one per CU, 106 KB LDS): every staged
-// element feeds twice the MFMA work of the 128x128 tile.
-template <int WM, int TN>
-__global__ void __launch_bounds__(128 * WM, 2) wgrad_x6_kernel(WgradArgs p) {
-    constexpr int TM = 2, WN = 2, NT = 128 * WM;
-    constexpr int BNo = 64 * WM, BKo = 64 * TN, MC = 32, MQ = MC / 4;
-    constexpr int PL = MC / 2;       // dwords per term plane of a row
-    constexpr int LSB = 3 * PL + 4;  // 52
-    constexpr int XT = MQ * (BKo / 4);  // threads staging X (256 or 128: whole waves)
-    static_assert(MQ * (BNo / 4) == NT && XT <= NT && XT % 64 == 0, "staging geometry: whole waves");
-    static_assert(MQ * BNo <= (BNo + BKo) * LSB, "bias partials fit in LDS");
-    __shared__ __attribute__((aligned(16))) float smem[(BNo + BKo) * LSB];
-    float* sY = smem;
-    float* sX = smem + BNo * LSB;
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int wm = wave / WN;
-    const int wn = wave % WN;
-    const int T = p.n_tiles_n * p.n_tiles_k;
-    const int b = blockIdx.x;
-    const int tile = (b >> 3) % T;
-    const int slice = (b & 7) + 8 * ((b >> 3) / T);
-    if (slice >= p.nslices) return;
-    const int tn = tile / p.n_tiles_k;
-    const int tk = tile % p.n_tiles_k;
-    const int n0 = tn * BNo;
-    const int k0 = tk * BKo;
-    const int mbeg = slice * p.rows_per_slice;
-    const int mend = min(p.M, mbeg + p.rows_per_slice);
-    const int nch = mend > mbeg ? cdiv(mend - mbeg, MC) : 0;
-    const int total = nch * p.npairs;
-    const bool do_bias = (tk == 0) && (p.bpart != nullptr);
-
-    const int mq = tid % MQ, cg = tid / MQ;
-    floatx4 ry[4], rx[4];
-    float bsum[4] = {0.f, 0.f, 0.f, 0.f};
-    auto gload = [&](int c) {
-        const int pair = c >= nch;
-        const int mrow = mbeg + (c - pair * nch) * MC;
-        const float* Y = pair ? p.Y1 : p.Y0;
-        const float* X = pair ? p.X1 : p.X0;
-        const int ly = pair ? p.ldy1 : p.ldy0;
-        const int lx = pair ? p.ldx1 : p.ldx0;
-        const int nrows = min(MC, mend - mrow);
-        const rsrc_t vY = make_view(Y + (int64_t)mrow * ly + n0, (nrows * ly - n0) * 4);
-        const rsrc_t vX = make_view(X + (int64_t)mrow * lx + k0, (nrows * lx - k0) * 4);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) ry[r] = bload4(vY, ((mq * 4 + r) * ly + cg * 4) * 4, 0);
-        if (XT == NT || tid < XT) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) rx[r] = bload4(vX, ((mq * 4 + r) * lx + cg * 4) * 4, 0);
-        }
-    };
-    auto lstore = [&](bool bias) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const floatx4 col = {ry[0][e], ry[1][e], ry[2][e], ry[3][e]};
-            if (bias) bsum[e] += (col[0] + col[1]) + (col[2] + col[3]);
-            bf16x4 t0, t1, t2;
-            split3(col, t0, t1, t2);
-            float* y = sY + (cg * 4 + e) * LSB + mq * 2;
-            *reinterpret_cast<bf16x4*>(y) = t0;
-            *reinterpret_cast<bf16x4*>(y + PL) = t1;
-            *reinterpret_cast<bf16x4*>(y + 2 * PL) = t2;
-        }
-        if (XT < NT && tid >= XT) return;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const floatx4 col = {rx[0][e], rx[1][e], rx[2][e], rx[3][e]};
-            bf16x4 t0, t1, t2;
-            split3(col, t0, t1, t2);
-            float* x = sX + (cg * 4 + e) * LSB + mq * 2;
-            *reinterpret_cast<bf16x4*>(x) = t0;
-            *reinterpret_cast<bf16x4*>(x + PL) = t1;
-            *reinterpret_cast<bf16x4*>(x + 2 * PL) = t2;
-        }
-    };
-
-    floatx16 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-
-    const int h = lane >> 5;
-    const float* yb = sY + (wm * TM * 32 + (lane & 31)) * LSB + 4 * h;
-    const float* xb = sX + (wn * TN * 32 + (lane & 31)) * LSB + 4 * h;
-    if (total > 0) gload(0);
-    for (int c = 0; c < total; ++c) {
-        if (c > 0) __syncthreads();  // the previous chunk's fragment reads are done
-        lstore(do_bias && c < nch);
-        __syncthreads();
-        if (c + 1 < total) gload(c + 1);
-#pragma unroll
-        for (int ks = 0; ks < MC / 16; ++ks) {
-            bf16x8 af[3][TM], bf[3][TN];
-#pragma unroll
-            for (int t = 0; t < 3; ++t) {
-#pragma unroll
-                for (int i = 0; i < TM; ++i) af[t][i] = *reinterpret_cast<const bf16x8*>(yb + i * 32 * LSB + t * PL + ks * 8);
-#pragma unroll
-                for (int j = 0; j < TN; ++j) bf[t][j] = *reinterpret_cast<const bf16x8*>(xb + j * 32 * LSB + t * PL + ks * 8);
-            }
-            constexpr int TA[6] = {0, 1, 0, 2, 1, 0};
-            constexpr int TB[6] = {0, 0, 1, 0, 1, 2};
-#pragma unroll
-            for (int u = 0; u < 6; ++u)
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[TA[u]][i], bf[TB[u]][j], acc[i][j], 0, 0, 0);
-        }
-    }
-    __syncthreads();  // LDS is reused for the bias partials
-
-    const rsrc_t vP = make_view(p.part + (int64_t)slice * p.Npad * p.Kpad, p.Npad * p.Kpad * 4);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int col = k0 + wn * TN * 32 + j * 32 + (lane & 31);
-            const int rbase = n0 + wm * TM * 32 + i * 32 + 4 * (lane >> 5);
-            const int vo = (rbase * p.Kpad + col) * 4;
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                bstore1(vP, vo, ((r & 3) + 8 * (r >> 2)) * p.Kpad * 4, acc[i][j][r]);
-        }
-    }
-    if (do_bias) {  // reduce the per-thread column partials over the m-quads (fixed order)
-        float* red = smem;  // [MQ][BNo]
-#pragma unroll
-        for (int e = 0; e < 4; ++e) red[mq * BNo + cg * 4 + e] = bsum[e];
-        __syncthreads();
-        if (tid < BNo) {
-            float t = 0.0f;
-            for (int q = 0; q < MQ; ++q) t += red[q * BNo + tid];
-            p.bpart[(int64_t)slice * p.Npad + n0 + tid] = t;
-        }
-    }
-}
-
-// Sum of nslab fp32 slabs: out[r*ldo + c] (+)= (sum_s part[s*stride + r*ldp + c]) / div
-// for r < rows, c < cols.  A workgroup owns 64 float4 column groups x 4 slab
-// groups; each thread sums its slab group in double with 4 loads in flight, the 4
-// groups combine through LDS in a fixed order (bitwise reproducible).
-// 256 threads = kSlabGroups slab groups x (256 / kSlabGroups) float4 column groups: slab
-// group sg sums slabs sg, sg + SG, ... in double, the groups meet in a fixed order in LDS.
-// (16 x 16: a 256-slab weight gradient is 16 loads per thread, 4x the blocks of a 4 x 64 split.)
-constexpr int kSlabGroups = 16;
-__global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ part, int nslab, int64_t stride,
-                                                          int rows, int cols, int64_t ldp, float* out, int64_t ldo,
-                                                          float div, int accumulate) {
-    constexpr int SG = kSlabGroups, CG = 256 / SG;
-    __shared__ double red[SG][CG][4];
-    const int c4n = cdiv(cols, 4);
-    const int t = threadIdx.x % CG;
-    const int sg = threadIdx.x / CG;
-    const int64_t g = (int64_t)blockIdx.x * CG + t;  // float4 group over rows x c4n
-    const bool valid = g < (int64_t)rows * c4n;
-    const int r = valid ? (int)(g / c4n) : 0;
-    const int c = valid ? (int)(g % c4n) * 4 : 0;
-    const bool vec = valid && (c + 3 < cols) && (ldp % 4 == 0) && (stride % 4 == 0);
-    double a[4] = {0.0, 0.0, 0.0, 0.0};
-    if (valid) {
-        const float* base = part + (int64_t)r * ldp + c;
-        int sl = sg;
-        for (; sl + 3 * SG < nslab; sl += 4 * SG) {
-            floatx4 v[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const float* q = base + (int64_t)(sl + SG * u) * stride;
-                if (vec) {
-                    v[u] = *reinterpret_cast<const floatx4*>(q);
-                } else {
-                    for (int e = 0; e < 4; ++e) v[u][e] = (c + e < cols) ? q[e] : 0.0f;
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) a[e] += (double)v[u][e];
-        }
-        for (; sl < nslab; sl += SG) {
-            const float* q = base + (int64_t)sl * stride;
-            for (int e = 0; e < 4; ++e) a[e] += (c + e < cols) ? (double)q[e] : 0.0;
-        }
-    }
-    for (int e = 0; e < 4; ++e) red[sg][t][e] = a[e];
-    __syncthreads();
-    if (sg == 0 && valid) {
-        for (int e = 0; e < 4 && c + e < cols; ++e) {
-            double tot = red[0][t][e];
-            for (int q = 1; q < SG; ++q) tot += red[q][t][e];
-            float v = (float)tot;
-            if (div != 1.0f) v = v / div;
-            float* o = out + (int64_t)r * ldo + c + e;
-            if (accumulate) v += *o;
-            *o = v;
-        }
-    }
-}
-
-static int launch_slab_reduce(const float* part, int nslab, int64_t stride, int rows, int cols, int64_t ldp, float* out,
-                              int64_t ldo, float div, int accumulate, hipStream_t s) {
-    const int64_t groups = (int64_t)rows * cdiv(cols, 4);
-    if (groups == 0) return CN_OK;
-    constexpr int CG = 256 / kSlabGroups;
-    slab_reduce_kernel<<<(int)((groups + CG - 1) / CG), 256, 0, s>>>(part, nslab, stride, rows, cols, ldp, out, ldo,
-                                                                     div, accumulate);
-    return check_launch("slab_reduce");
-}
 
 
 // ---------------------------------------------------------------------------
@@ -1762,53 +1126,6 @@ __global__ void __launch_bounds__(256) colsum_kernel(int M, int K, const float* 
     }
 }
 
-// ---------------------------------------------------------------------------
-// tile 0: 128x128 output tiles, 1: 128x64, 2 (bf16x6, operand rows at least 256-padded):
-// 256x256 tiles of 512-thread workgroups, one per CU (half the workgroup target).  Padding
-// columns of Y / X only feed output rows / columns past n_out / k_out, which the slab
-// reduction never reads.
-static bool wgrad_wide_on() {
-    static const bool on = [] {  // benchmarking aid: COPENERF_WGRAD_WIDE=0 keeps the 128x128 tiles
-        const char* e = getenv("COPENERF_WGRAD_WIDE");
-        return e ? atoi(e) != 0 : true;
-    }();
-    return on;
-}
-// 3 (bf16x6, K <= 64, Y rows 256-padded; COPENERF_WGRAD_NARROW=1): 256x64 tiles of 512-thread
-// workgroups.  Measured slower than the 128x64 tiles on the C2 first-layer shapes (0.418 vs
-// 0.388 ms, 0.207 vs 0.187 ms), so off by default.
-// Returns the wide mode: 0 none, 1 = 256x256, 2 = 256x64.
-static int wgrad_wide(const cn_wgrad_desc* d) {
-    static const bool narrow = [] {
-        const char* e = getenv("COPENERF_WGRAD_NARROW");
-        return e && atoi(e) != 0;
-    }();
-    const int64_t np = (int64_t)cdiv(d->N, 256) * 256, kp = (int64_t)cdiv(d->K, 256) * 256;
-    if (!wgrad_wide_on() || d->mfma_dtype != CN_MFMA_F32_BF16X6 || d->ldy0 < np || (d->npairs == 2 && d->ldy1 < np))
-        return 0;
-    if (d->ldx0 >= kp && (d->npairs == 1 || d->ldx1 >= kp)) return 1;
-    return narrow && d->K <= 64 ? 2 : 0;
-}
-
-static void wgrad_geometry(int M, int N, int K, int wide, int* tile, int* Npad, int* Kpad, int* nslices,
-                           int* rows_per_slice) {
-    const int t = wide == 1 ? 2 : wide == 2 ? 3 : (K % 128 == 0) ? 0 : 1;
-    const int BNo = t >= 2 ? 256 : 128, BKo = t == 2 ? 256 : t == 0 ? 128 : 64;
-    *tile = t;
-    *Npad = cdiv(N, BNo) * BNo;
-    *Kpad = cdiv(K, BKo) * BKo;
-    const int tiles = (*Npad / BNo) * (*Kpad / BKo);
-    static const int kTarget = [] {  // workgroups per cn_wgrad (benchmarking aid: COPENERF_WGRAD_BLOCKS)
-        const char* e = getenv("COPENERF_WGRAD_BLOCKS");
-        return e ? atoi(e) : 512;
-    }();
-    int ns = std::max(1, (t == 2 ? kTarget / 2 : kTarget) / tiles);  // (t 3: 2 workgroups per CU)
-    ns = std::min(ns, std::max(1, cdiv(M, 512)));
-    int rps = cdiv(cdiv(M, ns), 64) * 64;  // whole 32-row (fp32) / 64-row (bf16) chunks
-    ns = std::max(1, cdiv(M, rps));
-    *nslices = ns;
-    *rows_per_slice = rps;
-}
 
 }  // namespace cn
 
@@ -1898,7 +1215,6 @@ static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_
     return check_launch("cn_linear");
 }
 
-static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     CN_REQUIRE(d, CN_ERR_ARG, "cn_linear: null desc");
@@ -2036,78 +1352,6 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     return launch_linear_tile<4, 1, 1, 2, 32, 2, 1>(d, a, s);
 }
 
-extern "C" size_t cn_wgrad_workspace_bytes(int32_t M, int32_t N, int32_t K) {
-    size_t need = 0;  // the larger of the two tilings (the call's mfma_dtype picks one)
-    for (int w = 0; w < 3; ++w) {
-        int tile, Npad, Kpad, ns, rps;
-        wgrad_geometry(std::max(M, 1), N, K, wgrad_wide_on() ? w : 0, &tile, &Npad, &Kpad, &ns, &rps);
-        need = std::max(need, sizeof(float) * ((size_t)ns * Npad * Kpad + (size_t)ns * Npad));
-    }
-    return need;
-}
-
-extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
-    CN_REQUIRE(d, CN_ERR_ARG, "cn_wgrad: null desc");
-    CN_REQUIRE(d->Y0 && d->X0 && d->dW && d->workspace, CN_ERR_ARG, "cn_wgrad: Y0, X0, dW, workspace required");
-    CN_REQUIRE(d->npairs == 1 || (d->npairs == 2 && d->Y1 && d->X1), CN_ERR_ARG, "cn_wgrad: bad npairs");
-    CN_REQUIRE(d->M >= 0 && d->N > 0 && d->K > 0 && d->K % 64 == 0, CN_ERR_SHAPE,
-               "cn_wgrad: bad shape M=%d N=%d K=%d (K must be a multiple of 64)", d->M, d->N, d->K);
-    int tile, Npad, Kpad, ns, rps;
-    wgrad_geometry(std::max(d->M, 1), d->N, d->K, wgrad_wide(d), &tile, &Npad, &Kpad, &ns, &rps);
-    CN_REQUIRE(d->n_out <= Npad && d->k_out <= Kpad && d->n_out > 0 && d->k_out > 0, CN_ERR_SHAPE, "cn_wgrad: bad n_out/k_out");
-    CN_REQUIRE(d->ldy0 >= Npad && d->ldx0 >= Kpad && d->ldy0 % 4 == 0 && d->ldx0 % 4 == 0 && al16(d->Y0) && al16(d->X0),
-               CN_ERR_ALIGN, "cn_wgrad: Y0/X0 must be 16B aligned with ld >= padded tile (%d, %d)", Npad, Kpad);
-    if (d->npairs == 2)
-        CN_REQUIRE(d->ldy1 >= Npad && d->ldx1 >= Kpad && d->ldy1 % 4 == 0 && d->ldx1 % 4 == 0 && al16(d->Y1) && al16(d->X1),
-                   CN_ERR_ALIGN, "cn_wgrad: Y1/X1 alignment");
-    CN_REQUIRE(d->ldy0 < (1 << 20) && d->ldx0 < (1 << 20) && d->ldy1 < (1 << 20) && d->ldx1 < (1 << 20), CN_ERR_SHAPE,
-               "cn_wgrad: leading dimensions must be < 2^20");
-    const size_t need = cn_wgrad_workspace_bytes(d->M, d->N, d->K);
-    CN_REQUIRE((size_t)d->workspace_bytes >= need, CN_ERR_SHAPE, "cn_wgrad: workspace %lld < %zu", (long long)d->workspace_bytes, need);
-    hipStream_t s = (hipStream_t)stream;
-    WgradArgs a;
-    a.Y0 = d->Y0; a.X0 = d->X0; a.Y1 = d->Y1; a.X1 = d->X1;
-    a.part = d->workspace;
-    a.bpart = d->db ? d->workspace + (size_t)ns * Npad * Kpad : nullptr;
-    a.ldy0 = (int)d->ldy0; a.ldx0 = (int)d->ldx0; a.ldy1 = (int)d->ldy1; a.ldx1 = (int)d->ldx1;
-    a.M = d->M; a.Npad = Npad; a.Kpad = Kpad; a.npairs = d->npairs; a.rows_per_slice = rps;
-    const int BNo = tile >= 2 ? 256 : 128, BKo = tile == 2 ? 256 : tile == 0 ? 128 : 64;
-    a.n_tiles_k = Kpad / BKo;
-    a.n_tiles_n = Npad / BNo;
-    a.nslices = ns;
-    dim3 grid(cdiv(ns, 8) * 8 * a.n_tiles_n * a.n_tiles_k);
-    CN_REQUIRE(d->mfma_dtype == CN_MFMA_F32 || d->mfma_dtype == CN_MFMA_BF16 || d->mfma_dtype == CN_MFMA_F32_BF16X6,
-               CN_ERR_ARG, "cn_wgrad: bad mfma_dtype %d", d->mfma_dtype);
-    if (d->mfma_dtype == CN_MFMA_F32_BF16X6) {
-        if (tile == 2)
-            wgrad_x6_kernel<4, 4><<<grid, 512, 0, s>>>(a);
-        else if (tile == 3)
-            wgrad_x6_kernel<4, 1><<<grid, 512, 0, s>>>(a);
-        else if (tile == 0)
-            wgrad_x6_kernel<2, 2><<<grid, 256, 0, s>>>(a);
-        else
-            wgrad_x6_kernel<2, 1><<<grid, 256, 0, s>>>(a);
-    } else if (d->mfma_dtype == CN_MFMA_BF16) {
-        if (tile == 0)
-            wgrad_bf16_kernel<2, 2, 2, 2><<<grid, 256, 0, s>>>(a);
-        else
-            wgrad_bf16_kernel<2, 2, 2, 1><<<grid, 256, 0, s>>>(a);
-    } else if (tile == 0) {
-        wgrad_kernel<2, 2, 2, 2><<<grid, 256, 0, s>>>(a);
-    } else {
-        wgrad_kernel<2, 2, 2, 1><<<grid, 256, 0, s>>>(a);
-    }
-    int rc = check_launch("cn_wgrad");
-    if (rc) return rc;
-    rc = launch_slab_reduce(a.part, ns, (int64_t)Npad * Kpad, d->n_out, d->k_out, Kpad, d->dW, d->ld_dw, 1.0f,
-                            d->accumulate, s);
-    if (rc) return rc;
-    if (d->db) {
-        rc = launch_slab_reduce(a.bpart, ns, Npad, 1, d->n_out, Npad, d->db, d->n_out, 1.0f, d->accumulate, s);
-        if (rc) return rc;
-    }
-    return CN_OK;
-}
 
 extern "C" int cn_row_head(int32_t M, int32_t K, const float* A, int64_t lda, const float* W, int64_t ldw,
                            const float* b, int32_t C, int32_t act, float* out, int64_t ld_out,

@@ -1,0 +1,857 @@
+// cn_wgrad.hip — weight gradients dW = Σ_m Yᵀ X (+ a second pair) and db = Σ_m Y over the M sample
+// rows (the reduction of every Linear's backward, model/neus_fields.py:273-303, 364-373), split
+// over workgroups into fp32 slabs that slab_reduce_kernel sums in a fixed order (bitwise
+// reproducible, no atomics).
+#include "cn_mfma.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <type_traits>
+
+#ifndef WGRAD_EXP
+#define WGRAD_EXP 0  // benchmark-only ablations (1: L2-resident operands)
+#endif
+#ifndef WGRAD_SGB
+#define WGRAD_SGB 1  // sched_barrier segments of the stage-ring weight gradient (0: compiler's own order)
+#endif
+
+namespace cn {
+
+// ---------------------------------------------------------------------------
+// Weight gradient.
+struct WgradArgs {
+    const float* Y0;
+    const float* X0;
+    const float* Y1;
+    const float* X1;
+    float* part;   // [nslices][Npad][Kpad]
+    float* bpart;  // [nslices][Npad]
+    int ldy0, ldx0, ldy1, ldx1;
+    int M, Npad, Kpad, npairs, rows_per_slice, n_tiles_n, n_tiles_k, nslices;
+};
+
+template <int WM, int WN, int TM, int TN>
+__global__ void __launch_bounds__(64 * WM * WN, 2) wgrad_kernel(WgradArgs p) {
+    constexpr int NT = 64 * WM * WN;
+    constexpr int BNo = 32 * TM * WM;  // output rows (n) per tile
+    constexpr int BKo = 32 * TN * WN;  // output cols (k) per tile
+    constexpr int MC = 32;             // sample rows per chunk
+    constexpr int YF4 = MC * BNo / 4;
+    constexpr int XF4 = MC * BKo / 4;
+    static_assert(YF4 % NT == 0 && XF4 % NT == 0, "tile/thread mismatch");
+    constexpr int YLD = YF4 / NT;
+    constexpr int XLD = XF4 / NT;
+
+    __shared__ __attribute__((aligned(16))) float smem[2 * MC * (BNo + BKo)];
+    float* sY = smem;
+    float* sX = smem + 2 * MC * BNo;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave / WN;
+    const int wn = wave % WN;
+
+    // XCD-aware: blocks b and b+8 share an XCD (and its L2), so the T output tiles
+    // of one M-slice, which read the same Y / X rows, are placed 8 blocks apart
+    const int T = p.n_tiles_n * p.n_tiles_k;
+    const int b = blockIdx.x;
+    const int tile = (b >> 3) % T;
+    const int slice = (b & 7) + 8 * ((b >> 3) / T);
+    if (slice >= p.nslices) return;
+    const int tn = tile / p.n_tiles_k;
+    const int tk = tile % p.n_tiles_k;
+    const int n0 = tn * BNo;
+    const int k0 = tk * BKo;
+    const int mbeg = slice * p.rows_per_slice;
+    const int mend = min(p.M, mbeg + p.rows_per_slice);
+    const int nch = mend > mbeg ? cdiv(mend - mbeg, MC) : 0;
+    const int total = nch * p.npairs;
+    const bool do_bias = (tk == 0) && (p.bpart != nullptr);
+
+    // buffer views (see linear_kernel): the chunk's first row is the descriptor
+    // base (SALU), rows past mend read as zero through the range check
+    constexpr int YRS = NT / (BNo / 4);  // staged rows per Y load instruction
+    constexpr int XRS = NT / (BKo / 4);
+    const int yrow = tid / (BNo / 4), yc4 = tid % (BNo / 4);
+    const int xrow = tid / (BKo / 4), xc4 = tid % (BKo / 4);
+    floatx4 ry[YLD], rx[XLD];
+    auto gload = [&](int c) {
+        const int pair = c >= nch;
+        const int mrow = mbeg + (c - pair * nch) * MC;
+        const float* Y = pair ? p.Y1 : p.Y0;
+        const float* X = pair ? p.X1 : p.X0;
+        const int ly = pair ? p.ldy1 : p.ldy0;
+        const int lx = pair ? p.ldx1 : p.ldx0;
+        const int nrows = min(MC, mend - mrow);
+        const rsrc_t vY = make_view(Y + (int64_t)mrow * ly + n0, (nrows * ly - n0) * 4);
+        const rsrc_t vX = make_view(X + (int64_t)mrow * lx + k0, (nrows * lx - k0) * 4);
+#pragma unroll
+        for (int q = 0; q < YLD; ++q) ry[q] = bload4(vY, ((yrow + q * YRS) * ly + yc4 * 4) * 4, 0);
+#pragma unroll
+        for (int q = 0; q < XLD; ++q) rx[q] = bload4(vX, ((xrow + q * XRS) * lx + xc4 * 4) * 4, 0);
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < YLD; ++q) {
+            const int f = tid + q * NT;
+            *reinterpret_cast<floatx4*>(sY + buf * MC * BNo + f * 4) = ry[q];
+        }
+#pragma unroll
+        for (int q = 0; q < XLD; ++q) {
+            const int f = tid + q * NT;
+            *reinterpret_cast<floatx4*>(sX + buf * MC * BKo + f * 4) = rx[q];
+        }
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+    float bacc = 0.0f;
+
+    if (total > 0) {
+        gload(0);
+        lstore(0);
+    }
+    __syncthreads();
+    const int h = lane >> 5;
+    const int ycol = wm * TM * 32 + (lane & 31);
+    const int xcol = wn * TN * 32 + (lane & 31);
+    for (int c = 0; c < total; ++c) {
+        const int cur = c & 1;
+        if (c + 1 < total) gload(c + 1);
+        const float* yb = sY + cur * MC * BNo;
+        const float* xb = sX + cur * MC * BKo;
+        if (do_bias && c < nch && tid < BNo) {
+#pragma unroll 8
+            for (int r = 0; r < MC; ++r) bacc += yb[r * BNo + tid];
+        }
+#pragma unroll
+        for (int s = 0; s < MC / 2; ++s) {
+            float af[TM], bf[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) af[i] = yb[(2 * s + h) * BNo + ycol + i * 32];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bf[j] = xb[(2 * s + h) * BKo + xcol + j * 32];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
+        if (c + 1 < total) lstore(cur ^ 1);
+        __syncthreads();
+    }
+
+    // slab stores: lane offset in voffset, the accumulator row step in soffset
+    const rsrc_t vP = make_view(p.part + (int64_t)slice * p.Npad * p.Kpad, p.Npad * p.Kpad * 4);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = k0 + wn * TN * 32 + j * 32 + (lane & 31);
+            const int rbase = n0 + wm * TM * 32 + i * 32 + 4 * (lane >> 5);
+            const int vo = (rbase * p.Kpad + col) * 4;
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                bstore1(vP, vo, ((r & 3) + 8 * (r >> 2)) * p.Kpad * 4, acc[i][j][r]);
+        }
+    }
+    if (do_bias && tid < BNo) p.bpart[(int64_t)slice * p.Npad + n0 + tid] = bacc;
+}
+
+// bf16-operand weight gradient (config C3): the same tiles and slabs as
+// wgrad_kernel, with Y and X rounded to bf16 while staging and written
+// TRANSPOSED into LDS ([n][m] and [k][m], 64 m per row + 8 pad = 36 dwords), so
+// one ds_read_b128 gives a lane the 8 consecutive m of its
+// v_mfma_f32_32x32x16_bf16 fragment.  A thread stages 4 rows x 4 columns per
+// pass and packs each column's 4 m into one ds_write_b64; the 16-byte blocks of
+// a row are XOR-swizzled so those writes do not collide on banks.  db is summed from the
+// fp32 values in registers (partials reduced through LDS at the end).
+template <int WM, int WN, int TM, int TN>
+__global__ void __launch_bounds__(64 * WM * WN, 2) wgrad_bf16_kernel(WgradArgs p) {
+    constexpr int NT = 64 * WM * WN;
+    constexpr int BNo = 32 * TM * WM;
+    constexpr int BKo = 32 * TN * WN;
+    constexpr int MC = 64;
+    constexpr int LSB = MC / 2 + 4;  // dwords per LDS row
+    constexpr int YC = BNo / 4, XC = BKo / 4;        // float4 column groups per staged row
+    constexpr int YMQ = NT / YC, XMQ = NT / XC;      // m-quads per pass
+    constexpr int YP = (MC / 4) / YMQ, XP = (MC / 4) / XMQ;
+    static_assert(YP >= 1 && XP >= 1 && YMQ * YC == NT && XMQ * XC == NT, "staging geometry");
+    static_assert(2 * BNo <= (BNo + BKo) * LSB, "bias partials fit in LDS");
+
+    __shared__ __attribute__((aligned(16))) float smem[2 * (BNo + BKo) * LSB];
+    float* sY = smem;
+    float* sX = smem + 2 * BNo * LSB;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave / WN;
+    const int wn = wave % WN;
+    const int T = p.n_tiles_n * p.n_tiles_k;
+    const int b = blockIdx.x;
+    const int tile = (b >> 3) % T;
+    const int slice = (b & 7) + 8 * ((b >> 3) / T);
+    if (slice >= p.nslices) return;
+    const int tn = tile / p.n_tiles_k;
+    const int tk = tile % p.n_tiles_k;
+    const int n0 = tn * BNo;
+    const int k0 = tk * BKo;
+    const int mbeg = slice * p.rows_per_slice;
+    const int mend = min(p.M, mbeg + p.rows_per_slice);
+    const int nch = mend > mbeg ? cdiv(mend - mbeg, MC) : 0;
+    const int total = nch * p.npairs;
+    const bool do_bias = (tk == 0) && (p.bpart != nullptr);
+
+    const int yc = tid % YC, ymq = tid / YC;
+    const int xc = tid % XC, xmq = tid / XC;
+    floatx4 ry[YP][4], rx[XP][4];
+    float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+    auto gload = [&](int c) {
+        const int pair = c >= nch;
+        const int mrow = mbeg + (c - pair * nch) * MC;
+        const float* Y = pair ? p.Y1 : p.Y0;
+        const float* X = pair ? p.X1 : p.X0;
+        const int ly = pair ? p.ldy1 : p.ldy0;
+        const int lx = pair ? p.ldx1 : p.ldx0;
+        const int nrows = min(MC, mend - mrow);
+        const rsrc_t vY = make_view(Y + (int64_t)mrow * ly + n0, (nrows * ly - n0) * 4);
+        const rsrc_t vX = make_view(X + (int64_t)mrow * lx + k0, (nrows * lx - k0) * 4);
+#pragma unroll
+        for (int pp = 0; pp < YP; ++pp)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                ry[pp][r] = bload4(vY, (((ymq + pp * YMQ) * 4 + r) * ly + yc * 4) * 4, 0);
+#pragma unroll
+        for (int pp = 0; pp < XP; ++pp)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                rx[pp][r] = bload4(vX, (((xmq + pp * XMQ) * 4 + r) * lx + xc * 4) * 4, 0);
+    };
+    // XOR swizzle of the 16-byte blocks of a row by (row >> 2) & 7: the staging
+    // writes (threads on rows 4 apart) spread over all banks; reads undo it
+    auto swz = [&](int row, int mq) { return row * LSB + (((mq >> 1) ^ ((row >> 2) & 7)) << 2) + ((mq & 1) << 1); };
+    auto lstore = [&](int buf, bool bias) {
+        float* y = sY + buf * BNo * LSB;
+        float* x = sX + buf * BKo * LSB;
+#pragma unroll
+        for (int pp = 0; pp < YP; ++pp)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const floatx4 col = {ry[pp][0][e], ry[pp][1][e], ry[pp][2][e], ry[pp][3][e]};
+                if (bias) bsum[e] += (col[0] + col[1]) + (col[2] + col[3]);
+                *reinterpret_cast<bf16x4*>(y + swz(yc * 4 + e, ymq + pp * YMQ)) = __builtin_convertvector(col, bf16x4);
+            }
+#pragma unroll
+        for (int pp = 0; pp < XP; ++pp)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const floatx4 col = {rx[pp][0][e], rx[pp][1][e], rx[pp][2][e], rx[pp][3][e]};
+                *reinterpret_cast<bf16x4*>(x + swz(xc * 4 + e, xmq + pp * XMQ)) = __builtin_convertvector(col, bf16x4);
+            }
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+    if (total > 0) {
+        gload(0);
+        lstore(0, do_bias && nch > 0);
+    }
+    __syncthreads();
+    const int h = lane >> 5;
+    const int ycol = wm * TM * 32 + (lane & 31);
+    const int xcol = wn * TN * 32 + (lane & 31);
+    for (int c = 0; c < total; ++c) {
+        const int cur = c & 1;
+        const bool more = c + 1 < total;
+        if (more) gload(c + 1);
+        const float* yb = sY + cur * BNo * LSB + ycol * LSB;
+        const float* xb = sX + cur * BKo * LSB + xcol * LSB;
+        const int sw = ((lane & 31) >> 2) & 7;  // (row >> 2) & 7 of this lane's rows
+#pragma unroll
+        for (int ks = 0; ks < MC / 16; ++ks) {
+            const int blk = ((2 * ks + h) ^ sw) << 2;
+            bf16x8 af[TM], bf[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(yb + i * 32 * LSB + blk);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const bf16x8*>(xb + j * 32 * LSB + blk);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
+        if (more) lstore(cur ^ 1, do_bias && c + 1 < nch);
+        __syncthreads();
+    }
+
+    const rsrc_t vP = make_view(p.part + (int64_t)slice * p.Npad * p.Kpad, p.Npad * p.Kpad * 4);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = k0 + wn * TN * 32 + j * 32 + (lane & 31);
+            const int rbase = n0 + wm * TM * 32 + i * 32 + 4 * (lane >> 5);
+            const int vo = (rbase * p.Kpad + col) * 4;
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                bstore1(vP, vo, ((r & 3) + 8 * (r >> 2)) * p.Kpad * 4, acc[i][j][r]);
+        }
+    }
+    if (do_bias) {  // reduce the per-thread column partials over the m-quads (fixed order)
+        float* red = smem;  // [YMQ][BNo]
+#pragma unroll
+        for (int e = 0; e < 4; ++e) red[ymq * BNo + yc * 4 + e] = bsum[e];
+        __syncthreads();
+        if (tid < BNo) {
+            float t = 0.0f;
+            for (int q = 0; q < YMQ; ++q) t += red[q * BNo + tid];
+            p.bpart[(int64_t)slice * p.Npad + n0 + tid] = t;
+        }
+    }
+}
+
+// fp32 weight gradient on the bf16 MFMA (CN_MFMA_F32_BF16X6), 128x128 output
+// tiles: Y and X are split into three bf16 terms while staging (split3) and the
+// six term products with i + j <= 2 accumulate in fp32, as in linear_kernel
+// MODE 2.  Staging is transposed like wgrad_bf16_kernel's, 32 sample rows per
+// chunk: thread t holds m-quad t % 8 of column group t / 8 (4 m x 4 columns of
+// Y and of X), so 16 contiguous lanes write two LDS rows 4 apart whose 64-byte
+// segments fall on the two halves of the 32 write banks; an LDS row is the three
+// 16-dword term planes + 4 pad (52 dwords: the ds_read_b128 fragment reads of 16
+// consecutive rows hit 16 distinct bank quads).  One LDS buffer (53 KB, two
+// workgroups per CU): the next chunk's loads fly during the MFMAs.  TN = 1: 64
+// output columns, X staged by the first two waves.  WM = 4, TN = 4: a whole
+// 256x256 layer per workgroup of 8 waves (one per CU, 106 KB LDS): every staged
+// element feeds twice the MFMA work of the 128x128 tile.
+template <int WM, int TN>
+__global__ void __launch_bounds__(128 * WM, 2) wgrad_x6_kernel(WgradArgs p) {
+    constexpr int TM = 2, WN = 2, NT = 128 * WM;
+    constexpr int BNo = 64 * WM, BKo = 64 * TN, MC = 32, MQ = MC / 4;
+    constexpr int PL = MC / 2;       // dwords per term plane of a row
+    constexpr int LSB = 3 * PL + 4;  // 52
+    constexpr int XT = MQ * (BKo / 4);  // threads staging X (256 or 128: whole waves)
+    static_assert(MQ * (BNo / 4) == NT && XT <= NT && XT % 64 == 0, "staging geometry: whole waves");
+    static_assert(MQ * BNo <= (BNo + BKo) * LSB, "bias partials fit in LDS");
+    __shared__ __attribute__((aligned(16))) float smem[(BNo + BKo) * LSB];
+    float* sY = smem;
+    float* sX = smem + BNo * LSB;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave / WN;
+    const int wn = wave % WN;
+    const int T = p.n_tiles_n * p.n_tiles_k;
+    const int b = blockIdx.x;
+    const int tile = (b >> 3) % T;
+    const int slice = (b & 7) + 8 * ((b >> 3) / T);
+    if (slice >= p.nslices) return;
+    const int tn = tile / p.n_tiles_k;
+    const int tk = tile % p.n_tiles_k;
+    const int n0 = tn * BNo;
+    const int k0 = tk * BKo;
+    const int mbeg = slice * p.rows_per_slice;
+    const int mend = min(p.M, mbeg + p.rows_per_slice);
+    const int nch = mend > mbeg ? cdiv(mend - mbeg, MC) : 0;
+    const int total = nch * p.npairs;
+    const bool do_bias = (tk == 0) && (p.bpart != nullptr);
+
+    const int mq = tid % MQ, cg = tid / MQ;
+    floatx4 ry[4], rx[4];
+    float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+    auto gload = [&](int c) {
+        const int pair = c >= nch;
+        const int mrow = mbeg + (c - pair * nch) * MC;
+        const float* Y = pair ? p.Y1 : p.Y0;
+        const float* X = pair ? p.X1 : p.X0;
+        const int ly = pair ? p.ldy1 : p.ldy0;
+        const int lx = pair ? p.ldx1 : p.ldx0;
+        const int nrows = min(MC, mend - mrow);
+#if WGRAD_EXP == 1  // benchmark only: every chunk reads rows [0, 4096) (L2-resident operands)
+        const int mr = mrow & 4095;
+#else
+        const int mr = mrow;
+#endif
+        const rsrc_t vY = make_view(Y + (int64_t)mr * ly + n0, (nrows * ly - n0) * 4);
+        const rsrc_t vX = make_view(X + (int64_t)mr * lx + k0, (nrows * lx - k0) * 4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ry[r] = bload4(vY, ((mq * 4 + r) * ly + cg * 4) * 4, 0);
+        if (XT == NT || tid < XT) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) rx[r] = bload4(vX, ((mq * 4 + r) * lx + cg * 4) * 4, 0);
+        }
+    };
+    auto lstore = [&](bool bias) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const floatx4 col = {ry[0][e], ry[1][e], ry[2][e], ry[3][e]};
+            if (bias) bsum[e] += (col[0] + col[1]) + (col[2] + col[3]);
+            bf16x4 t0, t1, t2;
+            split3(col, t0, t1, t2);
+            float* y = sY + (cg * 4 + e) * LSB + mq * 2;
+            *reinterpret_cast<bf16x4*>(y) = t0;
+            *reinterpret_cast<bf16x4*>(y + PL) = t1;
+            *reinterpret_cast<bf16x4*>(y + 2 * PL) = t2;
+        }
+        if (XT < NT && tid >= XT) return;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const floatx4 col = {rx[0][e], rx[1][e], rx[2][e], rx[3][e]};
+            bf16x4 t0, t1, t2;
+            split3(col, t0, t1, t2);
+            float* x = sX + (cg * 4 + e) * LSB + mq * 2;
+            *reinterpret_cast<bf16x4*>(x) = t0;
+            *reinterpret_cast<bf16x4*>(x + PL) = t1;
+            *reinterpret_cast<bf16x4*>(x + 2 * PL) = t2;
+        }
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+    const int h = lane >> 5;
+    const float* yb = sY + (wm * TM * 32 + (lane & 31)) * LSB + 4 * h;
+    const float* xb = sX + (wn * TN * 32 + (lane & 31)) * LSB + 4 * h;
+    if (total > 0) gload(0);
+    for (int c = 0; c < total; ++c) {
+        if (c > 0) __syncthreads();  // the previous chunk's fragment reads are done
+        lstore(do_bias && c < nch);
+        __syncthreads();
+        if (c + 1 < total) gload(c + 1);
+#pragma unroll
+        for (int ks = 0; ks < MC / 16; ++ks) {
+            bf16x8 af[3][TM], bf[3][TN];
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i) af[t][i] = *reinterpret_cast<const bf16x8*>(yb + i * 32 * LSB + t * PL + ks * 8);
+#pragma unroll
+                for (int j = 0; j < TN; ++j) bf[t][j] = *reinterpret_cast<const bf16x8*>(xb + j * 32 * LSB + t * PL + ks * 8);
+            }
+            constexpr int TA[6] = {0, 1, 0, 2, 1, 0};
+            constexpr int TB[6] = {0, 0, 1, 0, 1, 2};
+#pragma unroll
+            for (int u = 0; u < 6; ++u)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[TA[u]][i], bf[TB[u]][j], acc[i][j], 0, 0, 0);
+        }
+    }
+    __syncthreads();  // LDS is reused for the bias partials
+
+    const rsrc_t vP = make_view(p.part + (int64_t)slice * p.Npad * p.Kpad, p.Npad * p.Kpad * 4);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = k0 + wn * TN * 32 + j * 32 + (lane & 31);
+            const int rbase = n0 + wm * TM * 32 + i * 32 + 4 * (lane >> 5);
+            const int vo = (rbase * p.Kpad + col) * 4;
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                bstore1(vP, vo, ((r & 3) + 8 * (r >> 2)) * p.Kpad * 4, acc[i][j][r]);
+        }
+    }
+    if (do_bias) {  // reduce the per-thread column partials over the m-quads (fixed order)
+        float* red = smem;  // [MQ][BNo]
+#pragma unroll
+        for (int e = 0; e < 4; ++e) red[mq * BNo + cg * 4 + e] = bsum[e];
+        __syncthreads();
+        if (tid < BNo) {
+            float t = 0.0f;
+            for (int q = 0; q < MQ; ++q) t += red[q * BNo + tid];
+            p.bpart[(int64_t)slice * p.Npad + n0 + tid] = t;
+        }
+    }
+}
+
+// Whole-layer (256x256) bf16x6 weight gradient on a stage ring: 16 sample rows per stage,
+// two split-image buffers (2 x 56 KB: rows of 3 term planes x 8 dwords + 4 pad, reads
+// conflict-free, staging writes 2-way) and NRAW register sets of raw fp32 rows, so ONE
+// barrier separates consecutive stages and everything else of stage c+1 -- the global
+// loads of stage c+NRAW, the bf16 split and the LDS writes of stage c+1 into the free
+// buffer -- sits in the same basic block as stage c's 48 MFMAs per wave.  The stage is four
+// segments pinned by sched_barrier (column block j's 12 MFMAs beside split column j), so
+// the scheduler interleaves each segment's split VALU and LDS writes with its MFMAs: in
+// the same wave's stream they fill MFMA issue gaps (a partner wave's VALU does not,
+// tools/probes/mfma_bf16_valu_probe.hip; sched_group_barrier patterns were not followed).
+// Waves 0-3 stage Y, waves 4-7 stage X (thread: m-quad t % 4 of column group t / 4,
+// t = tid % 256).  v_mfma_f32_32x32x16_bf16, 2x4 accumulators of 32x32 per wave (64 n x
+// 128 k).  Measured against wgrad_x6_kernel<4, 4> (tools/wgrad_ab.sh): 767-772 vs 790-794
+// us per 2-pair C2-shape call on random data, 641-644 vs 666-676 with L2-resident operands
+// (WGRAD_EXP=1: the kernel is not HBM-bound); 16x16x32 MFMAs (higher clock, more cycles)
+// and a register-held split of the next 32-row chunk measured equal to the old kernel.
+template <int NRAW>
+__global__ void __launch_bounds__(512, 2) wgrad_x6r_kernel(WgradArgs p) {
+    constexpr int BNo = 256, MC = 16, PL = 8, LSB = 3 * PL + 4;  // 28 dwords per LDS row
+    constexpr int IMG = 2 * BNo * LSB;                            // one buffer: Y rows then X rows
+    __shared__ __attribute__((aligned(16))) float smem[2 * IMG];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int slice = blockIdx.x;
+    if (slice >= p.nslices) return;
+    const int mbeg = slice * p.rows_per_slice;
+    const int mend = min(p.M, mbeg + p.rows_per_slice);
+    const int nch = mend > mbeg ? cdiv(mend - mbeg, MC) : 0;
+    const int total = nch * p.npairs;
+    const bool do_bias = p.bpart != nullptr;
+
+    const bool sx = wave >= 4;  // wave-uniform: this wave stages X
+    const int t = tid & 255, mq = t & 3, cg = t >> 2;
+    floatx4 raw[NRAW][4];
+    float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+    auto gload = [&](int c, floatx4 (&r4)[4]) {
+        const bool valid = c < total;
+        const int cc = valid ? c : 0;
+        const int pair = cc >= nch;
+        const int mrow = mbeg + (cc - pair * nch) * MC;
+        const float* src = sx ? (pair ? p.X1 : p.X0) : (pair ? p.Y1 : p.Y0);
+        const int ld = sx ? (pair ? p.ldx1 : p.ldx0) : (pair ? p.ldy1 : p.ldy0);
+        const int nrows = valid ? min(MC, mend - mrow) : 0;
+#if WGRAD_EXP == 1
+        const int mr = mrow & 4095;
+#else
+        const int mr = mrow;
+#endif
+        const rsrc_t v = make_view(src + (int64_t)mr * ld, nrows * ld * 4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) r4[r] = bload4(v, ((mq * 4 + r) * ld + cg * 4) * 4, 0);
+    };
+    // split column e of the 4 x 4 block of a register set into the stage image of buffer `buf`
+    auto split_col = [&](const floatx4 (&r4)[4], int e, int buf, bool bias) {
+        float* img = smem + buf * IMG + (sx ? BNo * LSB : 0) + mq * 2;
+        const floatx4 col = {r4[0][e], r4[1][e], r4[2][e], r4[3][e]};
+        const float s = (col[0] + col[1]) + (col[2] + col[3]);
+        bsum[e] += bias ? s : 0.0f;
+        bf16x4 t0, t1, t2;
+        split3(col, t0, t1, t2);
+        float* y = img + (cg * 4 + e) * LSB;
+        *reinterpret_cast<bf16x4*>(y) = t0;
+        *reinterpret_cast<bf16x4*>(y + PL) = t1;
+        *reinterpret_cast<bf16x4*>(y + 2 * PL) = t2;
+    };
+    auto splitw = [&](const floatx4 (&r4)[4], int buf, bool bias) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) split_col(r4, e, buf, bias);
+    };
+
+    floatx16 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+    const int frow = lane & 31, fh = lane >> 5;
+    constexpr int TA[6] = {0, 1, 0, 2, 1, 0};
+    constexpr int TB[6] = {0, 0, 1, 0, 1, 2};
+    // one stage from buffer `buf`, in four segments pinned by sched_barrier: segment j reads
+    // column block j+1's B fragments, issues block j's 12 MFMAs and `side(j)` (split column j
+    // of the next stage and its LDS writes), which the scheduler interleaves with the MFMAs
+    auto compute = [&](int buf, auto side) {
+        const float* ya = smem + buf * IMG + (wm * 64 + frow) * LSB + 4 * fh;
+        const float* xa = smem + buf * IMG + BNo * LSB + (wn * 128 + frow) * LSB + 4 * fh;
+        bf16x8 af[3][2], bj[2][3];
+#pragma unroll
+        for (int tt = 0; tt < 3; ++tt)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) af[tt][i] = *reinterpret_cast<const bf16x8*>(ya + i * 32 * LSB + tt * PL);
+#pragma unroll
+        for (int tt = 0; tt < 3; ++tt) bj[0][tt] = *reinterpret_cast<const bf16x8*>(xa + tt * PL);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (j + 1 < 4) {
+#pragma unroll
+                for (int tt = 0; tt < 3; ++tt)
+                    bj[(j + 1) & 1][tt] = *reinterpret_cast<const bf16x8*>(xa + (j + 1) * 32 * LSB + tt * PL);
+            }
+#pragma unroll
+            for (int u = 0; u < 6; ++u)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[TA[u]][i], bj[j & 1][TB[u]], acc[i][j], 0, 0, 0);
+            side(j);
+#if WGRAD_SGB
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+        }
+    };
+
+    // the bias sums take stage c's Y rows of pair 0 (Y threads only); bitwise, not &&, so
+    // the loop body stays one basic block
+    const bool ybias = do_bias & !sx;
+    auto bias_of = [&](int c) { return ybias & (c < nch); };
+#pragma unroll
+    for (int s = 0; s < NRAW; ++s) gload(s, raw[s]);
+    splitw(raw[0], 0, bias_of(0));
+    __syncthreads();
+    // stage c in set c % NRAW: the loop is unrolled NRAW-fold so the set indices are constants,
+    // and runs whole NRAW-groups of stages (the stages past `total` read zeros: an empty view)
+    for (int c0 = 0; c0 < total; c0 += NRAW) {
+#pragma unroll
+        for (int k = 0; k < NRAW; ++k) {
+            const int c = c0 + k;
+            {
+                gload(c + NRAW, raw[k]);  // set k held stage c (split in the previous stage)
+                const bool bnext = bias_of(c + 1);
+                compute(c & 1, [&](int j) { split_col(raw[(k + 1) % NRAW], j, (c + 1) & 1, bnext); });
+                __syncthreads();  // stage c+1 written, stage c's buffer free
+            }
+        }
+    }
+    __syncthreads();  // LDS is reused for the bias partials
+
+    const rsrc_t vP = make_view(p.part + (int64_t)slice * p.Npad * p.Kpad, p.Npad * p.Kpad * 4);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int col = wn * 128 + j * 32 + (lane & 31);
+            const int rbase = wm * 64 + i * 32 + 4 * (lane >> 5);
+            const int vo = (rbase * p.Kpad + col) * 4;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) bstore1(vP, vo, ((r & 3) + 8 * (r >> 2)) * p.Kpad * 4, acc[i][j][r]);
+        }
+    }
+    if (do_bias) {  // reduce the Y threads' column partials over the m-quads (fixed order)
+        float* red = smem;  // [4][BNo]
+        if (!sx) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) red[mq * BNo + cg * 4 + e] = bsum[e];
+        }
+        __syncthreads();
+        if (tid < BNo) {
+            const float tot = ((red[tid] + red[BNo + tid]) + red[2 * BNo + tid]) + red[3 * BNo + tid];
+            p.bpart[(int64_t)slice * p.Npad + tid] = tot;
+        }
+    }
+}
+
+// Sum of nslab fp32 slabs: out[r*ldo + c] (+)= (sum_s part[s*stride + r*ldp + c]) / div
+// for r < rows, c < cols.  A workgroup owns 64 float4 column groups x 4 slab
+// groups; each thread sums its slab group in double with 4 loads in flight, the 4
+// groups combine through LDS in a fixed order (bitwise reproducible).
+// 256 threads = kSlabGroups slab groups x (256 / kSlabGroups) float4 column groups: slab
+// group sg sums slabs sg, sg + SG, ... in double, the groups meet in a fixed order in LDS.
+// (16 x 16: a 256-slab weight gradient is 16 loads per thread, 4x the blocks of a 4 x 64 split.)
+constexpr int kSlabGroups = 16;
+__global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ part, int nslab, int64_t stride,
+                                                          int rows, int cols, int64_t ldp, float* out, int64_t ldo,
+                                                          float div, int accumulate) {
+    constexpr int SG = kSlabGroups, CG = 256 / SG;
+    __shared__ double red[SG][CG][4];
+    const int c4n = cdiv(cols, 4);
+    const int t = threadIdx.x % CG;
+    const int sg = threadIdx.x / CG;
+    const int64_t g = (int64_t)blockIdx.x * CG + t;  // float4 group over rows x c4n
+    const bool valid = g < (int64_t)rows * c4n;
+    const int r = valid ? (int)(g / c4n) : 0;
+    const int c = valid ? (int)(g % c4n) * 4 : 0;
+    const bool vec = valid && (c + 3 < cols) && (ldp % 4 == 0) && (stride % 4 == 0);
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    if (valid) {
+        const float* base = part + (int64_t)r * ldp + c;
+        int sl = sg;
+        for (; sl + 3 * SG < nslab; sl += 4 * SG) {
+            floatx4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const float* q = base + (int64_t)(sl + SG * u) * stride;
+                if (vec) {
+                    v[u] = *reinterpret_cast<const floatx4*>(q);
+                } else {
+                    for (int e = 0; e < 4; ++e) v[u][e] = (c + e < cols) ? q[e] : 0.0f;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) a[e] += (double)v[u][e];
+        }
+        for (; sl < nslab; sl += SG) {
+            const float* q = base + (int64_t)sl * stride;
+            for (int e = 0; e < 4; ++e) a[e] += (c + e < cols) ? (double)q[e] : 0.0;
+        }
+    }
+    for (int e = 0; e < 4; ++e) red[sg][t][e] = a[e];
+    __syncthreads();
+    if (sg == 0 && valid) {
+        for (int e = 0; e < 4 && c + e < cols; ++e) {
+            double tot = red[0][t][e];
+            for (int q = 1; q < SG; ++q) tot += red[q][t][e];
+            float v = (float)tot;
+            if (div != 1.0f) v = v / div;
+            float* o = out + (int64_t)r * ldo + c + e;
+            if (accumulate) v += *o;
+            *o = v;
+        }
+    }
+}
+
+int launch_slab_reduce(const float* part, int nslab, int64_t stride, int rows, int cols, int64_t ldp, float* out,
+                       int64_t ldo, float div, int accumulate, hipStream_t s) {
+    const int64_t groups = (int64_t)rows * cdiv(cols, 4);
+    if (groups == 0) return CN_OK;
+    constexpr int CG = 256 / kSlabGroups;
+    slab_reduce_kernel<<<(int)((groups + CG - 1) / CG), 256, 0, s>>>(part, nslab, stride, rows, cols, ldp, out, ldo,
+                                                                     div, accumulate);
+    return check_launch("slab_reduce");
+}
+
+// ---------------------------------------------------------------------------
+// tile 0: 128x128 output tiles, 1: 128x64, 2 (bf16x6, operand rows at least 256-padded):
+// 256x256 tiles of 512-thread workgroups, one per CU (half the workgroup target).  Padding
+// columns of Y / X only feed output rows / columns past n_out / k_out, which the slab
+// reduction never reads.
+static bool wgrad_wide_on() {
+    static const bool on = [] {  // benchmarking aid: COPENERF_WGRAD_WIDE=0 keeps the 128x128 tiles
+        const char* e = getenv("COPENERF_WGRAD_WIDE");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return on;
+}
+// 3 (bf16x6, K <= 64, Y rows 256-padded; COPENERF_WGRAD_NARROW=1): 256x64 tiles of 512-thread
+// workgroups.  Measured slower than the 128x64 tiles on the C2 first-layer shapes (0.418 vs
+// 0.388 ms, 0.207 vs 0.187 ms), so off by default.
+// Returns the wide mode: 0 none, 1 = 256x256, 2 = 256x64.
+static int wgrad_wide(const cn_wgrad_desc* d) {
+    static const bool narrow = [] {
+        const char* e = getenv("COPENERF_WGRAD_NARROW");
+        return e && atoi(e) != 0;
+    }();
+    const int64_t np = (int64_t)cdiv(d->N, 256) * 256, kp = (int64_t)cdiv(d->K, 256) * 256;
+    if (!wgrad_wide_on() || d->mfma_dtype != CN_MFMA_F32_BF16X6 || d->ldy0 < np || (d->npairs == 2 && d->ldy1 < np))
+        return 0;
+    if (d->ldx0 >= kp && (d->npairs == 1 || d->ldx1 >= kp)) return 1;
+    return narrow && d->K <= 64 ? 2 : 0;
+}
+
+static void wgrad_geometry(int M, int N, int K, int wide, int* tile, int* Npad, int* Kpad, int* nslices,
+                           int* rows_per_slice) {
+    const int t = wide == 1 ? 2 : wide == 2 ? 3 : (K % 128 == 0) ? 0 : 1;
+    const int BNo = t >= 2 ? 256 : 128, BKo = t == 2 ? 256 : t == 0 ? 128 : 64;
+    *tile = t;
+    *Npad = cdiv(N, BNo) * BNo;
+    *Kpad = cdiv(K, BKo) * BKo;
+    const int tiles = (*Npad / BNo) * (*Kpad / BKo);
+    static const int kTarget = [] {  // workgroups per cn_wgrad (benchmarking aid: COPENERF_WGRAD_BLOCKS)
+        const char* e = getenv("COPENERF_WGRAD_BLOCKS");
+        return e ? atoi(e) : 512;
+    }();
+    int ns = std::max(1, (t == 2 ? kTarget / 2 : kTarget) / tiles);  // (t 3: 2 workgroups per CU)
+    ns = std::min(ns, std::max(1, cdiv(M, 512)));
+    int rps = cdiv(cdiv(M, ns), 64) * 64;  // whole 32-row (fp32) / 64-row (bf16) chunks
+    ns = std::max(1, cdiv(M, rps));
+    *nslices = ns;
+    *rows_per_slice = rps;
+}
+
+}  // namespace cn
+
+using namespace cn;
+
+extern "C" size_t cn_wgrad_workspace_bytes(int32_t M, int32_t N, int32_t K) {
+    size_t need = 0;  // the larger of the two tilings (the call's mfma_dtype picks one)
+    for (int w = 0; w < 3; ++w) {
+        int tile, Npad, Kpad, ns, rps;
+        wgrad_geometry(std::max(M, 1), N, K, wgrad_wide_on() ? w : 0, &tile, &Npad, &Kpad, &ns, &rps);
+        need = std::max(need, sizeof(float) * ((size_t)ns * Npad * Kpad + (size_t)ns * Npad));
+    }
+    return need;
+}
+
+extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
+    CN_REQUIRE(d, CN_ERR_ARG, "cn_wgrad: null desc");
+    CN_REQUIRE(d->Y0 && d->X0 && d->dW && d->workspace, CN_ERR_ARG, "cn_wgrad: Y0, X0, dW, workspace required");
+    CN_REQUIRE(d->npairs == 1 || (d->npairs == 2 && d->Y1 && d->X1), CN_ERR_ARG, "cn_wgrad: bad npairs");
+    CN_REQUIRE(d->M >= 0 && d->N > 0 && d->K > 0 && d->K % 64 == 0, CN_ERR_SHAPE,
+               "cn_wgrad: bad shape M=%d N=%d K=%d (K must be a multiple of 64)", d->M, d->N, d->K);
+    int tile, Npad, Kpad, ns, rps;
+    wgrad_geometry(std::max(d->M, 1), d->N, d->K, wgrad_wide(d), &tile, &Npad, &Kpad, &ns, &rps);
+    CN_REQUIRE(d->n_out <= Npad && d->k_out <= Kpad && d->n_out > 0 && d->k_out > 0, CN_ERR_SHAPE, "cn_wgrad: bad n_out/k_out");
+    CN_REQUIRE(d->ldy0 >= Npad && d->ldx0 >= Kpad && d->ldy0 % 4 == 0 && d->ldx0 % 4 == 0 && al16(d->Y0) && al16(d->X0),
+               CN_ERR_ALIGN, "cn_wgrad: Y0/X0 must be 16B aligned with ld >= padded tile (%d, %d)", Npad, Kpad);
+    if (d->npairs == 2)
+        CN_REQUIRE(d->ldy1 >= Npad && d->ldx1 >= Kpad && d->ldy1 % 4 == 0 && d->ldx1 % 4 == 0 && al16(d->Y1) && al16(d->X1),
+                   CN_ERR_ALIGN, "cn_wgrad: Y1/X1 alignment");
+    CN_REQUIRE(d->ldy0 < (1 << 20) && d->ldx0 < (1 << 20) && d->ldy1 < (1 << 20) && d->ldx1 < (1 << 20), CN_ERR_SHAPE,
+               "cn_wgrad: leading dimensions must be < 2^20");
+    const size_t need = cn_wgrad_workspace_bytes(d->M, d->N, d->K);
+    CN_REQUIRE((size_t)d->workspace_bytes >= need, CN_ERR_SHAPE, "cn_wgrad: workspace %lld < %zu", (long long)d->workspace_bytes, need);
+    hipStream_t s = (hipStream_t)stream;
+    WgradArgs a;
+    a.Y0 = d->Y0; a.X0 = d->X0; a.Y1 = d->Y1; a.X1 = d->X1;
+    a.part = d->workspace;
+    a.bpart = d->db ? d->workspace + (size_t)ns * Npad * Kpad : nullptr;
+    a.ldy0 = (int)d->ldy0; a.ldx0 = (int)d->ldx0; a.ldy1 = (int)d->ldy1; a.ldx1 = (int)d->ldx1;
+    a.M = d->M; a.Npad = Npad; a.Kpad = Kpad; a.npairs = d->npairs; a.rows_per_slice = rps;
+    const int BNo = tile >= 2 ? 256 : 128, BKo = tile == 2 ? 256 : tile == 0 ? 128 : 64;
+    a.n_tiles_k = Kpad / BKo;
+    a.n_tiles_n = Npad / BNo;
+    a.nslices = ns;
+    dim3 grid(cdiv(ns, 8) * 8 * a.n_tiles_n * a.n_tiles_k);
+    CN_REQUIRE(d->mfma_dtype == CN_MFMA_F32 || d->mfma_dtype == CN_MFMA_BF16 || d->mfma_dtype == CN_MFMA_F32_BF16X6,
+               CN_ERR_ARG, "cn_wgrad: bad mfma_dtype %d", d->mfma_dtype);
+    if (d->mfma_dtype == CN_MFMA_F32_BF16X6) {
+        if (tile == 2) {
+            // the stage ring (one barrier per 16 rows, split and LDS writes beside the MFMAs): C2
+            // step 145.0-145.3k vs 142.1-143.3k rays/s with the 32-row single-buffer kernel
+            // (COPENERF_WGRAD_KERNEL=1, benchmarking aid; tools/env_ab.sh, same box)
+            static const int variant = [] {
+                const char* e = getenv("COPENERF_WGRAD_KERNEL");
+                return e ? atoi(e) : 0;
+            }();
+            if (variant == 1) wgrad_x6_kernel<4, 4><<<grid, 512, 0, s>>>(a);
+            else wgrad_x6r_kernel<2><<<grid, 512, 0, s>>>(a);
+        }
+        else if (tile == 3)
+            wgrad_x6_kernel<4, 1><<<grid, 512, 0, s>>>(a);
+        else if (tile == 0)
+            wgrad_x6_kernel<2, 2><<<grid, 256, 0, s>>>(a);
+        else
+            wgrad_x6_kernel<2, 1><<<grid, 256, 0, s>>>(a);
+    } else if (d->mfma_dtype == CN_MFMA_BF16) {
+        if (tile == 0)
+            wgrad_bf16_kernel<2, 2, 2, 2><<<grid, 256, 0, s>>>(a);
+        else
+            wgrad_bf16_kernel<2, 2, 2, 1><<<grid, 256, 0, s>>>(a);
+    } else if (tile == 0) {
+        wgrad_kernel<2, 2, 2, 2><<<grid, 256, 0, s>>>(a);
+    } else {
+        wgrad_kernel<2, 2, 2, 1><<<grid, 256, 0, s>>>(a);
+    }
+    int rc = check_launch("cn_wgrad");
+    if (rc) return rc;
+    rc = launch_slab_reduce(a.part, ns, (int64_t)Npad * Kpad, d->n_out, d->k_out, Kpad, d->dW, d->ld_dw, 1.0f,
+                            d->accumulate, s);
+    if (rc) return rc;
+    if (d->db) {
+        rc = launch_slab_reduce(a.bpart, ns, Npad, 1, d->n_out, Npad, d->db, d->n_out, 1.0f, d->accumulate, s);
+        if (rc) return rc;
+    }
+    return CN_OK;
+}

@@ -22,5 +22,7 @@ for k, cs in vals.items():
         extra = f"  ({avg[c] / wc:6.3f} of wave cycles)" if wc and c.startswith("SQ_") and c != "SQ_WAVE_CYCLES" and "INSTS" not in c else ""
         print(f"   {c:28s} {avg[c]:16.0f}{extra}")
     if "SQ_VALU_MFMA_BUSY_CYCLES" in avg and "GRBM_GUI_ACTIVE" in avg:
-        print(f"   MFMA busy fraction (busy / (GUI_ACTIVE*4 SIMD*256 CU)): "
-              f"{avg['SQ_VALU_MFMA_BUSY_CYCLES'] / (avg['GRBM_GUI_ACTIVE'] * 1024):.3f}")
+        # GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md, DVFS give-back): /8 = GPU cycles
+        cyc = avg["GRBM_GUI_ACTIVE"] / 8
+        print(f"   GPU cycles (GUI_ACTIVE / 8): {cyc:.0f}; MFMA busy fraction (busy / (cycles * 1024 SIMDs)): "
+              f"{avg['SQ_VALU_MFMA_BUSY_CYCLES'] / (cyc * 1024):.3f}")
