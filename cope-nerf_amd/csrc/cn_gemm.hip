@@ -83,6 +83,9 @@ struct LinearArgs {
 #ifndef EPI_EXP
 #define EPI_EXP 0  // benchmark-only: 1 = epilogue without its global stores (tools/ab_libs.sh)
 #endif
+#ifndef LIN_SEG
+#define LIN_SEG 1  // pinned MFMA / staging segments on the 256x256 bf16x6 tile (see kSeg)
+#endif
 #ifndef LSTORE_ALWAYS
 #define LSTORE_ALWAYS 0  // 1: branch-free staging (measured: main loop -1.5 %, epilogue variants +2-3 %)
 #endif
@@ -209,11 +212,13 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             rb[set][q] = bload4(rB, voB[q], MODE == 2 ? 0 : k0 * ESZB);
         }
     };
-    auto lstore = [&](int set, int buf) {
+    // piece < 0: the whole stage; piece q < ALD: A row q only; piece ALD: B only
+    auto lstore = [&](int set, int buf, int piece = -1) {
         float* a = sA + buf * BM * LS + lds_a;
         float* b = sB + buf * BN * LS + lds_b;
 #pragma unroll
         for (int q = 0; q < ALD; ++q) {
+            if (piece >= 0 && piece != q) continue;
             if constexpr (MODE == 2) {
                 bf16x4 x0, x1, x2;
 #if X6_EXP == 1
@@ -231,6 +236,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         }
 #pragma unroll
         for (int q = 0; q < BLD; ++q) {
+            if (piece >= 0 && piece != ALD) continue;
             if constexpr (MODE == 2) {
                 const int idx = tid + q * NT;
                 if (BN * KCB % NT == 0 || idx < BN * KCB)  // wave-uniform (NT, BN*KCB multiples of 64)
@@ -256,6 +262,9 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         return ntiles;
     };
 
+    // pinned compute/staging segments: the 256x256 bf16x6 tile (one workgroup per CU, so no
+    // partner workgroup's MFMAs cover a trailing staging block; LIN_SEG=0: compiler's order)
+    constexpr bool kSeg = LIN_SEG && MODE == 2 && TM * TN >= 8 && TN > ALD && DEPTH == 2 && OCC == 1 && BK == 16;
     const int arow = wm * TM * 32 + (lane & 31);
     const int brow = wn * TN * 32 + (lane & 31);
     const int kofs = (BK / 2) * (lane >> 5);
@@ -331,7 +340,10 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
-        auto compute = [&](int cur) {
+        // side(j) runs after column block j's MFMAs of the 64x128 wave tiles (kSeg: each
+        // block a segment pinned by sched_barrier, so the next stage's split and LDS writes
+        // handed to side() interleave with that block's MFMAs instead of trailing all of them)
+        auto compute = [&](int cur, auto side) {
             if constexpr (MODE == 2) {
                 const float* a_base = sA + cur * BM * LS + arow * LS + 4 * (lane >> 5);
                 const float* b_base = sB + cur * BN * LS + brow * LS + 4 * (lane >> 5);
@@ -360,6 +372,10 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                                 for (int i = 0; i < TM; ++i)
                                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[TA[u]][i], bj[TB[u]], acc[i][j],
                                                                                          0, 0, 0);
+                            if (ks == BK / 16 - 1) {
+                                side(j);
+                                if constexpr (kSeg) __builtin_amdgcn_sched_barrier(0);
+                            }
                         }
                     }
                     return;
@@ -447,7 +463,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 // chunk kc+1 of this tile, or the next tile's first chunk (consumed after the epilogue)
                 const bool more = kc + 1 < nk;
                 gload(0, more ? kc + 1 : 0, more ? m0 : m_next, more ? n0 : n_next, more || has_next);
-                compute(cur);
+                compute(cur, [](int) {});
                 if (LSTORE_ALWAYS || more) lstore(0, cur ^ 1);
                 __syncthreads();
             }
@@ -464,7 +480,18 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                     // past this tile: chunk cn - nk of the next one, issued before this tile's
                     // epilogue stores, so the next tile's first DEPTH stagings never wait for them
                     gload(j, here ? cn : cn - nk, here ? m0 : m_next, here ? n0 : n_next, here || has_next);
-                    compute(j & 1);
+                    if constexpr (kSeg) {
+                        // the next stage's staging (unconditional: after a tile's last chunk it
+                        // stages the next tile's first chunk, or zeros, into the free buffer,
+                        // which the epilogue parks over and the next tile stages again), one
+                        // piece per column block
+                        compute(j & 1, [&](int jj) {
+                            if (jj <= ALD) lstore((j + 1) % DEPTH, (j + 1) & 1, jj);
+                        });
+                        __syncthreads();
+                        continue;
+                    }
+                    compute(j & 1, [](int) {});
                     // unconditional (branch-free: compute and the next stage's staging share a
                     // basic block, so the scheduler can interleave the split VALU / LDS writes
                     // with the MFMAs).  After the last chunk this stages the next tile's first

@@ -512,13 +512,19 @@ __global__ void __launch_bounds__(512, 2) wgrad_x6r_kernel(WgradArgs p) {
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 1, wn = wave & 1;
-    const int slice = blockIdx.x;
+    // XCD-aware: the T output tiles of one M-slice (K or N > 256) are 8 blocks apart
+    const int T = p.n_tiles_n * p.n_tiles_k;
+    const int b = blockIdx.x;
+    const int tile = (b >> 3) % T;
+    const int slice = (b & 7) + 8 * ((b >> 3) / T);
     if (slice >= p.nslices) return;
+    const int n0 = (tile / p.n_tiles_k) * BNo;
+    const int k0 = (tile % p.n_tiles_k) * BNo;
     const int mbeg = slice * p.rows_per_slice;
     const int mend = min(p.M, mbeg + p.rows_per_slice);
     const int nch = mend > mbeg ? cdiv(mend - mbeg, MC) : 0;
     const int total = nch * p.npairs;
-    const bool do_bias = p.bpart != nullptr;
+    const bool do_bias = k0 == 0 && p.bpart != nullptr;
 
     const bool sx = wave >= 4;  // wave-uniform: this wave stages X
     const int t = tid & 255, mq = t & 3, cg = t >> 2;
@@ -537,7 +543,8 @@ __global__ void __launch_bounds__(512, 2) wgrad_x6r_kernel(WgradArgs p) {
 #else
         const int mr = mrow;
 #endif
-        const rsrc_t v = make_view(src + (int64_t)mr * ld, nrows * ld * 4);
+        const int col0 = sx ? k0 : n0;
+        const rsrc_t v = make_view(src + (int64_t)mr * ld + col0, (nrows * ld - col0) * 4);
 #pragma unroll
         for (int r = 0; r < 4; ++r) r4[r] = bload4(v, ((mq * 4 + r) * ld + cg * 4) * 4, 0);
     };
@@ -630,8 +637,8 @@ __global__ void __launch_bounds__(512, 2) wgrad_x6r_kernel(WgradArgs p) {
     for (int i = 0; i < 2; ++i) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int col = wn * 128 + j * 32 + (lane & 31);
-            const int rbase = wm * 64 + i * 32 + 4 * (lane >> 5);
+            const int col = k0 + wn * 128 + j * 32 + (lane & 31);
+            const int rbase = n0 + wm * 64 + i * 32 + 4 * (lane >> 5);
             const int vo = (rbase * p.Kpad + col) * 4;
 #pragma unroll
             for (int r = 0; r < 16; ++r) bstore1(vP, vo, ((r & 3) + 8 * (r >> 2)) * p.Kpad * 4, acc[i][j][r]);
@@ -646,7 +653,7 @@ __global__ void __launch_bounds__(512, 2) wgrad_x6r_kernel(WgradArgs p) {
         __syncthreads();
         if (tid < BNo) {
             const float tot = ((red[tid] + red[BNo + tid]) + red[2 * BNo + tid]) + red[3 * BNo + tid];
-            p.bpart[(int64_t)slice * p.Npad + tid] = tot;
+            p.bpart[(int64_t)slice * p.Npad + n0 + tid] = tot;
         }
     }
 }
