@@ -129,18 +129,29 @@ def cpu_baseline(rays=1024, steps=5):
                       f"(min {min(times):.2f} s, max {max(times):.2f} s per step)"}
 
 
+C3_TRAIN = dict(sdf_consistency_enable_pose_grad=True, rgb_weight=0.33333, end_sdf_weight_increase_iteration=-1)
 CONFIGS = {
     # name: (rays per GPU, trainer kwargs, workload text)
     "c2": (4096, {"mfma_dtype": "bf16x6"},
            "C2: synthetic scene, 4096 rays x 128 samples (64 coarse + 4x16 importance) per GPU, fp32, "
            "fixed poses, full train step (fwd + losses + bwd + Adam)"),
     "c2fp32": (4096, {"mfma_dtype": "fp32"}, "C2 with the exact-product fp32 MFMA GEMMs"),
-    "c3": (4096, {"joint_pose": True, "stage1": True, "mfma_dtype": "bf16", "start_it": 30000},
-           "C3-style: synthetic 10-frame scene, 4096 rays x 128 samples per GPU, bf16 MLP MFMA (fp32 accumulate), "
-           "joint pose optimisation (learnable SE(3) poses -> ray gradients) + the stage-1 losses (scene-flow SDF "
-           "loss, flow-RGB warp to the 3 next frames, SDF consistency at the world camera)"),
-    "c3fp32": (4096, {"joint_pose": True, "stage1": True, "mfma_dtype": "bf16x6", "start_it": 30000},
-               "C3-style as c3 with fp32 GEMMs (bf16x6)"),
+    # C3 = Co3D/skateboard.yaml's pose optimisation: stage 1 (epochs < start_query_world_epoch),
+    # where the camera motion is learned as the MotionNetwork jointly with the fields through the
+    # scene-flow SDF loss, the flow-RGB warp and the SDF consistency at the world camera
+    # (train.py:467-517); skateboard's options: sdf_consistency_enable_pose_grad, rgb_weight
+    # 0.33333, a fixed sdf_weight (end_sdf_weight_increase_iteration -1)
+    "c3": (4096, {"stage1": True, "mfma_dtype": "bf16", "start_it": 30000, "train_cfg": dict(C3_TRAIN)},
+           "C3: Co3D/skateboard stage 1 on a synthetic 10-frame scene, 4096 rays x 128 samples per GPU, bf16 MLP "
+           "MFMA (fp32 accumulate): MotionNetwork pose optimisation through the scene-flow SDF loss, flow-RGB warp "
+           "to the 3 next frames and SDF consistency at the world camera with pose gradient"),
+    "c3fp32": (4096, {"stage1": True, "mfma_dtype": "bf16x6", "start_it": 30000, "train_cfg": dict(C3_TRAIN)},
+               "C3 as c3 with fp32 GEMMs (bf16x6)"),
+    # stage 2 with pose refinement: rays from learnable SE(3) poses (PoseRetriever) in canonical
+    # space, ray gradients into r, t (train.py:425-431; freeze_camera_pose_period finite)
+    "c3pose": (4096, {"joint_pose": True, "mfma_dtype": "bf16x6", "start_it": 30000},
+               "stage 2 with pose refinement: synthetic 10-frame scene, 4096 rays x 128 samples per GPU, fp32 "
+               "(bf16x6), query in canonical space with learnable SE(3) camera poses (ray gradients)"),
     "infer": (518400, {"infer": True, "mfma_dtype": "bf16x6"},
               "inference: full 540x960 image (518,400 rays x 128 samples, eval mode, no jitter), forward only "
               "(sampler + SDF + ∇SDF + colour + compositing), 65,536-ray chunks, fp32"),
@@ -248,7 +259,9 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16 MFMA operands, fp32 accumulate/activations" if mode == "bf16" else "fp32",
         "data": "synthetic (10 random 540x960 frames cycled one per step, 4x4 patches, " +
-                ("learnable SE(3) poses" if kw.get("joint_pose") else "fixed identity pose") +
+                ("learnable SE(3) poses" if kw.get("joint_pose") else
+                 "identity camera, camera motion learned by the MotionNetwork (stage 1)" if kw.get("stage1") else
+                 "fixed identity pose") +
                 ", geometric-init SDF, seed 678)",
         "config": {"workload": workload, "gemm": MODE_TEXT[mode], "rays_per_gpu": rays, "samples_per_ray": S,
                    "global_rays": rays * world, "hip_graph": graph,

@@ -59,7 +59,28 @@ TRAIN_CFG = dict(learning_rate=1e-3, pose_learning_rate=5e-4, rgb_weight=1.0, ei
                  edge_aware_smoothness_weight=(1.0, 0.0), smoothness_weight=(1e-4, 0.0), nb_warm_up_it=5000,
                  nb_sample_timestep=10, end_sdf_weight_increase_iteration=100000,
                  end_consistency_weight_increase_iteration=100000, patch_size=4, world_idx="mid",
-                 random_ref_interval=(1, 2, 3), neus_anneal_end=50000, s=1)
+                 random_ref_interval=(1, 2, 3), neus_anneal_end=50000, s=1,
+                 sdf_consistency_enable_pose_grad=False)
+PAIR_WEIGHTS = ("sdf_weight", "flow_rgb_weight", "sdf_consistency_weight", "edge_aware_smoothness_weight",
+                "smoothness_weight")
+
+
+def normalise_train_cfg(cfg):
+    """Accept the reference's cfg['training'] as it is (default.yaml:40-46 stores every loss
+    weight as a [start, end] pair): rgb / eikonal weights use their first entry
+    (training.py:37-38 reads cfg[...][0]); the annealed weights are pairs (a scalar w
+    becomes (w, w))."""
+    out = dict(cfg)
+    for k in ("rgb_weight", "eikonal_weight"):
+        if isinstance(out[k], (list, tuple)):
+            out[k] = out[k][0]
+    for k in PAIR_WEIGHTS:
+        if not isinstance(out[k], (list, tuple)):
+            out[k] = (out[k], out[k])
+    out["random_ref_interval"] = tuple(int(j) for j in out["random_ref_interval"])
+    if not out["random_ref_interval"] or min(out["random_ref_interval"]) < 1:
+        raise ValueError(f"random_ref_interval must be positive frame offsets (got {out['random_ref_interval']})")
+    return out
 
 
 def flat_allreduce_mean(params, group=None):
@@ -156,7 +177,7 @@ class SyntheticTrainer:
         self.device = torch.device(device)
         self.R, self.H, self.W, self.patch = rays, H, W, patch
         self.depth_range = depth_range
-        self.cfg = dict(TRAIN_CFG, **(train_cfg or {}))
+        self.cfg = normalise_train_cfg(dict(TRAIN_CFG, **(train_cfg or {})))
         self.distributed = distributed
         self.group = (group if group is not None else dist.group.WORLD) if distributed else None
         self.rank = dist.get_rank(self.group) if distributed else 0
@@ -297,26 +318,31 @@ class SyntheticTrainer:
         sdf_loss = scene_flow_loss(out["sampled_points"], out["normals"], out["sdf_flows"], out["weights"], omega,
                                    vel, group=grp)
         K = P.shape[0]
-        # flow-RGB: w2c_j = P[i+j-1] @ ... @ P[i] for the reference frames j = 1..3
+        # flow-RGB: reference frame i + j maps through w2c_j = P[i+j-1] @ ... @ P[i]
+        # (compute_w2c_mappings(c2c)[ref - i], train.py:483): the running product up to the
+        # largest interval, taken at each interval (any random_ref_interval, e.g. [1, 5, 10])
         js = self.ref_intervals
         ref = img + js                                    # [T]
         valid = (ref <= n - 1)                            # next_time_step <= 1 (train.py:421)
-        w2c, cur = [], self.I
-        for j in range(js.numel()):
-            k = torch.clamp(img + j, max=K - 1)
+        chain, cur = [], self.I
+        for d in range(max(self.cfg["random_ref_interval"])):
+            k = torch.clamp(img + d, max=K - 1)           # past the last frame: masked by `valid`
             cur = P.index_select(0, k)[0] @ cur
-            w2c.append(cur)
-        w2c = torch.stack(w2c)
+            chain.append(cur)
+        w2c = torch.stack([chain[j - 1] for j in self.cfg["random_ref_interval"]])
         refc = torch.clamp(ref, max=n - 1)
         flows = project_flow(out["sampled_points"], out["weights"], w2c, self.camera_mats.index_select(0, refc),
                              self.I, batch["pixn"], (self.H, self.W))
         per = flow_rgb_loss(flows, batch["pix"], self.images.index_select(0, refc), batch["rgb_gt"], group=grp)
         flow_rgb = torch.where(valid, per, torch.zeros_like(per)).sum() / 3.0
-        # SDF consistency at the world frame (sdf_consistency_enable_pose_grad False: no pose gradient)
+        # SDF consistency at the world frame (train.py:495-505): with
+        # sdf_consistency_enable_pose_grad (most dataset configs, e.g. Co3D/skateboard.yaml:27)
+        # the loss reaches the motion network through c2c, i.e. through the SDF's input
+        # gradient at the world points; default.yaml:62 detaches the chain
         w = self.world_cam_idx
-        with torch.no_grad():
+        with torch.set_grad_enabled(bool(self.cfg["sdf_consistency_enable_pose_grad"]) and torch.is_grad_enabled()):
             lo, hi = torch.clamp(img, max=w), torch.clamp(img, min=w)
-            c2c = masked_chain(P.detach(), lo, hi)
+            c2c = masked_chain(P, lo, hi)
             cw2 = torch.where(img.view(1, 1) >= w, inv4x4(c2c), c2c)
             pw = affine_points(out["sampled_points"].detach().reshape(-1, 3), cw2)
             x = torch.cat([pw, torch.full_like(pw[:, :1], self.world_time_step)], 1)
@@ -341,6 +367,9 @@ class SyntheticTrainer:
             l_sdf, l_flow, l_cons = self.stage1_terms(out, batch)
             w = self.sched.stage1_w
             loss = loss + w[0] * l_sdf + w[1] * l_flow + w[2] * l_cons
+            # cn_train_loss flags its own terms; the stage-1 terms are added here (device op,
+            # no host sync, capturable; training.py:532 asserts on the total)
+            self.nonfinite.bitwise_or_((~torch.isfinite(loss)).to(torch.int32).view(1))
         self.opt.zero_grad(set_to_none=True)
         loss.backward()
         if self.distributed:

@@ -343,11 +343,12 @@ def relative_camera_pose(motion, lo, hi, n_images, nb_sample_timestep):
 
 def stage1_losses(out, motion, sdf_fn, *, image_idx, n_images, world_cam_idx, nb_sample_timestep, rgb_gt,
                   sampled_pixel, normalized_pixel, camera_mats, ref_images, scale_mat, img_hw,
-                  ref_intervals=(1, 2, 3)):
+                  ref_intervals=(1, 2, 3), consistency_pose_grad=False):
     """(sdf_loss, flow_rgb_loss, sdf_consistency_loss) of one stage-1 iteration,
     train.py:467-517 (query_in_canonical_space False).  motion(t [N,1]) -> (ω, v);
     sdf_fn(x [M,4]) -> sdf [M,1]; camera_mats [n_images, 4, 4]; ref_images
-    [n_images, 3, H, W]; ref frames image_idx + ref_intervals (dataset.py:231-250)."""
+    [n_images, 3, H, W]; ref frames image_idx + ref_intervals (dataset.py:231-250);
+    consistency_pose_grad: cfg['training']['sdf_consistency_enable_pose_grad'] (train.py:498)."""
     R = rgb_gt.shape[0]
     pts = out["sampled_points"].reshape(-1, 3)
     normals = out["normals"].reshape(-1, 3)
@@ -380,7 +381,7 @@ def stage1_losses(out, motion, sdf_fn, *, image_idx, n_images, world_cam_idx, nb
         f = torch.stack([f[:, 0] * (img_hw[1] / 2), f[:, 1] * (img_hw[0] / 2)], -1)
         flows.append(f)
     if image_idx != world_cam_idx:
-        with torch.no_grad():  # sdf_consistency_enable_pose_grad: False (default.yaml:62)
+        with torch.set_grad_enabled(consistency_pose_grad):  # train.py:498 (default.yaml:62: False)
             lo, hi = min(world_cam_idx, image_idx), max(world_cam_idx, image_idx)
             c2c = relative_camera_pose(motion, lo, hi, n_images, nb_sample_timestep)[-1]
             cw2 = torch.inverse(c2c) if world_cam_idx <= image_idx else c2c

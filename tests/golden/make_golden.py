@@ -403,6 +403,137 @@ def trainer_case():
     print("wrote trainer")
 
 
+def load_reference_stage1_block():
+    """The stage-1 loss block of the reference's training loop (train.py:467-517: the
+    `if not self.query_in_canonical_space:` statement inside Trainer.train) and
+    Trainer.warp_pixel (train.py:235-244), parsed from train.py's own source text and
+    compiled unmodified: train.py cannot be imported here (tensorboardX, dataloading,
+    cv2 are absent).  The block runs as the body of a function whose locals are the
+    training loop's variables it reads; the stub `self` carries the attributes it uses.
+    `pts_map` is one of them: a frame without a valid reference frame (the last one) never
+    assigns it in the block, and train.py:504 then takes only its shape from the previous
+    iteration's value (a loop local of Trainer.train); the first iteration on such a frame
+    would raise UnboundLocalError."""
+    import ast
+    src = open(os.path.join(REF, "train.py")).read()
+    tree = ast.parse(src)
+    cls = next(n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == "Trainer")
+    warp = next(f for f in cls.body if isinstance(f, ast.FunctionDef) and f.name == "warp_pixel")
+    train_fn = next(f for f in cls.body if isinstance(f, ast.FunctionDef) and f.name == "train")
+    block = next(n for n in ast.walk(train_fn) if isinstance(n, ast.If) and isinstance(n.test, ast.UnaryOp)
+                 and isinstance(n.test.op, ast.Not) and ast.unparse(n.test.operand) == "self.query_in_canonical_space")
+    names = ["self", "render_out", "query_time_step", "image_idx", "ref_image_idx_list", "nb_valid_next_time_step",
+             "ref_camera_mat_list", "scale_mat", "normalized_sampled_pixel", "img", "rgb_pred", "sampled_pixel",
+             "rgb_gt", "ref_image_list", "sdf", "flow_loss", "flow_rgb_loss", "sdf_consistency_loss", "sdf_loss",
+             "pts_map"]
+    ret = ast.parse("return sdf_loss, flow_rgb_loss, sdf_consistency_loss").body
+    fn = ast.FunctionDef(name="stage1_block", args=ast.arguments(
+        posonlyargs=[], args=[ast.arg(arg=n) for n in names], kwonlyargs=[], kw_defaults=[], defaults=[]),
+        body=[block] + ret, decorator_list=[], returns=None, type_params=[])
+    mod = ast.fix_missing_locations(ast.Module(body=[warp, fn], type_ignores=[]))
+    ns = {"torch": torch, "np": np}
+    exec(compile(mod, os.path.join(REF, "train.py"), "exec"), ns)
+    return ns["warp_pixel"], ns["stage1_block"]
+
+
+STAGE1_CASES = (  # (tag, image_idx, random_ref_interval, sdf_consistency_enable_pose_grad)
+    ("before", 2, (1, 2, 3), False), ("world", 4, (1, 2, 3), False), ("after", 6, (1, 2, 3), False),
+    ("last", 7, (1, 2, 3), False), ("iv1510", 2, (1, 5, 10), False), ("posegrad_before", 2, (1, 2, 3), True),
+    ("posegrad_after", 6, (1, 5, 10), True))
+
+
+def stage1_case(fields):
+    """Rows a22 / (f)1 of SURVEY.md §8: sdf_loss, flow_rgb_loss and sdf_consistency_loss
+    of one stage-1 iteration, and their gradients, from the reference's own code
+    (load_reference_stage1_block) for frames before / at / after the world camera (n = 8,
+    world 4) and the last frame, ref intervals (1, 2, 3) and (1, 5, 10), with and without
+    sdf_consistency_enable_pose_grad.  The renderer outputs the block reads are inputs
+    here (rays through 4x4-patch pixels of a 24x32 frame, points at depth 0.8..1.6, random
+    weights / normals / sdf flows; the renderer itself is pinned by the render_* fixtures):
+    gradients are taken with respect to them, the motion network and the SDF network."""
+    warp_pixel, block = load_reference_stage1_block()
+    import types as _t
+    n_images, world, H, W, R, S = 8, 4, 24, 32, 32, 8
+    rec = {"n_images": np.int32(n_images), "world": np.int32(world), "H": np.int32(H), "W": np.int32(W)}
+    torch.manual_seed(681)
+    motion = fields.MotionNetwork(**MOTION_CFG)
+    with torch.no_grad():  # non-trivial velocities
+        g = torch.Generator().manual_seed(682)
+        for p in motion.parameters():
+            p.add_(0.05 * torch.randn(p.shape, generator=g))
+    torch.manual_seed(683)
+    sdf_net = fields.SDFNetwork(**dict(SDF_CFG, d_hidden=64))
+    for k, v in motion.state_dict().items():
+        rec["motion." + k] = v.detach()
+    for k, v in sdf_net.state_dict().items():
+        rec["sdfnet." + k] = v.detach()
+    g = torch.Generator().manual_seed(684)
+    fx = 0.9 * W
+    K = torch.tensor([[2 * fx / W, 0, 0, 0], [0, -2 * fx / H, 0, 0], [0, 0, -1, 0], [0, 0, 0, 1.0]])
+    frames = torch.rand(n_images, 3, H, W, generator=g) * 0.8 + 0.1
+    rec["K"], rec["frames"] = K, frames
+    for tag, image, intervals, pose_grad in STAGE1_CASES:
+        # pixels of R/16 4x4 patches; rays through them from the origin (world_mat = I in stage 1)
+        corner = torch.stack([torch.randint(0, W - 4, (R // 16,), generator=g),
+                              torch.randint(0, H - 4, (R // 16,), generator=g)], -1)
+        off = torch.stack(torch.meshgrid(torch.arange(4), torch.arange(4), indexing="xy"), -1).reshape(16, 2)
+        pix = (corner[:, None, :] + off[None]).reshape(R, 2).float()
+        pixn = torch.stack([pix[:, 0] / (W - 1) * 2 - 1, pix[:, 1] / (H - 1) * 2 - 1], -1)
+        d = torch.stack([pixn[:, 0] / K[0, 0], pixn[:, 1] / K[1, 1], -torch.ones(R)], -1)
+        z = 0.8 + 0.8 * torch.rand(R, S, generator=g)
+        pts = (d[:, None, :] * z[..., None]).reshape(R, S, 3)
+        wts = torch.rand(R, S, generator=g)
+        wts = wts / wts.sum(-1, keepdim=True) * 0.9
+        leaves = {"sampled_points": pts, "weights": wts,
+                  "normals": torch.nn.functional.normalize(torch.randn(R * S, 3, generator=g), dim=-1),
+                  "sdf_flows": 0.1 * torch.randn(R * S, 1, generator=g),
+                  "sdf": 0.05 * torch.randn(R * S, 1, generator=g)}
+        leaves = {k: v.clone().requires_grad_(k != "sampled_points") for k, v in leaves.items()}
+        render_out = dict(leaves)
+        refs = [image + j for j in intervals]
+        ref_imgs = [torch.ones(1, 3, H, W) * 10e5 if r >= n_images else frames[r][None] for r in refs]  # dataset.py:243
+        ref_K = [torch.ones(1, 4, 4) * 10e5 if r >= n_images else K[None] for r in refs]               # dataset.py:289
+        ref_idx = torch.tensor(refs)
+        nxt = ref_idx / (n_images - 1) * 2 - 1
+        nb_valid = len(nxt[nxt <= 1.0])
+        t = image / (n_images - 1) * 2 - 1
+        cfg = {"training": {"flow_rgb_weight": [7.5, 7.5], "sdf_consistency_weight": [0.0, 1.0],
+                            "sdf_consistency_enable_pose_grad": pose_grad}}
+        self_ = _t.SimpleNamespace(device=torch.device("cpu"), motion_network=motion, cfg=cfg, total_nb_images=n_images,
+                                   query_in_canonical_space=False,
+                                   nb_sample_timestep=10, world_cam_idx=world, sdf_network=sdf_net,
+                                   world_time_step=world / (n_images - 1) * 2 - 1)
+        self_.warp_pixel = lambda src_frame, uv, normalize_pix=True, _s=self_: warp_pixel(_s, src_frame, uv, normalize_pix)
+        zero = lambda: torch.tensor(0.0)  # noqa: E731
+        rgb_gt = torch.rand(R, 3, generator=g)
+        l_sdf, l_flow, l_cons = block(self_, render_out, torch.tensor([t]).float(), torch.tensor([image]), ref_idx,
+                                      nb_valid, torch.cat(ref_K), torch.eye(4)[None], pixn, torch.zeros(1, 3, H, W),
+                                      torch.zeros(R, 3), pix, rgb_gt, torch.cat(ref_imgs), leaves["sdf"], zero(), zero(),
+                                      zero(), zero(), torch.zeros(R * S, 3))
+        total = 0.1 * l_sdf + 7.5 * l_flow + 0.3 * l_cons
+        wrt = ([("out." + k, v) for k, v in leaves.items() if v.requires_grad] +
+               [("motion." + k, p) for k, p in motion.named_parameters()] +
+               [("sdfnet." + k, p) for k, p in sdf_net.named_parameters()])
+        grads = torch.autograd.grad(total, [v for _, v in wrt], allow_unused=True)
+        c = f"{tag}."
+        rec.update({c + "image": np.int32(image), c + "intervals": np.array(intervals, np.int32),
+                    c + "pose_grad": np.int32(pose_grad), c + "pix": pix, c + "pixn": pixn, c + "rgb_gt": rgb_gt,
+                    c + "sdf_loss": l_sdf.detach(), c + "flow_rgb_loss": l_flow.detach(),
+                    c + "sdf_consistency_loss": torch.as_tensor(l_cons).detach()})
+        for k, v in leaves.items():
+            rec[c + "in." + k] = v.detach()
+        gen = torch.Generator().manual_seed(685)
+        for (k, _), gr in zip(wrt, grads):
+            if gr is None:
+                rec["grad." + c + k] = torch.zeros(0)
+            else:  # large motion-network gradients: 256 sampled entries + norm + sum
+                put_grad(rec, c + k, gr, k.startswith("out."), gen)
+        print(f"stage1 {tag}: sdf {l_sdf.item():.6f} flow {l_flow.item():.6f} cons {float(l_cons):.6f}")
+    np.savez_compressed(os.path.join(OUT, "stage1.npz"),
+                        **{k: (v.detach().numpy() if torch.is_tensor(v) else v) for k, v in rec.items()})
+    print("wrote stage1")
+
+
 def main():
     fields, rend = load_reference()
     motion_case(fields)
@@ -416,6 +547,7 @@ def main():
                 car=0.5, full_grads=False)
     seams_case(fields, rend)
     pretrained_case(fields, rend)
+    stage1_case(fields)
 
 
 def main_motion_only():
@@ -432,6 +564,8 @@ def main_pretrained_only():
 if __name__ == "__main__":
     if "--trainer-only" in sys.argv:
         trainer_case()
+    elif "--stage1-only" in sys.argv:
+        stage1_case(load_reference()[0])
     elif "--motion-only" in sys.argv:
         main_motion_only()
     elif "--pretrained-only" in sys.argv:

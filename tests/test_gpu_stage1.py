@@ -1,14 +1,24 @@
-"""The training step of copenerf.train_step.SyntheticTrainer -- joint pose
-(learnable SE(3) poses, train.py:425-431) and the stage-1 motion losses
-(scene-flow SDF loss, flow-RGB warp to the next frames, SDF consistency at the
-world camera; train.py:467-517) -- against the CPU oracle's restatement
-(oracle.stage1_losses, which integrates the motion network per interval as
-neus_fields.py:142-186 does) on identical sample positions, for frames before,
-at and after the world camera and for the last frame (no valid reference
-frame).  Gradients of the poses, the motion network and the fields are
-compared in every GEMM mode: fp32 and bf16x6 at 2e-3 of the gradient scale
-(fields) and 5e-3 (poses / motion), bf16 (config C3, reduced precision) at its
-own bar."""
+"""The training step of copenerf.train_step.SyntheticTrainer against the CPU oracle's
+restatement (oracle.stage1_losses is pinned to the reference's own stage-1 block by
+tests/test_stage1_golden.py) on identical sample positions, in three workloads:
+  stage1     the MotionNetwork losses of train.py:467-517 (scene-flow SDF loss, flow-RGB
+             warp, SDF consistency at the world camera) with the Co3D configs' options:
+             sdf_consistency_enable_pose_grad (the consistency term reaches the motion
+             network) and random_ref_interval [1, 5, 10];
+  canonical  query in canonical space with learnable SE(3) poses (train.py:425-431,
+             config C3's joint pose optimisation: ray gradients into r, t);
+  hybrid     both at once (not a reference workload: the reference applies the stage-1
+             losses only outside canonical space; kept as the widest coverage of the
+             backward: pose, motion and field gradients in one step);
+for frames before, at and after the world camera and the last frame (no valid reference
+frame).  Gradients of the poses, the motion network and the fields are compared in every
+GEMM mode: fp32 and bf16x6 at 2e-3 of the gradient scale (fields) and 5e-3 (poses /
+motion); bf16 (config C3, operands rounded to 8 bits) as the relative L2 error of each
+gradient tensor at about twice the error measured on the GPU (COPENERF_PARITY_LOG
+collects the measured values)."""
+import json
+import os
+
 import pytest
 import torch
 
@@ -22,12 +32,20 @@ R, H, W = 128, 48, 64
 # (loss rel., fields, poses / motion): fp32 modes: max |Δ| over the gradient's max |g|;
 # bf16 (operands rounded to 8 bits): relative L2 error of each gradient tensor
 BARS = {"fp32": (1e-4, 2e-3, 5e-3), "bf16x6": (1e-4, 2e-3, 5e-3), "bf16": (2e-2, 2.5e-1, 2.5e-1)}
+SCEN = {"hybrid": (True, True, {}),
+        "stage1": (False, True, {"sdf_consistency_enable_pose_grad": True, "random_ref_interval": (1, 5, 10)}),
+        "canonical": (True, False, {})}
+CASES = ([("hybrid", i, m, R) for i in (2, 4, 6, 7) for m in ("fp32", "bf16x6", "bf16")] +
+         [("stage1", i, m, R) for i in (2, 6, 7) for m in ("bf16x6", "bf16")] +
+         [("canonical", i, m, R) for i in (2, 5) for m in ("bf16x6", "bf16")] +
+         [("canonical", 2, "bf16", 1024)])  # the shipped n_training_points (default.yaml)
 
 
-def _trainer(mode, start_it, joint_pose=True, stage1=True):
+def _trainer(mode, start_it, joint_pose=True, stage1=True, train_cfg=None, rays=R):
     from copenerf.train_step import SyntheticTrainer
-    tr = SyntheticTrainer(DEV, rays=R, H=H, W=W, seed=11, joint_pose=joint_pose, stage1=stage1, n_images=N_IMAGES,
-                          start_it=start_it, schedule="reference", mfma_dtype=mode, depth_range=(0.01, 3.0))
+    tr = SyntheticTrainer(DEV, rays=rays, H=H, W=W, seed=11, joint_pose=joint_pose, stage1=stage1, n_images=N_IMAGES,
+                          start_it=start_it, schedule="reference", mfma_dtype=mode, depth_range=(0.01, 3.0),
+                          train_cfg=train_cfg)
     tr.images = smooth_frames(N_IMAGES, H, W, DEV)  # see smooth_frames: a well-conditioned flow-RGB gradient
     return tr
 
@@ -38,41 +56,45 @@ def _cpu_copy(mod, cls_args):
     return m
 
 
-def _close(got, ref, name, rtol, l2=False):
+def _err(got, ref, name, l2=False):
     assert got is not None, name
     got = got.detach().cpu()
     if l2:
-        err, scale = (got - ref).norm().item(), ref.norm().item() + 1e-12
-    else:
-        err, scale = (got - ref).abs().max().item(), ref.abs().max().item() + 1e-12
-    assert err <= rtol * scale, (name, err, scale)
+        return (got - ref).norm().item() / (ref.norm().item() + 1e-12)
+    return (got - ref).abs().max().item() / (ref.abs().max().item() + 1e-12)
 
 
-@pytest.mark.parametrize("mode", ["fp32", "bf16x6", "bf16"])
-@pytest.mark.parametrize("image", [2, 4, 6, 7])
-def test_training_step_matches_oracle(image, mode):
-    from copenerf.motion import MotionNetwork
+@pytest.mark.parametrize("scenario,image,mode,rays", CASES)
+def test_training_step_matches_oracle(scenario, image, mode, rays):
     from copenerf.rays import PoseRetriever, world_rays
     from copenerf.train_step import MOTION_CFG
+    joint_pose, stage1, tcfg = SCEN[scenario]
     # iteration it uses frame (it - 1) % n; it ~ 30000: cos_anneal_ratio 0.6, consistency weight 0.3
     start = 30000 + (image - 30000 % N_IMAGES) % N_IMAGES
-    tr = _trainer(mode, start)
+    tr = _trainer(mode, start, joint_pose, stage1, tcfg, rays)
     tr.begin_iteration()
     it, img = tr.it, tr.image_index(tr.it)
     assert img == image
     batch = tr.make_batch()
     # ---- oracle (CPU) on the same pixels, poses, weights and sample positions
     P, Pc, var, leaves = oracle_params(tr.sdf, tr.col, tr.var)
-    motion_c = _cpu_copy(tr.motion, MOTION_CFG)
-    poses_c = PoseRetriever(N_IMAGES)
-    poses_c.load_state_dict({k: v.detach().cpu() for k, v in tr.poses.state_dict().items()})
     pixn, pix = batch["pixn"].cpu(), batch["pix"].cpu()
     K = tr.K.cpu()
-    world_mat = torch.eye(4) if img == tr.world_cam_idx else poses_c(img)
+    pose_leaves, motion_c = [], None
+    world_mat = torch.eye(4)
+    if joint_pose:
+        poses_c = PoseRetriever(N_IMAGES)
+        poses_c.load_state_dict({k: v.detach().cpu() for k, v in tr.poses.state_dict().items()})
+        pose_leaves = [poses_c.r, poses_c.t]
+        if img != tr.world_cam_idx:
+            world_mat = poses_c(img)
+    if stage1:
+        motion_c = _cpu_copy(tr.motion, MOTION_CFG)
     o, d, n = world_rays(pixn, K, world_mat, torch.eye(4))
-    t = torch.tensor([img / (N_IMAGES - 1) * 2 - 1])
-    near, far = torch.full((R, 1), 0.01), torch.full((R, 1), 3.0)
-    t_rand = torch.rand(R, 64, generator=torch.Generator().manual_seed(img))
+    # train.py:440: the frame's time in stage 1, the world camera's time in canonical space
+    t = torch.tensor([(img if stage1 else tr.world_cam_idx) / (N_IMAGES - 1) * 2 - 1])
+    near, far = torch.full((rays, 1), 0.01), torch.full((rays, 1), 3.0)
+    t_rand = torch.rand(rays, 64, generator=torch.Generator().manual_seed(img))
     torch.set_num_threads(8)
     z = O.hierarchical_z(P, o.detach(), d.detach(), t, near, far, 64, 64, 4, t_rand)
     v = tr.sched.values(it, img)
@@ -81,34 +103,49 @@ def test_training_step_matches_oracle(image, mode):
     rgb_gt = batch["rgb_gt"].cpu()
     lw, sw = v["loss_w"], v["stage1_w"]
     loss_ref = O.train_loss(ref, rgb_gt, w_rgb=lw[0], w_eik=lw[1], w_edge=lw[2], w_smooth=lw[3])
-    l_sdf, l_flow, l_cons = O.stage1_losses(
-        ref, motion_c, lambda x: O.sdf_mlp(P, x)[:, :1], image_idx=img, n_images=N_IMAGES,
-        world_cam_idx=tr.world_cam_idx, nb_sample_timestep=10, rgb_gt=rgb_gt, sampled_pixel=pix,
-        normalized_pixel=pixn, camera_mats=tr.camera_mats.cpu(), ref_images=tr.images.cpu(), scale_mat=torch.eye(4)[None],
-        img_hw=(H, W))
-    loss_ref = loss_ref + sw[0] * l_sdf + sw[1] * l_flow + sw[2] * l_cons
-    pose_leaves = [poses_c.r, poses_c.t]
-    ref_leaves = pose_leaves + list(motion_c.parameters()) + list(leaves.values())
+    if stage1:
+        l_sdf, l_flow, l_cons = O.stage1_losses(
+            ref, motion_c, lambda x: O.sdf_mlp(P, x)[:, :1], image_idx=img, n_images=N_IMAGES,
+            world_cam_idx=tr.world_cam_idx, nb_sample_timestep=10, rgb_gt=rgb_gt, sampled_pixel=pix,
+            normalized_pixel=pixn, camera_mats=tr.camera_mats.cpu(), ref_images=tr.images.cpu(),
+            scale_mat=torch.eye(4)[None], img_hw=(H, W), ref_intervals=tr.cfg["random_ref_interval"],
+            consistency_pose_grad=tr.cfg["sdf_consistency_enable_pose_grad"])
+        loss_ref = loss_ref + sw[0] * l_sdf + sw[1] * l_flow + sw[2] * l_cons
+    motion_leaves = list(motion_c.parameters()) if stage1 else []
+    ref_leaves = pose_leaves + motion_leaves + list(leaves.values())
     gref = torch.autograd.grad(loss_ref, ref_leaves, allow_unused=True)
     # ---- HIP path: the trainer's own iteration with the oracle's sample positions
     loss = tr.iteration(batch, z_vals=z.to(DEV))
     l_bar, f_bar, pm_bar = BARS[mode]
     l2 = mode == "bf16"
-    assert abs(loss.item() - loss_ref.item()) <= l_bar * abs(loss_ref.item()) + 1e-6, (loss.item(), loss_ref.item())
-    if img != tr.world_cam_idx:  # the world camera's rays use the identity: no pose gradient
-        _close(tr.poses.r.grad[img], gref[0][img], "pose r", pm_bar, l2)
-        _close(tr.poses.t.grad[img], gref[1][img], "pose t", pm_bar, l2)
-    nm = len(list(motion_c.parameters()))
-    for (name, p), gr in zip(tr.motion.named_parameters(), gref[2:2 + nm]):
-        if gr is None:
-            assert p.grad is None or not p.grad.any(), name
-            continue
-        _close(p.grad, gr, "motion." + name, pm_bar, l2)
+    errs = {"loss": abs(loss.item() - loss_ref.item()) / abs(loss_ref.item())}
+    np_ = len(pose_leaves)
+    if joint_pose and img != tr.world_cam_idx:  # the world camera's rays use the identity: no pose gradient
+        errs["pose r"] = _err(tr.poses.r.grad[img], gref[0][img], "pose r", l2)
+        errs["pose t"] = _err(tr.poses.t.grad[img], gref[1][img], "pose t", l2)
+    if stage1:
+        for (name, p), gr in zip(tr.motion.named_parameters(), gref[np_:np_ + len(motion_leaves)]):
+            if gr is None:
+                assert p.grad is None or not p.grad.any(), name
+                continue
+            errs["motion." + name] = _err(p.grad, gr, "motion." + name, l2)
     keys = list(leaves)
     fields = ([("sdf." + k, p) for k, p in tr.sdf.named_parameters()] +
               [("col." + k, p) for k, p in tr.col.named_parameters()] + [("dev.variance", tr.var.variance)])
+    off = np_ + len(motion_leaves)
     for name, p in fields:
-        _close(p.grad, gref[2 + nm + keys.index(name)], name, f_bar, l2)
+        errs[name] = _err(p.grad, gref[off + keys.index(name)], name, l2)
+    worst_f = max(v for k, v in errs.items() if k.startswith(("sdf.", "col.", "dev.")))
+    worst_pm = max([v for k, v in errs.items() if k.startswith(("pose", "motion"))] or [0.0])
+    logp = os.environ.get("COPENERF_PARITY_LOG")
+    if logp:
+        with open(logp, "a") as f:
+            f.write(json.dumps({"scenario": scenario, "image": image, "mode": mode, "rays": rays,
+                                "loss": errs["loss"], "fields": worst_f, "pose_motion": worst_pm}) + "\n")
+    assert errs["loss"] <= l_bar + 1e-6 / abs(loss_ref.item()), errs["loss"]
+    for k, e in errs.items():
+        if k != "loss":
+            assert e <= (pm_bar if k.startswith(("pose", "motion")) else f_bar), (k, e)
 
 
 def test_stage1_terms_are_masked_not_branched():
@@ -169,4 +206,4 @@ def test_euler_chain_kernel_matches_torch_recurrence():
     g_ref = torch.autograd.grad((P_ref * G).sum(), list(m.parameters()))
     g = torch.autograd.grad((P * G.to(DEV)).sum(), list(mc.parameters()))
     for a, b in zip(g, g_ref):
-        _close(a, b, "motion grad", 1e-4)
+        assert _err(a, b, "motion grad") <= 1e-4
