@@ -1,7 +1,11 @@
 """CheckpointIO: drop-in for model/checkpoints.py:9-131 (train.py:94-113 saves and
 resumes through it).  Same directory layout (<dir>/models/weights[_<epoch>]/<file>),
 same dict format ({module name: state_dict} plus scalars), so checkpoints move
-between the reference and this build in both directions.  Loading uses
+between the reference and this build in both directions: tests/test_checkpoint_layout.py
+loads a checkpoint the reference's own CheckpointIO wrote (DataParallel renderer with
+`module.`-prefixed keys incl. the motion network, both Adam optimizers, epoch_it / it /
+depth_range; train.py:54, 94, 158-167) strictly, and checks that what this class saves
+has the same keys, shapes, dtypes and optimizer-state layout.  Loading uses
 torch.load(weights_only=True): a checkpoint is data, never code.  URL loading
 (model_zoo, checkpoints.py:102-112) is not offered: no network here."""
 from __future__ import annotations

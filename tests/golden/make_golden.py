@@ -534,6 +534,52 @@ def stage1_case(fields):
     print("wrote stage1")
 
 
+def checkpoint_case(fields, rend):
+    """what train.py checkpoints.  train.py:47-54 builds
+    DataParallel(NeuSRenderer(None, sdf, dev, col, motion)) and train.py:94 registers it
+    with the reference's CheckpointIO as `model`, beside the two Adam optimizers
+    (train.py:58-59); save_checkpoint (train.py:158-167) adds epoch_it / it /
+    depth_range.  Recorded: the module.-prefixed state-dict keys and shapes at the
+    default.yaml widths (state_keys.json), and a checkpoint file written by the
+    reference's own CheckpointIO (model/checkpoints.py) at 64-wide networks after one
+    Adam step of each optimizer (ref_checkpoint.pt: tensors, ints and floats only, so
+    torch.load(weights_only=True) reads it)."""
+    import json
+    import tempfile
+    ckio = importlib.util.spec_from_file_location("model.checkpoints", os.path.join(REF, "model", "checkpoints.py"))
+    ckmod = importlib.util.module_from_spec(ckio)
+    ckio.loader.exec_module(ckmod)
+
+    def build(width):
+        torch.manual_seed(700)
+        sdf = fields.SDFNetwork(**dict(SDF_CFG, d_hidden=width))
+        col = fields.RenderingNetwork(**dict(COL_CFG, d_hidden=width, d_feature=width))
+        dev = fields.SingleVarianceNetwork(0.3)
+        motion = fields.MotionNetwork(**dict(MOTION_CFG, d_hidden=width))
+        r = rend.NeuSRenderer(None, sdf, dev, col, motion, **REN_CFG)
+        return torch.nn.DataParallel(r), sdf, dev, col, motion
+
+    dp, *_ = build(256)
+    keys = {k: list(v.shape) for k, v in dp.state_dict().items()}
+    json.dump({"source": "DataParallel(NeuSRenderer) of train.py:47-54 at default.yaml widths", "keys": keys},
+              open(os.path.join(OUT, "state_keys.json"), "w"), indent=0)
+    dp, sdf, dev, col, motion = build(64)
+    opt = torch.optim.Adam(list(sdf.parameters()) + list(dev.parameters()) + list(col.parameters()), lr=1e-3)
+    mopt = torch.optim.Adam(motion.parameters(), lr=5e-4)
+    g = torch.Generator().manual_seed(701)
+    for o, mods in ((opt, (sdf, dev, col)), (mopt, (motion,))):
+        for m in mods:
+            for p in m.parameters():
+                p.grad = torch.randn(p.shape, generator=g) * 0.01
+        o.step()
+    with tempfile.TemporaryDirectory() as d:
+        io = ckmod.CheckpointIO(d, model=dp, optimizer=opt, motion_optimizer=mopt)
+        io.save("model.pt", lastest_checkpoint=True, epoch_it=12, it=3456, depth_range=[0.01, 5.0])
+        raw = open(os.path.join(d, "models", "weights", "model.pt"), "rb").read()
+    open(os.path.join(OUT, "ref_checkpoint.pt"), "wb").write(raw)
+    print("wrote state_keys.json, ref_checkpoint.pt", len(keys), "keys,", len(raw), "bytes")
+
+
 def main():
     fields, rend = load_reference()
     motion_case(fields)
@@ -548,6 +594,7 @@ def main():
     seams_case(fields, rend)
     pretrained_case(fields, rend)
     stage1_case(fields)
+    checkpoint_case(fields, rend)
 
 
 def main_motion_only():
@@ -566,6 +613,8 @@ if __name__ == "__main__":
         trainer_case()
     elif "--stage1-only" in sys.argv:
         stage1_case(load_reference()[0])
+    elif "--checkpoint-only" in sys.argv:
+        checkpoint_case(*load_reference())
     elif "--motion-only" in sys.argv:
         main_motion_only()
     elif "--pretrained-only" in sys.argv:

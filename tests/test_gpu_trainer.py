@@ -70,3 +70,44 @@ def test_train_py_sequence_on_hip():
         tr.backpropagation(loss_dict, train_motion_network=False)
         assert torch.isfinite(loss_dict["loss"]).item()
     assert all(not torch.equal(a, b.detach()) for a, b in zip(before, renderer.parameters()))
+
+
+def test_dataparallel_wrapped_renderer():
+    """train.py:54 wraps the renderer in torch.nn.DataParallel(renderer, device_ids=gpu_ids)
+    and calls it as train.py:441-444 does (query time repeated per GPU, background_rgb=None):
+    the wrapped HIP renderer returns the bare one's outputs and gradients bit for bit, and
+    its state dict carries the `module.` prefix the reference's checkpoints hold."""
+    sys.path.insert(0, os.path.join(ROOT, "cope-nerf_amd"))
+    from model import MotionNetwork, NeuSRenderer
+    from copenerf.train_step import MOTION_CFG
+    sdf, col, var = build_modules(21, device=DEV)
+    motion = MotionNetwork(**MOTION_CFG).to(DEV)
+    renderer = NeuSRenderer(None, sdf, var, col, motion, **REN_CFG).set_mfma_dtype("bf16x6")
+    dp = torch.nn.DataParallel(renderer, device_ids=[0])
+    assert all(k.startswith("module.") for k in dp.state_dict())
+    assert any(k.startswith("module.motion_network.") for k in dp.state_dict())
+    g = torch.Generator().manual_seed(22)
+    R = 512
+    d = torch.cat([(torch.rand(R, 2, generator=g) - 0.5) * 0.5, -torch.ones(R, 1)], -1)
+    norm = d.norm(dim=-1, keepdim=True)
+    rays_o = torch.tensor([[0.05, -0.03, 1.6]]).expand(R, 3).contiguous().to(DEV)
+    rays_d, norm = (d / norm).to(DEV), norm.to(DEV)
+    near, far = torch.full((R, 1), 0.01, device=DEV), torch.full((R, 1), 3.0, device=DEV)
+    t_rand = torch.rand(R, 64, generator=g).to(DEV)
+    q = torch.tensor([0.25], device=DEV).repeat(1)  # query_time_step.repeat(len(gpu_ids))
+    res = []
+    for mod in (renderer, dp):
+        for p in renderer.parameters():
+            p.grad = None
+        out = mod(rays_o, rays_d, norm, q, near, far, background_rgb=None, cos_anneal_ratio=0.5, it=10, eval=False,
+                  t_rand=t_rand)
+        loss = out["color_fine"].abs().sum() + out["depth_pred"].sum() + out["normals"].square().sum()
+        loss.backward()
+        res.append(({k: v.detach().clone() for k, v in out.items() if torch.is_tensor(v)},
+                    [p.grad.clone() if p.grad is not None else None for p in renderer.parameters()]))
+    (o1, g1), (o2, g2) = res
+    assert o1.keys() == o2.keys()
+    for k in o1:
+        assert torch.equal(o1[k], o2[k]), k
+    for a, b in zip(g1, g2):
+        assert (a is None and b is None) or torch.equal(a, b)
