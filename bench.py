@@ -12,8 +12,8 @@ and Adam.  Weak scaling: every rank renders its own 4096 rays.  The timed
 steps run uninstrumented.
 
 The JSON line also carries
-  roofline      the dominant kernel (the cn_linear launch class with the most
-                time), from a separate instrumented pass after the timed steps
+  roofline      the dominant kernel (the cn_linear / cn_wgrad launch class with the
+                most time), from a separate instrumented pass after the timed steps
                 (HIP events around each launch on the launching stream):
                 its algorithmic FLOPs and bytes per launch against the binding
                 ceiling, max(FLOPs / MFMA peak of the GEMM mode, bytes / HBM
@@ -55,20 +55,6 @@ SAMPLES = 128
 GFLOP_PER_RAY_REF = 1.4809  # reference GEMM FLOPs per ray per train step (64+4x16)
 
 
-def kernel_symbol(key):
-    """rocprofv3 name of the kernel a KernelTimer key times: cn_linear's tile choice is
-    mirrored in copenerf.ops (the key's second field names the bf16x6 tile); a cn_wgrad
-    call is its split-M MFMA kernel plus the fixed-order slab reduction."""
-    if key[0] == "linear":
-        from copenerf import ops
-        return ops.linear_kernel_symbol(key)
-    if "bf16" in key[2:]:
-        return "void cn::wgrad_bf16_kernel<2, 2, 2, 2>(cn::WgradArgs) + cn::slab_reduce_kernel"
-    if "x6" in key[2:]:
-        return "void cn::wgrad_x6_kernel<4, 4>(cn::WgradArgs) + cn::slab_reduce_kernel"
-    return "void cn::wgrad_kernel<2, 2, 2, 2>(cn::WgradArgs) + cn::slab_reduce_kernel"
-
-
 def pmc_traffic(symbol):
     """Per-launch HBM bytes of `symbol` from the newest committed counter pass."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
@@ -95,6 +81,21 @@ def _cpu_model():
     return "unknown"
 
 
+def _available_cpus():
+    """The cores this process may run on (BASELINE.md's CPU-baseline plan): its affinity
+    mask, capped by the cgroup CPU quota when one is set (a GPU box's share of a larger
+    host: the affinity mask there lists every core of the machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def cpu_baseline(rays=1024, steps=5):
     """Time the CPU oracle (torch restatement of the reference path) on the host:
     one warm-up step, then the median of `steps` steps at `rays` rays (BASELINE.md's
@@ -102,7 +103,7 @@ def cpu_baseline(rays=1024, steps=5):
     import statistics
     from tests.helpers import build_modules, oracle_params
     from oracle import neus_oracle as O
-    threads = int(os.environ.get("COPENERF_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    threads = int(os.environ.get("COPENERF_CPU_THREADS", _available_cpus()))
     torch.set_num_threads(threads)
     mods = build_modules(678)
     g = torch.Generator().manual_seed(0)
@@ -280,23 +281,27 @@ def main():
 
 def roofline_fields(timer, steps, rays_per_s, mode):
     agg = timer.summary()
-    # dominant single-kernel launch class (a cn_wgrad call is two kernels: the
-    # split-M MFMA kernel and its fixed-order slab reduction)
-    dom_key = max((k for k in agg if k[0] == "linear"), key=lambda k: agg[k]["ms"])
+    # the dominant launch class over every cn_linear and cn_wgrad class (a launch class is one
+    # kernel instance, named by the library: cn_linear_kernel_name / cn_wgrad_kernel_name; a
+    # cn_wgrad call is its split-M MFMA kernel plus the fixed-order slab reduction, both inside
+    # the class's HIP events)
+    dom_key = max(agg, key=lambda k: agg[k]["ms"])
     dom = agg[dom_key]
     avg_s = dom["ms"] / dom["launches"] * 1e-3
     flops, nbytes = dom["flops"] / dom["launches"], dom["bytes"] / dom["launches"]
     peak_tf = MODE_PEAK_TFLOPS[mode]
     t_flop, t_byte = flops / (peak_tf * 1e12), nbytes / (HBM_PEAK_GBS * 1e9)
     hbm = t_byte > t_flop  # the binding ceiling: the larger of the two times
-    symbol = kernel_symbol(dom_key)
+    symbol = timer.symbols[dom_key]
     traffic, traffic_src = pmc_traffic(symbol)
     kernels_ms = sum(a["ms"] for a in agg.values()) / steps
     roof = {"bound": "hbm" if hbm else "mfma",
             "achieved": round(nbytes / avg_s / 1e9, 1) if hbm else round(flops / avg_s / 1e12, 2),
             "peak": HBM_PEAK_GBS if hbm else round(peak_tf, 1), "unit": "GB/s" if hbm else "TFLOP/s",
             "frac": round(max(t_flop, t_byte) / avg_s, 4), "traffic": traffic, "traffic_source": traffic_src,
-            "kernel": symbol, "launches_per_step": dom["launches"] / steps, "avg_launch_ms": round(avg_s * 1e3, 4),
+            "kernel": symbol, "launch_class": "/".join(map(str, dom_key)),
+            "timed_region": "the cn_wgrad call: this kernel + cn::slab_reduce_kernel (dW, db)" if dom_key[0] == "wgrad"
+            else "this kernel", "launches_per_step": dom["launches"] / steps, "avg_launch_ms": round(avg_s * 1e3, 4),
             "algorithmic_gflop_per_launch": round(flops / 1e9, 3),
             "algorithmic_mb_per_launch": round(nbytes / 1e6, 1),
             "tflops": round(flops / avg_s / 1e12, 2), "gbs": round(nbytes / avg_s / 1e9, 1),
@@ -313,6 +318,7 @@ def roofline_fields(timer, steps, rays_per_s, mode):
                               for k, v in sorted(agg.items(), key=lambda kv: -kv[1]["ms"])},
         "kernel_breakdown_ms_per_step": {"/".join(map(str, k)): round(v["ms"] / steps, 3) for k, v in
                                          sorted(agg.items(), key=lambda kv: -kv[1]["ms"])},
+        "kernel_symbols": {"/".join(map(str, k)): timer.symbols[k] for k in agg},
     }
 
 

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libcopenerf.so"
 LIB_PATH = os.environ.get("COPENERF_LIB", os.path.join(_HERE, LIB_NAME))
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 c_f32p = ctypes.c_void_p  # device pointers are passed as integers
 c_i32 = ctypes.c_int32
@@ -79,6 +79,8 @@ SIGNATURES = {
     "cn_abi_version": (c_i32, []),
     "cn_last_error": (ctypes.c_char_p, []),
     "cn_linear": (c_i32, [ctypes.POINTER(LinearDesc), c_ptr]),
+    "cn_linear_kernel_name": (c_i32, [ctypes.POINTER(LinearDesc), ctypes.c_char_p, c_i32]),
+    "cn_wgrad_kernel_name": (c_i32, [ctypes.POINTER(WgradDesc), ctypes.c_char_p, c_i32]),
     "cn_weight_norm": (c_i32, [ctypes.POINTER(WnJob), c_i32, c_i32, c_ptr]),
     "cn_wgrad_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32]),
     "cn_wgrad": (c_i32, [ctypes.POINTER(WgradDesc), c_ptr]),

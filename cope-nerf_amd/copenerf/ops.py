@@ -7,6 +7,7 @@ leading dimension (stride(0)) is passed explicitly, so column views such as
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import os
 
@@ -26,6 +27,7 @@ class KernelTimer:
     def __init__(self, detail=False):
         self.records = []
         self.detail = detail  # key launches by shape as well
+        self.symbols = {}  # launch class -> rocprofv3 symbol of its kernel (named by the library)
 
     def start(self):
         e = torch.cuda.Event(enable_timing=True)
@@ -193,45 +195,25 @@ class ImagePacker:
         self.jobs, self.keep = [], []
 
 
-# cn_linear's bf16x6 tile choice (cn_gemm.hip, cn_linear; the same env knobs), for the kernel
-# timer's launch classes and the rocprofv3 names of their kernels
-_X6_SQ = int(os.environ.get("COPENERF_X6_SQ", "0x5f"), 0)
-_X6_TALL = int(os.environ.get("COPENERF_X6_TALL", "0x18"), 0)
-_WIDE_EPIS = int(os.environ.get("COPENERF_WIDE_EPIS", "0x1f"), 0)
-_WIDE_MINK = int(os.environ.get("COPENERF_WIDE_MINK", "128"))
-_X6_SQ_MINM = int(os.environ.get("COPENERF_X6_SQ_MINM", "0"))
-_LINEAR_TILES = {  # tag -> linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH> (bf16x6); tile 1 / other modes below
-    "sq": "4, 2, 2, 4, 16, 1, 2", "tall": "4, 2, 1, 4, 32, 1, 2", "wide": "4, 2, 2, 2, 32, 1, 2",
-    "t128": "2, 2, 2, 2, 16, 2, 2"}
+# launch-class tags of the kernel timer: linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, ...> arguments
+# (named by the library itself, cn_linear_kernel_name) -> a short tile name
+_TILE_TAGS = {"4, 2, 2, 4, 16, 1, 2": "sq", "4, 2, 1, 4, 32, 1, 2": "tall", "4, 2, 2, 2, 32, 1, 2": "wide",
+              "2, 2, 2, 2, 16, 2, 2": "t128", "4, 1, 1, 2, 16, 2, 2": "t1"}
 
 
-def _x6_tile(epi, N, K, ldb, rowv, split, M=None):
-    head = epi == EPI_SOFTPLUS_HEAD
-    longk = K >= _WIDE_MINK
-    if (_X6_SQ >> epi) & 1 and 128 < N <= 256 and (M is None or M >= _X6_SQ_MINM) and not rowv and not (epi == EPI_MUL and split) and K % 32 == 0 \
-            and ldb >= 256 and (longk or head):
-        return "sq"
-    tall = (_X6_TALL >> epi) & 1 or (head and N > 128)
-    if K % 64 == 0 and tall and N > 128 and ldb >= 256 and (longk or head):
-        return "tall"
-    if K % 64 == 0 and (_WIDE_EPIS >> epi) & 1 and longk:
-        return "wide"
-    return "t128"
+def kernel_name(query, d) -> str:
+    """The rocprofv3 symbol of the kernel a cn_linear / cn_wgrad descriptor launches, as the
+    library decides it (cn_linear_kernel_name / cn_wgrad_kernel_name)."""
+    buf = ctypes.create_string_buffer(256)
+    n = query(d, buf, 256)
+    if n < 0:
+        raise RuntimeError(f"kernel name query failed ({n}): {_lib.load().cn_last_error().decode()}")
+    return buf.value.decode()
 
 
-def linear_kernel_symbol(key):
-    """rocprofv3 name of the kernel behind a kernel-timer cn_linear key."""
-    _, tag, epi = key[:3]
-    rowv = epi.endswith("+rowv")
-    eid = {v: k for k, v in EPI_NAMES.items()}[epi.split("+")[0]]
-    mode = 1 if "bf16" in key[3:] else 2 if "x6" in key[3:] else 0
-    if mode == 2:
-        tiles = _LINEAR_TILES.get(tag, "4, 1, 1, 2, 16, 2, 2")
-    elif mode == 1:
-        tiles = "2, 2, 2, 2, 64, 2, 1" if tag == 0 else "4, 1, 1, 2, 64, 2, 1"
-    else:
-        tiles = "2, 2, 2, 2, 32, 2, 2" if tag == 0 else "4, 1, 1, 2, 32, 2, 2"
-    return f"void cn::linear_kernel<{tiles}, {eid}, {str(rowv).lower()}, {mode}>(cn::LinearArgs)"
+def _tile_tag(name, tile):
+    args = name[name.index("<") + 1:].split(", ")[:7]
+    return _TILE_TAGS.get(", ".join(args), tile)
 
 
 def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None, colv=None, aux0=None,
@@ -314,10 +296,11 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     if _timer is not None:
         e0 = _timer.start()
         _lib.check(_lib.load().cn_linear(d, _stream()), "cn_linear")
-        tag = _x6_tile(epilogue, N, K, d.ldb, rowv is not None,
-                       out_split is not None and d.nsplit < N, M=d.M) if x6 and tile == 0 else tile
+        name = kernel_name(_lib.load().cn_linear_kernel_name, d)
+        tag = _tile_tag(name, tile) if x6 else tile
         key = ("linear", tag, EPI_NAMES[epilogue] + ("+rowv" if rowv is not None else "")) + \
             (("bf16",) if bf else ("x6",) if x6 else ())
+        _timer.symbols[key] = name
         ka = kalg or K
         # algorithmic HBM bytes: A (unpadded K) and every aux row read once, each output
         # element written once, the weight image once (bf16x6: 3 bf16 terms per weight)
@@ -359,7 +342,11 @@ def wgrad(Y0, X0, N, K, dW, *, db=None, Y1=None, X1=None, accumulate=False, mode
     if _timer is not None:
         e0 = _timer.start()
         _lib.check(lib.cn_wgrad(d, _stream()), "cn_wgrad")
-        key = ("wgrad", d.npairs) + (("bf16",) if mode == "bf16" else ("x6",) if mode == "bf16x6" else ())
+        # one launch class per kernel instance (1- and 2-pair calls share it, as in rocprof's stats)
+        name = kernel_name(lib.cn_wgrad_kernel_name, d)
+        key = ("wgrad", name[len("void cn::"):name.index("(")].replace(" ", "")) + \
+            (("bf16",) if mode == "bf16" else ("x6",) if mode == "bf16x6" else ())
+        _timer.symbols[key] = name
         _timer.stop(key + ((M, d.n_out, d.k_out),) if _timer.detail else key, e0,
                     2.0 * M * d.n_out * d.k_out * d.npairs, 4.0 * d.npairs * M * (d.n_out + d.k_out))
     else:

@@ -1243,6 +1243,62 @@ static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_
 }
 
 
+// The kernel instance cn_linear launches for a descriptor: ONE function decides it, for the
+// launch and for cn_linear_kernel_name (a profiler's name of the launch), so the two cannot
+// disagree.  X-macro rows: (tile, WM, WN, TM, TN, BK, OCC, DEPTH, MODE).
+enum LinearTile { LT_BF_T0, LT_BF_T1, LT_X6_SQ, LT_X6_TALL, LT_X6_WIDE, LT_X6_T128, LT_X6_T1, LT_F_V2, LT_F_T0_D2,
+                  LT_F_T0_D1, LT_F_T1_D2, LT_F_T1_D1 };
+#define CN_LINEAR_TILES(X)                 \
+    X(LT_BF_T0, 2, 2, 2, 2, 64, 2, 1, 1)   \
+    X(LT_BF_T1, 4, 1, 1, 2, 64, 2, 1, 1)   \
+    X(LT_X6_SQ, 4, 2, 2, 4, 16, 1, 2, 2)   \
+    X(LT_X6_TALL, 4, 2, 1, 4, 32, 1, 2, 2) \
+    X(LT_X6_WIDE, 4, 2, 2, 2, 32, 1, 2, 2) \
+    X(LT_X6_T128, 2, 2, 2, 2, 16, 2, 2, 2) \
+    X(LT_X6_T1, 4, 1, 1, 2, 16, 2, 2, 2)   \
+    X(LT_F_V2, 2, 2, 2, 2, 16, 3, 2, 0)    \
+    X(LT_F_T0_D2, 2, 2, 2, 2, 32, 2, 2, 0) \
+    X(LT_F_T0_D1, 2, 2, 2, 2, 32, 2, 1, 0) \
+    X(LT_F_T1_D2, 4, 1, 1, 2, 32, 2, 2, 0) \
+    X(LT_F_T1_D1, 4, 1, 1, 2, 32, 2, 1, 0)
+
+static LinearTile choose_linear_tile(const cn_linear_desc* d) {
+    const bool head = d->epilogue == CN_EPI_SOFTPLUS_HEAD;
+    if (d->mfma_dtype == CN_MFMA_BF16) return d->tile == 0 ? LT_BF_T0 : LT_BF_T1;
+    if (d->mfma_dtype == CN_MFMA_F32_BF16X6) {
+        // K % 64 == 0, STORE / SOFTPLUS / RELU: 256x128 tiles of 8 waves, one workgroup per CU,
+        // 32-deep stages (whole 128-byte A row segments per load, half the barriers per K; main
+        // loop 366 vs 385 us at C2's layer shape); else 128x128 tiles of 16-deep chunks (K % 32
+        // == 0: an even number of chunks for the 2-deep prefetch)
+        if (d->tile != 0) return LT_X6_T1;
+        // (the wide tile only for the light epilogues: with one workgroup per CU an aux-reading
+        // epilogue no longer overlaps a partner workgroup's main loop, measured slower)
+        const bool light = (g_wide_epis >> d->epilogue) & 1;
+        // 128x256 ("tall-N") tiles: one workgroup owns whole 256-wide output rows, so A is
+        // read from HBM once (the two N-tiles of the 256x128 tiling re-fetch 30-50 % of it,
+        // PMC) and split once per row
+        const bool tall = ((g_x6_tall >> d->epilogue) & 1) || (head && d->N > 128);
+        // short K (a first layer): the main loop is two chunks, so the one-workgroup-per-CU tiles
+        // cannot hide their epilogue; the 2-per-CU 128x128 tile overlaps it with the partner's
+        // (COPENERF_WIDE_MINK: the smallest K for the 1-per-CU tiles)
+        const bool longk = d->K >= g_wide_min_k;
+        // (the epilogues with a direct form: STORE, SOFTPLUS, RELU, MUL, TANGENT, BWD_SOFTPLUS, BWD_RELU)
+        const bool sq = (g_x6_sq >> d->epilogue & 1) && d->N > 128 && d->N <= 256 && !d->rowv &&
+                        d->M >= g_x6_sq_min_m && !(d->epilogue == CN_EPI_MUL && d->out_split && d->nsplit < d->N);
+        if (d->K % 32 == 0 && sq && d->ldb >= 256 && g_linear_variant == 0 && (longk || head)) return LT_X6_SQ;
+        if (d->K % 64 == 0 && tall && d->N > 128 && d->ldb >= 256 && g_linear_variant == 0 && (longk || head))
+            return LT_X6_TALL;
+        if (d->K % 64 == 0 && g_linear_variant == 0 && light && longk) return LT_X6_WIDE;
+        return LT_X6_T128;
+    }
+    const bool even = (d->K % 64) == 0;  // DEPTH-2 prefetch consumes K in pairs of 32-chunks
+    if (d->tile == 0) {
+        if (g_linear_variant == 2) return LT_F_V2;
+        return even && g_linear_variant == 0 ? LT_F_T0_D2 : LT_F_T0_D1;
+    }
+    return even && g_linear_variant == 0 ? LT_F_T1_D2 : LT_F_T1_D1;
+}
+
 extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     CN_REQUIRE(d, CN_ERR_ARG, "cn_linear: null desc");
     const bool head = d->epilogue == CN_EPI_SOFTPLUS_HEAD;
@@ -1335,48 +1391,30 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     a.beta = d->beta;
     a.threshold = d->threshold;
     hipStream_t s = (hipStream_t)stream;
-    if (bf) {
-        if (d->tile == 0) return launch_linear_tile<2, 2, 2, 2, 64, 2, 1, 1>(d, a, s);
-        return launch_linear_tile<4, 1, 1, 2, 64, 2, 1, 1>(d, a, s);
+    switch (choose_linear_tile(d)) {
+#define CN_TILE_CASE(T, WM, WN, TM, TN, BK, OCC, DEPTH, MODE) \
+        case T: return launch_linear_tile<WM, WN, TM, TN, BK, OCC, DEPTH, MODE>(d, a, s);
+        CN_LINEAR_TILES(CN_TILE_CASE)
+#undef CN_TILE_CASE
     }
-    if (x6) {
-        // K % 64 == 0, STORE / SOFTPLUS / RELU: 256x128 tiles of 8 waves, one workgroup per CU,
-        // 32-deep stages (whole 128-byte A row segments per load, half the barriers per K; main
-        // loop 366 vs 385 us at C2's layer shape); else 128x128 tiles of 16-deep chunks (K % 32
-        // == 0: an even number of chunks for the 2-deep prefetch)
-        if (d->tile == 0) {
-            // (the wide tile only for the light epilogues: with one workgroup per CU an aux-reading
-            // epilogue no longer overlaps a partner workgroup's main loop, measured slower)
-            const bool light = (g_wide_epis >> d->epilogue) & 1;
-            // 128x256 ("tall-N") tiles: one workgroup owns whole 256-wide output rows, so A is
-            // read from HBM once (the two N-tiles of the 256x128 tiling re-fetch 30-50 % of it,
-            // PMC) and split once per row
-            const bool tall = ((g_x6_tall >> d->epilogue) & 1) || (head && d->N > 128);
-            // short K (a first layer): the main loop is two chunks, so the one-workgroup-per-CU tiles
-            // cannot hide their epilogue; the 2-per-CU 128x128 tile overlaps it with the partner's
-            // (COPENERF_WIDE_MINK: the smallest K for the 1-per-CU tiles)
-            const bool longk = d->K >= g_wide_min_k;
-            // (the epilogues with a direct form: STORE, SOFTPLUS, RELU, MUL, TANGENT, BWD_SOFTPLUS, BWD_RELU)
-            const bool sq = (g_x6_sq >> d->epilogue & 1) && d->N > 128 && d->N <= 256 && !d->rowv && d->M >= g_x6_sq_min_m &&
-                            !(d->epilogue == CN_EPI_MUL && d->out_split && d->nsplit < d->N);
-            if (d->K % 32 == 0 && sq && d->N > 128 && d->ldb >= 256 && g_linear_variant == 0 && (longk || head))
-                return launch_linear_tile<4, 2, 2, 4, 16, 1, 2, 2>(d, a, s);
-            if (d->K % 64 == 0 && tall && d->N > 128 && d->ldb >= 256 && g_linear_variant == 0 && (longk || head))
-                return launch_linear_tile<4, 2, 1, 4, 32, 1, 2, 2>(d, a, s);
-            if (d->K % 64 == 0 && g_linear_variant == 0 && light && longk)
-                return launch_linear_tile<4, 2, 2, 2, 32, 1, 2, 2>(d, a, s);
-            return launch_linear_tile<2, 2, 2, 2, 16, 2, 2, 2>(d, a, s);
-        }
-        return launch_linear_tile<4, 1, 1, 2, 16, 2, 2, 2>(d, a, s);
+    set_error("cn_linear: no tile");
+    return CN_ERR_UNSUPPORTED;
+}
+
+extern "C" int cn_linear_kernel_name(const cn_linear_desc* d, char* buf, int32_t len) {
+    CN_REQUIRE(d && buf && len > 0, CN_ERR_ARG, "cn_linear_kernel_name: null desc / buffer");
+    const char* args = "";
+    switch (choose_linear_tile(d)) {
+#define CN_TILE_NAME(T, WM, WN, TM, TN, BK, OCC, DEPTH, MODE) \
+        case T: args = #WM ", " #WN ", " #TM ", " #TN ", " #BK ", " #OCC ", " #DEPTH; break;
+        CN_LINEAR_TILES(CN_TILE_NAME)
+#undef CN_TILE_NAME
     }
-    const bool even = (d->K % 64) == 0;  // DEPTH-2 prefetch consumes K in pairs of 32-chunks
-    if (d->tile == 0) {
-        if (g_linear_variant == 2) return launch_linear_tile<2, 2, 2, 2, 16, 3, 2>(d, a, s);
-        if (even && g_linear_variant == 0) return launch_linear_tile<2, 2, 2, 2, 32, 2, 2>(d, a, s);
-        return launch_linear_tile<2, 2, 2, 2, 32, 2, 1>(d, a, s);
-    }
-    if (even && g_linear_variant == 0) return launch_linear_tile<4, 1, 1, 2, 32, 2, 2>(d, a, s);
-    return launch_linear_tile<4, 1, 1, 2, 32, 2, 1>(d, a, s);
+    const int mode = d->mfma_dtype == CN_MFMA_F32_BF16X6 ? 2 : d->mfma_dtype == CN_MFMA_BF16 ? 1 : 0;
+    const int n = snprintf(buf, (size_t)len, "void cn::linear_kernel<%s, %d, %s, %d>(cn::LinearArgs)", args,
+                           d->epilogue, d->rowv ? "true" : "false", mode);
+    CN_REQUIRE(n < len, CN_ERR_SHAPE, "cn_linear_kernel_name: buffer of %d bytes too small (%d)", len, n + 1);
+    return n;
 }
 
 

@@ -781,6 +781,30 @@ static void wgrad_geometry(int M, int N, int K, int wide, int* tile, int* Npad, 
 
 using namespace cn;
 
+static const int g_wgrad_variant = [] {  // benchmarking aid: COPENERF_WGRAD_KERNEL=1 (32-row kernel)
+    const char* e = getenv("COPENERF_WGRAD_KERNEL");
+    return e ? atoi(e) : 0;
+}();
+
+// The split-M kernel cn_wgrad launches for a descriptor (its fixed-order slab reduction,
+// cn::slab_reduce_kernel, follows it), decided by the same geometry as the launch.
+extern "C" int cn_wgrad_kernel_name(const cn_wgrad_desc* d, char* buf, int32_t len) {
+    CN_REQUIRE(d && buf && len > 0, CN_ERR_ARG, "cn_wgrad_kernel_name: null desc / buffer");
+    int tile, Npad, Kpad, ns, rps;
+    wgrad_geometry(std::max(d->M, 1), d->N, d->K, wgrad_wide(d), &tile, &Npad, &Kpad, &ns, &rps);
+    const char* k = "";
+    if (d->mfma_dtype == CN_MFMA_F32_BF16X6)
+        k = tile == 2 ? (g_wgrad_variant == 1 ? "wgrad_x6_kernel<4, 4>" : "wgrad_x6r_kernel<2>")
+            : tile == 3 ? "wgrad_x6_kernel<4, 1>" : tile == 0 ? "wgrad_x6_kernel<2, 2>" : "wgrad_x6_kernel<2, 1>";
+    else if (d->mfma_dtype == CN_MFMA_BF16)
+        k = tile == 0 ? "wgrad_bf16_kernel<2, 2, 2, 2>" : "wgrad_bf16_kernel<2, 2, 2, 1>";
+    else
+        k = tile == 0 ? "wgrad_kernel<2, 2, 2, 2>" : "wgrad_kernel<2, 2, 2, 1>";
+    const int n = snprintf(buf, (size_t)len, "void cn::%s(cn::WgradArgs)", k);
+    CN_REQUIRE(n < len, CN_ERR_SHAPE, "cn_wgrad_kernel_name: buffer of %d bytes too small (%d)", len, n + 1);
+    return n;
+}
+
 extern "C" size_t cn_wgrad_workspace_bytes(int32_t M, int32_t N, int32_t K) {
     size_t need = 0;  // the larger of the two tilings (the call's mfma_dtype picks one)
     for (int w = 0; w < 3; ++w) {
@@ -828,11 +852,7 @@ extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
             // the stage ring (one barrier per 16 rows, split and LDS writes beside the MFMAs): C2
             // step 145.0-145.3k vs 142.1-143.3k rays/s with the 32-row single-buffer kernel
             // (COPENERF_WGRAD_KERNEL=1, benchmarking aid; tools/env_ab.sh, same box)
-            static const int variant = [] {
-                const char* e = getenv("COPENERF_WGRAD_KERNEL");
-                return e ? atoi(e) : 0;
-            }();
-            if (variant == 1) wgrad_x6_kernel<4, 4><<<grid, 512, 0, s>>>(a);
+            if (g_wgrad_variant == 1) wgrad_x6_kernel<4, 4><<<grid, 512, 0, s>>>(a);
             else wgrad_x6r_kernel<2><<<grid, 512, 0, s>>>(a);
         }
         else if (tile == 3)

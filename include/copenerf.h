@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define CN_ABI_VERSION 5
+#define CN_ABI_VERSION 6
 
 typedef void* cn_stream_t; /* hipStream_t */
 
@@ -129,6 +129,12 @@ enum cn_mfma_dtype { CN_MFMA_F32 = 0, CN_MFMA_BF16 = 1, CN_MFMA_F32_BF16X6 = 2 }
 
 int cn_linear(const cn_linear_desc* d, cn_stream_t stream);
 
+/* The rocprofv3 symbol of the kernel cn_linear would launch for *d (no launch, no device
+ * access; the tile choice is the launch's own function): NUL-terminated into buf[len].
+ * Returns the name's length, or a negative cn_status.  For profilers and the bench's
+ * roofline (bench.py names the launch class it reports). */
+int cn_linear_kernel_name(const cn_linear_desc* d, char* buf, int32_t len);
+
 /* ------------------------------------------------------------------------ *
  * Weight images for cn_linear (the per-call `pack` of the effective weights,
  * neus_fields.py:273-283 / 364-373 weight_norm outputs): one launch builds
@@ -204,6 +210,8 @@ typedef struct cn_wgrad_desc {
 
 size_t cn_wgrad_workspace_bytes(int32_t M, int32_t N, int32_t K);
 int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream);
+/* As cn_linear_kernel_name for cn_wgrad's split-M kernel (cn::slab_reduce_kernel follows it). */
+int cn_wgrad_kernel_name(const cn_wgrad_desc* d, char* buf, int32_t len);
 
 /* ------------------------------------------------------------------------ *
  * Per-row heads (neus_fields.py:279-283 last Linear row 0 = sdf;

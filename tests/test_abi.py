@@ -86,3 +86,25 @@ def test_product_path_refuses_cpu_tensors():
     net = SDFNetwork(d_in=4, d_out=257, d_hidden=64, n_layers=8, skip_in=[4], multires=6)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         net.sdf(torch.zeros(8, 4))
+
+
+def test_kernel_name_queries_follow_the_launch_choice():
+    """cn_linear_kernel_name / cn_wgrad_kernel_name (no device access): C2's hidden-layer
+    SOFTPLUS on the 256x256 bf16x6 tile, the colour network's RELU with a rowv on the 256x128
+    tile, and a 256x256 bf16x6 weight gradient on the stage ring -- the rocprofv3 symbols the
+    bench's launch classes report."""
+    from copenerf import _lib, ops
+    d = _lib.LinearDesc()
+    d.M, d.N, d.K, d.K1, d.ldb, d.epilogue, d.tile, d.mfma_dtype = 524288, 256, 256, 256, 256, 1, 0, 2
+    assert ops.kernel_name(_lib.load().cn_linear_kernel_name, d) == \
+        "void cn::linear_kernel<4, 2, 2, 4, 16, 1, 2, 1, false, 2>(cn::LinearArgs)"
+    d.epilogue, d.rowv = 2, 16
+    assert ops.kernel_name(_lib.load().cn_linear_kernel_name, d) == \
+        "void cn::linear_kernel<4, 2, 2, 2, 32, 1, 2, 2, true, 2>(cn::LinearArgs)"
+    w = _lib.WgradDesc()
+    w.M, w.N, w.K, w.npairs, w.mfma_dtype = 524288, 256, 256, 2, 2
+    w.ldy0 = w.ldx0 = w.ldy1 = w.ldx1 = 256
+    assert ops.kernel_name(_lib.load().cn_wgrad_kernel_name, w) == "void cn::wgrad_x6r_kernel<2>(cn::WgradArgs)"
+    w.K, w.ldx0, w.ldx1 = 64, 64, 64
+    assert ops.kernel_name(_lib.load().cn_wgrad_kernel_name, w) == "void cn::wgrad_x6_kernel<2, 1>(cn::WgradArgs)"
+    assert _lib.load().cn_linear_kernel_name(d, ctypes.create_string_buffer(8), 8) == -2  # CN_ERR_SHAPE
