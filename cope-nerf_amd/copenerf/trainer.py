@@ -29,7 +29,8 @@ import torch
 import torch.nn.functional as F
 
 from .rays import get_patch_indices as _device_patch_indices
-from .rays import inv4x4, near_far_from_sphere as _near_far
+from .rays import near_far_from_sphere as _near_far
+from .rays import world_rays
 
 _WEIGHT_NAMES = ("rgb_weight", "eikonal_weight", "sdf_weight", "flow_rgb_weight", "sdf_consistency_weight",
                  "edge_aware_smoothness_weight", "smoothness_weight")  # training.py:493-497
@@ -126,17 +127,10 @@ class Trainer(object):
         """training.py:474-487 (origin_to_world / image_points_to_world, common.py:175-215):
         o = S⁻¹W⁻¹K⁻¹[0,0,0,1], p = S⁻¹W⁻¹K⁻¹[u,v,1,1], d = (p - o) / |p - o|;
         pixels [1, R, 2], matrices [1, 4, 4] or [4, 4]."""
-        mats = [m.reshape(-1, 4, 4)[0] for m in (scale_mat, world_mat, camera_mat)]
-        inv_s, inv_w, inv_c = inv4x4(torch.stack(mats)).unbind(0)
-        inv = inv_s @ inv_w @ inv_c
-        px = pixels.reshape(-1, 2)
-        R = px.shape[0]
-        o = inv[:3, 3]
-        ph = torch.cat([px, torch.ones(R, 2, device=px.device, dtype=px.dtype)], -1)
-        pw = (ph @ inv.t())[:, :3]
-        v = pw - o
-        n = v.norm(2, -1)
-        return o.expand(R, 3).contiguous(), (v / n.unsqueeze(-1)).contiguous(), n.view(-1, 1)
+        # the one ray generator of this build (rays.world_rays: also SyntheticTrainer's and the
+        # bench's), pinned here by trainer.npz
+        s, w, c = (m.reshape(-1, 4, 4)[0] for m in (scale_mat, world_mat, camera_mat))
+        return world_rays(pixels.reshape(-1, 2).to(c.dtype), c, w, s)
 
     # -- losses and the update ---------------------------------------------------
     def compute_loss(self, data, rendered_rgb, rgb_gt, gradient_loss, sdf_loss, flow_rgb_loss, sdf_consistency_loss,
