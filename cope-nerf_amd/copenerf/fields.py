@@ -41,6 +41,22 @@ def effective_weight(lin: nn.Linear) -> torch.Tensor:
     return lin.weight
 
 
+def release_weight_norm_graphs(module: nn.Module) -> nn.Module:
+    """nn.utils.weight_norm keeps the last weight it computed (g v / |v|, at construction and in
+    every forward pre-hook) as a plain attribute that carries its autograd graph, i.e. the
+    AccumulateGrad nodes of weight_g / weight_v, alive for the module's lifetime.  Autograd
+    then reuses those nodes in every later step, bound to the stream of construction, which
+    a HIP-graph capture on another stream reports as a stream mismatch (and may synchronise
+    on).  This build computes the effective weights itself (effective_weight(s)), so the
+    attribute is replaced by a detached copy: same values, no graph.  Not part of the state
+    dict either way."""
+    for m in module.modules():
+        w = m.__dict__.get("weight")
+        if hasattr(m, "weight_v") and torch.is_tensor(w) and w.grad_fn is not None:
+            m.weight = w.detach()
+    return module
+
+
 class _WeightNormFn(torch.autograd.Function):
     """W_l = g_l v_l / |v_l| for every weight-normed Linear of a network in one launch
     forward and one backward (cn_weight_norm) instead of one torch launch per layer each way."""
@@ -538,6 +554,7 @@ class SDFNetwork(nn.Module):
         self.activation = nn.Softplus(beta=100)
         self._layout = None
         self.mfma_dtype = "fp32"  # "bf16": bf16-operand MFMA GEMMs (config C3); not part of the state dict
+        release_weight_norm_graphs(self)
 
     # -- kernel plumbing ---------------------------------------------------
     def layout(self) -> SDFLayout:
@@ -771,6 +788,7 @@ class RenderingNetwork(nn.Module):
         self.relu = nn.ReLU()
         self._layout = None
         self.mfma_dtype = "fp32"  # see SDFNetwork.mfma_dtype
+        release_weight_norm_graphs(self)
 
     def layout(self) -> ColorLayout:
         if self._layout is None:

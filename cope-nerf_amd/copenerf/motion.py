@@ -22,8 +22,10 @@ from __future__ import annotations
 import numpy as np
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from .embedder import get_embedder
+from .fields import effective_weight, release_weight_norm_graphs
 
 
 def _axis_rotation(axis: str, angle: torch.Tensor) -> torch.Tensor:
@@ -88,6 +90,7 @@ class MotionNetwork(nn.Module):
                 lin = nn.utils.weight_norm(lin)
             setattr(self, f"lin{l}", lin)
         self.activation = nn.LeakyReLU(0.2)
+        release_weight_norm_graphs(self)
 
     def _device(self):
         return self.lin0.bias.device
@@ -99,7 +102,10 @@ class MotionNetwork(nn.Module):
         for l in range(self.num_layers - 1):
             if l in self.skip_in:
                 x = torch.cat([x, inputs], 1) / np.sqrt(2)
-            x = getattr(self, f"lin{l}")(x)
+            lin = getattr(self, f"lin{l}")
+            # the weight-norm weight computed here, not by the module's pre-hook (which would keep
+            # this step's graph alive on the module: release_weight_norm_graphs)
+            x = F.linear(x, effective_weight(lin), lin.bias)
             if l < self.num_layers - 2:
                 x = self.activation(x)
         x = x * self.scale

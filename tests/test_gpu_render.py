@@ -59,6 +59,35 @@ def test_render_matches_reference_golden(name, mode):
             check_grad(n, gr, fx, rtol=2e-2, atol=2e-4 * (gr.abs().max().item() + 1e-3))
 
 
+@pytest.mark.parametrize("mode", FP32_MODES)
+@pytest.mark.parametrize("name", ["render_small_train", "render_full_train"])
+def test_render_golden_gradients_on_reference_samples(name, mode):
+    """The training fixtures on the reference's own sample positions (the fixture's z_vals,
+    the renderer's z_vals hook): no importance sample can move, so the per-sample outputs
+    are held at the field-level bar and every parameter gradient within 2e-3 of its
+    scale -- the bar of the pretrained case, not the sampler-path 2e-2 above."""
+    fx = fixture(name)
+    mods = build_modules(int(fx["seed"]), int(fx["dh_sdf"]), int(fx["dh_col"]), device=DEV)
+    r = _renderer(mods, mode)
+    g = lambda k: fx[k].to(DEV)  # noqa: E731
+    out = r(g("rays_o"), g("rays_d"), g("rays_d_norm"), g("t"), g("near"), g("far"),
+            cos_anneal_ratio=float(fx["car"]), it=0, eval=False, z_vals=g("z_vals"))
+    for k in ("color_fine", "depth_pred"):
+        err = (out[k].detach().cpu() - fx["out_" + k]).abs().max().item()
+        assert err <= TOL_RGB_DEPTH, (k, err)
+    for k, tol in (("weights", 1e-4), ("sdf", 1e-4), ("sampled_points", 1e-5)):
+        err = (out[k].detach().cpu() - fx["out_" + k]).abs().max().item()
+        assert err <= tol, (k, err)
+    nerr = (out["normals"].detach().cpu() - fx["out_normals"]).abs().max().item()
+    assert nerr <= 1e-3 * fx["out_normals"].abs().max().item(), nerr
+    loss = O.train_loss(out, fx["rgb_gt"].to(DEV))
+    assert abs(loss.item() - fx["loss"].item()) <= 1e-4 * abs(fx["loss"].item()) + 1e-5
+    params = named_params(*mods)
+    grads = torch.autograd.grad(loss, [p for _, p in params])
+    for (n, _), gr in zip(params, grads):
+        check_grad(n, gr, fx, rtol=2e-3, atol=2e-3 * (gr.abs().max().item() + 1e-6))
+
+
 def _oracle_case(R, dh, seed=55, mode="fp32"):
     g = torch.Generator().manual_seed(R)
     mods_cpu = build_modules(seed, dh, dh)
