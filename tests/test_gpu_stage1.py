@@ -31,7 +31,9 @@ N_IMAGES = 8  # world camera n // 2 = 4 (world_idx 'mid', train.py:85)
 R, H, W = 128, 48, 64
 # (loss rel., fields, poses / motion): fp32 modes: max |Δ| over the gradient's max |g|;
 # bf16 (operands rounded to 8 bits): relative L2 error of each gradient tensor
-BARS = {"fp32": (1e-4, 2e-3, 5e-3), "bf16x6": (1e-4, 2e-3, 5e-3), "bf16": (2e-2, 2.5e-1, 2.5e-1)}
+# bf16 at about twice the largest error measured over these cases on an MI355X
+# (profiles/r3_stage1_parity.jsonl: loss 8.2e-4, fields 6.6e-2, pose / motion 4.9e-2)
+BARS = {"fp32": (1e-4, 2e-3, 5e-3), "bf16x6": (1e-4, 2e-3, 5e-3), "bf16": (2e-3, 1.3e-1, 1e-1)}
 SCEN = {"hybrid": (True, True, {}),
         "stage1": (False, True, {"sdf_consistency_enable_pose_grad": True, "random_ref_interval": (1, 5, 10)}),
         "canonical": (True, False, {})}
