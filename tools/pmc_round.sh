@@ -25,7 +25,7 @@ timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $O/pf -o run --output-format c
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $O/pw -o run --output-format csv -- $B > /dev/null
 python3 $R/tools/sq_summary.py $O/p1/p1_counter_collection.csv $O/p2/p2_counter_collection.csv > $O/sq_summary.txt
 python3 $R/tools/pmc_summary.py $O/pf/run_counter_collection.csv $O/pw/run_counter_collection.csv $O/pmc.json
-for v in ${WGRAD_VARIANTS:-0 3}; do
+for v in ${WGRAD_VARIANTS:-0 1}; do
   COPENERF_WGRAD_KERNEL=$v timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/wab$v -o run --output-format csv -- python3 $R/tools/wgrad_ab.py > $O/wab$v.json
   COPENERF_WGRAD_KERNEL=$v timeout -s KILL 200 rocprofv3 --pmc $P1 -d $O/wabp$v -o p1 --output-format csv -- python3 $R/tools/wgrad_ab.py > /dev/null
   python3 $R/tools/sq_summary.py $O/wabp$v/p1_counter_collection.csv > $O/wab${v}_sq.txt
