@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libcopenerf.so"
 LIB_PATH = os.environ.get("COPENERF_LIB", os.path.join(_HERE, LIB_NAME))
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 c_f32p = ctypes.c_void_p  # device pointers are passed as integers
 c_i32 = ctypes.c_int32
@@ -122,6 +122,12 @@ SIGNATURES = {
     "cn_train_loss_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32]),
     "cn_train_loss": (c_i32, [c_i32, c_i32, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_f32, c_ptr, c_ptr,
                               c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr]),
+    "cn_stage1_workspace_bytes": (ctypes.c_size_t, [c_i32]),
+    "cn_stage1_fwd": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_f32,
+                              c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_ptr]),
+    "cn_stage1_bwd": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr,
+                              c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_ptr,
+                              c_ptr]),
 }
 
 _lock = threading.Lock()

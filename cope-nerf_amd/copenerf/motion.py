@@ -4,6 +4,7 @@
   euler_angles_to_matrix (XYZ)    utils_poses/pose_pytorch3d.py (pytorch3d convention)
   scene_flow_loss                 train.py:467-477 (sdf_loss)
   project_flow / warp_pixel       train.py:478-496, 235-244 (flow-RGB warp)
+  stage1_terms_fused              train.py:467-504 per-sample work in one HIP pass each way
   sdf_consistency_points          train.py:497-505
 
 The motion network maps a time step to an angular and a linear velocity.  It is
@@ -282,6 +283,96 @@ def scene_flow_loss(pts, normals, sdf_flows, weights, angular_velocity, velocity
     return _world(group) * torch.sum(torch.abs(lhs + sdf_flows) * w) / (den + 1e-10)
 
 
+def _rows(t, c):
+    """t viewed as [M, c] rows of a common leading dimension (the renderer's outputs are
+    column slices of its [M, 4] buffers), and that leading dimension."""
+    v = t.reshape(-1, c)
+    if v.stride(-1) != 1 or (v.shape[0] > 1 and v.stride(0) < c):
+        v = v.contiguous()
+    return v, (v.stride(0) if v.shape[0] > 1 else c)
+
+
+class _Stage1Terms(torch.autograd.Function):
+    """cn_stage1_fwd / cn_stage1_bwd: the per-sample work of the stage-1 losses in one
+    HIP pass each way (train.py:467-477 scene-flow residual sums, the per-ray weighted
+    point sums the flow projection of train.py:484-495 reduces to, and the world points
+    of the SDF-consistency query, train.py:502-504).  Outputs (num, sumw, ray_acc, x):
+    num = Σ|(ω × p + v)·n + f| w and sumw = Σw over the rank's samples (w detached, as
+    the reference's weights.detach()); ray_acc [R, 4] = (Σ_s w p, Σ_s w); x [M, 4] =
+    (cw2 (p, 1), t_world).  x carries gradient to cw2 and the points only when
+    x_grad (sdf_consistency_enable_pose_grad, train.py:496)."""
+
+    @staticmethod
+    def forward(ctx, pts, normals, flows, weights, mv, cw2, t_world, x_grad):
+        from . import _lib
+        R, S = weights.shape
+        p, ldp = _rows(pts, 3)
+        n, ldn = _rows(normals, 3)
+        f, ldf = _rows(flows, 1)
+        w = weights.contiguous()
+        mv = mv.contiguous()
+        cw2 = cw2.contiguous()
+        dev = w.device
+        sums = torch.empty(2, device=dev, dtype=torch.float32)
+        ray_acc = torch.empty(R, 4, device=dev, dtype=torch.float32)
+        x = torch.empty(R * S, 4, device=dev, dtype=torch.float32)
+        ws = torch.empty(_lib.load().cn_stage1_workspace_bytes(R) // 4, device=dev, dtype=torch.float32)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        _lib.call("cn_stage1_fwd", R, S, p.data_ptr(), ldp, n.data_ptr(), ldn, f.data_ptr(), ldf, w.data_ptr(),
+                  mv.data_ptr(), cw2.data_ptr(), float(t_world), ray_acc.data_ptr(), x.data_ptr(), 4,
+                  sums.data_ptr(), ws.data_ptr(), stream)
+        ctx.save_for_backward(p, n, f, w, mv, cw2)
+        ctx.meta = (R, S, ldp, ldn, ldf, bool(x_grad), pts.shape)
+        num, sumw = sums[0:1], sums[1:2]
+        ctx.mark_non_differentiable(sumw)
+        if not x_grad:
+            ctx.mark_non_differentiable(x)
+        return num, sumw, ray_acc, x
+
+    @staticmethod
+    def backward(ctx, g_num, _g_sumw, g_ray, g_x):
+        from . import _lib
+        p, n, f, w, mv, cw2 = ctx.saved_tensors
+        R, S, ldp, ldn, ldf, x_grad, pshape = ctx.meta
+        dev = w.device
+        need = ctx.needs_input_grad
+        g_num = torch.zeros(1, device=dev) if g_num is None else g_num.contiguous()
+        g_ray = None if g_ray is None else g_ray.contiguous()
+        g_x = g_x.contiguous() if (x_grad and g_x is not None) else None
+        dG = torch.empty(R * S, 4, device=dev, dtype=torch.float32)
+        dw = torch.empty(R, S, device=dev, dtype=torch.float32) if (need[3] and g_ray is not None) else None
+        dp = torch.empty(R * S, 3, device=dev, dtype=torch.float32) if need[0] else None
+        dmc = torch.empty(18, device=dev, dtype=torch.float32)
+        ws = torch.empty(_lib.load().cn_stage1_workspace_bytes(R) // 4, device=dev, dtype=torch.float32)
+        ptr = lambda t: 0 if t is None else t.data_ptr()
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        _lib.call("cn_stage1_bwd", R, S, p.data_ptr(), ldp, n.data_ptr(), ldn, f.data_ptr(), ldf, w.data_ptr(),
+                  mv.data_ptr(), cw2.data_ptr(), g_num.data_ptr(), ptr(g_ray), ptr(g_x), 4, dG.data_ptr(), 4,
+                  dG[:, 3:].data_ptr(), 4, ptr(dw), ptr(dp), 3, dmc.data_ptr(), ws.data_ptr(), stream)
+        dnormals = dG[:, :3].reshape(pshape) if need[1] else None
+        dflows = dG[:, 3:].reshape(*pshape[:-1], 1) if need[2] else None
+        dpts = dp.reshape(pshape) if dp is not None else None
+        dmv = dmc[:6] if need[4] else None
+        dcw2 = None
+        if need[5] and g_x is not None:
+            dcw2 = torch.cat([dmc[6:].view(3, 4), torch.zeros(1, 4, device=dev)], 0)
+        return dpts, dnormals, dflows, dw, dmv, dcw2, None, None
+
+
+def stage1_terms_fused(pts, normals, sdf_flows, weights, angular_velocity, velocity, cw2, t_world, x_grad,
+                       group=None):
+    """The fused stage-1 pass (cn_stage1_fwd/bwd) -> (sdf_loss, pbar [R, 3], wbar [R, 1],
+    x [M, 4]): sdf_loss as scene_flow_loss, the per-ray sums project_flow_sums takes and
+    the world points (with the world time step) of the SDF-consistency re-query."""
+    R = weights.shape[0]
+    mv = torch.cat([angular_velocity.reshape(3), velocity.reshape(3)])
+    num, sumw, ray_acc, x = _Stage1Terms.apply(pts, normals, sdf_flows, weights.reshape(R, -1), mv, cw2, t_world,
+                                               x_grad)
+    den = _allreduce_sum(sumw, group)
+    sdf_loss = (_world(group) * num / (den + 1e-10)).reshape(())
+    return sdf_loss, ray_acc[:, :3], ray_acc[:, 3:], x
+
+
 def project_flow(pts, weights, w2c, ref_camera_mat, scale_mat, normalized_pixels, img_hw):
     """Forward optical flow to reference frames (train.py:484-495): the
     weight-averaged sample point of each ray, mapped by the relative pose w2c
@@ -290,13 +381,18 @@ def project_flow(pts, weights, w2c, ref_camera_mat, scale_mat, normalized_pixels
     The reference maps every sample and then averages; by linearity
     Σ_s w (R p + t) = R (Σ_s w p) + (Σ_s w) t, so the per-ray sums are formed once
     and each frame costs O(R), not O(R·S) (no [T, R·S, 3] intermediate)."""
-    single = w2c.dim() == 2
-    if single:
-        w2c, ref_camera_mat = w2c[None], ref_camera_mat.reshape(1, 4, 4)
     R = normalized_pixels.shape[0]
     w = weights.reshape(R, -1, 1)
     pbar = torch.sum(w * pts.reshape(R, -1, 3), dim=1)   # [R, 3]
     wbar = torch.sum(w, dim=1)                           # [R, 1]
+    return project_flow_sums(pbar, wbar, w2c, ref_camera_mat, scale_mat, normalized_pixels, img_hw)
+
+
+def project_flow_sums(pbar, wbar, w2c, ref_camera_mat, scale_mat, normalized_pixels, img_hw):
+    """project_flow from the per-ray sums pbar = Σ_s w p [R, 3], wbar = Σ_s w [R, 1]."""
+    single = w2c.dim() == 2
+    if single:
+        w2c, ref_camera_mat = w2c[None], ref_camera_mat.reshape(1, 4, 4)
     wp = torch.einsum("tij,rj->tri", w2c[:, :3, :3], pbar) + wbar[None] * w2c[:, None, :3, 3]  # [T, R, 3]
     KS = scale_mat.reshape(-1, 4, 4)[0, :3, :3] @ ref_camera_mat[:, :3, :3]  # [T, 3, 3]
     pix = torch.einsum("tij,trj->tri", KS, wp)

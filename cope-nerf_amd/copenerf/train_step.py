@@ -35,13 +35,16 @@ single-GPU gradient of the loss over all ranks' rays.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 import torch.distributed as dist
 
 from .fields import RenderingNetwork, SDFNetwork, SingleVarianceNetwork
 from .losses import EdgePreservingSmoothnessLoss, SmoothnessLoss, eikonal_loss, rgb_l1, train_losses
-from .motion import MotionNetwork, affine_points, flow_rgb_loss, masked_chain, project_flow, scene_flow_loss
+from .motion import (MotionNetwork, affine_points, flow_rgb_loss, masked_chain, project_flow, project_flow_sums,
+                     scene_flow_loss, stage1_terms_fused)
 from .rays import PoseRetriever, get_patch_indices, intrinsics_ndc, inv4x4, pixels_from_indices, world_rays
 from .renderer import NeuSRenderer
 
@@ -190,6 +193,9 @@ class SyntheticTrainer:
         self.renderer.expose_sdf_pack = stage1  # the stage-1 SDF re-query reuses the step's weight images
         self.params = list(self.sdf.parameters()) + list(self.var.parameters()) + list(self.col.parameters())
         self.joint_pose, self.stage1 = joint_pose, stage1
+        # stage-1 per-sample terms in the fused HIP pass; COPENERF_STAGE1_FUSED=0 keeps the
+        # torch expressions (device ops too; for A/B measurement and parity tests)
+        self.stage1_fused = os.environ.get("COPENERF_STAGE1_FUSED", "1") != "0"
         self.n_images = n_images
         self.nst = self.cfg["nb_sample_timestep"]
         wi = self.cfg["world_idx"]
@@ -315,8 +321,6 @@ class SyntheticTrainer:
         R = batch["rgb_gt"].shape[0]
         # one motion-network evaluation: the K*n Euler time steps and the frame's own time
         P, (omega, vel) = self.motion.batched_relative_poses(self.steps_grid, self.dts, extra_t=self.sched.t)
-        sdf_loss = scene_flow_loss(out["sampled_points"], out["normals"], out["sdf_flows"], out["weights"], omega,
-                                   vel, group=grp)
         K = P.shape[0]
         # flow-RGB: reference frame i + j maps through w2c_j = P[i+j-1] @ ... @ P[i]
         # (compute_w2c_mappings(c2c)[ref - i], train.py:483): the running product up to the
@@ -331,21 +335,32 @@ class SyntheticTrainer:
             chain.append(cur)
         w2c = torch.stack([chain[j - 1] for j in self.cfg["random_ref_interval"]])
         refc = torch.clamp(ref, max=n - 1)
-        flows = project_flow(out["sampled_points"], out["weights"], w2c, self.camera_mats.index_select(0, refc),
-                             self.I, batch["pixn"], (self.H, self.W))
-        per = flow_rgb_loss(flows, batch["pix"], self.images.index_select(0, refc), batch["rgb_gt"], group=grp)
-        flow_rgb = torch.where(valid, per, torch.zeros_like(per)).sum() / 3.0
         # SDF consistency at the world frame (train.py:495-505): with
         # sdf_consistency_enable_pose_grad (most dataset configs, e.g. Co3D/skateboard.yaml:27)
         # the loss reaches the motion network through c2c, i.e. through the SDF's input
         # gradient at the world points; default.yaml:62 detaches the chain
         w = self.world_cam_idx
-        with torch.set_grad_enabled(bool(self.cfg["sdf_consistency_enable_pose_grad"]) and torch.is_grad_enabled()):
+        pose_grad = bool(self.cfg["sdf_consistency_enable_pose_grad"]) and torch.is_grad_enabled()
+        with torch.set_grad_enabled(pose_grad):
             lo, hi = torch.clamp(img, max=w), torch.clamp(img, min=w)
             c2c = masked_chain(P, lo, hi)
             cw2 = torch.where(img.view(1, 1) >= w, inv4x4(c2c), c2c)
-            pw = affine_points(out["sampled_points"].detach().reshape(-1, 3), cw2)
-            x = torch.cat([pw, torch.full_like(pw[:, :1], self.world_time_step)], 1)
+        pts = out["sampled_points"]
+        if self.stage1_fused:
+            # one HIP pass each way over the samples (cn_stage1_fwd / cn_stage1_bwd)
+            sdf_loss, pbar, wbar, x = stage1_terms_fused(pts, out["normals"], out["sdf_flows"], out["weights"], omega,
+                                                         vel, cw2, self.world_time_step, pose_grad, group=grp)
+            flows = project_flow_sums(pbar, wbar, w2c, self.camera_mats.index_select(0, refc), self.I, batch["pixn"],
+                                      (self.H, self.W))
+        else:  # the same terms as torch expressions (A/B and tests: COPENERF_STAGE1_FUSED=0)
+            sdf_loss = scene_flow_loss(pts, out["normals"], out["sdf_flows"], out["weights"], omega, vel, group=grp)
+            flows = project_flow(pts, out["weights"], w2c, self.camera_mats.index_select(0, refc), self.I,
+                                 batch["pixn"], (self.H, self.W))
+            with torch.set_grad_enabled(pose_grad):
+                pw = affine_points(pts.reshape(-1, 3), cw2)
+                x = torch.cat([pw, torch.full_like(pw[:, :1], self.world_time_step)], 1)
+        per = flow_rgb_loss(flows, batch["pix"], self.images.index_select(0, refc), batch["rgb_gt"], group=grp)
+        flow_rgb = torch.where(valid, per, torch.zeros_like(per)).sum() / 3.0
         # SDFNetwork.sdf (train.py:504) on the weights the renderer packed for this step
         pack, self.renderer.last_sdf_pack = self.renderer.last_sdf_pack, None
         sdf_w = self.sdf.field(x, want_feat=False, want_grad=False, packed=pack)[0]

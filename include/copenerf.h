@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define CN_ABI_VERSION 6
+#define CN_ABI_VERSION 7
 
 typedef void* cn_stream_t; /* hipStream_t */
 
@@ -406,6 +406,38 @@ int cn_train_loss(int32_t R, int32_t patch, int64_t M, const float* color, const
                   const float* normals, int64_t ld_n, const float* weights, float gamma, float* loss,
                   float* dcolor, float* ddepth, float* dnormals, int64_t ld_dn, int32_t* nonfinite,
                   void* workspace, int64_t workspace_bytes, cn_stream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * Stage-1 per-sample terms (train.py:467-505), R rays of S samples, M = R*S,
+ * in one pass each way (replaces the ~40 torch ops of train.py:468-477, the
+ * per-ray sums the flow projection reduces to (train.py:484-495) and the
+ * point transform of the SDF-consistency term (train.py:502-504)):
+ *   pts [M][ld_p], normals [M][ld_n] (columns 0..2), flows [M] (stride ld_f),
+ *   weights [R][S]; mv: DEVICE [6] = (angular_velocity, velocity);
+ *   cw2: DEVICE [4][4] (row-major) or null -- camera-of-frame -> world-camera;
+ * forward:
+ *   sums [2]       = (sum_m |(w x p_m + v) . n_m + f_m| w_m, sum_m w_m)
+ *   ray_acc [R][4] = (sum_s w p, sum_s w) per ray (16B aligned)
+ *   x_out [M][ld_x] (nullable, needs cw2) = (cw2 (p_m, 1))[0..2], t_world
+ * backward (g_num: DEVICE [1] = dL/d sums[0]; the weights are detached there,
+ * as in the reference; d_ray [R][4] and dx [M][ld_dx] (columns 0..2) nullable):
+ *   dnormals [M][ld_dn], dflows [M] (stride ld_df): written;
+ *   dweights [R][S] (nullable) = d_ray . (p, 1);
+ *   dpts [M][ld_dp] (nullable): written;
+ *   dmv_dcw2 [18] = (dL/d mv [6], dL/d cw2 rows 0..2 [12]).
+ * The cross-ray sums are per-workgroup partials reduced in a fixed order
+ * (bitwise reproducible); workspace: cn_stage1_workspace_bytes(R).
+ * ------------------------------------------------------------------------ */
+size_t cn_stage1_workspace_bytes(int32_t R);
+int cn_stage1_fwd(int32_t R, int32_t S, const float* pts, int64_t ld_p, const float* normals, int64_t ld_n,
+                  const float* flows, int64_t ld_f, const float* weights, const float* mv, const float* cw2,
+                  float t_world, float* ray_acc, float* x_out, int64_t ld_x, float* sums, float* workspace,
+                  cn_stream_t stream);
+int cn_stage1_bwd(int32_t R, int32_t S, const float* pts, int64_t ld_p, const float* normals, int64_t ld_n,
+                  const float* flows, int64_t ld_f, const float* weights, const float* mv, const float* cw2,
+                  const float* g_num, const float* d_ray, const float* dx, int64_t ld_dx, float* dnormals,
+                  int64_t ld_dn, float* dflows, int64_t ld_df, float* dweights, float* dpts, int64_t ld_dp,
+                  float* dmv_dcw2, float* workspace, cn_stream_t stream);
 
 #ifdef __cplusplus
 }
