@@ -1,0 +1,117 @@
+"""Evaluation-time test-pose optimisation (eval.py:44-93) on the HIP renderer
+(copenerf.evaluation.EvalPoseOptimizer):
+  * the pose gradient of eval.py's loss (compute_loss's L1 rgb term, cos_anneal_ratio 1,
+    world time step) through the HIP backward and make_c2w against the CPU oracle's
+    autograd on identical rays and sample positions;
+  * the loop itself: a test view rendered from a known pose is re-found from a perturbed
+    start (the epoch L2 falls, the pose error shrinks), the networks are left untouched
+    and their requires_grad restored, and the saved poses load back (eval.py:88-91)."""
+import os
+import sys
+import tempfile
+
+import pytest
+import torch
+
+from helpers import REN_CFG, build_modules, oracle_params
+from oracle import neus_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+H, W = 24, 32
+CFG = dict(n_training_points=512, rgb_weight=[1.0, 1.0], eikonal_weight=[0.1, 0.1], sdf_weight=[0.1, 0.1],
+           flow_rgb_weight=[7.5, 7.5], sdf_consistency_weight=[0.0, 1.0], edge_aware_smoothness_weight=[1.0, 0.0],
+           smoothness_weight=[1e-4, 0.0])
+
+
+def _setup(seed=31):
+    sys.path.insert(0, os.path.join(ROOT, "cope-nerf_amd"))
+    from model import NeuSRenderer, Trainer
+    sdf, col, var = build_modules(seed, device=DEV)
+    renderer = NeuSRenderer(None, sdf, var, col, None, **REN_CFG).set_mfma_dtype("bf16x6")
+    tr = Trainer(renderer, None, None, CFG, device=torch.device(DEV), total_nb_images=5,
+                 cfg_all={"rendering": {"depth_range": [0.01, 3.0]}}, logger=None, gt_depths=None, world_cam_idx=2)
+    f = 0.9 * W
+    K = torch.tensor([[2 * f / W, 0, 0, 0], [0, -2 * f / H, 0, 0], [0, 0, -1, 0], [0, 0, 0, 1.0]], device=DEV)
+    base = torch.eye(4, device=DEV)
+    base[2, 3] = -1.6  # world -> camera: the camera 1.6 in front of the unit-scale SDF, looking down -z
+    return renderer, tr, K, base
+
+
+def test_eval_pose_gradient_matches_oracle():
+    from copenerf.rays import PoseRetriever, world_rays
+    renderer, tr, K, base = _setup()
+    for p in renderer.parameters():
+        p.requires_grad_(False)
+    poses = PoseRetriever(1, init_c2w=base[None].clone()).to(DEV)
+    with torch.no_grad():
+        poses.r.copy_(torch.tensor([[0.01, -0.02, 0.015]]))
+        poses.t.copy_(torch.tensor([[0.02, 0.01, -0.03]]))
+    g = torch.Generator().manual_seed(4)
+    R = 256
+    pn = (torch.rand(R, 2, generator=g) * 2 - 1).to(DEV)
+    gt = torch.rand(R, 3, generator=g)
+    t = torch.tensor([0.0])
+    # oracle: same pose arithmetic on the CPU, rays into the oracle renderer
+    P, Pc, varc, _ = oracle_params(*build_modules(31))
+    pc = PoseRetriever(1, init_c2w=base[None].cpu().clone())
+    pc.load_state_dict({k: v.cpu() for k, v in poses.state_dict().items()})
+    o, d, nrm = world_rays(pn.cpu(), K.cpu(), pc(0), torch.eye(4))
+    near, far = torch.full((R, 1), 0.01), torch.full((R, 1), 3.0)
+    z = O.hierarchical_z(P, o.detach(), d.detach(), t, near, far, 64, 64, 4, torch.rand(R, 64, generator=g))
+    ref = O.render_core(P, Pc, varc, o, d, nrm, t, z, (far[0, 0] - near[0, 0]) / 64, 1.0)
+    loss_ref = torch.sum(torch.abs(ref["color_fine"] - gt)) / R  # compute_loss's loss_rgb
+    gr_ref, gt_ref = torch.autograd.grad(loss_ref, [pc.r, pc.t])
+    # HIP: the same rays from the device pose, identical sample positions
+    o2, d2, n2 = world_rays(pn, K, poses(0), torch.eye(4, device=DEV))
+    out = renderer(o2, d2, n2, t.to(DEV), near.to(DEV), far.to(DEV), cos_anneal_ratio=1.0, it=0, eval=False,
+                   z_vals=z.to(DEV))
+    loss = tr.compute_loss(None, out["color_fine"], gt.to(DEV), 0.0, 0.0, 0.0, 0.0, 0.0, 0.0)["loss_rgb"]
+    gr, gtr = torch.autograd.grad(loss, [poses.r, poses.t])
+    assert abs(loss.item() - loss_ref.item()) <= 1e-4 * abs(loss_ref.item())
+    for a, b, n in ((gr, gr_ref, "r"), (gtr, gt_ref, "t")):
+        scale = b.abs().max().item()
+        assert scale > 1e-4 and (a.cpu() - b).abs().max().item() <= 2e-3 * scale, (n, a, b)
+
+
+def test_eval_optimization_refinds_a_perturbed_pose():
+    from copenerf.evaluation import EvalPoseOptimizer, mse2psnr
+    from copenerf.inference import render_image
+    from copenerf.rays import PoseRetriever
+    renderer, tr, K, base = _setup()
+    true = PoseRetriever(1, init_c2w=base[None].clone()).to(DEV)
+    with torch.no_grad():
+        true.r.copy_(torch.tensor([[0.015, -0.01, 0.01]]))
+        true.t.copy_(torch.tensor([[0.02, -0.015, 0.01]]))
+        target = render_image(renderer, K, true(0), torch.eye(4, device=DEV), (H, W), torch.tensor([0.0]),
+                              depth_range=(0.01, 3.0))["rgb"]
+    assert target.std().item() > 1e-2  # the view sees the surface
+    data = {"img": target.permute(2, 0, 1)[None].contiguous(), "img.camera_mat": K[None], "img.scale_mat":
+            torch.eye(4, device=DEV)[None], "img.idx": torch.tensor([3]), "img.ref_imgs": target.new_zeros(1, 3, H, W),
+            "img.ref_idxs": [torch.tensor([4])]}
+    before = [p.detach().clone() for p in renderer.parameters()]
+    flags = [p.requires_grad for p in renderer.parameters()]
+    ev = EvalPoseOptimizer(tr, [3], base[None].clone(), 0.0,
+                           {"eval_pose_epoch": 60, "eval_pose_lr": 1e-2, "eval_pose_scheduler_gamma": 0.5})
+    err0 = (torch.cat([true.r, true.t], 1) - torch.cat([ev.pose_retriever_test.r, ev.pose_retriever_test.t], 1)).norm()
+    psnrs = []
+    with tempfile.TemporaryDirectory() as d:
+        torch.manual_seed(9)
+        ev.eval_optimization([data], out_dir=d, on_epoch=lambda i, p: psnrs.append(p))
+        saved = os.path.join(d, "models", "weights", "model_eval_pose.pt")
+        assert os.path.isfile(saved)
+        ev2 = EvalPoseOptimizer(tr, [3], base[None].clone(), 0.0,
+                                {"eval_pose_epoch": 60, "eval_pose_lr": 1e-2, "eval_pose_scheduler_gamma": 0.5})
+        ev2.eval_optimization([data], out_dir=d)  # found: loaded, not optimised
+        for a, b in zip(ev.pose_retriever_test.parameters(), ev2.pose_retriever_test.parameters()):
+            assert torch.equal(a, b)
+    err1 = (torch.cat([true.r, true.t], 1) - torch.cat([ev.pose_retriever_test.r, ev.pose_retriever_test.t], 1)).norm()
+    assert len(psnrs) == 60 and all(p is not None for p in psnrs)
+    print('psnr', psnrs[:3], psnrs[-3:], 'pose error', err0.item(), err1.item())
+    assert sum(psnrs[-5:]) / 5 > sum(psnrs[:5]) / 5 + 3.0, psnrs
+    assert err1.item() < 0.6 * err0.item(), (err0.item(), err1.item())
+    assert all(torch.equal(a, b) for a, b in zip(before, renderer.parameters()))
+    assert [p.requires_grad for p in renderer.parameters()] == flags
+    assert ev.scheduler.get_last_lr()[0] < 1e-2  # MultiStepLR milestones every num_epoch/5 epochs
+    assert float(mse2psnr(1e-2)) == pytest.approx(20.0)
