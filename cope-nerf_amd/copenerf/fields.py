@@ -423,8 +423,10 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
     dWs[L8], dbs[L8] = dW8, db8
     share = want_dx and not second  # Z_l == P_l: dx from the parameter adjoint chain
     PE = _empty(M, KE, dev) if (share and sk >= 0) else None
+    lane = ops.SideLane(dev)
     for l in range(L8 - 1, -1, -1):
         Zl = Z
+        lane.fork()  # Z_l is ready: its weight gradient may run beside the next adjoint GEMM
         if l > 0:
             Z = _empty(M, HL, dev)
             if share and l == sk:  # + the embedding columns of the skip input (sdf_input_grad's PE)
@@ -440,17 +442,23 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
                            kalg=lay.out_dim[l], **second_order(l - 1))
         dW = torch.empty(lay.out_dim[l], lay.in_dim[l], device=dev)
         db = torch.empty(lay.out_dim[l], device=dev)
-        ops.wgrad(Zl, U[l], lay.out_dim[l], lay.in_dim[l], dW, db=db,
-                  Y1=S[l] if second else None, X1=Ud[l] if second else None, mode=wmode)
+        with lane:
+            ops.wgrad(Zl, U[l], lay.out_dim[l], lay.in_dim[l], dW, db=db,
+                      Y1=S[l] if second else None, X1=Ud[l] if second else None, mode=wmode)
+        lane.hold(Zl)
         dWs[l], dbs[l] = dW, db
     if not want_dx:
+        lane.join()
         return dWs, dbs
     if not share:
-        return dWs, dbs, sdf_input_grad(lay, pk, st, dsdf, dfeat, dh=dh)
+        dx = sdf_input_grad(lay, pk, st, dsdf, dfeat, dh=dh)
+        lane.join()
+        return dWs, dbs, dx
     P0 = _empty(M, KE, dev)  # Zl is Z_0 here
     ops.linear(Zl, pk.Bt[0], lay.E, rup(lay.out_dim[0], 32), P0, EPI_STORE, nzero=KE, kalg=lay.out_dim[0])
     dx = _empty(M, 4, dev)
     ops.sdf_grad_assemble(lay.multires, lay.scale, U[0], P0, PE, dx)
+    lane.join()
     return dWs, dbs, dx
 
 
@@ -719,10 +727,14 @@ class _ColorFieldFn(torch.autograd.Function):
         dbs[n - 1] = torch.empty(3, device=dev)
         dZ = _empty(M, lay.HL, dev)
         ops.rgb_head_bwd(drgb, rgb, H[-1], lay.in_dim[n - 1], pk.W3, dZ, dWs[n - 1], dbs[n - 1])
+        lane = ops.SideLane(dev)
         for l in range(n - 2, 0, -1):
             dW = torch.empty(lay.out_dim[l], lay.in_dim[l], device=dev)
             db = torch.empty(lay.out_dim[l], device=dev)
-            ops.wgrad(dZ, H[l - 1], lay.out_dim[l], lay.in_dim[l], dW, db=db, mode=wmode)
+            lane.fork()
+            with lane:  # beside the next adjoint GEMM (both only read dZ_l)
+                ops.wgrad(dZ, H[l - 1], lay.out_dim[l], lay.in_dim[l], dW, db=db, mode=wmode)
+            lane.hold(dZ)
             dWs[l], dbs[l] = dW, db
             dZp = _empty(M, lay.HL, dev)
             ops.linear(dZ, pk.Bt[l], lay.out_dim[l - 1], rup(lay.out_dim[l], 32), dZp, EPI_BWD_RELU, aux0=H[l - 1],
@@ -731,13 +743,13 @@ class _ColorFieldFn(torch.autograd.Function):
         o0 = lay.out_dim[0]
         dWf = torch.empty(o0, lay.F, device=dev)
         db0 = torch.empty(o0, device=dev)
-        ops.wgrad(dZ, feat, o0, lay.F, dWf, db=db0, mode=wmode)
         dWx = torch.empty(o0, lay.KX, device=dev)
-        ops.wgrad(dZ, ext, o0, lay.KX, dWx, mode=wmode)
+        lane.fork()
+        with lane:  # beside the input-gradient GEMMs below
+            ops.wgrad(dZ, feat, o0, lay.F, dWf, db=db0, mode=wmode)
+            ops.wgrad(dZ, ext, o0, lay.KX, dWx, mode=wmode)
+        lane.hold(dZ)
         P, V, Gd = lay.P, lay.V, lay.Gd
-        # back to the reference column order [pts | emb(dirs) | gradients | feature]
-        dWs[0] = torch.cat([dWx[:, Gd:Gd + P], dWx[:, Gd + P:Gd + P + V], dWx[:, 0:Gd], dWf], 1)
-        dbs[0] = db0
         dfeat = None
         if ctx.needs_input_grad[4]:
             dfeat = _empty(M, lay.F, dev)
@@ -758,6 +770,10 @@ class _ColorFieldFn(torch.autograd.Function):
         elif ctx.needs_input_grad[3]:
             dG = _empty(M, Gd, dev)
             ops.row_head(dZ, o0, pk.Wg, None, Gd, 0, dG)
+        lane.join()
+        # back to the reference column order [pts | emb(dirs) | gradients | feature]
+        dWs[0] = torch.cat([dWx[:, Gd:Gd + P], dWx[:, Gd + P:Gd + P + V], dWx[:, 0:Gd], dWf], 1)
+        dbs[0] = db0
         grads = []
         for w, b in zip(dWs, dbs):
             grads += [w, b]

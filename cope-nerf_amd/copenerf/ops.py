@@ -77,6 +77,61 @@ def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
+_SIDE_STREAMS = {}
+
+
+class SideLane(object):
+    """Weight gradients on a second stream beside the adjoint chain that produced their
+    operands (a layer's dW needs Z_l, which the next adjoint GEMM also reads: the two are
+    independent, so the MFMA-bound weight gradient runs under the HBM-bound adjoint).
+    fork() records the point where the next side launch's inputs are ready; `with lane:`
+    runs launches on the side stream after it; hold() keeps buffers alive (the caching
+    allocator must not hand their memory out before the side stream is done); join() makes
+    the current stream wait for everything launched on the side.  Fork / join are stream
+    events, so a graph capture records them as graph edges.  Off unless COPENERF_WGRAD_STREAM=1:
+    then every method is a no-op and the launches stay on the current stream."""
+
+    enabled = os.environ.get("COPENERF_WGRAD_STREAM", "0") != "0"
+
+    def __init__(self, device):
+        self.side = None
+        if self.enabled:
+            key = (torch.device(device).index, torch.cuda.current_stream(device).cuda_stream)
+            if key not in _SIDE_STREAMS:
+                _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
+            self.side = _SIDE_STREAMS[key]
+        self.ev = None
+        self.held = []
+        self._ctx = None
+
+    def fork(self):
+        if self.side is not None:
+            self.ev = torch.cuda.Event()
+            self.ev.record()
+
+    def __enter__(self):
+        if self.side is not None:
+            self.side.wait_event(self.ev)
+            self._ctx = torch.cuda.stream(self.side)
+            self._ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self._ctx is not None:
+            self._ctx.__exit__(*exc)
+            self._ctx = None
+        return False
+
+    def hold(self, *tensors):
+        if self.side is not None:
+            self.held.extend(t for t in tensors if t is not None)
+
+    def join(self):
+        if self.side is not None:
+            torch.cuda.current_stream().wait_stream(self.side)
+            self.held.clear()
+
+
 def _need(t, name, *, ndim=2):
     if t is None:
         return
