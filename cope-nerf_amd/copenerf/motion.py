@@ -322,7 +322,7 @@ class _Stage1Terms(torch.autograd.Function):
                   mv.data_ptr(), cw2.data_ptr(), float(t_world), ray_acc.data_ptr(), x.data_ptr(), 4,
                   sums.data_ptr(), ws.data_ptr(), stream)
         ctx.save_for_backward(p, n, f, w, mv, cw2)
-        ctx.meta = (R, S, ldp, ldn, ldf, bool(x_grad), pts.shape)
+        ctx.meta = (R, S, ldp, ldn, ldf, bool(x_grad), (pts.shape, normals.shape, flows.shape))
         num, sumw = sums[0:1], sums[1:2]
         ctx.mark_non_differentiable(sumw)
         if not x_grad:
@@ -333,7 +333,7 @@ class _Stage1Terms(torch.autograd.Function):
     def backward(ctx, g_num, _g_sumw, g_ray, g_x):
         from . import _lib
         p, n, f, w, mv, cw2 = ctx.saved_tensors
-        R, S, ldp, ldn, ldf, x_grad, pshape = ctx.meta
+        R, S, ldp, ldn, ldf, x_grad, (pshape, nshape, fshape) = ctx.meta
         dev = w.device
         need = ctx.needs_input_grad
         g_num = torch.zeros(1, device=dev) if g_num is None else g_num.contiguous()
@@ -349,8 +349,8 @@ class _Stage1Terms(torch.autograd.Function):
         _lib.call("cn_stage1_bwd", R, S, p.data_ptr(), ldp, n.data_ptr(), ldn, f.data_ptr(), ldf, w.data_ptr(),
                   mv.data_ptr(), cw2.data_ptr(), g_num.data_ptr(), ptr(g_ray), ptr(g_x), 4, dG.data_ptr(), 4,
                   dG[:, 3:].data_ptr(), 4, ptr(dw), ptr(dp), 3, dmc.data_ptr(), ws.data_ptr(), stream)
-        dnormals = dG[:, :3].reshape(pshape) if need[1] else None
-        dflows = dG[:, 3:].reshape(*pshape[:-1], 1) if need[2] else None
+        dnormals = dG[:, :3].reshape(nshape) if need[1] else None
+        dflows = dG[:, 3:].reshape(fshape) if need[2] else None
         dpts = dp.reshape(pshape) if dp is not None else None
         dmv = dmc[:6] if need[4] else None
         dcw2 = None
