@@ -118,36 +118,51 @@ __global__ void sdf_tangent_prep_kernel(int M, int L, float scale, int G, const 
     }
 }
 
-// Colour-network extras: [g(4) | pts_time(4) | embed_view(dirs) (3+6L) | 0...].
-__global__ void color_extras_kernel(int M, const float* __restrict__ Gm, int64_t ld_g, const float* __restrict__ pts,
-                                    int64_t ld_p, const float* __restrict__ dirs, int64_t ld_d, int dir_div, int L,
-                                    int G, float* ext, int64_t ld_ext) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t m = idx / G;
-    const int g = idx % G;
-    if (m >= M) return;
-    floatx4 o = {0.f, 0.f, 0.f, 0.f};
-    if (g == 0) {
-        o = ld4(Gm + m * ld_g);
-    } else if (g == 1) {
-        o = ld4(pts + m * ld_p);
-    } else {
-        const int nv = 3 + 6 * L;
-        const float* d = dirs + (m / dir_div) * ld_d;
-        for (int q = 0; q < 4; ++q) {
-            const int e = 4 * (g - 2) + q;
-            if (e >= nv) break;
+// Colour-network extras, rows [g(4) | pts_time(4) | embed_view(dirs) (3+6L) | 0...]: the view encoding (sin / cos of the ray direction at
+// 2^k) is computed once per ray into LDS, not once per sample (dir_div samples share a ray),
+// then every row is a copy.  kExtRows rows per workgroup, so at most kExtRows / dir_div + 2 rays.
+constexpr int kExtRows = 64;
+__global__ void __launch_bounds__(256) color_extras_kernel(int M, const float* __restrict__ Gm, int64_t ld_g,
+                                                           const float* __restrict__ pts, int64_t ld_p,
+                                                           const float* __restrict__ dirs, int64_t ld_d, int dir_div,
+                                                           int L, int G, float* ext, int64_t ld_ext) {
+    __shared__ __attribute__((aligned(16))) float emb[kExtRows + 1][32];
+    const int64_t m0 = (int64_t)blockIdx.x * kExtRows;
+    const int64_t r0 = m0 / dir_div;
+    const int64_t mlast = min((int64_t)M, m0 + kExtRows) - 1;
+    const int nr = (int)(mlast / dir_div - r0) + 1;
+    const int nv = 3 + 6 * L;
+    for (int i = threadIdx.x; i < nr * 32; i += blockDim.x) {
+        const int rr = i >> 5, e = i & 31;
+        float v = 0.f;
+        if (e < nv) {
+            const float* d = dirs + (r0 + rr) * ld_d;
             if (e < 3) {
-                o[q] = d[e];
+                v = d[e];
             } else {
                 const int j = e - 3;
                 const int k = j / 6, w = j % 6;
                 const float t = d[w % 3] * (float)(1 << k);
-                o[q] = (w < 3) ? sinf(t) : cosf(t);
+                v = (w < 3) ? sinf(t) : cosf(t);
             }
         }
+        emb[rr][e] = v;
     }
-    st4(ext + m * ld_ext + 4 * g, o);
+    __syncthreads();
+    for (int i = threadIdx.x; i < kExtRows * G; i += blockDim.x) {
+        const int64_t m = m0 + i / G;
+        const int g = i % G;
+        if (m >= M) break;  // rows grow with i
+        floatx4 o = {0.f, 0.f, 0.f, 0.f};
+        if (g == 0) {
+            o = ld4(Gm + m * ld_g);
+        } else if (g == 1) {
+            o = ld4(pts + m * ld_p);
+        } else if (4 * (g - 2) < 32) {
+            o = *reinterpret_cast<const floatx4*>(&emb[m / dir_div - r0][4 * (g - 2)]);
+        }
+        st4(ext + m * ld_ext + 4 * g, o);
+    }
 }
 
 // Gradient of the per-ray view directions through the view encoding.  Block =
@@ -244,10 +259,10 @@ extern "C" int cn_color_extras(int32_t M, const float* G, int64_t ld_g, const fl
                "cn_color_extras: kpad=%d too small for multires_view=%d", kpad, multires_view);
     CN_REQUIRE(al16(G) && al16(pts) && al16(ext) && ld_g % 4 == 0 && ld_p % 4 == 0 && ld_ext % 4 == 0,
                CN_ERR_ALIGN, "cn_color_extras: alignment");
+    CN_REQUIRE(3 + 6 * multires_view <= 32, CN_ERR_UNSUPPORTED, "cn_color_extras: multires_view=%d", multires_view);
     if (M == 0) return CN_OK;
     const int Gc = kpad / 4;
-    const int64_t tot = (int64_t)M * Gc;
-    color_extras_kernel<<<(int)((tot + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+    color_extras_kernel<<<cdiv(M, kExtRows), 256, 0, (hipStream_t)stream>>>(
         M, G, ld_g, pts, ld_p, dirs, ld_d, dir_div, multires_view, Gc, ext, ld_ext);
     return check_launch("cn_color_extras");
 }

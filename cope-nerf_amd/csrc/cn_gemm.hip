@@ -1466,8 +1466,10 @@ extern "C" int cn_softplus_adjoint(int32_t M, int32_t N, const float* D, int64_t
                        (size_t)workspace_bytes >= cn_softplus_adjoint_workspace_bytes(M, N),
                    CN_ERR_SHAPE, "cn_softplus_adjoint: column sums need N <= 1024 and the workspace");
         if (M == 0) {
-            const int rc = launch_slab_reduce(workspace, 0, N, 1, N, N, cs_out, N, 1.0f, 0, (hipStream_t)stream);
-            return (rc || !rs_out) ? rc : launch_slab_reduce(workspace, 0, 1, 1, 1, 1, rs_out, 1, 1.0f, 0, (hipStream_t)stream);
+            // no rows: zero sums (one reduction launch for both)
+            return launch_slab_jobs(slab_job(workspace, 0, N, 1, N, N, cs_out, N, 1.0f, 0),
+                                    rs_out ? slab_job(workspace, 0, 1, 1, 1, 1, rs_out, 1, 1.0f, 0) : SlabJob{},
+                                    (hipStream_t)stream);
         }
         const int nblk = cdiv(M, kSaRows);
         hipStream_t s = (hipStream_t)stream;
@@ -1478,9 +1480,8 @@ extern "C" int cn_softplus_adjoint(int32_t M, int32_t N, const float* D, int64_t
         int rc = check_launch("cn_softplus_adjoint");
         if (rc) return rc;
         const float dv = cs_div == 0.f ? 1.f : cs_div;
-        rc = launch_slab_reduce(workspace, nblk, N, 1, N, N, cs_out, N, dv, 0, s);
-        if (rc || !rs_out) return rc;
-        return launch_slab_reduce(rpart, nblk, 1, 1, 1, 1, rs_out, 1, dv, 0, s);
+        return launch_slab_jobs(slab_job(workspace, nblk, N, 1, N, N, cs_out, N, dv, 0),
+                                rs_out ? slab_job(rpart, nblk, 1, 1, 1, 1, rs_out, 1, dv, 0) : SlabJob{}, s);
     }
     if ((int64_t)M * N == 0) return CN_OK;
     const int64_t tot = (int64_t)M * (N / 4);
@@ -1508,9 +1509,8 @@ extern "C" int cn_rgb_head_bwd(int32_t M, int32_t K, const float* drgb, const fl
     rgb_head_bwd_kernel<<<nblk, 256, 0, s>>>(M, K, drgb, rgb, H3, ld_h, W3, dZ2, ld_dz, workspace);
     int rc = check_launch("cn_rgb_head_bwd");
     if (rc) return rc;
-    rc = launch_slab_reduce(workspace, nblk, 4 * K, 3, K, K, dW3, K, 1.0f, 0, s);
-    if (rc) return rc;
-    return launch_slab_reduce(workspace + 3 * K, nblk, 4 * K, 1, 3, 3, db3, 3, 1.0f, 0, s);
+    return launch_slab_jobs(slab_job(workspace, nblk, 4 * K, 3, K, K, dW3, K, 1.0f, 0),
+                            slab_job(workspace + 3 * K, nblk, 4 * K, 1, 3, 3, db3, 3, 1.0f, 0), s);
 }
 
 extern "C" size_t cn_colsum_workspace_bytes(int32_t M, int32_t K) {

@@ -111,6 +111,17 @@ __device__ __forceinline__ void tile_coords(int vt, int T, int& tm, int& tn) {
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // Fixed-order sum of nslab fp32 slabs (cn_wgrad.hip): out[r*ldo + c] (+)= (sum_s part[s*stride + r*ldp + c]) / div.
+struct SlabJob {
+    const float* part;
+    float* out;
+    int64_t stride, ldp, ldo;
+    int nslab, rows, cols, accumulate, blocks;
+    float div;
+};
+SlabJob slab_job(const float* part, int nslab, int64_t stride, int rows, int cols, int64_t ldp, float* out,
+                 int64_t ldo, float div, int accumulate);
+// two reductions in one launch (j1 may be SlabJob{}: empty)
+int launch_slab_jobs(const SlabJob& j0, const SlabJob& j1, hipStream_t s);
 int launch_slab_reduce(const float* part, int nslab, int64_t stride, int rows, int cols, int64_t ldp, float* out,
                        int64_t ldo, float div, int accumulate, hipStream_t s);
 

@@ -666,32 +666,44 @@ __global__ void __launch_bounds__(512, 2) wgrad_x6r_kernel(WgradArgs p) {
 // group sg sums slabs sg, sg + SG, ... in double, the groups meet in a fixed order in LDS.
 // (16 x 16: a 256-slab weight gradient is 16 loads per thread, 4x the blocks of a 4 x 64 split.)
 constexpr int kSlabGroups = 16;
-__global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ part, int nslab, int64_t stride,
-                                                          int rows, int cols, int64_t ldp, float* out, int64_t ldo,
-                                                          float div, int accumulate) {
-    constexpr int SG = kSlabGroups, CG = 256 / SG;
+constexpr int kSlabCG = 256 / kSlabGroups;  // float4 column groups per workgroup
+
+SlabJob slab_job(const float* part, int nslab, int64_t stride, int rows, int cols, int64_t ldp, float* out,
+                 int64_t ldo, float div, int accumulate) {
+    const int64_t groups = (int64_t)rows * cdiv(cols, 4);
+    return SlabJob{part, out, stride, ldp, ldo, nslab, rows, cols, accumulate,
+                   (int)((groups + kSlabCG - 1) / kSlabCG), div};
+}
+
+// Two reductions in one launch (a weight gradient's dW and db): workgroups [0, j0.blocks) take
+// j0, the rest j1 -- one launch and one tail instead of two.
+__global__ void __launch_bounds__(256) slab_reduce_kernel(SlabJob j0, SlabJob j1) {
+    constexpr int SG = kSlabGroups, CG = kSlabCG;
     __shared__ double red[SG][CG][4];
-    const int c4n = cdiv(cols, 4);
+    const bool second = (int)blockIdx.x >= j0.blocks;  // workgroup-uniform
+    const SlabJob& j = second ? j1 : j0;
+    const int blk = second ? (int)blockIdx.x - j0.blocks : (int)blockIdx.x;
+    const int c4n = cdiv(j.cols, 4);
     const int t = threadIdx.x % CG;
     const int sg = threadIdx.x / CG;
-    const int64_t g = (int64_t)blockIdx.x * CG + t;  // float4 group over rows x c4n
-    const bool valid = g < (int64_t)rows * c4n;
+    const int64_t g = (int64_t)blk * CG + t;  // float4 group over rows x c4n
+    const bool valid = g < (int64_t)j.rows * c4n;
     const int r = valid ? (int)(g / c4n) : 0;
     const int c = valid ? (int)(g % c4n) * 4 : 0;
-    const bool vec = valid && (c + 3 < cols) && (ldp % 4 == 0) && (stride % 4 == 0);
+    const bool vec = valid && (c + 3 < j.cols) && (j.ldp % 4 == 0) && (j.stride % 4 == 0);
     double a[4] = {0.0, 0.0, 0.0, 0.0};
     if (valid) {
-        const float* base = part + (int64_t)r * ldp + c;
+        const float* base = j.part + (int64_t)r * j.ldp + c;
         int sl = sg;
-        for (; sl + 3 * SG < nslab; sl += 4 * SG) {
+        for (; sl + 3 * SG < j.nslab; sl += 4 * SG) {
             floatx4 v[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const float* q = base + (int64_t)(sl + SG * u) * stride;
+                const float* q = base + (int64_t)(sl + SG * u) * j.stride;
                 if (vec) {
                     v[u] = *reinterpret_cast<const floatx4*>(q);
                 } else {
-                    for (int e = 0; e < 4; ++e) v[u][e] = (c + e < cols) ? q[e] : 0.0f;
+                    for (int e = 0; e < 4; ++e) v[u][e] = (c + e < j.cols) ? q[e] : 0.0f;
                 }
             }
 #pragma unroll
@@ -699,34 +711,37 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restric
 #pragma unroll
                 for (int e = 0; e < 4; ++e) a[e] += (double)v[u][e];
         }
-        for (; sl < nslab; sl += SG) {
-            const float* q = base + (int64_t)sl * stride;
-            for (int e = 0; e < 4; ++e) a[e] += (c + e < cols) ? (double)q[e] : 0.0;
+        for (; sl < j.nslab; sl += SG) {
+            const float* q = base + (int64_t)sl * j.stride;
+            for (int e = 0; e < 4; ++e) a[e] += (c + e < j.cols) ? (double)q[e] : 0.0;
         }
     }
     for (int e = 0; e < 4; ++e) red[sg][t][e] = a[e];
     __syncthreads();
     if (sg == 0 && valid) {
-        for (int e = 0; e < 4 && c + e < cols; ++e) {
+        for (int e = 0; e < 4 && c + e < j.cols; ++e) {
             double tot = red[0][t][e];
             for (int q = 1; q < SG; ++q) tot += red[q][t][e];
             float v = (float)tot;
-            if (div != 1.0f) v = v / div;
-            float* o = out + (int64_t)r * ldo + c + e;
-            if (accumulate) v += *o;
+            if (j.div != 1.0f) v = v / j.div;
+            float* o = j.out + (int64_t)r * j.ldo + c + e;
+            if (j.accumulate) v += *o;
             *o = v;
         }
     }
 }
 
+int launch_slab_jobs(const SlabJob& j0, const SlabJob& j1, hipStream_t s) {
+    const int blocks = j0.blocks + j1.blocks;
+    if (blocks == 0) return CN_OK;
+    slab_reduce_kernel<<<blocks, 256, 0, s>>>(j0, j1);
+    return check_launch("slab_reduce");
+}
+
 int launch_slab_reduce(const float* part, int nslab, int64_t stride, int rows, int cols, int64_t ldp, float* out,
                        int64_t ldo, float div, int accumulate, hipStream_t s) {
-    const int64_t groups = (int64_t)rows * cdiv(cols, 4);
-    if (groups == 0) return CN_OK;
-    constexpr int CG = 256 / kSlabGroups;
-    slab_reduce_kernel<<<(int)((groups + CG - 1) / CG), 256, 0, s>>>(part, nslab, stride, rows, cols, ldp, out, ldo,
-                                                                     div, accumulate);
-    return check_launch("slab_reduce");
+    SlabJob none{};
+    return launch_slab_jobs(slab_job(part, nslab, stride, rows, cols, ldp, out, ldo, div, accumulate), none, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -873,12 +888,10 @@ extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
     }
     int rc = check_launch("cn_wgrad");
     if (rc) return rc;
-    rc = launch_slab_reduce(a.part, ns, (int64_t)Npad * Kpad, d->n_out, d->k_out, Kpad, d->dW, d->ld_dw, 1.0f,
-                            d->accumulate, s);
-    if (rc) return rc;
-    if (d->db) {
-        rc = launch_slab_reduce(a.bpart, ns, Npad, 1, d->n_out, Npad, d->db, d->n_out, 1.0f, d->accumulate, s);
-        if (rc) return rc;
-    }
-    return CN_OK;
+    // dW and db (when asked for) in one reduction launch
+    const SlabJob jw = slab_job(a.part, ns, (int64_t)Npad * Kpad, d->n_out, d->k_out, Kpad, d->dW, d->ld_dw, 1.0f,
+                                d->accumulate);
+    const SlabJob jb = d->db ? slab_job(a.bpart, ns, Npad, 1, d->n_out, Npad, d->db, d->n_out, 1.0f, d->accumulate)
+                             : SlabJob{};
+    return launch_slab_jobs(jw, jb, s);
 }
