@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libcopenerf.so"
 LIB_PATH = os.environ.get("COPENERF_LIB", os.path.join(_HERE, LIB_NAME))
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 c_f32p = ctypes.c_void_p  # device pointers are passed as integers
 c_i32 = ctypes.c_int32
@@ -128,6 +128,8 @@ SIGNATURES = {
     "cn_stage1_bwd": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr,
                               c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_ptr,
                               c_ptr]),
+    "cn_mat4_chain_fwd": (c_i32, [c_i32, c_ptr, c_ptr, c_ptr]),
+    "cn_mat4_chain_bwd": (c_i32, [c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr]),
 }
 
 _lock = threading.Lock()

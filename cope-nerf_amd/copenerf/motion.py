@@ -20,6 +20,8 @@ parameters' device.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -230,6 +232,45 @@ class _EulerChainFn(torch.autograd.Function):
         return domega, dvel, None, None, None
 
 
+class _Mat4Chain(torch.autograd.Function):
+    """Running products C_j = A_j ... A_0 of A [n, 4, 4] (cn_mat4_chain_fwd / _bwd): one
+    launch each way instead of a 4x4 GEMM launch per product and two per product back."""
+
+    @staticmethod
+    def forward(ctx, A):
+        from . import _lib
+        A = A.contiguous()
+        C = torch.empty_like(A)
+        _lib.call("cn_mat4_chain_fwd", A.shape[0], A.data_ptr(), C.data_ptr(),
+                  torch.cuda.current_stream(A.device).cuda_stream)
+        ctx.save_for_backward(A, C)
+        return C
+
+    @staticmethod
+    def backward(ctx, dC):
+        from . import _lib
+        A, C = ctx.saved_tensors
+        dA = torch.empty_like(A)
+        _lib.call("cn_mat4_chain_bwd", A.shape[0], A.data_ptr(), C.data_ptr(), dC.contiguous().data_ptr(),
+                  dA.data_ptr(), torch.cuda.current_stream(A.device).cuda_stream)
+        return dA
+
+
+_CHAIN_KERNEL = os.environ.get("COPENERF_CHAIN_KERNEL", "1") != "0"
+
+
+def mat4_chain(A):
+    """[n, 4, 4] -> the running products [A_0, A_1 A_0, ..., A_{n-1} ... A_0] (fp32, device).
+    COPENERF_CHAIN_KERNEL=0: the same products as one torch matmul each (A/B measurement)."""
+    if _CHAIN_KERNEL:
+        return _Mat4Chain.apply(A)
+    out, cur = [], None
+    for a in A.unbind(0):
+        cur = a if cur is None else a @ cur
+        out.append(cur)
+    return torch.stack(out)
+
+
 def masked_chain(P, lo, hi):
     """w2c of the frames lo -> hi from consecutive relative poses P [K, 4, 4]:
     P[hi-1] @ ... @ P[lo] (= compute_w2c_mappings(rel[lo:hi])[-1], neus_fields.py:174-186),
@@ -239,11 +280,7 @@ def masked_chain(P, lo, hi):
     k = torch.arange(K, device=P.device)
     m = ((k >= lo) & (k < hi)).view(K, 1, 1)
     eye = torch.eye(4, device=P.device)
-    Q = torch.where(m, P, eye)
-    out = eye
-    for j in range(K):
-        out = Q[j] @ out
-    return out
+    return mat4_chain(torch.where(m, P, eye))[K - 1]
 
 
 def _allreduce_sum(x, group):

@@ -43,7 +43,8 @@ import torch.distributed as dist
 
 from .fields import RenderingNetwork, SDFNetwork, SingleVarianceNetwork
 from .losses import EdgePreservingSmoothnessLoss, SmoothnessLoss, eikonal_loss, rgb_l1, train_losses
-from .motion import (MotionNetwork, affine_points, flow_rgb_loss, masked_chain, project_flow, project_flow_sums,
+from .motion import (MotionNetwork, affine_points, flow_rgb_loss, masked_chain, mat4_chain, project_flow,
+                     project_flow_sums,
                      scene_flow_loss, stage1_terms_fused)
 from .rays import PoseRetriever, get_patch_indices, intrinsics_ndc, inv4x4, pixels_from_indices, world_rays
 from .renderer import NeuSRenderer
@@ -223,6 +224,7 @@ class SyntheticTrainer:
             self.base_lr.append(None)  # the warm-up does not touch the motion optimizer (train.py:268-270)
             self.steps_grid, self.dts = self.motion.interval_time_grid(n_images, self.nst)
             self.ref_intervals = torch.tensor(self.cfg["random_ref_interval"], device=self.device)
+            self.chain_steps = torch.arange(max(self.cfg["random_ref_interval"]), device=self.device)
         self.all_params = [p for g in groups for p in g["params"]]
         self.opt = torch.optim.Adam(groups, lr=lr, capturable=capturable)
         # data: rank-independent (every rank sees the same frames); sampling: per rank
@@ -328,12 +330,9 @@ class SyntheticTrainer:
         js = self.ref_intervals
         ref = img + js                                    # [T]
         valid = (ref <= n - 1)                            # next_time_step <= 1 (train.py:421)
-        chain, cur = [], self.I
-        for d in range(max(self.cfg["random_ref_interval"])):
-            k = torch.clamp(img + d, max=K - 1)           # past the last frame: masked by `valid`
-            cur = P.index_select(0, k)[0] @ cur
-            chain.append(cur)
-        w2c = torch.stack([chain[j - 1] for j in self.cfg["random_ref_interval"]])
+        # (one launch each way: motion.mat4_chain over the gathered poses)
+        k = torch.clamp(img + self.chain_steps, max=K - 1)  # past the last frame: masked by `valid`
+        w2c = mat4_chain(P.index_select(0, k)).index_select(0, self.ref_intervals - 1)
         refc = torch.clamp(ref, max=n - 1)
         # SDF consistency at the world frame (train.py:495-505): with
         # sdf_consistency_enable_pose_grad (most dataset configs, e.g. Co3D/skateboard.yaml:27)

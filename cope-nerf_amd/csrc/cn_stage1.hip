@@ -172,6 +172,71 @@ __global__ void __launch_bounds__(256) stage1_bwd_kernel(int R, int S, Stage1Ptr
     block_partials<18>(acc, smem, part);
 }
 
+// Running products of 4x4 matrices, C_0 = A_0, C_j = A_j C_{j-1} (the relative-pose chains of
+// stage 1: compute_w2c_mappings, neus_fields.py:171-183, and the masked world-camera chain),
+// and their adjoint: G_j = dC_j + A_{j+1}^T G_{j+1}, dA_j = G_j C_{j-1}^T (C_{-1} = I).  A
+// chain is a few dozen 4x4 steps: one lane walks it (sequential by nature), instead of a
+// rocBLAS launch per product each way.
+__device__ __forceinline__ void mm4(const float* a, const float* b, float* c) {  // c = a b
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            c[r * 4 + q] = ((a[r * 4] * b[q] + a[r * 4 + 1] * b[4 + q]) + a[r * 4 + 2] * b[8 + q]) + a[r * 4 + 3] * b[12 + q];
+}
+
+__global__ void mat4_chain_fwd_kernel(int n, const float* __restrict__ A, float* C) {
+    if (threadIdx.x != 0) return;
+    float cur[16], nxt[16], a[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) cur[i] = A[i];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) C[i] = cur[i];
+    for (int j = 1; j < n; ++j) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) a[i] = A[j * 16 + i];
+        mm4(a, cur, nxt);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            cur[i] = nxt[i];
+            C[j * 16 + i] = nxt[i];
+        }
+    }
+}
+
+__global__ void mat4_chain_bwd_kernel(int n, const float* __restrict__ A, const float* __restrict__ C,
+                                      const float* __restrict__ dC, float* dA) {
+    if (threadIdx.x != 0) return;
+    float G[16], t[16], at[16], ct[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) G[i] = 0.0f;
+    for (int j = n - 1; j >= 0; --j) {
+        if (j + 1 < n) {  // G <- A_{j+1}^T G
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) at[r * 4 + q] = A[(j + 1) * 16 + q * 4 + r];
+            mm4(at, G, t);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) G[i] = t[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) G[i] += dC[j * 16 + i];
+        if (j == 0) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) dA[i] = G[i];
+        } else {  // dA_j = G C_{j-1}^T
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) ct[r * 4 + q] = C[(j - 1) * 16 + q * 4 + r];
+            mm4(G, ct, t);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) dA[j * 16 + i] = t[i];
+        }
+    }
+}
+
 }  // namespace cn
 
 using namespace cn;
@@ -223,4 +288,20 @@ extern "C" int cn_stage1_bwd(int32_t R, int32_t S, const float* pts, int64_t ld_
                                            dpts, ld_dp, workspace);
     int rc = check_launch("cn_stage1_bwd");
     return rc ? rc : launch_slab_reduce(workspace, nblk, 18, 1, 18, 18, dmv_dcw2, 18, 1.0f, 0, s);
+}
+
+extern "C" int cn_mat4_chain_fwd(int32_t n, const float* A, float* C, cn_stream_t stream) {
+    CN_REQUIRE(n >= 0 && (n == 0 || (A && C)), CN_ERR_ARG, "cn_mat4_chain_fwd: n=%d, A and C required", n);
+    if (n == 0) return CN_OK;
+    mat4_chain_fwd_kernel<<<1, 64, 0, (hipStream_t)stream>>>(n, A, C);
+    return check_launch("cn_mat4_chain_fwd");
+}
+
+extern "C" int cn_mat4_chain_bwd(int32_t n, const float* A, const float* C, const float* dC, float* dA,
+                                 cn_stream_t stream) {
+    CN_REQUIRE(n >= 0 && (n == 0 || (A && C && dC && dA)), CN_ERR_ARG,
+               "cn_mat4_chain_bwd: n=%d, A, C, dC and dA required", n);
+    if (n == 0) return CN_OK;
+    mat4_chain_bwd_kernel<<<1, 64, 0, (hipStream_t)stream>>>(n, A, C, dC, dA);
+    return check_launch("cn_mat4_chain_bwd");
 }

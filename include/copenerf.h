@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define CN_ABI_VERSION 7
+#define CN_ABI_VERSION 8
 
 typedef void* cn_stream_t; /* hipStream_t */
 
@@ -438,6 +438,13 @@ int cn_stage1_bwd(int32_t R, int32_t S, const float* pts, int64_t ld_p, const fl
                   const float* g_num, const float* d_ray, const float* dx, int64_t ld_dx, float* dnormals,
                   int64_t ld_dn, float* dflows, int64_t ld_df, float* dweights, float* dpts, int64_t ld_dp,
                   float* dmv_dcw2, float* workspace, cn_stream_t stream);
+
+/* Running products of n 4x4 matrices (row-major [n][4][4]), ABI v8: C_0 = A_0,
+ * C_j = A_j C_{j-1} -- the relative-pose chains of stage 1 (compute_w2c_mappings,
+ * model/neus_fields.py:171-183; the world-camera chain of train.py:498-501) -- and the
+ * adjoint: dA from dC (every C_j may carry a gradient).  One lane walks the chain. */
+int cn_mat4_chain_fwd(int32_t n, const float* A, float* C, cn_stream_t stream);
+int cn_mat4_chain_bwd(int32_t n, const float* A, const float* C, const float* dC, float* dA, cn_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -115,3 +115,23 @@ def test_trainer_stage1_fused_matches_torch_expressions(monkeypatch):
     for a, b in zip(gf, gt):
         scale = max(1e-8, b.abs().max().item())
         assert (a - b).abs().max().item() <= 1e-4 * scale
+
+
+@pytest.mark.parametrize("n", [1, 3, 10, 21])
+def test_mat4_chain_matches_torch_products(n):
+    """cn_mat4_chain_fwd / _bwd: the running products of the stage-1 pose chains and their
+    gradient (every product may carry one) against torch matmuls in fp32."""
+    from copenerf.motion import _Mat4Chain
+    g = torch.Generator(device="cpu").manual_seed(n)
+    A = (torch.eye(4) + 0.2 * torch.randn(n, 4, 4, generator=g)).to(DEV).requires_grad_(True)
+    dC = torch.randn(n, 4, 4, generator=g).to(DEV)
+    C = _Mat4Chain.apply(A)
+    (gk,) = torch.autograd.grad(C, A, dC)
+    out, cur = [], None
+    for a in A.unbind(0):
+        cur = a if cur is None else a @ cur
+        out.append(cur)
+    Ct = torch.stack(out)
+    (gt,) = torch.autograd.grad(Ct, A, dC)
+    torch.testing.assert_close(C, Ct, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(gk, gt, rtol=1e-4, atol=1e-4 * gt.abs().max().item())
