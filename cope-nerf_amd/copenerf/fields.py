@@ -176,6 +176,10 @@ def pack_sdf(lay: SDFLayout, Ws, bs, mfma_dtype: str = "fp32") -> SDFPack:
 
 
 FUSE_HEAD = os.environ.get("COPENERF_FUSE_HEAD", "1") != "0"
+# the positional encoding computed inside the first layer's operand load (cn_linear emb_x) instead
+# of a cn_sdf_embed pass writing U0 that the first GEMM reads back (COPENERF_FUSE_EMB=1; off by
+# default: the C2 step measured 0.6 % slower on the 128x128 tile, which encodes each row per N-tile)
+FUSE_EMB = os.environ.get("COPENERF_FUSE_EMB", "0") != "0"
 
 
 def _fuse_head(lay: SDFLayout, pk: SDFPack) -> bool:
@@ -214,13 +218,17 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
     nl, sk, HL, KE = lay.n_lin, lay.skip, lay.HL, lay.KE
     keep_u = keep or want_grad
     U = [None] * nl
-    U[0] = _empty(M, KE, dev)
+    # the encoding U0 is stored only for the backward / ∇ pass (not on the sampler path when fused)
+    fuse_emb = FUSE_EMB and KE <= 64 and x.shape[1] == 4 and x.stride(1) == 1 and x.stride(0) % 4 == 0 and \
+        x.data_ptr() % 16 == 0
+    U[0] = _empty(M, KE, dev) if (keep_u or not fuse_emb) else None
     Usk, e_view = None, None
     if sk >= 0:
         Usk = _empty(M, HL, dev)
         o = lay.out_dim[sk - 1]
         e_view = Usk[:, o:o + lay.E]
-    ops.sdf_embed(x, lay.multires, lay.scale, U[0], e_view, SQRT2)
+    if not fuse_emb:
+        ops.sdf_embed(x, lay.multires, lay.scale, U[0], e_view, SQRT2)
     L8 = nl - 1
     sdf = sdf_out if sdf_out is not None else _empty(M, 1, dev)
     fuse = _fuse_head(lay, pk)
@@ -239,9 +247,10 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
                        head_idx=dst, M=M)
         else:
             out = Usk if into else _empty(M, HL, dev)
-            ops.linear(U[l], pk.Bf[l], lay.out_dim[l], K, out, EPI_SOFTPLUS, bias=pk.b[l],
+            emb = (x, lay.multires, lay.scale, U[0], e_view, SQRT2) if (l == 0 and fuse_emb) else None
+            ops.linear(None if emb else U[l], pk.Bf[l], lay.out_dim[l], K, out, EPI_SOFTPLUS, bias=pk.b[l],
                        nzero=lay.out_dim[l] if into else HL, odiv=SQRT2 if into else 1.0, beta=lay.beta,
-                       threshold=lay.threshold, kalg=lay.in_dim[l])
+                       threshold=lay.threshold, kalg=lay.in_dim[l], emb=emb)
         U[l + 1] = out
         if not keep_u and l >= 1 and (l != sk):
             U[l] = None  # free as we go on the no-grad sampler path
@@ -424,6 +433,7 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
     share = want_dx and not second  # Z_l == P_l: dx from the parameter adjoint chain
     PE = _empty(M, KE, dev) if (share and sk >= 0) else None
     lane = ops.SideLane(dev)
+    wq = ops.WgradQueue()  # the hidden layers' weight gradients: one launch after the chain
     for l in range(L8 - 1, -1, -1):
         Zl = Z
         lane.fork()  # Z_l is ready: its weight gradient may run beside the next adjoint GEMM
@@ -443,10 +453,11 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
         dW = torch.empty(lay.out_dim[l], lay.in_dim[l], device=dev)
         db = torch.empty(lay.out_dim[l], device=dev)
         with lane:
-            ops.wgrad(Zl, U[l], lay.out_dim[l], lay.in_dim[l], dW, db=db,
-                      Y1=S[l] if second else None, X1=Ud[l] if second else None, mode=wmode)
+            wq.add(Zl, U[l], lay.out_dim[l], lay.in_dim[l], dW, db=db,
+                   Y1=S[l] if second else None, X1=Ud[l] if second else None, mode=wmode)
         lane.hold(Zl)
         dWs[l], dbs[l] = dW, db
+    wq.flush()
     if not want_dx:
         lane.join()
         return dWs, dbs
@@ -728,12 +739,13 @@ class _ColorFieldFn(torch.autograd.Function):
         dZ = _empty(M, lay.HL, dev)
         ops.rgb_head_bwd(drgb, rgb, H[-1], lay.in_dim[n - 1], pk.W3, dZ, dWs[n - 1], dbs[n - 1])
         lane = ops.SideLane(dev)
+        wq = ops.WgradQueue()  # the 256x256 weight gradients: one launch after the chain
         for l in range(n - 2, 0, -1):
             dW = torch.empty(lay.out_dim[l], lay.in_dim[l], device=dev)
             db = torch.empty(lay.out_dim[l], device=dev)
             lane.fork()
             with lane:  # beside the next adjoint GEMM (both only read dZ_l)
-                ops.wgrad(dZ, H[l - 1], lay.out_dim[l], lay.in_dim[l], dW, db=db, mode=wmode)
+                wq.add(dZ, H[l - 1], lay.out_dim[l], lay.in_dim[l], dW, db=db, mode=wmode)
             lane.hold(dZ)
             dWs[l], dbs[l] = dW, db
             dZp = _empty(M, lay.HL, dev)
@@ -746,9 +758,10 @@ class _ColorFieldFn(torch.autograd.Function):
         dWx = torch.empty(o0, lay.KX, device=dev)
         lane.fork()
         with lane:  # beside the input-gradient GEMMs below
-            ops.wgrad(dZ, feat, o0, lay.F, dWf, db=db0, mode=wmode)
+            wq.add(dZ, feat, o0, lay.F, dWf, db=db0, mode=wmode)
             ops.wgrad(dZ, ext, o0, lay.KX, dWx, mode=wmode)
         lane.hold(dZ)
+        wq.flush()
         P, V, Gd = lay.P, lay.V, lay.Gd
         dfeat = None
         if ctx.needs_input_grad[4]:

@@ -274,7 +274,7 @@ def _tile_tag(name, tile):
 def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None, colv=None, aux0=None,
            aux1=None, aux2=None, out_split=None, nsplit=None, nzero=None, adiv=1.0, odiv=1.0, beta=100.0,
            threshold=20.0, aux_beta=0.0, aux2_scale=0.0, tile=None, M=None, kalg=None, out1=None, head_w=None,
-           head_b=None, head_out=None, head_idx=None):
+           head_b=None, head_out=None, head_idx=None, emb=None):
     """out = epilogue((A|A2) @ B[:N].T / adiv) -- cn_linear.  MUL / TANGENT /
     BWD_SOFTPLUS read softplus' as sg = 1 - exp(-aux_beta * aux0) from the stored
     softplus output aux0 (include/copenerf.h).  kalg: the unpadded
@@ -285,8 +285,18 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     GEMM computed from three bf16 terms per operand on the bf16 MFMA.
     EPI_SOFTPLUS_HEAD (the last SDF hidden layer): out0 = softplus activation (or
     None: not stored), out1 = colv * softplus' (or None), head_out[head_idx[m] or m]
-    = out0[m] · head_w + head_b."""
+    = out0[m] · head_w + head_b.
+    emb=(x, multires, scale, U0, U4e, u4div) (A None): the first SDF layer with the encoding
+    fused into its operand load -- A's rows are cn_sdf_embed's encoding of x [M, 4], computed
+    while staging; U0 / U4e (or None) receive the encoding and the skip input's tail / u4div,
+    as cn_sdf_embed would write them."""
     x6 = B.dim() == 3
+    if emb is not None:
+        if A is not None or A2 is not None:
+            raise RuntimeError("cn_linear: emb replaces A (pass A=None)")
+        _need(emb[0], "emb x")
+        _need(emb[3], "emb U0")
+        _need(emb[4], "emb U4e")
     if x6 and (B.dtype != torch.bfloat16 or B.shape[2] != 48 or not B.is_contiguous()):
         raise RuntimeError(f"cn_linear: a 3-D B must be split_bf16x3's [K/16, N, 48] bfloat16 image (got "
                            f"{tuple(B.shape)}, {B.dtype}, strides {B.stride()})")
@@ -301,9 +311,9 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     if bf:
         K = rup(K, 64)
         K1 = rup(K1, 64) if K1 is not None else None
-        if (A.stride(0) < (K1 or K)) or (A2 is not None and A2.stride(0) < K - K1):
+        if A is not None and ((A.stride(0) < (K1 or K)) or (A2 is not None and A2.stride(0) < K - K1)):
             raise RuntimeError(f"cn_linear (bf16): A rows too short for K={K}")
-    M = A.shape[0] if M is None else M
+    M = (A if emb is None else emb[0]).shape[0] if M is None else M
     # the epilogue reads bias / colv as float4
     bias = bias if bias is None or bias.data_ptr() % 16 == 0 else bias.clone()
     colv = colv if colv is None or colv.data_ptr() % 16 == 0 else colv.clone()
@@ -344,6 +354,10 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     d.epilogue, d.tile = epilogue, tile
     d.adiv, d.odiv, d.beta, d.threshold = adiv, odiv, beta, threshold
     d.mfma_dtype = 2 if x6 else (1 if bf else 0)
+    if emb is not None:
+        ex, d.emb_multires, d.emb_scale, eu0, eu4, d.emb_u4_div = emb
+        d.emb_x, d.ld_emb_x = _ptr(ex), _ld(ex)
+        d.emb_u0, d.ld_emb_u0, d.emb_u4, d.ld_emb_u4 = _ptr(eu0), _ld(eu0), _ptr(eu4), _ld(eu4)
     global _flip
     if ALTERNATE_TILE_ORDER:  # consecutive launches walk the rows in opposite directions
         _flip ^= 1
@@ -353,7 +367,8 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
         _lib.check(_lib.load().cn_linear(d, _stream()), "cn_linear")
         name = kernel_name(_lib.load().cn_linear_kernel_name, d)
         tag = _tile_tag(name, tile) if x6 else tile
-        key = ("linear", tag, EPI_NAMES[epilogue] + ("+rowv" if rowv is not None else "")) + \
+        key = ("linear", tag, EPI_NAMES[epilogue] + ("+rowv" if rowv is not None else "") +
+               ("+emb" if emb is not None else "")) + \
             (("bf16",) if bf else ("x6",) if x6 else ())
         _timer.symbols[key] = name
         ka = kalg or K
@@ -371,11 +386,8 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
 WGRAD_MODES = {"fp32": 0, "bf16": 1, "bf16x6": 2}
 
 
-def wgrad(Y0, X0, N, K, dW, *, db=None, Y1=None, X1=None, accumulate=False, mode="fp32"):
-    """dW[:n_out, :k_out] (+)= Y0ᵀX0 (+ Y1ᵀX1), db = colsum(Y0) -- cn_wgrad.
-    mode: "fp32" (exact fp32 MFMA), "bf16x6" (fp32 from three bf16 terms per
-    operand on the bf16 MFMA) or "bf16" (operands rounded to bf16 on load,
-    config C3's reduced-precision mode)."""
+def _wgrad_desc(Y0, X0, N, K, dW, db, Y1, X1, accumulate, mode):
+    """The cn_wgrad descriptor of one weight gradient and the workspace it points into."""
     if mode not in WGRAD_MODES:
         raise ValueError(f"wgrad: mode must be one of {tuple(WGRAD_MODES)} (got {mode!r})")
     for t, n in ((Y0, "Y0"), (X0, "X0"), (Y1, "Y1"), (X1, "X1"), (dW, "dW")):
@@ -394,19 +406,79 @@ def wgrad(Y0, X0, N, K, dW, *, db=None, Y1=None, X1=None, accumulate=False, mode
     d.n_out, d.k_out = dW.shape[0], dW.shape[1]
     d.accumulate = 1 if accumulate else 0
     d.mfma_dtype = WGRAD_MODES[mode]
+    return d, ws
+
+
+def _wgrad_key(d, mode):
+    # one launch class per kernel instance (1- and 2-pair calls share it, as in rocprof's stats)
+    name = kernel_name(_lib.load().cn_wgrad_kernel_name, d)
+    key = ("wgrad", name[len("void cn::"):name.index("(")].replace(" ", "")) + \
+        (("bf16",) if mode == "bf16" else ("x6",) if mode == "bf16x6" else ())
+    _timer.symbols[key] = name
+    return key
+
+
+def wgrad(Y0, X0, N, K, dW, *, db=None, Y1=None, X1=None, accumulate=False, mode="fp32"):
+    """dW[:n_out, :k_out] (+)= Y0ᵀX0 (+ Y1ᵀX1), db = colsum(Y0) -- cn_wgrad.
+    mode: "fp32" (exact fp32 MFMA), "bf16x6" (fp32 from three bf16 terms per
+    operand on the bf16 MFMA) or "bf16" (operands rounded to bf16 on load,
+    config C3's reduced-precision mode)."""
+    d, ws = _wgrad_desc(Y0, X0, N, K, dW, db, Y1, X1, accumulate, mode)
+    lib = _lib.load()
     if _timer is not None:
         e0 = _timer.start()
         _lib.check(lib.cn_wgrad(d, _stream()), "cn_wgrad")
-        # one launch class per kernel instance (1- and 2-pair calls share it, as in rocprof's stats)
-        name = kernel_name(lib.cn_wgrad_kernel_name, d)
-        key = ("wgrad", name[len("void cn::"):name.index("(")].replace(" ", "")) + \
-            (("bf16",) if mode == "bf16" else ("x6",) if mode == "bf16x6" else ())
-        _timer.symbols[key] = name
+        key = _wgrad_key(d, mode)
+        M = d.M
         _timer.stop(key + ((M, d.n_out, d.k_out),) if _timer.detail else key, e0,
                     2.0 * M * d.n_out * d.k_out * d.npairs, 4.0 * d.npairs * M * (d.n_out + d.k_out))
     else:
         _lib.check(lib.cn_wgrad(d, _stream()), "cn_wgrad")
     return dW
+
+
+# COPENERF_WGRAD_BATCH=0 (benchmarking aid): every weight gradient its own cn_wgrad launch
+WGRAD_BATCH = os.environ.get("COPENERF_WGRAD_BATCH", "1") != "0"
+
+
+class WgradQueue(object):
+    """Collects a backward pass's 256x256 stage-ring weight gradients and runs them with ONE
+    cn_wgrad_batch call at flush(): one launch and one slab reduction instead of a launch, a
+    full-chip slab write and a reduction each (other tile classes launch at add()).  The
+    queue holds the operand tensors, so their memory stays allocated until the flush; the
+    gradients are written by the flush (call it before anything reads them).  With
+    COPENERF_WGRAD_BATCH=0, add() launches at once."""
+
+    def __init__(self):
+        self.jobs = []
+
+    def add(self, Y0, X0, N, K, dW, *, db=None, Y1=None, X1=None, mode="fp32"):
+        if not WGRAD_BATCH:
+            return wgrad(Y0, X0, N, K, dW, db=db, Y1=Y1, X1=X1, mode=mode)
+        d, ws = _wgrad_desc(Y0, X0, N, K, dW, db, Y1, X1, False, mode)
+        if "WgradBatch" not in kernel_name(_lib.load().cn_wgrad_kernel_name, d):
+            # not a stage-ring job (e.g. K = 64 first layers): nothing to share, launch it now
+            return wgrad(Y0, X0, N, K, dW, db=db, Y1=Y1, X1=X1, mode=mode)
+        self.jobs.append((d, mode, (Y0, X0, Y1, X1, ws)))
+        return dW
+
+    def flush(self):
+        if not self.jobs:
+            return
+        lib = _lib.load()
+        n = len(self.jobs)
+        arr = (_lib.WgradDesc * n)(*[d for d, _, _ in self.jobs])
+        if _timer is not None:
+            # the batch's time goes to the class of its first job; the FLOPs of all of them
+            e0 = _timer.start()
+            _lib.check(lib.cn_wgrad_batch(arr, n, _stream()), "cn_wgrad_batch")
+            key = _wgrad_key(self.jobs[0][0], self.jobs[0][1])
+            fl = sum(2.0 * d.M * d.n_out * d.k_out * d.npairs for d, _, _ in self.jobs)
+            nb = sum(4.0 * d.npairs * d.M * (d.n_out + d.k_out) for d, _, _ in self.jobs)
+            _timer.stop(key + (("batch", n),) if _timer.detail else key, e0, fl, nb)
+        else:
+            _lib.check(lib.cn_wgrad_batch(arr, n, _stream()), "cn_wgrad_batch")
+        self.jobs = []
 
 
 def row_head(A, K, W, b, C, act, out, dst_index=None, ld_out=None):

@@ -23,6 +23,27 @@ void set_error(const char* fmt, ...);
 int check_launch(const char* what);
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// Column group g (4 columns) of the SDF positional encoding of x' = scale * x (neus_embedder.py:17-36:
+// include_input, log bands, periodic_fns [sin, cos], d = 4): g 0 = x', g 1 + 2k = sin(2^k x'), g 2 + 2k
+// = cos(2^k x') for k < L, zero for g >= 1 + 2L.  The one definition of the encoding: cn_sdf_embed and
+// the first layer's fused operand load (cn_linear with emb_x) give the same bits.
+__device__ __forceinline__ floatx4 sdf_embed_group(floatx4 xv, int g, int L, float scale) {
+    floatx4 xs, o = {0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < 4; ++c) xs[c] = xv[c] * scale;
+    if (g == 0) {
+        o = xs;
+    } else if (g < 1 + 2 * L) {
+        const int k = (g - 1) >> 1;
+        const float f = (float)(1 << k);
+        const bool is_sin = ((g - 1) & 1) == 0;
+        for (int c = 0; c < 4; ++c) {
+            const float t = xs[c] * f;
+            o[c] = is_sin ? sinf(t) : cosf(t);
+        }
+    }
+    return o;
+}
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int kWave = 64;

@@ -21,22 +21,8 @@ __global__ void sdf_embed_kernel(int M, const float* __restrict__ x, int64_t ldx
     const int64_t m = idx / G;
     const int g = idx % G;
     if (m >= M) return;
-    const floatx4 xv = ld4(x + m * ldx);
-    floatx4 xs;
-    for (int c = 0; c < 4; ++c) xs[c] = xv[c] * scale;
-    floatx4 o = {0.f, 0.f, 0.f, 0.f};
+    const floatx4 o = sdf_embed_group(ld4(x + m * ldx), g, L, scale);
     const int ng = 1 + 2 * L;
-    if (g == 0) {
-        o = xs;
-    } else if (g < ng) {
-        const int k = (g - 1) >> 1;
-        const float f = (float)(1 << k);
-        const bool is_sin = ((g - 1) & 1) == 0;
-        for (int c = 0; c < 4; ++c) {
-            const float t = xs[c] * f;
-            o[c] = is_sin ? sinf(t) : cosf(t);
-        }
-    }
     st4(U0 + m * ld_u0 + 4 * g, o);
     if (U4e && g < ng) {
         floatx4 q;

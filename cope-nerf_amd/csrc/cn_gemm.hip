@@ -48,6 +48,14 @@ struct LinearArgs {
     float* head_out;
     const int* head_idx;
     int flags;
+    // MODE >= 4: A is the SDF encoding of the points emb_x (cn_linear_desc.emb_*): gload fetches one
+    // point per row, lstore encodes it; the N-tile-0 workgroups also write the encoding (emb_u0) and
+    // the skip input's tail (emb_u4, divided by emb_u4_div)
+    const float* emb_x;
+    float* emb_u0;
+    float* emb_u4;
+    int ld_emb_x, ld_emb_u0, ld_emb_u4, emb_L;
+    float emb_scale, emb_u4_div;
 };
 
 
@@ -91,8 +99,10 @@ struct LinearArgs {
 #endif
 constexpr int kTblCols = 512;  // widest N with a bias / colv (the LDS column table)
 
-template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int EPI, bool ROWV, int MODE>
+template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int EPI, bool ROWV, int MODE_>
 __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel(LinearArgs p) {
+    constexpr int MODE = MODE_ & 3;    // the GEMM mode (0 fp32, 1 bf16, 2 bf16x6)
+    constexpr bool EMB = MODE_ >= 4;   // A generated from the points (the first SDF layer)
     constexpr int NT = 64 * WM * WN;
     constexpr int BM = 32 * TM * WM;
     constexpr int BN = 32 * TN * WN;
@@ -176,6 +186,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     const int lds_b = srowb * LS + scb * 4;
 
     floatx4 ra[DEPTH][ALD], rb[DEPTH][BLD];
+    int egrp[DEPTH], erow[DEPTH], erows[DEPTH];  // EMB: encoding group, side-output tile row (-1: none), rows
     // Straight-line staging: every call issues exactly ALD + BLD loads (an empty
     // view when `valid` is false, reads return zero) with no data-dependent branch,
     // so the compiler tracks vmcnt precisely and the LDS writes of one register
@@ -189,6 +200,16 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 #else
         const int ma = m0;
 #endif
+        if constexpr (EMB) {
+            // the rows' points (lstore encodes them: this thread's columns are encoding group
+            // k0 / 4 + sc4); rows past M read zero, their outputs are dropped
+            const rsrc_t rX = make_view(p.emb_x + (int64_t)ma * p.ld_emb_x, rows * p.ld_emb_x * 4);
+#pragma unroll
+            for (int q = 0; q < ALD; ++q) ra[set][q] = bload4(rX, (srow + q * RSTEP) * p.ld_emb_x * 4, 0);
+            egrp[set] = (k0 >> 2) + sc4;
+            erow[set] = (valid && n0 == 0) ? m0 : -1;
+            erows[set] = rows;
+        } else {
         const float* abase = second ? p.A2 + (int64_t)ma * p.lda2 : p.A + (int64_t)ma * p.lda;
         const int ald = second ? p.lda2 : p.lda;
         const int ak = second ? k0 - p.K1 : k0;
@@ -199,6 +220,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             if (MODE == 2) { ra[set][q] = floatx4{(float)k0, (float)rows, (float)q, 1.0f}; continue; }
 #endif
             ra[set][q] = bload4(rA, second ? voA2[q] : voA[q], ak * 4);
+        }
         }
         // MODE 2: chunk kc of the image is [ldb rows][48 bf16]; the tile's BN rows are 96 * BN contiguous bytes
         const int64_t bofs = MODE == 2 ? ((int64_t)kc * (BK / 16) * p.ldb + n0) * 96 : (int64_t)n0 * p.ldb * ESZB;
@@ -219,6 +241,23 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 #pragma unroll
         for (int q = 0; q < ALD; ++q) {
             if (piece >= 0 && piece != q) continue;
+            if constexpr (EMB) {
+                const int g = egrp[set];
+                const floatx4 e = sdf_embed_group(ra[set][q], g, p.emb_L, p.emb_scale);
+                ra[set][q] = e;
+                if (erow[set] >= 0) {  // the encoding itself and the skip input's tail, once per row
+                    const int r = srow + q * RSTEP;
+                    const rsrc_t rU = make_view(p.emb_u0 + (int64_t)erow[set] * p.ld_emb_u0, p.emb_u0 ? erows[set] * p.ld_emb_u0 * 4 : 0);
+                    bstore4(rU, (r * p.ld_emb_u0 + 4 * g) * 4, 0, e);
+                    if (g < 1 + 2 * p.emb_L) {
+                        floatx4 h;
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) h[c] = e[c] / p.emb_u4_div;
+                        const rsrc_t r4 = make_view(p.emb_u4 + (int64_t)erow[set] * p.ld_emb_u4, p.emb_u4 ? erows[set] * p.ld_emb_u4 * 4 : 0);
+                        bstore4(r4, (r * p.ld_emb_u4 + 4 * g) * 4, 0, h);
+                    }
+                }
+            }
             if constexpr (MODE == 2) {
                 bf16x4 x0, x1, x2;
 #if X6_EXP == 1
@@ -1221,6 +1260,18 @@ static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_
     }
     const int grid = std::min(ntiles, OCC * cus);  // OCC resident workgroups per CU
     dim3 block(64 * WM * WN);
+    if (a.emb_x) {  // the fused-encoding first layer: SOFTPLUS or STORE on the 128x128 tiles (host-checked)
+        if constexpr ((WM == 2 && WN == 2 && TM == 2 && TN == 2 && OCC <= 2) ||
+                      (MODE == 2 && WM == 4 && WN == 2 && TM == 2 && TN == 4 && BK == 16)) {
+            if (d->epilogue == CN_EPI_SOFTPLUS)
+                linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, CN_EPI_SOFTPLUS, false, MODE + 4><<<grid, block, 0, s>>>(a);
+            else
+                linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, CN_EPI_STORE, false, MODE + 4><<<grid, block, 0, s>>>(a);
+            return check_launch("cn_linear");
+        }
+        set_error("cn_linear: no fused-encoding kernel for this tile");
+        return CN_ERR_UNSUPPORTED;
+    }
     switch (d->epilogue) {
 #define CN_EPI_CASE(E)                                                                     \
         case E:                                                                            \
@@ -1265,6 +1316,15 @@ enum LinearTile { LT_BF_T0, LT_BF_T1, LT_X6_SQ, LT_X6_TALL, LT_X6_WIDE, LT_X6_T1
 static LinearTile choose_linear_tile(const cn_linear_desc* d) {
     const bool head = d->epilogue == CN_EPI_SOFTPLUS_HEAD;
     if (d->mfma_dtype == CN_MFMA_BF16) return d->tile == 0 ? LT_BF_T0 : LT_BF_T1;
+    if (d->emb_x) {  // the fused-encoding first layer (K <= 64): the 2-per-CU 128x128 tiles
+        // (COPENERF_EMB_SQ=1: the 256x256 tile, every row encoded once instead of per N-tile)
+        static const bool emb_sq = [] {
+            const char* e = getenv("COPENERF_EMB_SQ");
+            return e && atoi(e) != 0;
+        }();
+        if (d->mfma_dtype == CN_MFMA_F32_BF16X6) return emb_sq && d->N > 128 && d->N <= 256 ? LT_X6_SQ : LT_X6_T128;
+        return (d->K % 64) == 0 && g_linear_variant == 0 ? LT_F_T0_D2 : LT_F_T0_D1;
+    }
     if (d->mfma_dtype == CN_MFMA_F32_BF16X6) {
         // K % 64 == 0, STORE / SOFTPLUS / RELU: 256x128 tiles of 8 waves, one workgroup per CU,
         // 32-deep stages (whole 128-byte A row segments per load, half the barriers per K; main
@@ -1302,7 +1362,19 @@ static LinearTile choose_linear_tile(const cn_linear_desc* d) {
 extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     CN_REQUIRE(d, CN_ERR_ARG, "cn_linear: null desc");
     const bool head = d->epilogue == CN_EPI_SOFTPLUS_HEAD;
-    CN_REQUIRE(d->A && d->B && (d->out0 || head), CN_ERR_ARG, "cn_linear: A, B and out0 are required");
+    const bool emb = d->emb_x != nullptr;
+    if (emb) {
+        CN_REQUIRE(!d->A && !d->A2 && !d->rowv && d->tile == 0 &&
+                       (d->epilogue == CN_EPI_SOFTPLUS || d->epilogue == CN_EPI_STORE),
+                   CN_ERR_ARG, "cn_linear: emb_x replaces A (no A / A2 / rowv, tile 0, SOFTPLUS or STORE)");
+        CN_REQUIRE(d->emb_multires >= 0 && d->emb_multires < 16 && 4 * (1 + 2 * d->emb_multires) <= d->K && d->K <= 64,
+                   CN_ERR_SHAPE, "cn_linear: emb_multires=%d does not fit K=%d (<= 64)", d->emb_multires, d->K);
+        CN_REQUIRE(al16(d->emb_x) && d->ld_emb_x % 4 == 0 && d->ld_emb_x >= 4 && d->ld_emb_x < (1 << 20) &&
+                       (!d->emb_u0 || (al16(d->emb_u0) && d->ld_emb_u0 % 4 == 0 && d->ld_emb_u0 >= d->K && d->ld_emb_u0 < (1 << 20))) &&
+                       (!d->emb_u4 || (al16(d->emb_u4) && d->ld_emb_u4 % 4 == 0 && d->ld_emb_u4 < (1 << 20))),
+                   CN_ERR_ALIGN, "cn_linear: emb_x / emb_u0 / emb_u4 alignment or leading dimensions");
+    }
+    CN_REQUIRE((d->A || emb) && d->B && (d->out0 || head), CN_ERR_ARG, "cn_linear: A, B and out0 are required");
     CN_REQUIRE(d->M >= 0 && d->N > 0 && d->K > 0, CN_ERR_SHAPE, "cn_linear: bad M/N/K %d/%d/%d", d->M, d->N, d->K);
     CN_REQUIRE(d->mfma_dtype == CN_MFMA_F32 || d->mfma_dtype == CN_MFMA_BF16 || d->mfma_dtype == CN_MFMA_F32_BF16X6,
                CN_ERR_ARG, "cn_linear: bad mfma_dtype %d", d->mfma_dtype);
@@ -1312,7 +1384,8 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     CN_REQUIRE(d->tile == 0 || d->tile == 1, CN_ERR_ARG, "cn_linear: bad tile %d", d->tile);
     const int K1 = d->A2 ? d->K1 : d->K;
     CN_REQUIRE(K1 > 0 && K1 <= d->K && K1 % (bf ? 64 : 32) == 0, CN_ERR_SHAPE, "cn_linear: bad K1=%d", K1);
-    CN_REQUIRE(d->lda >= K1 && d->lda % 4 == 0 && al16(d->A), CN_ERR_ALIGN, "cn_linear: A must be 16B aligned with lda>=K1, lda%%4==0");
+    CN_REQUIRE(emb || (d->lda >= K1 && d->lda % 4 == 0 && al16(d->A)), CN_ERR_ALIGN,
+               "cn_linear: A must be 16B aligned with lda>=K1, lda%%4==0");
     if (d->A2) CN_REQUIRE(d->lda2 >= d->K - K1 && d->lda2 % 4 == 0 && al16(d->A2), CN_ERR_ALIGN, "cn_linear: bad A2/lda2");
     if (x6)  // ldb = rows of the chunk-major term image
         CN_REQUIRE(d->ldb >= cdiv(d->N, d->tile == 0 ? 128 : 64) * (d->tile == 0 ? 128 : 64) && al16(d->B), CN_ERR_ALIGN,
@@ -1381,6 +1454,11 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     a.stagger = g_stagger;
     a.head_w = d->head_w; a.head_b = d->head_b; a.head_out = d->head_out; a.head_idx = d->head_idx;
     a.flags = d->flags;
+    a.emb_x = d->emb_x; a.emb_u0 = d->emb_u0; a.emb_u4 = d->emb_u4;
+    a.ld_emb_x = (int)d->ld_emb_x; a.ld_emb_u0 = (int)d->ld_emb_u0; a.ld_emb_u4 = (int)d->ld_emb_u4;
+    a.emb_L = d->emb_multires;
+    a.emb_scale = d->emb_scale;
+    a.emb_u4_div = d->emb_u4_div == 0.0f ? 1.0f : d->emb_u4_div;
     a.ld_out0 = (int)d->ld_out0; a.ld_out1 = (int)d->ld_out1; a.ld_split = (int)d->ld_split;
     a.M = d->M; a.N = d->N; a.K = d->K; a.K1 = K1; a.nzero = nzero;
     a.nsplit = (e == CN_EPI_MUL && d->out_split) ? d->nsplit : d->N;
@@ -1410,7 +1488,8 @@ extern "C" int cn_linear_kernel_name(const cn_linear_desc* d, char* buf, int32_t
         CN_LINEAR_TILES(CN_TILE_NAME)
 #undef CN_TILE_NAME
     }
-    const int mode = d->mfma_dtype == CN_MFMA_F32_BF16X6 ? 2 : d->mfma_dtype == CN_MFMA_BF16 ? 1 : 0;
+    const int mode = (d->mfma_dtype == CN_MFMA_F32_BF16X6 ? 2 : d->mfma_dtype == CN_MFMA_BF16 ? 1 : 0) +
+                     (d->emb_x ? 4 : 0);  // (MODE + 4: the fused-encoding first layer)
     const int n = snprintf(buf, (size_t)len, "void cn::linear_kernel<%s, %d, %s, %d>(cn::LinearArgs)", args,
                            d->epilogue, d->rowv ? "true" : "false", mode);
     CN_REQUIRE(n < len, CN_ERR_SHAPE, "cn_linear_kernel_name: buffer of %d bytes too small (%d)", len, n + 1);

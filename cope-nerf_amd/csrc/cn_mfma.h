@@ -120,8 +120,15 @@ struct SlabJob {
 };
 SlabJob slab_job(const float* part, int nslab, int64_t stride, int rows, int cols, int64_t ldp, float* out,
                  int64_t ldo, float div, int accumulate);
+// up to kSlabMax reductions in one launch: workgroups [blk0[i], blk0[i] + j[i].blocks) take job i
+constexpr int kSlabMax = 32;
+struct SlabBatch {
+    SlabJob j[kSlabMax];
+    int n;
+};
 // two reductions in one launch (j1 may be SlabJob{}: empty)
 int launch_slab_jobs(const SlabJob& j0, const SlabJob& j1, hipStream_t s);
+int launch_slab_batch(const SlabJob* jobs, int n, hipStream_t s);
 int launch_slab_reduce(const float* part, int nslab, int64_t stride, int rows, int cols, int64_t ldp, float* out,
                        int64_t ldo, float div, int accumulate, hipStream_t s);
 

@@ -30,6 +30,15 @@ struct WgradArgs {
     int M, Npad, Kpad, npairs, rows_per_slice, n_tiles_n, n_tiles_k, nslices;
 };
 
+// Several independent weight gradients in one launch of the stage-ring kernel (cn_wgrad_batch):
+// job i takes the next blocks[i] workgroups, each job its own M-slices and slabs.
+constexpr int kWgradBatchMax = 16;
+struct WgradBatch {
+    WgradArgs job[kWgradBatchMax];
+    int blocks[kWgradBatchMax];
+    int njobs;
+};
+
 template <int WM, int WN, int TM, int TN>
 __global__ void __launch_bounds__(64 * WM * WN, 2) wgrad_kernel(WgradArgs p) {
     constexpr int NT = 64 * WM * WN;
@@ -503,20 +512,27 @@ __global__ void __launch_bounds__(128 * WM, 2) wgrad_x6_kernel(WgradArgs p) {
 // (WGRAD_EXP=1: the kernel is not HBM-bound); 16x16x32 MFMAs (higher clock, more cycles)
 // and a register-held split of the next 32-row chunk measured equal to the old kernel.
 template <int NRAW>
-__global__ void __launch_bounds__(512, 2) wgrad_x6r_kernel(WgradArgs p) {
+__global__ void __launch_bounds__(512, 2) wgrad_x6r_kernel(WgradBatch batch) {
     constexpr int BNo = 256, MC = 16, PL = 8, LSB = 3 * PL + 4;  // 28 dwords per LDS row
     constexpr int IMG = 2 * BNo * LSB;                            // one buffer: Y rows then X rows
     __shared__ __attribute__((aligned(16))) float smem[2 * IMG];
+
+    // the job of this workgroup (scalar lookup)
+    int ji = 0, b = (int)blockIdx.x;
+    while (ji + 1 < batch.njobs && b >= batch.blocks[ji]) b -= batch.blocks[ji++];
+    const WgradArgs& p = batch.job[ji];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 1, wn = wave & 1;
-    // XCD-aware: the T output tiles of one M-slice (K or N > 256) are 8 blocks apart
+    // XCD-aware (single job): the T output tiles of one M-slice (K or N > 256) are 8 blocks apart.
+    // A batch's grid is dense (nslices x T blocks per job, no padding to whole groups of 8): the
+    // dispatcher deals block ids round-robin over the 8 XCDs, so padding blocks at fixed local
+    // ids would leave some XCDs more working workgroups than CUs (a second round of slices)
     const int T = p.n_tiles_n * p.n_tiles_k;
-    const int b = blockIdx.x;
-    const int tile = (b >> 3) % T;
-    const int slice = (b & 7) + 8 * ((b >> 3) / T);
+    const int tile = batch.njobs > 1 ? b % T : (b >> 3) % T;
+    const int slice = batch.njobs > 1 ? b / T : (b & 7) + 8 * ((b >> 3) / T);
     if (slice >= p.nslices) return;
     const int n0 = (tile / p.n_tiles_k) * BNo;
     const int k0 = (tile % p.n_tiles_k) * BNo;
@@ -675,14 +691,14 @@ SlabJob slab_job(const float* part, int nslab, int64_t stride, int rows, int col
                    (int)((groups + kSlabCG - 1) / kSlabCG), div};
 }
 
-// Two reductions in one launch (a weight gradient's dW and db): workgroups [0, j0.blocks) take
-// j0, the rest j1 -- one launch and one tail instead of two.
-__global__ void __launch_bounds__(256) slab_reduce_kernel(SlabJob j0, SlabJob j1) {
+// Several reductions in one launch (a weight gradient's dW and db, or every job of a batched
+// weight gradient): job i takes the next j[i].blocks workgroups -- one launch and one tail.
+__global__ void __launch_bounds__(256) slab_reduce_kernel(SlabBatch jobs) {
     constexpr int SG = kSlabGroups, CG = kSlabCG;
     __shared__ double red[SG][CG][4];
-    const bool second = (int)blockIdx.x >= j0.blocks;  // workgroup-uniform
-    const SlabJob& j = second ? j1 : j0;
-    const int blk = second ? (int)blockIdx.x - j0.blocks : (int)blockIdx.x;
+    int ji = 0, blk = (int)blockIdx.x;  // workgroup-uniform job lookup (scalar)
+    while (ji + 1 < jobs.n && blk >= jobs.j[ji].blocks) blk -= jobs.j[ji++].blocks;
+    const SlabJob& j = jobs.j[ji];
     const int c4n = cdiv(j.cols, 4);
     const int t = threadIdx.x % CG;
     const int sg = threadIdx.x / CG;
@@ -731,11 +747,23 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(SlabJob j0, SlabJob j1
     }
 }
 
-int launch_slab_jobs(const SlabJob& j0, const SlabJob& j1, hipStream_t s) {
-    const int blocks = j0.blocks + j1.blocks;
+int launch_slab_batch(const SlabJob* jobs, int n, hipStream_t s) {
+    CN_REQUIRE(n >= 0 && n <= kSlabMax, CN_ERR_ARG, "slab_reduce: %d jobs (at most %d)", n, kSlabMax);
+    SlabBatch b{};
+    int blocks = 0;
+    for (int i = 0; i < n; ++i) {
+        if (jobs[i].blocks == 0) continue;  // empty job (e.g. no db)
+        b.j[b.n++] = jobs[i];
+        blocks += jobs[i].blocks;
+    }
     if (blocks == 0) return CN_OK;
-    slab_reduce_kernel<<<blocks, 256, 0, s>>>(j0, j1);
+    slab_reduce_kernel<<<blocks, 256, 0, s>>>(b);
     return check_launch("slab_reduce");
+}
+
+int launch_slab_jobs(const SlabJob& j0, const SlabJob& j1, hipStream_t s) {
+    const SlabJob jobs[2] = {j0, j1};
+    return launch_slab_batch(jobs, 2, s);
 }
 
 int launch_slab_reduce(const float* part, int nslab, int64_t stride, int rows, int cols, int64_t ldp, float* out,
@@ -772,8 +800,10 @@ static int wgrad_wide(const cn_wgrad_desc* d) {
     return narrow && d->K <= 64 ? 2 : 0;
 }
 
+// budget: workgroups this weight gradient may use (< 0: the default target; cn_wgrad_batch hands
+// each job its share of one launch)
 static void wgrad_geometry(int M, int N, int K, int wide, int* tile, int* Npad, int* Kpad, int* nslices,
-                           int* rows_per_slice) {
+                           int* rows_per_slice, int budget = -1) {
     const int t = wide == 1 ? 2 : wide == 2 ? 3 : (K % 128 == 0) ? 0 : 1;
     const int BNo = t >= 2 ? 256 : 128, BKo = t == 2 ? 256 : t == 0 ? 128 : 64;
     *tile = t;
@@ -784,7 +814,8 @@ static void wgrad_geometry(int M, int N, int K, int wide, int* tile, int* Npad, 
         const char* e = getenv("COPENERF_WGRAD_BLOCKS");
         return e ? atoi(e) : 512;
     }();
-    int ns = std::max(1, (t == 2 ? kTarget / 2 : kTarget) / tiles);  // (t 3: 2 workgroups per CU)
+    const int target = budget >= 0 ? budget : (t == 2 ? kTarget / 2 : kTarget);  // (t 2: 1 workgroup per CU)
+    int ns = std::max(1, target / tiles);
     ns = std::min(ns, std::max(1, cdiv(M, 512)));
     int rps = cdiv(cdiv(M, ns), 64) * 64;  // whole 32-row (fp32) / 64-row (bf16) chunks
     ns = std::max(1, cdiv(M, rps));
@@ -815,7 +846,8 @@ extern "C" int cn_wgrad_kernel_name(const cn_wgrad_desc* d, char* buf, int32_t l
         k = tile == 0 ? "wgrad_bf16_kernel<2, 2, 2, 2>" : "wgrad_bf16_kernel<2, 2, 2, 1>";
     else
         k = tile == 0 ? "wgrad_kernel<2, 2, 2, 2>" : "wgrad_kernel<2, 2, 2, 1>";
-    const int n = snprintf(buf, (size_t)len, "void cn::%s(cn::WgradArgs)", k);
+    const bool ring = d->mfma_dtype == CN_MFMA_F32_BF16X6 && tile == 2 && g_wgrad_variant != 1;
+    const int n = snprintf(buf, (size_t)len, "void cn::%s(cn::%s)", k, ring ? "WgradBatch" : "WgradArgs");
     CN_REQUIRE(n < len, CN_ERR_SHAPE, "cn_wgrad_kernel_name: buffer of %d bytes too small (%d)", len, n + 1);
     return n;
 }
@@ -830,14 +862,19 @@ extern "C" size_t cn_wgrad_workspace_bytes(int32_t M, int32_t N, int32_t K) {
     return need;
 }
 
-extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
+// Checks a descriptor and lays out its launch: kernel arguments, the tile class, the grid and
+// the slab reductions of dW and db.  budget as in wgrad_geometry.
+static int wgrad_plan(const cn_wgrad_desc* d, int budget, WgradArgs* a, int* tile_out, int* grid_out, SlabJob* jw,
+                      SlabJob* jb) {
     CN_REQUIRE(d, CN_ERR_ARG, "cn_wgrad: null desc");
     CN_REQUIRE(d->Y0 && d->X0 && d->dW && d->workspace, CN_ERR_ARG, "cn_wgrad: Y0, X0, dW, workspace required");
     CN_REQUIRE(d->npairs == 1 || (d->npairs == 2 && d->Y1 && d->X1), CN_ERR_ARG, "cn_wgrad: bad npairs");
     CN_REQUIRE(d->M >= 0 && d->N > 0 && d->K > 0 && d->K % 64 == 0, CN_ERR_SHAPE,
                "cn_wgrad: bad shape M=%d N=%d K=%d (K must be a multiple of 64)", d->M, d->N, d->K);
+    CN_REQUIRE(d->mfma_dtype == CN_MFMA_F32 || d->mfma_dtype == CN_MFMA_BF16 || d->mfma_dtype == CN_MFMA_F32_BF16X6,
+               CN_ERR_ARG, "cn_wgrad: bad mfma_dtype %d", d->mfma_dtype);
     int tile, Npad, Kpad, ns, rps;
-    wgrad_geometry(std::max(d->M, 1), d->N, d->K, wgrad_wide(d), &tile, &Npad, &Kpad, &ns, &rps);
+    wgrad_geometry(std::max(d->M, 1), d->N, d->K, wgrad_wide(d), &tile, &Npad, &Kpad, &ns, &rps, budget);
     CN_REQUIRE(d->n_out <= Npad && d->k_out <= Kpad && d->n_out > 0 && d->k_out > 0, CN_ERR_SHAPE, "cn_wgrad: bad n_out/k_out");
     CN_REQUIRE(d->ldy0 >= Npad && d->ldx0 >= Kpad && d->ldy0 % 4 == 0 && d->ldx0 % 4 == 0 && al16(d->Y0) && al16(d->X0),
                CN_ERR_ALIGN, "cn_wgrad: Y0/X0 must be 16B aligned with ld >= padded tile (%d, %d)", Npad, Kpad);
@@ -846,29 +883,46 @@ extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
                    CN_ERR_ALIGN, "cn_wgrad: Y1/X1 alignment");
     CN_REQUIRE(d->ldy0 < (1 << 20) && d->ldx0 < (1 << 20) && d->ldy1 < (1 << 20) && d->ldx1 < (1 << 20), CN_ERR_SHAPE,
                "cn_wgrad: leading dimensions must be < 2^20");
-    const size_t need = cn_wgrad_workspace_bytes(d->M, d->N, d->K);
+    const size_t need = cn_wgrad_workspace_bytes(d->M, d->N, d->K);  // covers every budget (ns <= the default's)
     CN_REQUIRE((size_t)d->workspace_bytes >= need, CN_ERR_SHAPE, "cn_wgrad: workspace %lld < %zu", (long long)d->workspace_bytes, need);
-    hipStream_t s = (hipStream_t)stream;
-    WgradArgs a;
-    a.Y0 = d->Y0; a.X0 = d->X0; a.Y1 = d->Y1; a.X1 = d->X1;
-    a.part = d->workspace;
-    a.bpart = d->db ? d->workspace + (size_t)ns * Npad * Kpad : nullptr;
-    a.ldy0 = (int)d->ldy0; a.ldx0 = (int)d->ldx0; a.ldy1 = (int)d->ldy1; a.ldx1 = (int)d->ldx1;
-    a.M = d->M; a.Npad = Npad; a.Kpad = Kpad; a.npairs = d->npairs; a.rows_per_slice = rps;
+    a->Y0 = d->Y0; a->X0 = d->X0; a->Y1 = d->Y1; a->X1 = d->X1;
+    a->part = d->workspace;
+    a->bpart = d->db ? d->workspace + (size_t)ns * Npad * Kpad : nullptr;
+    a->ldy0 = (int)d->ldy0; a->ldx0 = (int)d->ldx0; a->ldy1 = (int)d->ldy1; a->ldx1 = (int)d->ldx1;
+    a->M = d->M; a->Npad = Npad; a->Kpad = Kpad; a->npairs = d->npairs; a->rows_per_slice = rps;
     const int BNo = tile >= 2 ? 256 : 128, BKo = tile == 2 ? 256 : tile == 0 ? 128 : 64;
-    a.n_tiles_k = Kpad / BKo;
-    a.n_tiles_n = Npad / BNo;
-    a.nslices = ns;
-    dim3 grid(cdiv(ns, 8) * 8 * a.n_tiles_n * a.n_tiles_k);
-    CN_REQUIRE(d->mfma_dtype == CN_MFMA_F32 || d->mfma_dtype == CN_MFMA_BF16 || d->mfma_dtype == CN_MFMA_F32_BF16X6,
-               CN_ERR_ARG, "cn_wgrad: bad mfma_dtype %d", d->mfma_dtype);
+    a->n_tiles_k = Kpad / BKo;
+    a->n_tiles_n = Npad / BNo;
+    a->nslices = ns;
+    *tile_out = tile;
+    *grid_out = cdiv(ns, 8) * 8 * a->n_tiles_n * a->n_tiles_k;
+    // dW and db (when asked for) in one reduction launch
+    *jw = slab_job(a->part, ns, (int64_t)Npad * Kpad, d->n_out, d->k_out, Kpad, d->dW, d->ld_dw, 1.0f, d->accumulate);
+    *jb = d->db ? slab_job(a->bpart, ns, Npad, 1, d->n_out, Npad, d->db, d->n_out, 1.0f, d->accumulate) : SlabJob{};
+    return CN_OK;
+}
+
+extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
+    WgradArgs a;
+    int tile, grid;
+    SlabJob js[2];
+    int rc = wgrad_plan(d, -1, &a, &tile, &grid, &js[0], &js[1]);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
     if (d->mfma_dtype == CN_MFMA_F32_BF16X6) {
         if (tile == 2) {
             // the stage ring (one barrier per 16 rows, split and LDS writes beside the MFMAs): C2
             // step 145.0-145.3k vs 142.1-143.3k rays/s with the 32-row single-buffer kernel
             // (COPENERF_WGRAD_KERNEL=1, benchmarking aid; tools/env_ab.sh, same box)
-            if (g_wgrad_variant == 1) wgrad_x6_kernel<4, 4><<<grid, 512, 0, s>>>(a);
-            else wgrad_x6r_kernel<2><<<grid, 512, 0, s>>>(a);
+            if (g_wgrad_variant == 1) {
+                wgrad_x6_kernel<4, 4><<<grid, 512, 0, s>>>(a);
+            } else {
+                WgradBatch b{};
+                b.job[0] = a;
+                b.blocks[0] = grid;
+                b.njobs = 1;
+                wgrad_x6r_kernel<2><<<grid, 512, 0, s>>>(b);
+            }
         }
         else if (tile == 3)
             wgrad_x6_kernel<4, 1><<<grid, 512, 0, s>>>(a);
@@ -886,12 +940,60 @@ extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
     } else {
         wgrad_kernel<2, 2, 2, 1><<<grid, 256, 0, s>>>(a);
     }
-    int rc = check_launch("cn_wgrad");
-    if (rc) return rc;
-    // dW and db (when asked for) in one reduction launch
-    const SlabJob jw = slab_job(a.part, ns, (int64_t)Npad * Kpad, d->n_out, d->k_out, Kpad, d->dW, d->ld_dw, 1.0f,
-                                d->accumulate);
-    const SlabJob jb = d->db ? slab_job(a.bpart, ns, Npad, 1, d->n_out, Npad, d->db, d->n_out, 1.0f, d->accumulate)
-                             : SlabJob{};
-    return launch_slab_jobs(jw, jb, s);
+    rc = check_launch("cn_wgrad");
+    return rc ? rc : launch_slab_batch(js, 2, s);
+}
+
+// Whether cn_wgrad_batch runs a descriptor inside its shared stage-ring launch.
+static bool wgrad_batchable(const cn_wgrad_desc* d) {
+    return d->mfma_dtype == CN_MFMA_F32_BF16X6 && g_wgrad_variant != 1 && wgrad_wide(d) == 1;
+}
+
+extern "C" int cn_wgrad_batch(const cn_wgrad_desc* descs, int32_t n, cn_stream_t stream) {
+    CN_REQUIRE(descs && n >= 0, CN_ERR_ARG, "cn_wgrad_batch: null descs / n < 0");
+    hipStream_t s = (hipStream_t)stream;
+    // the stage-ring (256x256) jobs share one launch of one workgroup per CU: each takes a share of
+    // the workgroups proportional to its work (rows x pairs x output tiles), so they end together
+    double work[kWgradBatchMax];
+    int idx[kWgradBatchMax];
+    int nb = 0;
+    double total = 0.0;
+    for (int i = 0; i < n; ++i) {
+        const cn_wgrad_desc* d = descs + i;
+        if (!d || !wgrad_batchable(d) || nb == kWgradBatchMax) {
+            int rc = cn_wgrad(d, stream);  // another tile class (or a full batch): its own launch
+            if (rc) return rc;
+            continue;
+        }
+        const int tiles = cdiv(d->N, 256) * cdiv(d->K, 256);
+        work[nb] = (double)std::max(d->M, 1) * d->npairs * tiles;
+        total += work[nb];
+        idx[nb++] = i;
+    }
+    if (nb == 0) return CN_OK;
+    static const int kCUs = [] {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        return cus > 0 ? cus : 256;
+    }();
+    WgradBatch b{};
+    SlabJob js[2 * kWgradBatchMax];
+    int grid = 0;
+    for (int q = 0; q < nb; ++q) {
+        const cn_wgrad_desc* d = descs + idx[q];
+        const int tiles = cdiv(d->N, 256) * cdiv(d->K, 256);
+        // floor of the proportional share: the slices of all jobs never exceed one workgroup per CU
+        const int budget = std::max(tiles, (int)(kCUs * work[q] / total) / tiles * tiles);
+        int tile, g;
+        int rc = wgrad_plan(d, budget, &b.job[q], &tile, &g, &js[2 * q], &js[2 * q + 1]);
+        if (rc) return rc;
+        g = b.job[q].nslices * b.job[q].n_tiles_n * b.job[q].n_tiles_k;  // dense (see the kernel)
+        b.blocks[q] = g;
+        grid += g;
+    }
+    b.njobs = nb;
+    if (nb == 1) b.blocks[0] = grid = cdiv(b.job[0].nslices, 8) * 8 * b.job[0].n_tiles_n * b.job[0].n_tiles_k;
+    wgrad_x6r_kernel<2><<<grid, 512, 0, s>>>(b);
+    int rc = check_launch("cn_wgrad_batch");
+    return rc ? rc : launch_slab_batch(js, 2 * nb, s);
 }

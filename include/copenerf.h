@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define CN_ABI_VERSION 8
+#define CN_ABI_VERSION 9
 
 typedef void* cn_stream_t; /* hipStream_t */
 
@@ -123,6 +123,22 @@ typedef struct cn_linear_desc {
     const float* head_b;
     float* head_out;           /* [M] (or indexed by head_idx) */
     const int32_t* head_idx;   /* [M] destination rows or NULL */
+    /* ABI v9 -- the first SDF layer with the positional encoding fused into its operand load
+       (neus_embedder.py:6-51 feeding neus_fields.py:268-272): when emb_x != NULL, A must be NULL and
+       row m of A is the encoding of emb_scale * emb_x[m][0:4] (column group 0: the scaled point, groups
+       1 + 2k / 2 + 2k: sin / cos(2^k x') for k < emb_multires, zero up to K <= 64), computed while the
+       tile is staged; SOFTPLUS or STORE, tile 0.  Optional side outputs, written once per row: emb_u0
+       = the encoding [M][K] (what cn_sdf_embed writes), emb_u4 = its first 4 (1 + 2 emb_multires)
+       columns divided by emb_u4_div (0 means 1: the skip input's tail, neus_fields.py:276-277). */
+    const float* emb_x;
+    int64_t ld_emb_x;
+    int32_t emb_multires;
+    float emb_scale;
+    float* emb_u0;
+    int64_t ld_emb_u0;
+    float* emb_u4;
+    int64_t ld_emb_u4;
+    float emb_u4_div;
 } cn_linear_desc;
 
 enum cn_mfma_dtype { CN_MFMA_F32 = 0, CN_MFMA_BF16 = 1, CN_MFMA_F32_BF16X6 = 2 };
@@ -212,6 +228,13 @@ size_t cn_wgrad_workspace_bytes(int32_t M, int32_t N, int32_t K);
 int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream);
 /* As cn_linear_kernel_name for cn_wgrad's split-M kernel (cn::slab_reduce_kernel follows it). */
 int cn_wgrad_kernel_name(const cn_wgrad_desc* d, char* buf, int32_t len);
+/* Several independent weight gradients (ABI v9).  The descriptors that cn_wgrad would run on the
+ * 256x256 bf16x6 stage-ring kernel share ONE launch of it (each takes a share of the workgroups
+ * proportional to its rows x pairs x output tiles, its own M-slices and slabs in its own
+ * workspace) and ONE cn::slab_reduce_kernel launch; any other descriptor is run as by cn_wgrad.
+ * Results equal cn_wgrad's up to the slice count (fixed-order sums: bitwise reproducible).
+ * Replaces the per-layer dW of neus_fields.py:291-303 (SDF) and 364-373 (colour) as one call. */
+int cn_wgrad_batch(const cn_wgrad_desc* descs, int32_t n, cn_stream_t stream);
 
 /* ------------------------------------------------------------------------ *
  * Per-row heads (neus_fields.py:279-283 last Linear row 0 = sdf;

@@ -62,6 +62,10 @@ def test_argument_validation_without_gpu():
     assert lib.cn_up_sample_merge(1, 300, 16, 1.0, 16, 16, 16, 16, None, None, None) == -5
     w = _lib.WgradDesc()
     assert lib.cn_wgrad(ctypes.byref(w), None) == -1
+    assert lib.cn_wgrad_batch(None, 1, None) == -1
+    ws2 = (_lib.WgradDesc * 2)()
+    assert lib.cn_wgrad_batch(ws2, 2, None) == -1  # checked before anything launches
+    assert lib.cn_wgrad_batch(ws2, 0, None) == 0
     assert lib.cn_wgrad_workspace_bytes(524288, 256, 256) >= 4 * 256 * 256
     ws = lib.cn_train_loss_workspace_bytes(4096, 4)
     assert ws >= 8 * (4096 // 16 // 256)
@@ -104,7 +108,7 @@ def test_kernel_name_queries_follow_the_launch_choice():
     w = _lib.WgradDesc()
     w.M, w.N, w.K, w.npairs, w.mfma_dtype = 524288, 256, 256, 2, 2
     w.ldy0 = w.ldx0 = w.ldy1 = w.ldx1 = 256
-    assert ops.kernel_name(_lib.load().cn_wgrad_kernel_name, w) == "void cn::wgrad_x6r_kernel<2>(cn::WgradArgs)"
+    assert ops.kernel_name(_lib.load().cn_wgrad_kernel_name, w) == "void cn::wgrad_x6r_kernel<2>(cn::WgradBatch)"
     w.K, w.ldx0, w.ldx1 = 64, 64, 64
     assert ops.kernel_name(_lib.load().cn_wgrad_kernel_name, w) == "void cn::wgrad_x6_kernel<2, 1>(cn::WgradArgs)"
     assert _lib.load().cn_linear_kernel_name(d, ctypes.create_string_buffer(8), 8) == -2  # CN_ERR_SHAPE

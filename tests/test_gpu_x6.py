@@ -161,3 +161,85 @@ def test_linear_x6_narrow_n_on_the_wide_tile(nzero):
         torch.testing.assert_close(got[:, :N], ref[:, :N], rtol=2e-5, atol=2e-6, msg=lambda m: f"epi {epi}: {m}")
         assert torch.all(got[:, N:nzero] == 0), epi
         assert torch.all(got[:, nzero:] == 7.0), epi
+
+
+def test_wgrad_batch_matches_single_calls():
+    """cn_wgrad_batch (ops.WgradQueue): the stage-ring jobs share one launch and one slab
+    reduction, each with its share of the workgroups; every job's dW / db equals its own
+    cn_wgrad call's up to the summation order (fewer, longer M-slices): within fp32
+    rounding of the float64 products (longer slices: see the bar), and bitwise repeatable.  Jobs: C2-shape two-pair and
+    one-pair 256x256 layers, two output tiles (K = 512), a ragged M, a 204-wide layer on
+    256-wide rows and a K = 64 first layer (another tile class: launched at add())."""
+    from copenerf import ops
+    specs = [(70000, 256, 256, 2, 256), (70000, 256, 256, 1, 256), (5000, 256, 512, 2, 512),
+             (1001, 256, 256, 1, 256), (3000, 204, 256, 2, 256), (20000, 256, 64, 2, 64)]
+    jobs = []
+    for i, (M, N, K, pairs, ldk) in enumerate(specs):
+        Y0, X0 = _rnd(M, 256, seed=40 + 4 * i), _rnd(M, ldk, seed=41 + 4 * i)
+        Y1, X1 = (_rnd(M, 256, seed=42 + 4 * i), _rnd(M, ldk, seed=43 + 4 * i)) if pairs == 2 else (None, None)
+        jobs.append((Y0, X0, Y1, X1, N, K))
+
+    def run_batch():
+        q = ops.WgradQueue()
+        outs = []
+        for Y0, X0, Y1, X1, N, K in jobs:
+            dW, db = torch.full((N, K), float("nan"), device=DEV), torch.full((N,), float("nan"), device=DEV)
+            q.add(Y0, X0, N, K, dW, db=db, Y1=Y1, X1=X1, mode="bf16x6")
+            outs.append((dW, db))
+        q.flush()
+        return outs
+
+    got = run_batch()
+    again = run_batch()
+    for (Y0, X0, Y1, X1, N, K), (dW, db), (dW2, db2) in zip(jobs, got, again):
+        ref, rb = torch.empty(N, K, device=DEV), torch.empty(N, device=DEV)
+        ops.wgrad(Y0, X0, N, K, ref, db=rb, Y1=Y1, X1=X1, mode="bf16x6")
+        exact = Y0[:, :N].double().t() @ X0[:, :K].double()
+        if Y1 is not None:
+            exact = exact + Y1[:, :N].double().t() @ X1[:, :K].double()
+        scale = exact.abs().max().item()
+        e_single = (ref.double() - exact).abs().max().item()
+        e_batch = (dW.double() - exact).abs().max().item()
+        print(f"M={Y0.shape[0]} N={N} K={K}: single {e_single:.3e} batch {e_batch:.3e} (|dW| max {scale:.1f})")
+        assert torch.isfinite(dW).all() and torch.isfinite(db).all()
+        # fewer, longer M-slices: each slice's fp32 accumulation runs over more rows (C2's 7-job
+        # SDF batch: 36 slices of 14,592 rows instead of 256 of 2,048), so the error may grow by
+        # about the square root of the length ratio -- still ~1e-6 of |dW|, fp32 class
+        assert e_batch <= 4.0 * e_single + 1e-7 * scale and e_batch <= 4e-6 * scale
+        torch.testing.assert_close(db, rb, rtol=1e-5, atol=1e-6 * Y0.shape[0] ** 0.5)
+        assert torch.equal(dW, dW2) and torch.equal(db, db2)
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16x6", "bf16"])
+def test_fused_encoding_first_layer_bitwise(mode):
+    """The first SDF layer with the positional encoding computed in its operand load (cn_linear
+    emb_x, COPENERF_FUSE_EMB) against the cn_sdf_embed pass + GEMM: the encoding is one device
+    function and the GEMM tile is the same, so sdf, ∇ₓsdf, the feature, every parameter gradient
+    and the stored encoding / skip tail are bitwise equal -- on the grad path (U0 stored) and on
+    the sampler path (keep=False: no U0 at all).  A ragged M exercises the rows past the end."""
+    from copenerf import SDFNetwork, fields
+    from helpers import SDF_CFG
+    torch.manual_seed(5)
+    net = SDFNetwork(**SDF_CFG).to(DEV)
+    net.mfma_dtype = mode
+    x = (torch.rand(5001, 4, device=DEV) * 2 - 1)
+    res = {}
+    saved = fields.FUSE_EMB
+    try:
+        for fuse in (False, True):
+            fields.FUSE_EMB = fuse
+            sdf, feat, g = net.field(x)
+            loss = ((g.norm(dim=-1) - 1) ** 2).mean() + sdf.abs().mean() + 1e-2 * feat.square().mean()
+            grads = torch.autograd.grad(loss, list(net.parameters()))
+            Ws, bs, pk = net.params_and_pack()
+            st = fields.sdf_forward(net.layout(), pk, x, want_feat=False, want_grad=False, keep=False)
+            stk = fields.sdf_forward(net.layout(), pk, x, want_feat=False, want_grad=False, keep=True)
+            res[fuse] = (sdf.detach(), feat.detach(), g.detach(), grads, st["sdf"], stk["U"][0], stk["U"][1],
+                         stk["U"][net.layout().skip])
+    finally:
+        fields.FUSE_EMB = saved
+    a, b = res[False], res[True]
+    assert all(torch.equal(u, v) for u, v in zip(a[:3], b[:3]))
+    assert all(torch.equal(u, v) for u, v in zip(a[3], b[3]))
+    for u, v in zip(a[4:], b[4:]):
+        assert torch.equal(u, v)
