@@ -674,6 +674,140 @@ __global__ void __launch_bounds__(512, 2) wgrad_x6r_kernel(WgradBatch batch) {
     }
 }
 
+// 256 x 64 weight gradient (the K = 64 first layers: the SDF's dW0 = Z_0ᵀ U0 + S_0ᵀ U̇_0 and the colour
+// network's extras columns, neus_fields.py:268-272, 364-366) on the stage ring of wgrad_x6r_kernel:
+// 16 sample rows per stage, two split-image buffers (2 x 35 KB: 256 Y rows + 64 X rows of 28 dwords),
+// NRAW register sets of raw rows in flight, one barrier per stage.  These shapes move ~6 bytes per
+// bf16x6 FLOP-pair more than the 256-wide layers (HBM-bound), so the ring keeps NRAW stages of loads in
+// flight and every wave does MFMA work: wave w owns output rows 32w .. 32w+31 (1 x 2 accumulators of
+// 32 x 32).  Waves 0-3 stage Y (m-quad t % 4 of column group t / 4), wave 4 stages X.
+template <int NRAW>
+__global__ void __launch_bounds__(512, 4) wgrad_x6n_kernel(WgradArgs p) {  // 2 per CU: <= 128 VGPRs
+    constexpr int BNo = 256, BKo = 64, MC = 16, PL = 8, LSB = 3 * PL + 4;
+    constexpr int IMG = (BNo + BKo) * LSB;
+    __shared__ __attribute__((aligned(16))) float smem[2 * IMG];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int T = p.n_tiles_n * p.n_tiles_k;
+    const int b = blockIdx.x;
+    const int tile = (b >> 3) % T;
+    const int slice = (b & 7) + 8 * ((b >> 3) / T);
+    if (slice >= p.nslices) return;
+    const int n0 = (tile / p.n_tiles_k) * BNo;
+    const int k0 = (tile % p.n_tiles_k) * BKo;
+    const int mbeg = slice * p.rows_per_slice;
+    const int mend = min(p.M, mbeg + p.rows_per_slice);
+    const int nch = mend > mbeg ? cdiv(mend - mbeg, MC) : 0;
+    const int total = nch * p.npairs;
+    const bool do_bias = k0 == 0 && p.bpart != nullptr;
+
+    const bool sy = wave < 4;    // wave-uniform staging roles: Y (waves 0-3), X (wave 4), none (5-7)
+    const bool sxw = wave == 4;
+    const bool stager = sy || sxw;
+    const int t = tid & 255, mq = t & 3, cg = t >> 2;
+    floatx4 raw[NRAW][4];
+    float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+    auto gload = [&](int c, floatx4 (&r4)[4]) {
+        if (!stager) return;  // waves 5-7 stage nothing (their raw sets are never read)
+        const bool valid = c < total;
+        const int cc = c < total ? c : 0;
+        const int pair = cc >= nch;
+        const int mrow = mbeg + (cc - pair * nch) * MC;
+        const float* src = sy ? (pair ? p.Y1 : p.Y0) : (pair ? p.X1 : p.X0);
+        const int ld = sy ? (pair ? p.ldy1 : p.ldy0) : (pair ? p.ldx1 : p.ldx0);
+        const int nrows = valid ? min(MC, mend - mrow) : 0;
+        const int col0 = sy ? n0 : k0;
+        const rsrc_t v = make_view(src + (int64_t)mrow * ld + col0, (nrows * ld - col0) * 4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) r4[r] = bload4(v, ((mq * 4 + r) * ld + cg * 4) * 4, 0);
+    };
+    auto split_col = [&](const floatx4 (&r4)[4], int e, int buf, bool bias) {
+        if (!stager) return;
+        float* img = smem + buf * IMG + (sy ? 0 : BNo * LSB) + mq * 2;
+        const floatx4 col = {r4[0][e], r4[1][e], r4[2][e], r4[3][e]};
+        const float sm = (col[0] + col[1]) + (col[2] + col[3]);
+        bsum[e] += bias ? sm : 0.0f;
+        bf16x4 t0, t1, t2;
+        split3(col, t0, t1, t2);
+        float* y = img + (cg * 4 + e) * LSB;
+        *reinterpret_cast<bf16x4*>(y) = t0;
+        *reinterpret_cast<bf16x4*>(y + PL) = t1;
+        *reinterpret_cast<bf16x4*>(y + 2 * PL) = t2;
+    };
+
+    floatx16 acc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+    const int frow = lane & 31, fh = lane >> 5;
+    constexpr int TA[6] = {0, 1, 0, 2, 1, 0};
+    constexpr int TB[6] = {0, 0, 1, 0, 1, 2};
+    // one stage in two segments: segment j issues k block j's 6 MFMAs beside split columns 2j, 2j+1
+    auto compute = [&](int buf, auto side) {
+        const float* ya = smem + buf * IMG + (wave * 32 + frow) * LSB + 4 * fh;
+        const float* xa = smem + buf * IMG + BNo * LSB + frow * LSB + 4 * fh;
+        bf16x8 af[3], bj[3];
+#pragma unroll
+        for (int tt = 0; tt < 3; ++tt) af[tt] = *reinterpret_cast<const bf16x8*>(ya + tt * PL);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+#pragma unroll
+            for (int tt = 0; tt < 3; ++tt) bj[tt] = *reinterpret_cast<const bf16x8*>(xa + j * 32 * LSB + tt * PL);
+#pragma unroll
+            for (int u = 0; u < 6; ++u)
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[TA[u]], bj[TB[u]], acc[j], 0, 0, 0);
+            side(2 * j);
+            side(2 * j + 1);
+#if WGRAD_SGB
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+        }
+    };
+    const bool ybias = do_bias & sy;
+    auto bias_of = [&](int c) { return ybias & (c < nch); };
+#pragma unroll
+    for (int st = 0; st < NRAW; ++st) gload(st, raw[st]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) split_col(raw[0], e, 0, bias_of(0));
+    __syncthreads();
+    for (int c0 = 0; c0 < total; c0 += NRAW) {
+#pragma unroll
+        for (int k = 0; k < NRAW; ++k) {
+            const int c = c0 + k;
+            gload(c + NRAW, raw[k]);  // set k held stage c (split in the previous stage)
+            const bool bnext = bias_of(c + 1);
+            compute(c & 1, [&](int e) { split_col(raw[(k + 1) % NRAW], e, (c + 1) & 1, bnext); });
+            __syncthreads();  // stage c+1 written, stage c's buffer free
+        }
+    }
+    __syncthreads();  // LDS is reused for the bias partials
+
+    const rsrc_t vP = make_view(p.part + (int64_t)slice * p.Npad * p.Kpad, p.Npad * p.Kpad * 4);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int col = k0 + j * 32 + (lane & 31);
+        const int rbase = n0 + wave * 32 + 4 * (lane >> 5);
+        const int vo = (rbase * p.Kpad + col) * 4;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) bstore1(vP, vo, ((r & 3) + 8 * (r >> 2)) * p.Kpad * 4, acc[j][r]);
+    }
+    if (do_bias) {  // reduce the Y threads' column partials over the m-quads (fixed order)
+        float* red = smem;  // [4][BNo]
+        if (sy) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) red[mq * BNo + cg * 4 + e] = bsum[e];
+        }
+        __syncthreads();
+        if (tid < BNo) {
+            const float tot = ((red[tid] + red[BNo + tid]) + red[2 * BNo + tid]) + red[3 * BNo + tid];
+            p.bpart[(int64_t)slice * p.Npad + n0 + tid] = tot;
+        }
+    }
+}
+
 // Sum of nslab fp32 slabs: out[r*ldo + c] (+)= (sum_s part[s*stride + r*ldp + c]) / div
 // for r < rows, c < cols.  A workgroup owns 64 float4 column groups x 4 slab
 // groups; each thread sums its slab group in double with 4 loads in flight, the 4
@@ -784,14 +918,13 @@ static bool wgrad_wide_on() {
     }();
     return on;
 }
-// 3 (bf16x6, K <= 64, Y rows 256-padded; COPENERF_WGRAD_NARROW=1): 256x64 tiles of 512-thread
-// workgroups.  Measured slower than the 128x64 tiles on the C2 first-layer shapes (0.418 vs
-// 0.388 ms, 0.207 vs 0.187 ms), so off by default.
+// 3 (bf16x6, K <= 64, Y rows 256-padded): 256x64 tiles of 512-thread workgroups on the stage ring
+// (wgrad_x6n_kernel; COPENERF_WGRAD_NARROW=0: the 128x64 tiles of wgrad_x6_kernel<2, 1>).
 // Returns the wide mode: 0 none, 1 = 256x256, 2 = 256x64.
 static int wgrad_wide(const cn_wgrad_desc* d) {
-    static const bool narrow = [] {
+    static const bool narrow = [] {  // COPENERF_WGRAD_NARROW=0: the 128x64 tiles for K <= 64
         const char* e = getenv("COPENERF_WGRAD_NARROW");
-        return e && atoi(e) != 0;
+        return e ? atoi(e) != 0 : true;
     }();
     const int64_t np = (int64_t)cdiv(d->N, 256) * 256, kp = (int64_t)cdiv(d->K, 256) * 256;
     if (!wgrad_wide_on() || d->mfma_dtype != CN_MFMA_F32_BF16X6 || d->ldy0 < np || (d->npairs == 2 && d->ldy1 < np))
@@ -841,7 +974,7 @@ extern "C" int cn_wgrad_kernel_name(const cn_wgrad_desc* d, char* buf, int32_t l
     const char* k = "";
     if (d->mfma_dtype == CN_MFMA_F32_BF16X6)
         k = tile == 2 ? (g_wgrad_variant == 1 ? "wgrad_x6_kernel<4, 4>" : "wgrad_x6r_kernel<2>")
-            : tile == 3 ? "wgrad_x6_kernel<4, 1>" : tile == 0 ? "wgrad_x6_kernel<2, 2>" : "wgrad_x6_kernel<2, 1>";
+            : tile == 3 ? "wgrad_x6n_kernel<3>" : tile == 0 ? "wgrad_x6_kernel<2, 2>" : "wgrad_x6_kernel<2, 1>";
     else if (d->mfma_dtype == CN_MFMA_BF16)
         k = tile == 0 ? "wgrad_bf16_kernel<2, 2, 2, 2>" : "wgrad_bf16_kernel<2, 2, 2, 1>";
     else
@@ -925,7 +1058,7 @@ extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
             }
         }
         else if (tile == 3)
-            wgrad_x6_kernel<4, 1><<<grid, 512, 0, s>>>(a);
+            wgrad_x6n_kernel<3><<<grid, 512, 0, s>>>(a);
         else if (tile == 0)
             wgrad_x6_kernel<2, 2><<<grid, 256, 0, s>>>(a);
         else

@@ -95,7 +95,7 @@ def test_product_path_refuses_cpu_tensors():
 def test_kernel_name_queries_follow_the_launch_choice():
     """cn_linear_kernel_name / cn_wgrad_kernel_name (no device access): C2's hidden-layer
     SOFTPLUS on the 256x256 bf16x6 tile, the colour network's RELU with a rowv on the 256x128
-    tile, and a 256x256 bf16x6 weight gradient on the stage ring -- the rocprofv3 symbols the
+    tile, 256x256 and 256x64 bf16x6 weight gradients on the stage rings -- the rocprofv3 symbols the
     bench's launch classes report."""
     from copenerf import _lib, ops
     d = _lib.LinearDesc()
@@ -109,6 +109,8 @@ def test_kernel_name_queries_follow_the_launch_choice():
     w.M, w.N, w.K, w.npairs, w.mfma_dtype = 524288, 256, 256, 2, 2
     w.ldy0 = w.ldx0 = w.ldy1 = w.ldx1 = 256
     assert ops.kernel_name(_lib.load().cn_wgrad_kernel_name, w) == "void cn::wgrad_x6r_kernel<2>(cn::WgradBatch)"
-    w.K, w.ldx0, w.ldx1 = 64, 64, 64
+    w.K, w.ldx0, w.ldx1 = 64, 64, 64  # a K = 64 first layer: the narrow stage ring
+    assert ops.kernel_name(_lib.load().cn_wgrad_kernel_name, w) == "void cn::wgrad_x6n_kernel<3>(cn::WgradArgs)"
+    w.ldy0 = w.ldy1 = 128  # Y rows not 256-padded: the 128x64 tiles
     assert ops.kernel_name(_lib.load().cn_wgrad_kernel_name, w) == "void cn::wgrad_x6_kernel<2, 1>(cn::WgradArgs)"
     assert _lib.load().cn_linear_kernel_name(d, ctypes.create_string_buffer(8), 8) == -2  # CN_ERR_SHAPE
