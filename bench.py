@@ -283,8 +283,8 @@ def roofline_fields(timer, steps, rays_per_s, mode):
     agg = timer.summary()
     # the dominant launch class over every cn_linear and cn_wgrad class (a launch class is one
     # kernel instance, named by the library: cn_linear_kernel_name / cn_wgrad_kernel_name; a
-    # cn_wgrad call is its split-M MFMA kernel plus the fixed-order slab reduction, both inside
-    # the class's HIP events)
+    # cn_wgrad / cn_wgrad_batch call is its split-M MFMA kernel plus the fixed-order slab reduction,
+    # both inside the class's HIP events)
     dom_key = max(agg, key=lambda k: agg[k]["ms"])
     dom = agg[dom_key]
     avg_s = dom["ms"] / dom["launches"] * 1e-3
@@ -300,7 +300,10 @@ def roofline_fields(timer, steps, rays_per_s, mode):
             "peak": HBM_PEAK_GBS if hbm else round(peak_tf, 1), "unit": "GB/s" if hbm else "TFLOP/s",
             "frac": round(max(t_flop, t_byte) / avg_s, 4), "traffic": traffic, "traffic_source": traffic_src,
             "kernel": symbol, "launch_class": "/".join(map(str, dom_key)),
-            "timed_region": "the cn_wgrad call: this kernel + cn::slab_reduce_kernel (dW, db)" if dom_key[0] == "wgrad"
+            "timed_region": ("the cn_wgrad_batch call (a backward pass's 256x256 weight gradients in one launch): "
+                             "this kernel + one cn::slab_reduce_kernel (every job's dW, db)"
+                             if "WgradBatch" in symbol else
+                             "the cn_wgrad call: this kernel + cn::slab_reduce_kernel (dW, db)") if dom_key[0] == "wgrad"
             else "this kernel", "launches_per_step": dom["launches"] / steps, "avg_launch_ms": round(avg_s * 1e3, 4),
             "algorithmic_gflop_per_launch": round(flops / 1e9, 3),
             "algorithmic_mb_per_launch": round(nbytes / 1e6, 1),

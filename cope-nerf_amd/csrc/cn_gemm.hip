@@ -787,6 +787,17 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             int voj[TN];
             bool live[TN];
             direct_cols(vo, lcol, voj, live);
+            // EPI_MUL with a split output (the skip layer's ∇ pass: columns [nsplit, N) are the
+            // embedding's adjoint, written raw (A·Bᵀ)/adiv to out_split while out0 is zero-filled
+            // there; p.nsplit = N without a split)
+            bool spl[TN];
+            int vsj[TN];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int c = n0 + lcol + 32 * j;
+                spl[j] = EPI == CN_EPI_MUL && c >= p.nsplit && c < p.N;
+                vsj[j] = (lrow * p.ld_split + lcol + 32 * j) * 4;
+            }
             constexpr int RG = kAux1 ? 2 : 4;          // accumulator rows r per group
             constexpr int NGD = TM * 16 / RG;          // groups per tile
             float xa[2][RG][TN], xb[2][RG][TN], xc[2][RG][TN];
@@ -812,10 +823,18 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 #pragma unroll
                 for (int q = 0; q < RG; ++q) {
                     const int r = r0 + q;
-                    const rsrc_t vw = view_at(tO0, i * 32 + (r & 3) + 8 * (r >> 2));
+                    const int rowi = i * 32 + (r & 3) + 8 * (r >> 2);
+                    const rsrc_t vw = view_at(tO0, rowi);
 #pragma unroll
                     for (int j = 0; j < TN; ++j) {
                         const float u = acc[i][j][r] * p.inv_adiv;
+                        if constexpr (EPI == CN_EPI_MUL) {
+                            if (spl[j]) {
+                                bstore1(view_at(tS, rowi), vsj[j], 0, u);
+                                bstore1(vw, voj[j], 0, 0.0f);
+                                continue;
+                            }
+                        }
                         const float sg = EPI == CN_EPI_BWD_RELU ? 0.0f : sigma_from_act(xa[sl][q][j], p.aux_c);
                         float o;
                         if constexpr (EPI == CN_EPI_BWD_RELU) {
@@ -1234,6 +1253,10 @@ static int g_x6_sq = [] {
     const char* e = getenv("COPENERF_X6_SQ");
     return e ? (int)strtol(e, nullptr, 0) : 0x5f;
 }();
+static bool g_sq_nosplit = [] {  // COPENERF_SQ_NOSPLIT=1: MUL with a split output on the 128x256 tile
+    const char* e = getenv("COPENERF_SQ_NOSPLIT");
+    return e && atoi(e) != 0;
+}();
 static int g_x6_sq_min_m = [] {  // smallest M for the 256x256 tile (COPENERF_X6_SQ_MINM)
     const char* e = getenv("COPENERF_X6_SQ_MINM");
     return e ? atoi(e) : 0;
@@ -1343,8 +1366,10 @@ static LinearTile choose_linear_tile(const cn_linear_desc* d) {
         // (COPENERF_WIDE_MINK: the smallest K for the 1-per-CU tiles)
         const bool longk = d->K >= g_wide_min_k;
         // (the epilogues with a direct form: STORE, SOFTPLUS, RELU, MUL, TANGENT, BWD_SOFTPLUS, BWD_RELU)
+        // (MUL with a split output too: the direct epilogue writes the split columns raw)
         const bool sq = (g_x6_sq >> d->epilogue & 1) && d->N > 128 && d->N <= 256 && !d->rowv &&
-                        d->M >= g_x6_sq_min_m && !(d->epilogue == CN_EPI_MUL && d->out_split && d->nsplit < d->N);
+                        d->M >= g_x6_sq_min_m && !(g_sq_nosplit && d->epilogue == CN_EPI_MUL && d->out_split &&
+                                                   d->nsplit < d->N);
         if (d->K % 32 == 0 && sq && d->ldb >= 256 && g_linear_variant == 0 && (longk || head)) return LT_X6_SQ;
         if (d->K % 64 == 0 && tall && d->N > 128 && d->ldb >= 256 && g_linear_variant == 0 && (longk || head))
             return LT_X6_TALL;

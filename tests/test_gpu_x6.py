@@ -243,3 +243,31 @@ def test_fused_encoding_first_layer_bitwise(mode):
     assert all(torch.equal(u, v) for u, v in zip(a[3], b[3]))
     for u, v in zip(a[4:], b[4:]):
         assert torch.equal(u, v)
+
+
+def test_linear_x6_mul_split_on_the_wide_tile():
+    """The skip layer's ∇-pass MUL with a split output (neus_fields.py:276-277: the input adjoint's
+    embedding columns go out raw) on the 256x256 tile's direct epilogue: columns < nsplit are
+    (A·Bᵀ)/adiv ⊙ σ, [nsplit, 256) of out0 are zero, the split buffer's first N - nsplit columns
+    hold the raw product and its tail is untouched; ragged M."""
+    from copenerf import _lib, ops
+    M, N, K = 1537, 256, 256
+    A = _rnd(M, K, seed=31)
+    W = _rnd(N, K, seed=32, scale=0.1)
+    B = ops.split_bf16x3(W)
+    ab = 100.0 * ops.SQRT2
+    aux0 = (torch.nn.functional.softplus(_rnd(M, N, seed=33, scale=0.05), beta=100) / ops.SQRT2).contiguous()
+    sg = -torch.expm1(-ab * aux0.double())
+    out = torch.full((M, 256), float("nan"), device=DEV)
+    split = torch.full((M, 64), float("nan"), device=DEV)
+    d = _lib.LinearDesc()
+    d.M, d.N, d.K, d.K1, d.ldb, d.epilogue, d.tile, d.mfma_dtype = M, N, K, K, B.shape[1], ops.EPI_MUL, 0, 2
+    d.out_split, d.nsplit = 16, 204
+    assert "linear_kernel<4, 2, 2, 4, 16, 1, 2, 3," in ops.kernel_name(_lib.load().cn_linear_kernel_name, d)
+    ops.linear(A, B, N, K, out, ops.EPI_MUL, aux0=aux0, aux_beta=ab, nsplit=204, out_split=split, nzero=256,
+               adiv=ops.SQRT2)
+    v = A.double() @ W.double().t() / ops.SQRT2
+    torch.testing.assert_close(out[:, :204], (v * sg)[:, :204].float(), rtol=2e-5, atol=2e-6)
+    assert torch.all(out[:, 204:] == 0)
+    torch.testing.assert_close(split[:, :52], v[:, 204:].float(), rtol=2e-5, atol=2e-6)
+    assert torch.isnan(split[:, 52:]).all()
