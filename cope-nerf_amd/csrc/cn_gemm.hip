@@ -761,9 +761,13 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                                     (EPI == CN_EPI_MUL || EPI == CN_EPI_TANGENT || EPI == CN_EPI_BWD_SOFTPLUS ||
                                      EPI == CN_EPI_BWD_RELU);
         constexpr bool kDirect = DIRECT_EPI && ((!kAnyAux && EPI != 7) || kDirectAux);
+        // SOFTPLUS_HEAD on the 64x128 wave tiles: the activation, the ∇-pass seed and the sdf row-dot
+        // from the MFMA layout too (row sums: butterfly over the 32 lanes of a row, then the two
+        // column waves' partials through LDS)
+        constexpr bool kDirectHead = DIRECT_EPI && kHead && TM * TN >= 8;
         // 64x128 wave tiles are dispatched only where one tile spans all columns (128 < N <= 256, no
-        // split, no rowv: host-checked), so their kernels carry no LDS-park path (and its registers)
-        constexpr bool kDirectOnly = kDirect && TM * TN >= 8;
+        // rowv: host-checked), so their kernels carry no LDS-park path (and its registers)
+        constexpr bool kDirectOnly = (kDirect || kDirectHead) && TM * TN >= 8;
         // per column block j of this lane: the store offset, or one past any view (the buffer
         // drops the store) for columns >= nzero; live = column < N (else the zero fill of
         // [N, nzero)).  On main tiles every column is live; the 256x256 tile also takes
@@ -878,8 +882,56 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                     }
                 }
         };
+        auto direct_head = [&]() {
+            const int lrow = wm * TM * 32 + 4 * (lane >> 5);
+            const int lcol = wn * TN * 32 + (lane & 31);
+            int voj[TN], vo1[TN];
+            bool live[TN];
+            direct_cols((lrow * p.ld_out0 + lcol) * 4, lcol, voj, live);
+            float bj[TN], cj[TN], hj[TN];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int c = min(n0 + lcol + 32 * j, TBLC - 1);
+                bj[j] = sBias[c];
+                cj[j] = sColv[c];
+                hj[j] = sHeadW[c];  // zero past N (the table's view ends at N)
+                vo1[j] = voj[j] == (1 << 30) ? voj[j] : (lrow * p.ld_out1 + lcol + 32 * j) * 4;
+            }
+            float* sRed = sA + BM * LS;  // staging buffer 1 is free after the main loop (its last reader)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int rowi = i * 32 + (r & 3) + 8 * (r >> 2);
+                    const rsrc_t vw = view_at(tO0, rowi);
+                    const rsrc_t vw1 = view_at(tO1, rowi);
+                    float part = 0.0f;
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        const float a = softplus_hw(acc[i][j][r] * p.inv_adiv + bj[j], c_exp, c_thr, c_log) * p.inv_odiv;
+                        const float o = live[j] ? a : 0.0f;
+                        bstore1(vw, voj[j], 0, o);  // (out0 NULL: empty view)
+                        bstore1(vw1, vo1[j], 0, live[j] ? cj[j] * sigma_from_act(a, p.aux_c) : 0.0f);
+                        part += o * hj[j];
+                    }
+                    // the 32 lanes holding this row (lane >> 5 fixed), fixed butterfly order
+#pragma unroll
+                    for (int off = 16; off > 0; off >>= 1) part += __shfl_xor(part, off, 64);
+                    if ((lane & 31) == 0) sRed[(lrow + rowi) * 2 + wn] = part;
+                }
+            __syncthreads();  // (the next tile's first staging barrier orders these reads before buffer 1's reuse)
+            if (tid < BM) {
+                const int row = m0 + tid;
+                if (row < p.M) {
+                    const float sum = sRed[tid * 2] + sRed[tid * 2 + 1];
+                    const int dst = p.head_idx ? p.head_idx[row] : row;
+                    p.head_out[dst] = sum + sHeadW[TBLC];
+                }
+            }
+        };
         if constexpr (kDirectOnly) {
-            if constexpr (kDirectAux) direct_aux();
+            if constexpr (kDirectHead) direct_head();
+            else if constexpr (kDirectAux) direct_aux();
             else direct_plain();
         } else {
             if (kDirectAux && tile_main) {
@@ -1247,11 +1299,11 @@ static int g_x6_tall = [] {
 // loop 316-320 vs 374 us at C2's layer shape; with the epilogue (tools/sq_check.py, bitwise equal
 // outputs): SOFTPLUS 445 vs 480-509, STORE 467 vs 491, RELU 385 vs 408-420, MUL / TANGENT 443-451 vs
 // 470 (their aux rows read in the MFMA layout); BWD_RELU 455-463 vs 477-479; BWD_SOFTPLUS 667 vs 614
-// (stays on 128x128).  Only for 128 < N <= 256 without a split output: one tile spans every column
+// (stays on 128x128); SOFTPLUS_HEAD (round 3) and MUL with a split output too.  Only for 128 < N <= 256: one tile spans every column
 // and takes the direct (MFMA-layout) epilogue, columns >= N masked (zero fill up to nzero).
 static int g_x6_sq = [] {
     const char* e = getenv("COPENERF_X6_SQ");
-    return e ? (int)strtol(e, nullptr, 0) : 0x5f;
+    return e ? (int)strtol(e, nullptr, 0) : 0x15f;  // bit e: epilogue e (SOFTPLUS_HEAD = 8 since round 3)
 }();
 static bool g_sq_nosplit = [] {  // COPENERF_SQ_NOSPLIT=1: MUL with a split output on the 128x256 tile
     const char* e = getenv("COPENERF_SQ_NOSPLIT");
