@@ -49,6 +49,8 @@ from .motion import (MotionNetwork, affine_points, flow_rgb_loss, masked_chain, 
 from .rays import PoseRetriever, get_patch_indices, intrinsics_ndc, inv4x4, pixels_from_indices, world_rays
 from .renderer import NeuSRenderer
 
+FUSED_ADAM = os.environ.get("COPENERF_FUSED_ADAM", "1") != "0"
+
 SDF_CFG = dict(d_in=4, d_out=257, d_hidden=256, n_layers=8, skip_in=[4], multires=6, bias=0.5, scale=1.0,
                geometric_init=True, weight_norm=True)
 COL_CFG = dict(d_feature=256, mode="idr", d_in=11, d_out=3, d_hidden=256, n_layers=4, weight_norm=True,
@@ -226,7 +228,10 @@ class SyntheticTrainer:
             self.ref_intervals = torch.tensor(self.cfg["random_ref_interval"], device=self.device)
             self.chain_steps = torch.arange(max(self.cfg["random_ref_interval"]), device=self.device)
         self.all_params = [p for g in groups for p in g["params"]]
-        self.opt = torch.optim.Adam(groups, lr=lr, capturable=capturable)
+        # torch's fused multi-tensor Adam: one kernel chain per step instead of the foreach
+        # implementation's ~8 launches (same update rule, training.py:552-558 / train.py:57-60);
+        # COPENERF_FUSED_ADAM=0 restores foreach
+        self.opt = torch.optim.Adam(groups, lr=lr, capturable=capturable, fused=True if FUSED_ADAM else None)
         # data: rank-independent (every rank sees the same frames); sampling: per rank
         gdata = torch.Generator(device=self.device).manual_seed(seed)
         self.images = torch.rand(n_images, 3, H, W, device=self.device, generator=gdata)

@@ -1328,10 +1328,15 @@ static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_
     a.n_tiles_m = cdiv(d->M, BM);
     a.n_tiles_n = cdiv(d->N, BN);
     const int ntiles = cdiv(a.n_tiles_m, 8) * 8 * a.n_tiles_n;
+    static thread_local int cached_dev = -1, cached_cus = 256;  // per-launch attribute query avoided
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) {
-        int v = 0;
-        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) cus = v;
+        if (dev != cached_dev) {
+            int v = 0;
+            cached_cus = (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
+            cached_dev = dev;
+        }
+        cus = cached_cus;
     }
     const int grid = std::min(ntiles, OCC * cus);  // OCC resident workgroups per CU
     dim3 block(64 * WM * WN);
