@@ -253,7 +253,7 @@ class ImagePacker:
 # launch-class tags of the kernel timer: linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, ...> arguments
 # (named by the library itself, cn_linear_kernel_name) -> a short tile name
 _TILE_TAGS = {"4, 2, 2, 4, 16, 1, 2": "sq", "4, 2, 1, 4, 32, 1, 2": "tall", "4, 2, 2, 2, 32, 1, 2": "wide",
-              "2, 2, 2, 2, 16, 2, 2": "t128", "4, 1, 1, 2, 16, 2, 2": "t1"}
+              "2, 2, 2, 2, 16, 2, 2": "t128", "4, 1, 1, 2, 16, 2, 2": "t1", "2, 2, 2, 4, 16, 2, 2": "t2w"}
 
 
 def kernel_name(query, d) -> str:

@@ -123,7 +123,11 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     constexpr int ESZB = BF ? 2 : 4;             // bytes per B element
     constexpr int PIECES_PL = BK / 8;            // MODE 2: 16-byte pieces per plane of a staged row
     constexpr int CS = BN + 4;
-    constexpr int LDS_FLOATS = 2 * (BM + BN) * LS;
+    // kB1: the two-per-CU 128x256 bf16x6 tile (BWD_SOFTPLUS: every workgroup owns whole 256-wide rows, so A
+    // is read once, and the partner workgroup hides the epilogue's aux streams) fits two workgroups in the
+    // LDS only with ONE B stage buffer: A stays double-buffered, B is re-staged between two barriers
+    constexpr bool kB1 = MODE == 2 && OCC == 2 && TM * TN >= 8;
+    constexpr int LDS_FLOATS = 2 * BM * LS + (kB1 ? 1 : 2) * BN * LS;
     // the epilogue parks the C tile in the staging LDS, in NPART row slabs if it does not fit
     constexpr int NPART = (BM * CS <= LDS_FLOATS) ? 1 : ((BM / 2) * CS <= LDS_FLOATS ? 2 : 4);
     static_assert((BM / NPART) * CS <= LDS_FLOATS, "C tile slab must fit in the staging LDS");
@@ -237,7 +241,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     // piece < 0: the whole stage; piece q < ALD: A row q only; piece ALD: B only
     auto lstore = [&](int set, int buf, int piece = -1) {
         float* a = sA + buf * BM * LS + lds_a;
-        float* b = sB + buf * BN * LS + lds_b;
+        float* b = sB + (kB1 ? 0 : buf) * BN * LS + lds_b;
 #pragma unroll
         for (int q = 0; q < ALD; ++q) {
             if (piece >= 0 && piece != q) continue;
@@ -279,7 +283,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             if constexpr (MODE == 2) {
                 const int idx = tid + q * NT;
                 if (BN * KCB % NT == 0 || idx < BN * KCB)  // wave-uniform (NT, BN*KCB multiples of 64)
-                    *reinterpret_cast<floatx4*>(sB + buf * BN * LS + ldsB[q]) = rb[set][q];
+                    *reinterpret_cast<floatx4*>(sB + (kB1 ? 0 : buf) * BN * LS + ldsB[q]) = rb[set][q];
             } else {
                 *reinterpret_cast<floatx4*>(b + q * RSTEPB * LS) = rb[set][q];
             }
@@ -385,7 +389,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         auto compute = [&](int cur, auto side) {
             if constexpr (MODE == 2) {
                 const float* a_base = sA + cur * BM * LS + arow * LS + 4 * (lane >> 5);
-                const float* b_base = sB + cur * BN * LS + brow * LS + 4 * (lane >> 5);
+                const float* b_base = sB + (kB1 ? 0 : cur) * BN * LS + brow * LS + 4 * (lane >> 5);
                 if constexpr (TM * TN >= 8) {
                     // 64x128 wave tiles: the B fragments of one column block at a time (12 VGPRs
                     // instead of 48 live); a single accumulation chain issues back to back
@@ -455,7 +459,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             } else if constexpr (BF) {
                 // lane half h holds k = 8h + j of each 16-deep MFMA step (8 bf16 = 4 dwords)
                 const float* a_base = sA + cur * BM * LS + arow * LS + 4 * (lane >> 5);
-                const float* b_base = sB + cur * BN * LS + brow * LS + 4 * (lane >> 5);
+                const float* b_base = sB + (kB1 ? 0 : cur) * BN * LS + brow * LS + 4 * (lane >> 5);
 #pragma unroll
                 for (int ks = 0; ks < BK / 16; ++ks) {
                     bf16x8 af[TM], bf[TN];
@@ -474,7 +478,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 return;
             }
             const float* a_base = sA + cur * BM * LS + arow * LS + kofs;
-            const float* b_base = sB + cur * BN * LS + brow * LS + kofs;
+            const float* b_base = sB + (kB1 ? 0 : cur) * BN * LS + brow * LS + kofs;
 #pragma unroll
             for (int q4 = 0; q4 < BK / 8; ++q4) {
                 floatx4 af[TM], bf[TN];
@@ -531,6 +535,17 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         continue;
                     }
                     compute(j & 1, [](int) {});
+                    if constexpr (kB1) {  // A into the free buffer; B after every wave is done reading it
+                        const bool more = LSTORE_ALWAYS || kc + j + 1 < nk;
+                        if (more) {
+#pragma unroll
+                            for (int q = 0; q < ALD; ++q) lstore((j + 1) % DEPTH, (j + 1) & 1, q);
+                        }
+                        __syncthreads();
+                        if (more) lstore((j + 1) % DEPTH, 0, ALD);
+                        __syncthreads();
+                        continue;
+                    }
                     // unconditional (branch-free: compute and the next stage's staging share a
                     // basic block, so the scheduler can interleave the split VALU / LDS writes
                     // with the MFMAs).  After the last chunk this stages the next tile's first
@@ -1305,6 +1320,10 @@ static int g_x6_sq = [] {
     const char* e = getenv("COPENERF_X6_SQ");
     return e ? (int)strtol(e, nullptr, 0) : 0x15f;  // bit e: epilogue e (SOFTPLUS_HEAD = 8 since round 3)
 }();
+static int g_x6_t2w = [] {  // epilogues on the 128x256 two-per-CU tile (COPENERF_X6_T2W)
+    const char* e = getenv("COPENERF_X6_T2W");
+    return e ? (int)strtol(e, nullptr, 0) : 0;
+}();
 static bool g_sq_nosplit = [] {  // COPENERF_SQ_NOSPLIT=1: MUL with a split output on the 128x256 tile
     const char* e = getenv("COPENERF_SQ_NOSPLIT");
     return e && atoi(e) != 0;
@@ -1377,7 +1396,7 @@ static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_
 // The kernel instance cn_linear launches for a descriptor: ONE function decides it, for the
 // launch and for cn_linear_kernel_name (a profiler's name of the launch), so the two cannot
 // disagree.  X-macro rows: (tile, WM, WN, TM, TN, BK, OCC, DEPTH, MODE).
-enum LinearTile { LT_BF_T0, LT_BF_T1, LT_X6_SQ, LT_X6_TALL, LT_X6_WIDE, LT_X6_T128, LT_X6_T1, LT_F_V2, LT_F_T0_D2,
+enum LinearTile { LT_BF_T0, LT_BF_T1, LT_X6_SQ, LT_X6_TALL, LT_X6_WIDE, LT_X6_T128, LT_X6_T1, LT_X6_T2W, LT_F_V2, LT_F_T0_D2,
                   LT_F_T0_D1, LT_F_T1_D2, LT_F_T1_D1 };
 #define CN_LINEAR_TILES(X)                 \
     X(LT_BF_T0, 2, 2, 2, 2, 64, 2, 1, 1)   \
@@ -1387,6 +1406,7 @@ enum LinearTile { LT_BF_T0, LT_BF_T1, LT_X6_SQ, LT_X6_TALL, LT_X6_WIDE, LT_X6_T1
     X(LT_X6_WIDE, 4, 2, 2, 2, 32, 1, 2, 2) \
     X(LT_X6_T128, 2, 2, 2, 2, 16, 2, 2, 2) \
     X(LT_X6_T1, 4, 1, 1, 2, 16, 2, 2, 2)   \
+    X(LT_X6_T2W, 2, 2, 2, 4, 16, 2, 2, 2)  \
     X(LT_F_V2, 2, 2, 2, 2, 16, 3, 2, 0)    \
     X(LT_F_T0_D2, 2, 2, 2, 2, 32, 2, 2, 0) \
     X(LT_F_T0_D1, 2, 2, 2, 2, 32, 2, 1, 0) \
@@ -1428,6 +1448,11 @@ static LinearTile choose_linear_tile(const cn_linear_desc* d) {
                         d->M >= g_x6_sq_min_m && !(g_sq_nosplit && d->epilogue == CN_EPI_MUL && d->out_split &&
                                                    d->nsplit < d->N);
         if (d->K % 32 == 0 && sq && d->ldb >= 256 && g_linear_variant == 0 && (longk || head)) return LT_X6_SQ;
+        // 128x256, two per CU (single-buffered B): the epilogues with aux streams whose partner-workgroup
+        // overlap matters (COPENERF_X6_T2W: bit e = epilogue e)
+        if ((g_x6_t2w >> d->epilogue & 1) && d->K % 32 == 0 && d->N > 128 && d->N <= 256 && !d->rowv &&
+            d->ldb >= 256 && g_linear_variant == 0 && !(d->epilogue == CN_EPI_MUL && d->out_split && d->nsplit < d->N))
+            return LT_X6_T2W;
         if (d->K % 64 == 0 && tall && d->N > 128 && d->ldb >= 256 && g_linear_variant == 0 && (longk || head))
             return LT_X6_TALL;
         if (d->K % 64 == 0 && g_linear_variant == 0 && light && longk) return LT_X6_WIDE;
