@@ -87,6 +87,7 @@ SIGNATURES = {
     "cn_wgrad_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32]),
     "cn_wgrad": (c_i32, [ctypes.POINTER(WgradDesc), c_ptr]),
     "cn_wgrad_batch": (c_i32, [ctypes.POINTER(WgradDesc), c_i32, c_ptr]),
+    "cn_linear_chain": (c_i32, [ctypes.POINTER(LinearDesc), c_i32, c_ptr]),
     "cn_pack_weights": (c_i32, [ctypes.POINTER(PackJob), c_i32, c_ptr]),
     "cn_row_head": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i32, c_i32, c_ptr, c_i64,
                             c_ptr, c_ptr]),

@@ -180,6 +180,22 @@ FUSE_HEAD = os.environ.get("COPENERF_FUSE_HEAD", "1") != "0"
 # of a cn_sdf_embed pass writing U0 that the first GEMM reads back (COPENERF_FUSE_EMB=1; off by
 # default: the C2 step measured 0.6 % slower on the 128x128 tile, which encodes each row per N-tile)
 FUSE_EMB = os.environ.get("COPENERF_FUSE_EMB", "0") != "0"
+# the SOFTPLUS hidden layers after the first in one cn_linear_chain launch (a 256-row block through every
+# layer in one workgroup; COPENERF_LAYER_CHAIN=1)
+LAYER_CHAIN = os.environ.get("COPENERF_LAYER_CHAIN", "0") != "0"
+
+
+def _chain_layers(lay: SDFLayout, pk: SDFPack, fuse_head: bool):
+    """The SDF layers cn_linear_chain can run in one launch (bf16x6 256x256 tiles, K = 256 operands)."""
+    if not LAYER_CHAIN:
+        return ()
+    L8 = lay.n_lin - 1
+    ls = tuple(range(1, L8 - 1 if fuse_head else L8))
+    for l in ls:
+        B = pk.Bf[l]
+        if B.dim() != 3 or B.shape[1] < 256 or not (128 < lay.out_dim[l] <= 256) or rup(lay.in_dim[l], 32) != 256:
+            return ()
+    return ls if len(ls) >= 2 else ()
 
 
 def _fuse_head(lay: SDFLayout, pk: SDFPack) -> bool:
@@ -233,6 +249,8 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
     sdf = sdf_out if sdf_out is not None else _empty(M, 1, dev)
     fuse = _fuse_head(lay, pk)
     S7 = None
+    chain = _chain_layers(lay, pk, fuse)
+    pending = []
     for l in range(nl - 1):
         into = (l + 1) == sk
         K = KE if l == 0 else rup(lay.in_dim[l], 32)
@@ -248,9 +266,16 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
         else:
             out = Usk if into else _empty(M, HL, dev)
             emb = (x, lay.multires, lay.scale, U[0], e_view, SQRT2) if (l == 0 and fuse_emb) else None
-            ops.linear(None if emb else U[l], pk.Bf[l], lay.out_dim[l], K, out, EPI_SOFTPLUS, bias=pk.b[l],
-                       nzero=lay.out_dim[l] if into else HL, odiv=SQRT2 if into else 1.0, beta=lay.beta,
-                       threshold=lay.threshold, kalg=lay.in_dim[l], emb=emb)
+            args = (None if emb else U[l], pk.Bf[l], lay.out_dim[l], K, out, EPI_SOFTPLUS)
+            kw = dict(bias=pk.b[l], nzero=lay.out_dim[l] if into else HL, odiv=SQRT2 if into else 1.0, beta=lay.beta,
+                      threshold=lay.threshold, kalg=lay.in_dim[l], emb=emb)
+            if l in chain:  # queued; the chain's last layer launches them all
+                pending.append((args, kw))
+                if l == chain[-1]:
+                    ops.linear_chain(pending)
+                    pending = []
+            else:
+                ops.linear(*args, **kw)
         U[l + 1] = out
         if not keep_u and l >= 1 and (l != sk):
             U[l] = None  # free as we go on the no-grad sampler path

@@ -274,7 +274,7 @@ def _tile_tag(name, tile):
 def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None, colv=None, aux0=None,
            aux1=None, aux2=None, out_split=None, nsplit=None, nzero=None, adiv=1.0, odiv=1.0, beta=100.0,
            threshold=20.0, aux_beta=0.0, aux2_scale=0.0, tile=None, M=None, kalg=None, out1=None, head_w=None,
-           head_b=None, head_out=None, head_idx=None, emb=None):
+           head_b=None, head_out=None, head_idx=None, emb=None, _desc_only=False):
     """out = epilogue((A|A2) @ B[:N].T / adiv) -- cn_linear.  MUL / TANGENT /
     BWD_SOFTPLUS read softplus' as sg = 1 - exp(-aux_beta * aux0) from the stored
     softplus output aux0 (include/copenerf.h).  kalg: the unpadded
@@ -362,6 +362,9 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     if ALTERNATE_TILE_ORDER:  # consecutive launches walk the rows in opposite directions
         _flip ^= 1
         d.flags = _flip
+    if _desc_only:  # for linear_chain: the descriptor and the FLOP / byte counts of this layer
+        nb = 4.0 * M * N * 2 + 4.0 * M * (kalg or K) + 6.0 * N * (kalg or K)
+        return d, 2.0 * M * N * (kalg or K), nb, (bias, colv, head_w)
     if _timer is not None:
         e0 = _timer.start()
         _lib.check(_lib.load().cn_linear(d, _stream()), "cn_linear")
@@ -381,6 +384,28 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     else:
         _lib.check(_lib.load().cn_linear(d, _stream()), "cn_linear")
     return out0
+
+
+def linear_chain(layers):
+    """A chain of SOFTPLUS layers in one cn_linear_chain launch (each layer's A is the previous
+    layer's out0): `layers` is a list of ops.linear argument tuples (args, kwargs).  Every layer
+    must satisfy cn_linear_chain's conditions (include/copenerf.h); the outputs equal the
+    per-layer cn_linear calls' bitwise."""
+    built = [linear(*a, **dict(kw, _desc_only=True)) for a, kw in layers]
+    n = len(built)
+    arr = (_lib.LinearDesc * n)(*[b[0] for b in built])
+    for i in range(1, n):
+        arr[i].flags = arr[0].flags  # one tile order for the whole chain
+    lib = _lib.load()
+    if _timer is not None:
+        e0 = _timer.start()
+        _lib.check(lib.cn_linear_chain(arr, n, _stream()), "cn_linear_chain")
+        key = ("linear", "sq", "softplus_chain", "x6")
+        _timer.symbols[key] = "void cn::linear_kernel<4, 2, 2, 4, 16, 1, 2, 1, false, 10>(cn::LinearArgs)"
+        _timer.stop(key, e0, sum(b[1] for b in built), sum(b[2] for b in built))
+    else:
+        _lib.check(lib.cn_linear_chain(arr, n, _stream()), "cn_linear_chain")
+    return layers[-1][0][4]
 
 
 WGRAD_MODES = {"fp32": 0, "bf16": 1, "bf16x6": 2}

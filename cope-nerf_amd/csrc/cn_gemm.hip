@@ -24,6 +24,15 @@
 
 namespace cn {
 
+constexpr int kChainMax = 8;
+struct ChainLayer {  // the per-layer part of a chained SOFTPLUS launch (the rest is shared)
+    const float* B;
+    const float* bias;
+    float* out0;
+    int N, nzero;
+    float inv_odiv;
+};
+
 struct LinearArgs {
     const float* A;
     const float* A2;
@@ -56,6 +65,10 @@ struct LinearArgs {
     float* emb_u4;
     int ld_emb_x, ld_emb_u0, ld_emb_u4, emb_L;
     float emb_scale, emb_u4_div;
+    // MODE & 8: a layer chain (cn_linear_chain) -- one 256-row block goes through every layer in the
+    // same workgroup: layer j's A is layer j-1's out0 rows, just written (L2 / memory-side cache)
+    ChainLayer chain[kChainMax];
+    int nchain;
 };
 
 
@@ -101,9 +114,17 @@ constexpr int kTblCols = 512;  // widest N with a bias / colv (the LDS column ta
 
 template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int EPI, bool ROWV, int MODE_>
 __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel(LinearArgs p) {
-    constexpr int MODE = MODE_ & 3;    // the GEMM mode (0 fp32, 1 bf16, 2 bf16x6)
-    constexpr bool EMB = MODE_ >= 4;   // A generated from the points (the first SDF layer)
+    constexpr int MODE = MODE_ & 3;         // the GEMM mode (0 fp32, 1 bf16, 2 bf16x6)
+    constexpr bool EMB = (MODE_ & 4) != 0;  // A generated from the points (the first SDF layer)
+    constexpr bool CHAIN = (MODE_ & 8) != 0;  // a layer chain (p.chain): row block through every layer
     constexpr int NT = 64 * WM * WN;
+    // the per-layer operands (CHAIN: updated per layer from p.chain; p itself stays the read-only kernarg)
+    const float* cA = p.A;
+    const float* cB = p.B;
+    const float* cBias = p.bias;
+    float* cOut0 = p.out0;
+    int cN = p.N, cNzero = p.nzero;
+    float cInvOdiv = p.inv_odiv;
     constexpr int BM = 32 * TM * WM;
     constexpr int BN = 32 * TN * WN;
     constexpr bool BF = MODE != 0;               // bf16 MFMA (modes 1, 2)
@@ -214,7 +235,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             erow[set] = (valid && n0 == 0) ? m0 : -1;
             erows[set] = rows;
         } else {
-        const float* abase = second ? p.A2 + (int64_t)ma * p.lda2 : p.A + (int64_t)ma * p.lda;
+        const float* abase = second ? p.A2 + (int64_t)ma * p.lda2 : cA + (int64_t)ma * p.lda;
         const int ald = second ? p.lda2 : p.lda;
         const int ak = second ? k0 - p.K1 : k0;
         const rsrc_t rA = make_view(abase, rows * ald * 4);
@@ -228,7 +249,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         }
         // MODE 2: chunk kc of the image is [ldb rows][48 bf16]; the tile's BN rows are 96 * BN contiguous bytes
         const int64_t bofs = MODE == 2 ? ((int64_t)kc * (BK / 16) * p.ldb + n0) * 96 : (int64_t)n0 * p.ldb * ESZB;
-        const rsrc_t rB = make_view(reinterpret_cast<const float*>(reinterpret_cast<const char*>(p.B) + bofs),
+        const rsrc_t rB = make_view(reinterpret_cast<const float*>(reinterpret_cast<const char*>(cB) + bofs),
                                     valid ? (MODE == 2 ? ((BK / 16 - 1) * p.ldb + BN) * 96 : BN * p.ldb * ESZB) : 0);
 #pragma unroll
         for (int q = 0; q < BLD; ++q) {
@@ -311,7 +332,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     const int arow = wm * TM * 32 + (lane & 31);
     const int brow = wn * TN * 32 + (lane & 31);
     const int kofs = (BK / 2) * (lane >> 5);
-    const int Nmain = (EPI == CN_EPI_MUL && p.nsplit < p.N) ? p.nsplit : p.N;
+    const int Nmain = (EPI == CN_EPI_MUL && p.nsplit < cN) ? p.nsplit : cN;
     constexpr int C4 = BN / 4;
     constexpr int RPP = NT / C4;
     constexpr int GMAX = OCC >= 3 ? 2 : 4;  // rows of aux loads in flight per thread (VGPR budget)
@@ -336,10 +357,24 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 
     int vt = next_valid(blockIdx.x);
     if (vt >= ntiles) return;
+    int jl = 0;  // CHAIN: the layer of the current unit
+    bool first_unit = true;
+    const float* const chain_A = cA;
+    auto set_layer = [&](int j) {  // layer j's operands / outputs (shared: K, lda = ld_out0, tiling)
+        const ChainLayer& L = p.chain[j];
+        cA = j == 0 ? chain_A : p.chain[j - 1].out0;
+        cB = L.B;
+        cBias = L.bias;
+        cOut0 = L.out0;
+        cN = L.N;
+        cNzero = L.nzero;
+        cInvOdiv = L.inv_odiv;
+    };
+    if constexpr (CHAIN) set_layer(0);
     if constexpr (TBL > 0) {  // visible after the first tile's staging barrier
-        const rsrc_t rbias = make_view(p.bias, kBias && p.bias ? p.N * 4 : 0);
-        const rsrc_t rcolv = make_view(p.colv, kColv && p.colv ? p.N * 4 : 0);
-        const rsrc_t rhw = make_view(p.head_w, kHead ? p.N * 4 : 0);
+        const rsrc_t rbias = make_view(cBias, kBias && cBias ? cN * 4 : 0);
+        const rsrc_t rcolv = make_view(p.colv, kColv && p.colv ? cN * 4 : 0);
+        const rsrc_t rhw = make_view(p.head_w, kHead ? cN * 4 : 0);
         for (int i = tid; i < TBLC / 4; i += NT) {
             if (kBias) *reinterpret_cast<floatx4*>(sBias + 4 * i) = bload4(rbias, 16 * i, 0);
             if (kColv) *reinterpret_cast<floatx4*>(sColv + 4 * i) = bload4(rcolv, 16 * i, 0);
@@ -368,6 +403,18 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 
     while (vt < ntiles) {
         const int m0 = tm * BM, n0 = tn * BN;
+        if constexpr (CHAIN) {
+            // a unit = (row block, layer): nothing of it could be prefetched during the previous unit
+            // (its A rows were being written), so its first chunks are fetched here, and the layer's
+            // bias table is re-read (the previous unit's readers passed the barrier that ended it)
+            if (!first_unit) {
+                set_layer(jl);
+#pragma unroll
+                for (int d = 0; d < DEPTH; ++d) gload(d, d, m0, n0, true);
+                const rsrc_t rbias = make_view(cBias, cBias ? cN * 4 : 0);
+                for (int i = tid; i < TBLC / 4; i += NT) *reinterpret_cast<floatx4*>(sBias + 4 * i) = bload4(rbias, 16 * i, 0);
+            }
+        }
         const int vt_next = next_valid(vt + gridDim.x);
         int tm_next = 0, tn_next = 0;
         if (vt_next < ntiles) coords(vt_next, tm_next, tn_next);
@@ -505,7 +552,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 const int cur = kc & 1;
                 // chunk kc+1 of this tile, or the next tile's first chunk (consumed after the epilogue)
                 const bool more = kc + 1 < nk;
-                gload(0, more ? kc + 1 : 0, more ? m0 : m_next, more ? n0 : n_next, more || has_next);
+                gload(0, more ? kc + 1 : 0, more ? m0 : m_next, more ? n0 : n_next, more || (!CHAIN && has_next));
                 compute(cur, [](int) {});
                 if (LSTORE_ALWAYS || more) lstore(0, cur ^ 1);
                 __syncthreads();
@@ -522,7 +569,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                     const bool here = cn < nk;
                     // past this tile: chunk cn - nk of the next one, issued before this tile's
                     // epilogue stores, so the next tile's first DEPTH stagings never wait for them
-                    gload(j, here ? cn : cn - nk, here ? m0 : m_next, here ? n0 : n_next, here || has_next);
+                    gload(j, here ? cn : cn - nk, here ? m0 : m_next, here ? n0 : n_next, here || (!CHAIN && has_next));
                     if constexpr (kSeg) {
                         // the next stage's staging (unconditional: after a tile's last chunk it
                         // stages the next tile's first chunk, or zeros, into the free buffer,
@@ -576,7 +623,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 for (int j = 0; j < TN; ++j)
 #pragma unroll
                     for (int r = 0; r < 16; ++r) sum += acc[i][j][r];
-            p.out0[(int64_t)(m0 + (tid & 127)) * p.ld_out0 + n0 + (tid >> 7)] = sum;
+            cOut0[(int64_t)(m0 + (tid & 127)) * p.ld_out0 + n0 + (tid >> 7)] = sum;
             vt = vt_next;
             tm = tm_next;
             tn = tn_next;
@@ -589,7 +636,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         // row = (r&3) + 8*(r>>2) + 4*(lane>>5).
         const int rows = min(BM, p.M - m0);
         // per-tile views, re-based on the pass's first row by SALU arithmetic (view_at)
-        const TileView tO0 = {p.out0 + (int64_t)m0 * p.ld_out0 + n0, p.ld_out0, p.out0 ? (rows * p.ld_out0 - n0) * 4 : 0};
+        const TileView tO0 = {cOut0 + (int64_t)m0 * p.ld_out0 + n0, p.ld_out0, cOut0 ? (rows * p.ld_out0 - n0) * 4 : 0};
         const TileView tO1 = {p.out1 + (int64_t)m0 * p.ld_out1 + n0, p.ld_out1, p.out1 ? (rows * p.ld_out1 - n0) * 4 : 0};
         const TileView tX0 = {p.aux0 + (int64_t)m0 * p.ld_aux0 + n0, p.ld_aux0, p.aux0 ? (rows * p.ld_aux0 - n0) * 4 : 0};
         const TileView tX1 = {p.aux1 + (int64_t)m0 * p.ld_aux1 + n0, p.ld_aux1, p.aux1 ? (rows * p.ld_aux1 - n0) * 4 : 0};
@@ -601,7 +648,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 
         const bool tile_main = n0 + BN <= Nmain;
         const int col = n0 + 4 * c4;
-        const int region = col < Nmain ? 0 : (col < p.N ? 1 : (col < p.nzero ? 2 : 3));
+        const int region = col < Nmain ? 0 : (col < cN ? 1 : (col < cNzero ? 2 : 3));
         // (columns >= N read zeros from the table: their lanes are not region 0 anyway)
         const int tcol = min(col, TBLC - 4);
         floatx4 bias = {0.f, 0.f, 0.f, 0.f}, colv = {0.f, 0.f, 0.f, 0.f}, hw = {0.f, 0.f, 0.f, 0.f};
@@ -644,14 +691,14 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 if constexpr (EPI == CN_EPI_STORE) {
                     o0[e] = u + bias[e];
                 } else if constexpr (EPI == CN_EPI_SOFTPLUS || kHead) {
-                    o0[e] = softplus_hw(u + bias[e], c_exp, c_thr, c_log) * p.inv_odiv;
+                    o0[e] = softplus_hw(u + bias[e], c_exp, c_thr, c_log) * cInvOdiv;
                 } else if constexpr (EPI == CN_EPI_RELU) {
                     const float z = u + bias[e];
                     o0[e] = z > 0.0f ? z : 0.0f;
                 } else if constexpr (EPI == CN_EPI_MUL) {
                     o0[e] = u * sigma_from_act(x0[slot][q][e], p.aux_c);
                 } else if constexpr (EPI == CN_EPI_TANGENT) {
-                    o0[e] = u * sigma_from_act(x0[slot][q][e], p.aux_c) * p.inv_odiv;
+                    o0[e] = u * sigma_from_act(x0[slot][q][e], p.aux_c) * cInvOdiv;
                 } else if constexpr (EPI == CN_EPI_BWD_SOFTPLUS) {
                     // Z = v sigma + beta s (1 - sigma) z', with z' = u' / sigma from the
                     // stored tangent u' = sigma z' (aux2_scale = beta * its divisor):
@@ -755,7 +802,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 #pragma unroll
                             for (int e = 0; e < 4; ++e) o0[e] = v[e] * p.inv_adiv;
                             bstore4(view_at(tS, lrow), voS, 0, o0);
-                            if (col < p.nzero) bstore4(view_at(tO0, lrow), voO0, 0, floatx4{0.f, 0.f, 0.f, 0.f});
+                            if (col < cNzero) bstore4(view_at(tO0, lrow), voO0, 0, floatx4{0.f, 0.f, 0.f, 0.f});
                         } else if (region == 2) {  // zero fill (region 3: past nzero, untouched)
                             bstore4(view_at(tO0, lrow), voO0, 0, floatx4{0.f, 0.f, 0.f, 0.f});
                         }
@@ -792,8 +839,8 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 const int col = n0 + lcol + 32 * j;
-                voj[j] = col < p.nzero ? vo + 128 * j : (1 << 30);
-                live[j] = col < p.N;
+                voj[j] = col < cNzero ? vo + 128 * j : (1 << 30);
+                live[j] = col < cN;
             }
         };
         auto direct_aux = [&]() {
@@ -814,7 +861,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 const int c = n0 + lcol + 32 * j;
-                spl[j] = EPI == CN_EPI_MUL && c >= p.nsplit && c < p.N;
+                spl[j] = EPI == CN_EPI_MUL && c >= p.nsplit && c < cN;
                 vsj[j] = (lrow * p.ld_split + lcol + 32 * j) * 4;
             }
             constexpr int RG = kAux1 ? 2 : 4;          // accumulator rows r per group
@@ -861,7 +908,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         } else if constexpr (EPI == CN_EPI_MUL) {
                             o = u * sg;
                         } else if constexpr (EPI == CN_EPI_TANGENT) {
-                            o = u * sg * p.inv_odiv;
+                            o = u * sg * cInvOdiv;
                         } else {  // BWD_SOFTPLUS, as main_vals
                             const float rr2 = sg > 0.0f ? (1.0f - sg) * __builtin_amdgcn_rcpf(sg) : 0.0f;
                             o = u * sg + xb[sl][q][j] * xc[sl][q][j] * (p.aux2_scale * rr2);
@@ -890,7 +937,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                     for (int j = 0; j < TN; ++j) {
                         const float z = acc[i][j][r] * p.inv_adiv + bj[j];
                         float o;
-                        if constexpr (EPI == CN_EPI_SOFTPLUS) o = softplus_hw(z, c_exp, c_thr, c_log) * p.inv_odiv;
+                        if constexpr (EPI == CN_EPI_SOFTPLUS) o = softplus_hw(z, c_exp, c_thr, c_log) * cInvOdiv;
                         else if constexpr (EPI == CN_EPI_RELU) o = z > 0.0f ? z : 0.0f;
                         else o = z;
                         bstore1(vw, voj[j], 0, live[j] ? o : 0.0f);
@@ -923,7 +970,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                     float part = 0.0f;
 #pragma unroll
                     for (int j = 0; j < TN; ++j) {
-                        const float a = softplus_hw(acc[i][j][r] * p.inv_adiv + bj[j], c_exp, c_thr, c_log) * p.inv_odiv;
+                        const float a = softplus_hw(acc[i][j][r] * p.inv_adiv + bj[j], c_exp, c_thr, c_log) * cInvOdiv;
                         const float o = live[j] ? a : 0.0f;
                         bstore1(vw, voj[j], 0, o);  // (out0 NULL: empty view)
                         bstore1(vw1, vo1[j], 0, live[j] ? cj[j] * sigma_from_act(a, p.aux_c) : 0.0f);
@@ -958,6 +1005,15 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 else passes(std::false_type{});
                 __syncthreads();  // sC is the next tile's staging buffer
             }
+        }
+        if constexpr (CHAIN) {
+            first_unit = false;
+            // this layer's rows are the next layer's A, read back by other waves of this workgroup:
+            // stores complete (workgroup scope: the CU's L1 is shared, write-through) before the barrier
+            __threadfence_block();
+            __syncthreads();
+            if (++jl < p.nchain) continue;  // same row block, next layer
+            jl = 0;
         }
         vt = vt_next;
         tm = tm_next;
@@ -1466,7 +1522,8 @@ static LinearTile choose_linear_tile(const cn_linear_desc* d) {
     return even && g_linear_variant == 0 ? LT_F_T1_D2 : LT_F_T1_D1;
 }
 
-extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
+// Validates a descriptor and builds its kernel arguments (a.M == 0: nothing to launch).
+static int linear_plan(const cn_linear_desc* d, LinearArgs& a) {
     CN_REQUIRE(d, CN_ERR_ARG, "cn_linear: null desc");
     const bool head = d->epilogue == CN_EPI_SOFTPLUS_HEAD;
     const bool emb = d->emb_x != nullptr;
@@ -1549,9 +1606,7 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     CN_REQUIRE(d->lda < kMaxLd && d->lda2 < kMaxLd && d->ldb < kMaxLd && d->ld_aux0 < kMaxLd && d->ld_aux1 < kMaxLd && d->ld_aux2 < kMaxLd &&
                    d->ld_out0 < kMaxLd && d->ld_out1 < kMaxLd && d->ld_split < kMaxLd,
                CN_ERR_SHAPE, "cn_linear: leading dimensions must be < 2^20");
-    if (d->M == 0) return CN_OK;
-
-    LinearArgs a;
+    a = LinearArgs{};
     a.A = d->A; a.A2 = d->A2; a.B = d->B; a.bias = d->bias; a.rowv = d->rowv; a.colv = d->colv;
     a.aux0 = d->aux0; a.aux1 = d->aux1; a.aux2 = d->aux2; a.out0 = d->out0; a.out1 = d->out1; a.out_split = d->out_split;
     a.lda = (int)d->lda; a.lda2 = (int)d->lda2; a.ldb = (int)d->ldb;
@@ -1575,6 +1630,13 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     a.inv_odiv = 1.0f / odiv;
     a.beta = d->beta;
     a.threshold = d->threshold;
+    return CN_OK;
+}
+
+extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
+    LinearArgs a;
+    int rc = linear_plan(d, a);
+    if (rc || d->M == 0) return rc;
     hipStream_t s = (hipStream_t)stream;
     switch (choose_linear_tile(d)) {
 #define CN_TILE_CASE(T, WM, WN, TM, TN, BK, OCC, DEPTH, MODE) \
@@ -1584,6 +1646,51 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     }
     set_error("cn_linear: no tile");
     return CN_ERR_UNSUPPORTED;
+}
+
+// A chain of SOFTPLUS layers (the SDF's hidden layers 1..6, neus_fields.py:273-282) in one launch of the
+// 256x256 bf16x6 tile: each workgroup takes a 256-row block through every layer (layer j's A = layer j-1's
+// out0), so the chain's A operands come back from L2 / the memory-side cache and the launches' boundaries
+// go.  Every descriptor must be a valid cn_linear on that tile with the same M, K, leading dimensions and
+// tile order; outputs / biases / weights / N / nzero / odiv may differ per layer.
+extern "C" int cn_linear_chain(const cn_linear_desc* descs, int32_t n, cn_stream_t stream) {
+    CN_REQUIRE(descs && n >= 1 && n <= kChainMax, CN_ERR_ARG, "cn_linear_chain: %d layers (1..%d)", n, kChainMax);
+    LinearArgs a;
+    int rc = linear_plan(descs, a);
+    if (rc) return rc;
+    for (int j = 0; j < n; ++j) {
+        const cn_linear_desc* d = descs + j;
+        LinearArgs t;
+        rc = j ? linear_plan(d, t) : CN_OK;
+        if (rc) return rc;
+        CN_REQUIRE(d->epilogue == CN_EPI_SOFTPLUS && d->mfma_dtype == CN_MFMA_F32_BF16X6 && !d->A2 && !d->rowv &&
+                       !d->emb_x && choose_linear_tile(d) == LT_X6_SQ,
+                   CN_ERR_UNSUPPORTED, "cn_linear_chain: layer %d is not a bf16x6 SOFTPLUS on the 256x256 tile", j);
+        CN_REQUIRE(d->M == descs->M && d->K == descs->K && d->lda == descs->lda && d->ld_out0 == descs->lda &&
+                       d->ldb == descs->ldb && d->flags == descs->flags && d->beta == descs->beta &&
+                       d->threshold == descs->threshold && (d->adiv == descs->adiv) &&
+                       (j == 0 || d->A == descs[j - 1].out0),
+                   CN_ERR_ARG, "cn_linear_chain: layer %d does not continue the chain (A = the previous out0, same M, "
+                   "K, lda = ld_out0, ldb, flags, softplus)", j);
+        const float odiv = d->odiv == 0.0f ? 1.0f : d->odiv;
+        a.chain[j] = ChainLayer{d->B, d->bias, d->out0, d->N, std::max(d->nzero, d->N), 1.0f / odiv};
+    }
+    a.nchain = n;
+    if (descs->M == 0) return CN_OK;
+    hipStream_t s = (hipStream_t)stream;
+    a.n_tiles_m = cdiv(descs->M, 256);
+    a.n_tiles_n = 1;
+    const int ntiles = cdiv(a.n_tiles_m, 8) * 8;
+    static thread_local int cached_dev = -1, cached_cus = 256;
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && dev != cached_dev) {
+        int v = 0;
+        cached_cus = (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
+        cached_dev = dev;
+    }
+    const int grid = std::min(ntiles, cached_cus);
+    linear_kernel<4, 2, 2, 4, 16, 1, 2, CN_EPI_SOFTPLUS, false, 2 + 8><<<grid, 512, 0, s>>>(a);
+    return check_launch("cn_linear_chain");
 }
 
 extern "C" int cn_linear_kernel_name(const cn_linear_desc* d, char* buf, int32_t len) {

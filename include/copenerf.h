@@ -144,6 +144,13 @@ typedef struct cn_linear_desc {
 enum cn_mfma_dtype { CN_MFMA_F32 = 0, CN_MFMA_BF16 = 1, CN_MFMA_F32_BF16X6 = 2 };
 
 int cn_linear(const cn_linear_desc* d, cn_stream_t stream);
+/* ABI v9: a chain of n <= 8 SOFTPLUS layers (the SDF's hidden layers, neus_fields.py:273-282) in one launch:
+ * each workgroup takes a 256-row block through every layer, so layer j's A (= layer j-1's out0) is read back
+ * from L2 / the memory-side cache instead of HBM and the launches' boundaries go.  Each descriptor must be a
+ * valid cn_linear, bf16x6, on the 256x256 tile (128 < N <= 256, K a multiple of 32, no A2 / rowv / emb_x),
+ * with the same M, K, lda == every ld_out0, ldb, flags, beta, threshold, adiv; descs[j].A == descs[j-1].out0.
+ * Results equal the n cn_linear calls' bitwise. */
+int cn_linear_chain(const cn_linear_desc* descs, int32_t n, cn_stream_t stream);
 
 /* The rocprofv3 symbol of the kernel cn_linear would launch for *d (no launch, no device
  * access; the tile choice is the launch's own function): NUL-terminated into buf[len].

@@ -271,3 +271,34 @@ def test_linear_x6_mul_split_on_the_wide_tile():
     assert torch.all(out[:, 204:] == 0)
     torch.testing.assert_close(split[:, :52], v[:, 204:].float(), rtol=2e-5, atol=2e-6)
     assert torch.isnan(split[:, 52:]).all()
+
+
+def test_layer_chain_bitwise():
+    """cn_linear_chain (COPENERF_LAYER_CHAIN): the SDF's SOFTPLUS hidden layers 1..6 in one launch, each
+    workgroup taking a 256-row block through every layer, against one cn_linear per layer: every stored
+    activation (incl. the skip input assembled in place), the sdf, ∇ₓsdf and every parameter gradient are
+    bitwise equal (same tile, same K order), on the grad path and the sampler path; ragged M."""
+    from copenerf import SDFNetwork, fields
+    from helpers import SDF_CFG
+    torch.manual_seed(9)
+    net = SDFNetwork(**SDF_CFG).to(DEV)
+    net.mfma_dtype = "bf16x6"
+    x = (torch.rand(70001, 4, device=DEV) * 2 - 1)
+    res = {}
+    saved = fields.LAYER_CHAIN
+    try:
+        for chain in (False, True):
+            fields.LAYER_CHAIN = chain
+            Ws, bs, pk = net.params_and_pack()
+            assert bool(fields._chain_layers(net.layout(), pk, fields._fuse_head(net.layout(), pk))) == chain
+            sdf, feat, g = net.field(x)
+            loss = ((g.norm(dim=-1) - 1) ** 2).mean() + sdf.abs().mean() + 1e-2 * feat.square().mean()
+            grads = torch.autograd.grad(loss, list(net.parameters()))
+            st = fields.sdf_forward(net.layout(), pk, x, want_feat=False, want_grad=False, keep=False)
+            stk = fields.sdf_forward(net.layout(), pk, x, want_feat=False, want_grad=False, keep=True)
+            res[chain] = ([sdf.detach(), feat.detach(), g.detach(), st["sdf"]] + list(grads) +
+                          [u for u in stk["U"] if u is not None])
+    finally:
+        fields.LAYER_CHAIN = saved
+    for a, b in zip(res[False], res[True]):
+        assert torch.equal(a, b)
