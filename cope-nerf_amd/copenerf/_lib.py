@@ -54,6 +54,7 @@ class LinearDesc(ctypes.Structure):
         ("head_w", c_ptr), ("head_b", c_ptr), ("head_out", c_ptr), ("head_idx", c_ptr),
         ("emb_x", c_ptr), ("ld_emb_x", c_i64), ("emb_multires", c_i32), ("emb_scale", c_f32),
         ("emb_u0", c_ptr), ("ld_emb_u0", c_i64), ("emb_u4", c_ptr), ("ld_emb_u4", c_i64), ("emb_u4_div", c_f32),
+        ("out_mask", c_ptr), ("aux_mask", c_ptr), ("ld_mask", c_i64),
     ]
 
 

@@ -183,6 +183,8 @@ FUSE_EMB = os.environ.get("COPENERF_FUSE_EMB", "0") != "0"
 # the SOFTPLUS hidden layers after the first in one cn_linear_chain launch (a 256-row block through every
 # layer in one workgroup; COPENERF_LAYER_CHAIN=1)
 LAYER_CHAIN = os.environ.get("COPENERF_LAYER_CHAIN", "0") != "0"
+# the colour backward's ReLU masks read as sign bits written by the forward (COPENERF_RELU_MASK=1)
+RELU_MASK = os.environ.get("COPENERF_RELU_MASK", "0") != "0"
 
 
 def _chain_layers(lay: SDFLayout, pk: SDFPack, fuse_head: bool):
@@ -731,18 +733,24 @@ class _ColorFieldFn(torch.autograd.Function):
         M, dev = pts.shape[0], pts.device
         ext = _empty(M, lay.KX, dev)
         ops.color_extras(G, pts, dirs, dir_div, lay.multires_view, ext)
-        H = []
+        H, masks = [], []
         A, A2, K1, K = feat, ext, lay.F, lay.F + lay.KX
         for l in range(lay.n_lin - 1):
             out = _empty(M, lay.HL, dev)
+            # the ReLU sign bits for the backward (bf16x6 on the 256x256 tile: N = 256 hidden layers)
+            mk = None
+            if RELU_MASK and pk.Bf[l].dim() == 3 and lay.out_dim[l] == 256 and lay.HL == 256 and M > 0:
+                mk = torch.empty(M, 8, dtype=torch.int32, device=dev)
             ops.linear(A, pk.Bf[l], lay.out_dim[l], K, out, EPI_RELU, bias=pk.b[l], A2=A2, K1=K1, nzero=lay.HL,
-                       kalg=lay.in_dim[l])
+                       kalg=lay.in_dim[l], out_mask=mk)
             H.append(out)
+            masks.append(mk)
             A, A2, K1, K = out, None, None, rup(lay.out_dim[l], 32)
         rgb = _empty(M, 3, dev)
         ops.row_head(H[-1], lay.in_dim[-1], pk.W3, pk.b3, 3, 1, rgb)
         ctx.lay, ctx.pk = lay, pk
         ctx.bufs = (feat, ext, H, rgb)
+        ctx.masks = masks
         ctx.dirs, ctx.dir_div = (dirs, dir_div) if ctx.needs_input_grad[1] else (None, 1)
         return rgb
 
@@ -751,7 +759,8 @@ class _ColorFieldFn(torch.autograd.Function):
         lay, pk = ctx.lay, ctx.pk
         wmode = _wgrad_mode(pk)
         feat, ext, H, rgb = ctx.bufs
-        ctx.bufs = None
+        masks = ctx.masks
+        ctx.bufs = ctx.masks = None
         nparams = 2 * lay.n_lin
         if drgb is None:
             return (None,) * (7 + nparams)
@@ -775,7 +784,7 @@ class _ColorFieldFn(torch.autograd.Function):
             dWs[l], dbs[l] = dW, db
             dZp = _empty(M, lay.HL, dev)
             ops.linear(dZ, pk.Bt[l], lay.out_dim[l - 1], rup(lay.out_dim[l], 32), dZp, EPI_BWD_RELU, aux0=H[l - 1],
-                       nzero=lay.HL)
+                       nzero=lay.HL, aux_mask=masks[l - 1])
             dZ = dZp
         o0 = lay.out_dim[0]
         dWf = torch.empty(o0, lay.F, device=dev)

@@ -274,7 +274,7 @@ def _tile_tag(name, tile):
 def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None, colv=None, aux0=None,
            aux1=None, aux2=None, out_split=None, nsplit=None, nzero=None, adiv=1.0, odiv=1.0, beta=100.0,
            threshold=20.0, aux_beta=0.0, aux2_scale=0.0, tile=None, M=None, kalg=None, out1=None, head_w=None,
-           head_b=None, head_out=None, head_idx=None, emb=None, _desc_only=False):
+           head_b=None, head_out=None, head_idx=None, emb=None, out_mask=None, aux_mask=None, _desc_only=False):
     """out = epilogue((A|A2) @ B[:N].T / adiv) -- cn_linear.  MUL / TANGENT /
     BWD_SOFTPLUS read softplus' as sg = 1 - exp(-aux_beta * aux0) from the stored
     softplus output aux0 (include/copenerf.h).  kalg: the unpadded
@@ -354,6 +354,12 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     d.epilogue, d.tile = epilogue, tile
     d.adiv, d.odiv, d.beta, d.threshold = adiv, odiv, beta, threshold
     d.mfma_dtype = 2 if x6 else (1 if bf else 0)
+    if out_mask is not None or aux_mask is not None:  # ReLU sign bits (int32 [M, ceil(N / 32)])
+        mk = out_mask if out_mask is not None else aux_mask
+        _need(mk, "mask")
+        if mk.dtype != torch.int32 or mk.shape[0] < M or mk.shape[1] * 32 < N:
+            raise RuntimeError("cn_linear: a mask is int32 [M, ceil(N / 32)]")
+        d.out_mask, d.aux_mask, d.ld_mask = _ptr(out_mask), _ptr(aux_mask), mk.stride(0)
     if emb is not None:
         ex, d.emb_multires, d.emb_scale, eu0, eu4, d.emb_u4_div = emb
         d.emb_x, d.ld_emb_x = _ptr(ex), _ld(ex)

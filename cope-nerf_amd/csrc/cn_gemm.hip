@@ -25,6 +25,7 @@
 namespace cn {
 
 constexpr int kChainMax = 8;
+constexpr int kEpiReluMask = 9;  // internal: RELU that also writes the sign bits (cn_linear_desc.out_mask)
 struct ChainLayer {  // the per-layer part of a chained SOFTPLUS launch (the rest is shared)
     const float* B;
     const float* bias;
@@ -69,6 +70,11 @@ struct LinearArgs {
     // same workgroup: layer j's A is layer j-1's out0 rows, just written (L2 / memory-side cache)
     ChainLayer chain[kChainMax];
     int nchain;
+    // RELU: the sign bits of the output (bit c of word c / 32 of a row: out > 0), written beside it;
+    // BWD_RELU: the same bits read instead of the stored activation (4 bytes per 32 columns, not 128)
+    unsigned* mask_out;
+    const unsigned* mask_in;
+    int ld_mask;
 };
 
 
@@ -161,7 +167,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     // pass -- each pass waited for the previous pass's stores)
     // (SOFTPLUS_HEAD: + the head weights and bias; its rows fit one tile, N <= 256)
     constexpr bool kHead = EPI == CN_EPI_SOFTPLUS_HEAD;
-    constexpr bool kBias = EPI == CN_EPI_STORE || EPI == CN_EPI_SOFTPLUS || EPI == CN_EPI_RELU || kHead;
+    constexpr bool kBias = EPI == CN_EPI_STORE || EPI == CN_EPI_SOFTPLUS || EPI == CN_EPI_RELU || EPI == kEpiReluMask || kHead;
     constexpr bool kColv = ROWV || kHead;
     constexpr int TBLC = kHead ? 256 : kTblCols;
     constexpr int TBL = (kBias ? TBLC : 0) + (kColv ? TBLC : 0) + (kHead ? TBLC + 4 : 0);
@@ -867,6 +873,12 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             constexpr int RG = kAux1 ? 2 : 4;          // accumulator rows r per group
             constexpr int NGD = TM * 16 / RG;          // groups per tile
             float xa[2][RG][TN], xb[2][RG][TN], xc[2][RG][TN];
+            // BWD_RELU from sign bits: every lane of a half-wave loads its row's word of the column block
+            // (one dword per 32 columns) and takes bit lane % 32
+            const bool use_mask = EPI == CN_EPI_BWD_RELU && p.mask_in != nullptr;
+            const TileView tMk = {reinterpret_cast<const float*>(p.mask_in) + (int64_t)m0 * p.ld_mask, p.ld_mask,
+                                  use_mask ? min(BM, p.M - m0) * p.ld_mask * 4 : 0};
+            const int vmk = (lrow * p.ld_mask + (n0 >> 5) + wn * TN) * 4;
             auto dload = [&](int g, int sl) {
                 const int i = g / (16 / RG), r0 = (g % (16 / RG)) * RG;
 #pragma unroll
@@ -874,7 +886,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                     const int r = r0 + q, row = i * 32 + (r & 3) + 8 * (r >> 2);
 #pragma unroll
                     for (int j = 0; j < TN; ++j) {
-                        xa[sl][q][j] = bload1(view_at(tX0, row), v0, 128 * j);
+                        xa[sl][q][j] = use_mask ? bload1(view_at(tMk, row), vmk, 4 * j) : bload1(view_at(tX0, row), v0, 128 * j);
                         if (kAux1) xb[sl][q][j] = bload1(view_at(tX1, row), v1, 128 * j);
                         if (kAux1) xc[sl][q][j] = bload1(view_at(tX2, row), v2, 128 * j);
                     }
@@ -904,7 +916,9 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         const float sg = EPI == CN_EPI_BWD_RELU ? 0.0f : sigma_from_act(xa[sl][q][j], p.aux_c);
                         float o;
                         if constexpr (EPI == CN_EPI_BWD_RELU) {
-                            o = xa[sl][q][j] > 0.0f ? u : 0.0f;
+                            const bool pos = use_mask ? ((__float_as_uint(xa[sl][q][j]) >> (lane & 31)) & 1u) != 0
+                                                      : xa[sl][q][j] > 0.0f;
+                            o = pos ? u : 0.0f;
                         } else if constexpr (EPI == CN_EPI_MUL) {
                             o = u * sg;
                         } else if constexpr (EPI == CN_EPI_TANGENT) {
@@ -928,19 +942,29 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             float bj[TN];
 #pragma unroll
             for (int j = 0; j < TN; ++j) bj[j] = kBias ? sBias[min(n0 + lcol + 32 * j, kTblCols - 1)] : 0.0f;
+            const TileView tMo = {reinterpret_cast<const float*>(p.mask_out) + (int64_t)m0 * p.ld_mask, p.ld_mask,
+                                  EPI == kEpiReluMask ? min(BM, p.M - m0) * p.ld_mask * 4 : 0};
+            const int vmo = ((wm * TM * 32 + 4 * (lane >> 5)) * p.ld_mask + (n0 >> 5) + wn * TN) * 4;
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const rsrc_t vw = view_at(tO0, i * 32 + (r & 3) + 8 * (r >> 2));
+                    const rsrc_t vmr = view_at(tMo, i * 32 + (r & 3) + 8 * (r >> 2));  // (kEpiReluMask only)
 #pragma unroll
                     for (int j = 0; j < TN; ++j) {
                         const float z = acc[i][j][r] * p.inv_adiv + bj[j];
                         float o;
                         if constexpr (EPI == CN_EPI_SOFTPLUS) o = softplus_hw(z, c_exp, c_thr, c_log) * cInvOdiv;
-                        else if constexpr (EPI == CN_EPI_RELU) o = z > 0.0f ? z : 0.0f;
+                        else if constexpr (EPI == CN_EPI_RELU || EPI == kEpiReluMask) o = z > 0.0f ? z : 0.0f;
                         else o = z;
                         bstore1(vw, voj[j], 0, live[j] ? o : 0.0f);
+                        if constexpr (EPI == kEpiReluMask) {
+                            // lanes 0-31 hold row R, 32-63 row R + 4 of this column block: one word each
+                            const unsigned long long bal = __ballot(live[j] && o > 0.0f);
+                            const unsigned word = lane < 32 ? (unsigned)bal : (unsigned)(bal >> 32);
+                            if ((lane & 31) == 0) bstore1(vmr, vmo, 4 * j, __uint_as_float(word));
+                        }
                     }
                 }
         };
@@ -1427,6 +1451,14 @@ static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_
         set_error("cn_linear: no fused-encoding kernel for this tile");
         return CN_ERR_UNSUPPORTED;
     }
+    if (a.mask_out) {  // RELU + sign bits: the 256x256 tile's direct epilogue only (host-checked)
+        if constexpr (MODE == 2 && TM * TN >= 8 && OCC == 1 && BK == 16) {
+            linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, kEpiReluMask, false, MODE><<<grid, block, 0, s>>>(a);
+            return check_launch("cn_linear");
+        }
+        set_error("cn_linear: out_mask needs the bf16x6 256x256 tile");
+        return CN_ERR_UNSUPPORTED;
+    }
     switch (d->epilogue) {
 #define CN_EPI_CASE(E)                                                                     \
         case E:                                                                            \
@@ -1563,7 +1595,15 @@ static int linear_plan(const cn_linear_desc* d, LinearArgs& a) {
     CN_REQUIRE(!d->out0 || d->ld_out0 >= nzero, CN_ERR_SHAPE, "cn_linear: ld_out0=%lld < nzero=%d",
                (long long)d->ld_out0, nzero);
     const int e = d->epilogue;
-    if (e == CN_EPI_MUL || e == CN_EPI_TANGENT || e == CN_EPI_BWD_SOFTPLUS || e == CN_EPI_BWD_RELU)
+    if (d->out_mask || d->aux_mask) {  // sign bits: RELU writes them, BWD_RELU reads them (256x256 tile only)
+        CN_REQUIRE((d->out_mask ? e == CN_EPI_RELU : e == CN_EPI_BWD_RELU) && !(d->out_mask && d->aux_mask) &&
+                       choose_linear_tile(d) == LT_X6_SQ,
+                   CN_ERR_UNSUPPORTED, "cn_linear: out_mask (RELU) / aux_mask (BWD_RELU) need the bf16x6 256x256 tile");
+        CN_REQUIRE(al16(d->out_mask ? (const void*)d->out_mask : (const void*)d->aux_mask) &&
+                       d->ld_mask >= (d->N + 31) / 32 && d->ld_mask < (1 << 20),
+                   CN_ERR_ALIGN, "cn_linear: mask rows need ld_mask >= ceil(N / 32) words");
+    }
+    if (e == CN_EPI_MUL || e == CN_EPI_TANGENT || e == CN_EPI_BWD_SOFTPLUS || (e == CN_EPI_BWD_RELU && !d->aux_mask))
         CN_REQUIRE(d->aux0 && d->ld_aux0 >= d->N, CN_ERR_ARG, "cn_linear: epilogue %d needs aux0", e);
     if (e == CN_EPI_MUL || e == CN_EPI_TANGENT || e == CN_EPI_BWD_SOFTPLUS)
         CN_REQUIRE(d->aux_beta > 0.0f, CN_ERR_ARG, "cn_linear: epilogue %d needs aux_beta > 0 (sigma from aux0)", e);
@@ -1630,6 +1670,9 @@ static int linear_plan(const cn_linear_desc* d, LinearArgs& a) {
     a.inv_odiv = 1.0f / odiv;
     a.beta = d->beta;
     a.threshold = d->threshold;
+    a.mask_out = reinterpret_cast<unsigned*>(d->out_mask);
+    a.mask_in = reinterpret_cast<const unsigned*>(d->aux_mask);
+    a.ld_mask = (int)d->ld_mask;
     return CN_OK;
 }
 

@@ -139,6 +139,12 @@ typedef struct cn_linear_desc {
     float* emb_u4;
     int64_t ld_emb_u4;
     float emb_u4_div;
+    /* ABI v9 -- ReLU sign bits (the colour network, neus_fields.py:364-373): RELU may write out_mask[m][c / 32]
+       bit c % 32 = (out[m][c] > 0); BWD_RELU may read aux_mask instead of the stored activation aux0 (the same
+       result, 4 bytes per 32 columns).  bf16x6 on the 256x256 tile only; ld_mask >= ceil(N / 32) words. */
+    uint32_t* out_mask;
+    const uint32_t* aux_mask;
+    int64_t ld_mask;
 } cn_linear_desc;
 
 enum cn_mfma_dtype { CN_MFMA_F32 = 0, CN_MFMA_BF16 = 1, CN_MFMA_F32_BF16X6 = 2 };

@@ -302,3 +302,33 @@ def test_layer_chain_bitwise():
         fields.LAYER_CHAIN = saved
     for a, b in zip(res[False], res[True]):
         assert torch.equal(a, b)
+
+
+def test_relu_sign_bit_masks_bitwise():
+    """COPENERF_RELU_MASK: the colour network's forward RELUs write the sign bits of their outputs and the
+    backward's BWD_RELU reads them instead of the stored activations -- rgb and every gradient (parameters,
+    points, normals, directions, feature) bitwise equal to the activation-reading backward; ragged M."""
+    from copenerf import RenderingNetwork, fields
+    torch.manual_seed(11)
+    from copenerf.train_step import COL_CFG
+    net = RenderingNetwork(**COL_CFG).to(DEV)
+    net.mfma_dtype = "bf16x6"
+    M = 5003
+    pts = torch.rand(M, 4, device=DEV, requires_grad=True)
+    nrm = torch.randn(M, 4, device=DEV, requires_grad=True)
+    dirs = torch.randn(M, 3, device=DEV, requires_grad=True)
+    feat = (0.1 * torch.randn(M, 256, device=DEV)).requires_grad_(True)
+    res = {}
+    saved = fields.RELU_MASK
+    try:
+        for on in (False, True):
+            fields.RELU_MASK = on
+            rgb = net(pts, nrm, dirs, feat)
+            loss = (rgb * torch.linspace(0.5, 1.5, 3, device=DEV)).square().sum()
+            grads = torch.autograd.grad(loss, [pts, nrm, dirs, feat] + list(net.parameters()), allow_unused=True)
+            res[on] = [rgb.detach()] + [g for g in grads if g is not None]
+    finally:
+        fields.RELU_MASK = saved
+    assert len(res[False]) == len(res[True])
+    for a, b in zip(res[False], res[True]):
+        assert torch.equal(a, b)
