@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libcopenerf.so"
 LIB_PATH = os.environ.get("COPENERF_LIB", os.path.join(_HERE, LIB_NAME))
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 c_f32p = ctypes.c_void_p  # device pointers are passed as integers
 c_i32 = ctypes.c_int32
@@ -52,9 +52,8 @@ class LinearDesc(ctypes.Structure):
         ("mfma_dtype", c_i32), ("aux_beta", c_f32), ("aux2", c_ptr), ("ld_aux2", c_i64),
         ("aux2_scale", c_f32), ("flags", c_i32),
         ("head_w", c_ptr), ("head_b", c_ptr), ("head_out", c_ptr), ("head_idx", c_ptr),
-        ("emb_x", c_ptr), ("ld_emb_x", c_i64), ("emb_multires", c_i32), ("emb_scale", c_f32),
-        ("emb_u0", c_ptr), ("ld_emb_u0", c_i64), ("emb_u4", c_ptr), ("ld_emb_u4", c_i64), ("emb_u4_div", c_f32),
-        ("out_mask", c_ptr), ("aux_mask", c_ptr), ("ld_mask", c_i64),
+        ("a_bf16", c_i32), ("aux0_bf16", c_i32), ("out0_b", c_ptr), ("ld_out0_b", c_i64),
+        ("out1_b", c_ptr), ("ld_out1_b", c_i64),
     ]
 
 
@@ -66,6 +65,7 @@ class WgradDesc(ctypes.Structure):
         ("workspace_bytes", c_i64),
         ("M", c_i32), ("N", c_i32), ("K", c_i32), ("npairs", c_i32),
         ("n_out", c_i32), ("k_out", c_i32), ("accumulate", c_i32), ("mfma_dtype", c_i32),
+        ("y_bf16", c_i32), ("x_bf16", c_i32),
     ]
 
 
@@ -88,7 +88,6 @@ SIGNATURES = {
     "cn_wgrad_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32]),
     "cn_wgrad": (c_i32, [ctypes.POINTER(WgradDesc), c_ptr]),
     "cn_wgrad_batch": (c_i32, [ctypes.POINTER(WgradDesc), c_i32, c_ptr]),
-    "cn_linear_chain": (c_i32, [ctypes.POINTER(LinearDesc), c_i32, c_ptr]),
     "cn_pack_weights": (c_i32, [ctypes.POINTER(PackJob), c_i32, c_ptr]),
     "cn_row_head": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i32, c_i32, c_ptr, c_i64,
                             c_ptr, c_ptr]),

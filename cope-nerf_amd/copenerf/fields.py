@@ -20,7 +20,6 @@ from __future__ import annotations
 
 import dataclasses
 import math
-import os
 from typing import List, Optional
 
 import numpy as np
@@ -175,38 +174,13 @@ def pack_sdf(lay: SDFLayout, Ws, bs, mfma_dtype: str = "fp32") -> SDFPack:
         return SDFPack(Bf, Bt, b, w80.contiguous()[None], b80.contiguous(), w80p, Bf8, Bt8, b8[1:].contiguous())
 
 
-FUSE_HEAD = os.environ.get("COPENERF_FUSE_HEAD", "1") != "0"
-# the positional encoding computed inside the first layer's operand load (cn_linear emb_x) instead
-# of a cn_sdf_embed pass writing U0 that the first GEMM reads back (COPENERF_FUSE_EMB=1; off by
-# default: the C2 step measured 0.6 % slower on the 128x128 tile, which encodes each row per N-tile)
-FUSE_EMB = os.environ.get("COPENERF_FUSE_EMB", "0") != "0"
-# the SOFTPLUS hidden layers after the first in one cn_linear_chain launch (a 256-row block through every
-# layer in one workgroup; COPENERF_LAYER_CHAIN=1)
-LAYER_CHAIN = os.environ.get("COPENERF_LAYER_CHAIN", "0") != "0"
-# the colour backward's ReLU masks read as sign bits written by the forward (COPENERF_RELU_MASK=1)
-RELU_MASK = os.environ.get("COPENERF_RELU_MASK", "0") != "0"
-
-
-def _chain_layers(lay: SDFLayout, pk: SDFPack, fuse_head: bool):
-    """The SDF layers cn_linear_chain can run in one launch (bf16x6 256x256 tiles, K = 256 operands)."""
-    if not LAYER_CHAIN:
-        return ()
-    L8 = lay.n_lin - 1
-    ls = tuple(range(1, L8 - 1 if fuse_head else L8))
-    for l in ls:
-        B = pk.Bf[l]
-        if B.dim() != 3 or B.shape[1] < 256 or not (128 < lay.out_dim[l] <= 256) or rup(lay.in_dim[l], 32) != 256:
-            return ()
-    return ls if len(ls) >= 2 else ()
-
-
 def _fuse_head(lay: SDFLayout, pk: SDFPack) -> bool:
     """The last hidden layer computes the sdf head in its epilogue (EPI_SOFTPLUS_HEAD)
     when one GEMM tile spans its whole output row: N <= 128 in every mode, N <= 256
     with the bf16x6 128x256 tile."""
     L8 = lay.n_lin - 1
     N = lay.out_dim[L8 - 1]
-    if not FUSE_HEAD or lay.in_dim[L8] != N or N % 4 or L8 == lay.skip or L8 - 1 == 0:
+    if lay.in_dim[L8] != N or N % 4 or L8 == lay.skip or L8 - 1 == 0:
         return False
     B = pk.Bf[L8 - 1]
     x6 = B.dim() == 3
@@ -236,23 +210,17 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
     nl, sk, HL, KE = lay.n_lin, lay.skip, lay.HL, lay.KE
     keep_u = keep or want_grad
     U = [None] * nl
-    # the encoding U0 is stored only for the backward / ∇ pass (not on the sampler path when fused)
-    fuse_emb = FUSE_EMB and KE <= 64 and x.shape[1] == 4 and x.stride(1) == 1 and x.stride(0) % 4 == 0 and \
-        x.data_ptr() % 16 == 0
-    U[0] = _empty(M, KE, dev) if (keep_u or not fuse_emb) else None
+    U[0] = _empty(M, KE, dev)
     Usk, e_view = None, None
     if sk >= 0:
         Usk = _empty(M, HL, dev)
         o = lay.out_dim[sk - 1]
         e_view = Usk[:, o:o + lay.E]
-    if not fuse_emb:
-        ops.sdf_embed(x, lay.multires, lay.scale, U[0], e_view, SQRT2)
+    ops.sdf_embed(x, lay.multires, lay.scale, U[0], e_view, SQRT2)
     L8 = nl - 1
     sdf = sdf_out if sdf_out is not None else _empty(M, 1, dev)
     fuse = _fuse_head(lay, pk)
     S7 = None
-    chain = _chain_layers(lay, pk, fuse)
-    pending = []
     for l in range(nl - 1):
         into = (l + 1) == sk
         K = KE if l == 0 else rup(lay.in_dim[l], 32)
@@ -267,17 +235,9 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
                        head_idx=dst, M=M)
         else:
             out = Usk if into else _empty(M, HL, dev)
-            emb = (x, lay.multires, lay.scale, U[0], e_view, SQRT2) if (l == 0 and fuse_emb) else None
-            args = (None if emb else U[l], pk.Bf[l], lay.out_dim[l], K, out, EPI_SOFTPLUS)
-            kw = dict(bias=pk.b[l], nzero=lay.out_dim[l] if into else HL, odiv=SQRT2 if into else 1.0, beta=lay.beta,
-                      threshold=lay.threshold, kalg=lay.in_dim[l], emb=emb)
-            if l in chain:  # queued; the chain's last layer launches them all
-                pending.append((args, kw))
-                if l == chain[-1]:
-                    ops.linear_chain(pending)
-                    pending = []
-            else:
-                ops.linear(*args, **kw)
+            ops.linear(U[l], pk.Bf[l], lay.out_dim[l], K, out, EPI_SOFTPLUS, bias=pk.b[l],
+                       nzero=lay.out_dim[l] if into else HL, odiv=SQRT2 if into else 1.0, beta=lay.beta,
+                       threshold=lay.threshold, kalg=lay.in_dim[l])
         U[l + 1] = out
         if not keep_u and l >= 1 and (l != sk):
             U[l] = None  # free as we go on the no-grad sampler path
@@ -459,11 +419,9 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
     dWs[L8], dbs[L8] = dW8, db8
     share = want_dx and not second  # Z_l == P_l: dx from the parameter adjoint chain
     PE = _empty(M, KE, dev) if (share and sk >= 0) else None
-    lane = ops.SideLane(dev)
     wq = ops.WgradQueue()  # the hidden layers' weight gradients: one launch after the chain
     for l in range(L8 - 1, -1, -1):
         Zl = Z
-        lane.fork()  # Z_l is ready: its weight gradient may run beside the next adjoint GEMM
         if l > 0:
             Z = _empty(M, HL, dev)
             if share and l == sk:  # + the embedding columns of the skip input (sdf_input_grad's PE)
@@ -479,24 +437,19 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
                            kalg=lay.out_dim[l], **second_order(l - 1))
         dW = torch.empty(lay.out_dim[l], lay.in_dim[l], device=dev)
         db = torch.empty(lay.out_dim[l], device=dev)
-        with lane:
-            wq.add(Zl, U[l], lay.out_dim[l], lay.in_dim[l], dW, db=db,
-                   Y1=S[l] if second else None, X1=Ud[l] if second else None, mode=wmode)
-        lane.hold(Zl)
+        wq.add(Zl, U[l], lay.out_dim[l], lay.in_dim[l], dW, db=db,
+               Y1=S[l] if second else None, X1=Ud[l] if second else None, mode=wmode)
         dWs[l], dbs[l] = dW, db
     wq.flush()
     if not want_dx:
-        lane.join()
         return dWs, dbs
     if not share:
         dx = sdf_input_grad(lay, pk, st, dsdf, dfeat, dh=dh)
-        lane.join()
         return dWs, dbs, dx
     P0 = _empty(M, KE, dev)  # Zl is Z_0 here
     ops.linear(Zl, pk.Bt[0], lay.E, rup(lay.out_dim[0], 32), P0, EPI_STORE, nzero=KE, kalg=lay.out_dim[0])
     dx = _empty(M, 4, dev)
     ops.sdf_grad_assemble(lay.multires, lay.scale, U[0], P0, PE, dx)
-    lane.join()
     return dWs, dbs, dx
 
 
@@ -733,24 +686,18 @@ class _ColorFieldFn(torch.autograd.Function):
         M, dev = pts.shape[0], pts.device
         ext = _empty(M, lay.KX, dev)
         ops.color_extras(G, pts, dirs, dir_div, lay.multires_view, ext)
-        H, masks = [], []
+        H = []
         A, A2, K1, K = feat, ext, lay.F, lay.F + lay.KX
         for l in range(lay.n_lin - 1):
             out = _empty(M, lay.HL, dev)
-            # the ReLU sign bits for the backward (bf16x6 on the 256x256 tile: N = 256 hidden layers)
-            mk = None
-            if RELU_MASK and pk.Bf[l].dim() == 3 and lay.out_dim[l] == 256 and lay.HL == 256 and M > 0:
-                mk = torch.empty(M, 8, dtype=torch.int32, device=dev)
             ops.linear(A, pk.Bf[l], lay.out_dim[l], K, out, EPI_RELU, bias=pk.b[l], A2=A2, K1=K1, nzero=lay.HL,
-                       kalg=lay.in_dim[l], out_mask=mk)
+                       kalg=lay.in_dim[l])
             H.append(out)
-            masks.append(mk)
             A, A2, K1, K = out, None, None, rup(lay.out_dim[l], 32)
         rgb = _empty(M, 3, dev)
         ops.row_head(H[-1], lay.in_dim[-1], pk.W3, pk.b3, 3, 1, rgb)
         ctx.lay, ctx.pk = lay, pk
         ctx.bufs = (feat, ext, H, rgb)
-        ctx.masks = masks
         ctx.dirs, ctx.dir_div = (dirs, dir_div) if ctx.needs_input_grad[1] else (None, 1)
         return rgb
 
@@ -759,8 +706,7 @@ class _ColorFieldFn(torch.autograd.Function):
         lay, pk = ctx.lay, ctx.pk
         wmode = _wgrad_mode(pk)
         feat, ext, H, rgb = ctx.bufs
-        masks = ctx.masks
-        ctx.bufs = ctx.masks = None
+        ctx.bufs = None
         nparams = 2 * lay.n_lin
         if drgb is None:
             return (None,) * (7 + nparams)
@@ -772,29 +718,22 @@ class _ColorFieldFn(torch.autograd.Function):
         dbs[n - 1] = torch.empty(3, device=dev)
         dZ = _empty(M, lay.HL, dev)
         ops.rgb_head_bwd(drgb, rgb, H[-1], lay.in_dim[n - 1], pk.W3, dZ, dWs[n - 1], dbs[n - 1])
-        lane = ops.SideLane(dev)
         wq = ops.WgradQueue()  # the 256x256 weight gradients: one launch after the chain
         for l in range(n - 2, 0, -1):
             dW = torch.empty(lay.out_dim[l], lay.in_dim[l], device=dev)
             db = torch.empty(lay.out_dim[l], device=dev)
-            lane.fork()
-            with lane:  # beside the next adjoint GEMM (both only read dZ_l)
-                wq.add(dZ, H[l - 1], lay.out_dim[l], lay.in_dim[l], dW, db=db, mode=wmode)
-            lane.hold(dZ)
+            wq.add(dZ, H[l - 1], lay.out_dim[l], lay.in_dim[l], dW, db=db, mode=wmode)
             dWs[l], dbs[l] = dW, db
             dZp = _empty(M, lay.HL, dev)
             ops.linear(dZ, pk.Bt[l], lay.out_dim[l - 1], rup(lay.out_dim[l], 32), dZp, EPI_BWD_RELU, aux0=H[l - 1],
-                       nzero=lay.HL, aux_mask=masks[l - 1])
+                       nzero=lay.HL)
             dZ = dZp
         o0 = lay.out_dim[0]
         dWf = torch.empty(o0, lay.F, device=dev)
         db0 = torch.empty(o0, device=dev)
         dWx = torch.empty(o0, lay.KX, device=dev)
-        lane.fork()
-        with lane:  # beside the input-gradient GEMMs below
-            wq.add(dZ, feat, o0, lay.F, dWf, db=db0, mode=wmode)
-            ops.wgrad(dZ, ext, o0, lay.KX, dWx, mode=wmode)
-        lane.hold(dZ)
+        wq.add(dZ, feat, o0, lay.F, dWf, db=db0, mode=wmode)
+        ops.wgrad(dZ, ext, o0, lay.KX, dWx, mode=wmode)
         wq.flush()
         P, V, Gd = lay.P, lay.V, lay.Gd
         dfeat = None
@@ -817,7 +756,6 @@ class _ColorFieldFn(torch.autograd.Function):
         elif ctx.needs_input_grad[3]:
             dG = _empty(M, Gd, dev)
             ops.row_head(dZ, o0, pk.Wg, None, Gd, 0, dG)
-        lane.join()
         # back to the reference column order [pts | emb(dirs) | gradients | feature]
         dWs[0] = torch.cat([dWx[:, Gd:Gd + P], dWx[:, Gd + P:Gd + P + V], dWx[:, 0:Gd], dWf], 1)
         dbs[0] = db0

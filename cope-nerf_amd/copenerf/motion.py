@@ -20,7 +20,6 @@ parameters' device.
 """
 from __future__ import annotations
 
-import os
 
 import numpy as np
 import torch
@@ -256,19 +255,9 @@ class _Mat4Chain(torch.autograd.Function):
         return dA
 
 
-_CHAIN_KERNEL = os.environ.get("COPENERF_CHAIN_KERNEL", "1") != "0"
-
-
 def mat4_chain(A):
-    """[n, 4, 4] -> the running products [A_0, A_1 A_0, ..., A_{n-1} ... A_0] (fp32, device).
-    COPENERF_CHAIN_KERNEL=0: the same products as one torch matmul each (A/B measurement)."""
-    if _CHAIN_KERNEL:
-        return _Mat4Chain.apply(A)
-    out, cur = [], None
-    for a in A.unbind(0):
-        cur = a if cur is None else a @ cur
-        out.append(cur)
-    return torch.stack(out)
+    """[n, 4, 4] -> the running products [A_0, A_1 A_0, ..., A_{n-1} ... A_0] (fp32, device)."""
+    return _Mat4Chain.apply(A)
 
 
 def masked_chain(P, lo, hi):

@@ -9,7 +9,6 @@ from __future__ import annotations
 
 import ctypes
 import math
-import os
 
 import torch
 
@@ -54,10 +53,9 @@ class KernelTimer:
 _timer = None
 # cn_linear_desc.flags bit 0 alternated launch to launch (the memory-side cache holds the last
 # rows a layer wrote when the next one starts; see include/copenerf.h)
-ALTERNATE_TILE_ORDER = os.environ.get("COPENERF_ALT_ORDER", "1") != "0"
 _flip = 0
 EPI_NAMES = {0: "store", 1: "softplus", 2: "relu", 3: "mul", 4: "tangent", 5: "bwd_softplus", 6: "bwd_relu",
-             7: "bench_mainloop", 8: "softplus_head"}
+             8: "softplus_head"}
 
 
 def set_kernel_timer(t):
@@ -75,61 +73,6 @@ def _ptr(t):
 
 def _stream():
     return torch.cuda.current_stream().cuda_stream
-
-
-_SIDE_STREAMS = {}
-
-
-class SideLane(object):
-    """Weight gradients on a second stream beside the adjoint chain that produced their
-    operands (a layer's dW needs Z_l, which the next adjoint GEMM also reads: the two are
-    independent, so the MFMA-bound weight gradient runs under the HBM-bound adjoint).
-    fork() records the point where the next side launch's inputs are ready; `with lane:`
-    runs launches on the side stream after it; hold() keeps buffers alive (the caching
-    allocator must not hand their memory out before the side stream is done); join() makes
-    the current stream wait for everything launched on the side.  Fork / join are stream
-    events, so a graph capture records them as graph edges.  Off unless COPENERF_WGRAD_STREAM=1:
-    then every method is a no-op and the launches stay on the current stream."""
-
-    enabled = os.environ.get("COPENERF_WGRAD_STREAM", "0") != "0"
-
-    def __init__(self, device):
-        self.side = None
-        if self.enabled:
-            key = (torch.device(device).index, torch.cuda.current_stream(device).cuda_stream)
-            if key not in _SIDE_STREAMS:
-                _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
-            self.side = _SIDE_STREAMS[key]
-        self.ev = None
-        self.held = []
-        self._ctx = None
-
-    def fork(self):
-        if self.side is not None:
-            self.ev = torch.cuda.Event()
-            self.ev.record()
-
-    def __enter__(self):
-        if self.side is not None:
-            self.side.wait_event(self.ev)
-            self._ctx = torch.cuda.stream(self.side)
-            self._ctx.__enter__()
-        return self
-
-    def __exit__(self, *exc):
-        if self._ctx is not None:
-            self._ctx.__exit__(*exc)
-            self._ctx = None
-        return False
-
-    def hold(self, *tensors):
-        if self.side is not None:
-            self.held.extend(t for t in tensors if t is not None)
-
-    def join(self):
-        if self.side is not None:
-            torch.cuda.current_stream().wait_stream(self.side)
-            self.held.clear()
 
 
 def _need(t, name, *, ndim=2):
@@ -253,7 +196,8 @@ class ImagePacker:
 # launch-class tags of the kernel timer: linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, ...> arguments
 # (named by the library itself, cn_linear_kernel_name) -> a short tile name
 _TILE_TAGS = {"4, 2, 2, 4, 16, 1, 2": "sq", "4, 2, 1, 4, 32, 1, 2": "tall", "4, 2, 2, 2, 32, 1, 2": "wide",
-              "2, 2, 2, 2, 16, 2, 2": "t128", "4, 1, 1, 2, 16, 2, 2": "t1", "2, 2, 2, 4, 16, 2, 2": "t2w"}
+              "2, 2, 2, 2, 16, 2, 2": "t128", "4, 1, 1, 2, 16, 2, 2": "t1", "4, 2, 2, 4, 32, 1, 2": "sq",
+              "2, 2, 2, 2, 64, 2, 1": "t128", "4, 1, 1, 2, 64, 2, 1": "t1"}
 
 
 def kernel_name(query, d) -> str:
@@ -274,7 +218,7 @@ def _tile_tag(name, tile):
 def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None, colv=None, aux0=None,
            aux1=None, aux2=None, out_split=None, nsplit=None, nzero=None, adiv=1.0, odiv=1.0, beta=100.0,
            threshold=20.0, aux_beta=0.0, aux2_scale=0.0, tile=None, M=None, kalg=None, out1=None, head_w=None,
-           head_b=None, head_out=None, head_idx=None, emb=None, out_mask=None, aux_mask=None, _desc_only=False):
+           head_b=None, head_out=None, head_idx=None):
     """out = epilogue((A|A2) @ B[:N].T / adiv) -- cn_linear.  MUL / TANGENT /
     BWD_SOFTPLUS read softplus' as sg = 1 - exp(-aux_beta * aux0) from the stored
     softplus output aux0 (include/copenerf.h).  kalg: the unpadded
@@ -286,17 +230,8 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     EPI_SOFTPLUS_HEAD (the last SDF hidden layer): out0 = softplus activation (or
     None: not stored), out1 = colv * softplus' (or None), head_out[head_idx[m] or m]
     = out0[m] · head_w + head_b.
-    emb=(x, multires, scale, U0, U4e, u4div) (A None): the first SDF layer with the encoding
-    fused into its operand load -- A's rows are cn_sdf_embed's encoding of x [M, 4], computed
-    while staging; U0 / U4e (or None) receive the encoding and the skip input's tail / u4div,
-    as cn_sdf_embed would write them."""
+    tile: None (the library's choice), 1 (128x64), 2 (128x128 only: tests compare the tiles)."""
     x6 = B.dim() == 3
-    if emb is not None:
-        if A is not None or A2 is not None:
-            raise RuntimeError("cn_linear: emb replaces A (pass A=None)")
-        _need(emb[0], "emb x")
-        _need(emb[3], "emb U0")
-        _need(emb[4], "emb U4e")
     if x6 and (B.dtype != torch.bfloat16 or B.shape[2] != 48 or not B.is_contiguous()):
         raise RuntimeError(f"cn_linear: a 3-D B must be split_bf16x3's [K/16, N, 48] bfloat16 image (got "
                            f"{tuple(B.shape)}, {B.dtype}, strides {B.stride()})")
@@ -311,9 +246,9 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     if bf:
         K = rup(K, 64)
         K1 = rup(K1, 64) if K1 is not None else None
-        if A is not None and ((A.stride(0) < (K1 or K)) or (A2 is not None and A2.stride(0) < K - K1)):
+        if (A.stride(0) < (K1 or K)) or (A2 is not None and A2.stride(0) < K - K1):
             raise RuntimeError(f"cn_linear (bf16): A rows too short for K={K}")
-    M = (A if emb is None else emb[0]).shape[0] if M is None else M
+    M = A.shape[0] if M is None else M
     # the epilogue reads bias / colv as float4
     bias = bias if bias is None or bias.data_ptr() % 16 == 0 else bias.clone()
     colv = colv if colv is None or colv.data_ptr() % 16 == 0 else colv.clone()
@@ -354,30 +289,15 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     d.epilogue, d.tile = epilogue, tile
     d.adiv, d.odiv, d.beta, d.threshold = adiv, odiv, beta, threshold
     d.mfma_dtype = 2 if x6 else (1 if bf else 0)
-    if out_mask is not None or aux_mask is not None:  # ReLU sign bits (int32 [M, ceil(N / 32)])
-        mk = out_mask if out_mask is not None else aux_mask
-        _need(mk, "mask")
-        if mk.dtype != torch.int32 or mk.shape[0] < M or mk.shape[1] * 32 < N:
-            raise RuntimeError("cn_linear: a mask is int32 [M, ceil(N / 32)]")
-        d.out_mask, d.aux_mask, d.ld_mask = _ptr(out_mask), _ptr(aux_mask), mk.stride(0)
-    if emb is not None:
-        ex, d.emb_multires, d.emb_scale, eu0, eu4, d.emb_u4_div = emb
-        d.emb_x, d.ld_emb_x = _ptr(ex), _ld(ex)
-        d.emb_u0, d.ld_emb_u0, d.emb_u4, d.ld_emb_u4 = _ptr(eu0), _ld(eu0), _ptr(eu4), _ld(eu4)
     global _flip
-    if ALTERNATE_TILE_ORDER:  # consecutive launches walk the rows in opposite directions
-        _flip ^= 1
-        d.flags = _flip
-    if _desc_only:  # for linear_chain: the descriptor and the FLOP / byte counts of this layer
-        nb = 4.0 * M * N * 2 + 4.0 * M * (kalg or K) + 6.0 * N * (kalg or K)
-        return d, 2.0 * M * N * (kalg or K), nb, (bias, colv, head_w)
+    _flip ^= 1  # consecutive launches walk the rows in opposite directions
+    d.flags = _flip
     if _timer is not None:
         e0 = _timer.start()
         _lib.check(_lib.load().cn_linear(d, _stream()), "cn_linear")
         name = kernel_name(_lib.load().cn_linear_kernel_name, d)
-        tag = _tile_tag(name, tile) if x6 else tile
-        key = ("linear", tag, EPI_NAMES[epilogue] + ("+rowv" if rowv is not None else "") +
-               ("+emb" if emb is not None else "")) + \
+        tag = _tile_tag(name, tile) if (x6 or bf) else tile
+        key = ("linear", tag, EPI_NAMES[epilogue] + ("+rowv" if rowv is not None else "")) + \
             (("bf16",) if bf else ("x6",) if x6 else ())
         _timer.symbols[key] = name
         ka = kalg or K
@@ -390,28 +310,6 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     else:
         _lib.check(_lib.load().cn_linear(d, _stream()), "cn_linear")
     return out0
-
-
-def linear_chain(layers):
-    """A chain of SOFTPLUS layers in one cn_linear_chain launch (each layer's A is the previous
-    layer's out0): `layers` is a list of ops.linear argument tuples (args, kwargs).  Every layer
-    must satisfy cn_linear_chain's conditions (include/copenerf.h); the outputs equal the
-    per-layer cn_linear calls' bitwise."""
-    built = [linear(*a, **dict(kw, _desc_only=True)) for a, kw in layers]
-    n = len(built)
-    arr = (_lib.LinearDesc * n)(*[b[0] for b in built])
-    for i in range(1, n):
-        arr[i].flags = arr[0].flags  # one tile order for the whole chain
-    lib = _lib.load()
-    if _timer is not None:
-        e0 = _timer.start()
-        _lib.check(lib.cn_linear_chain(arr, n, _stream()), "cn_linear_chain")
-        key = ("linear", "sq", "softplus_chain", "x6")
-        _timer.symbols[key] = "void cn::linear_kernel<4, 2, 2, 4, 16, 1, 2, 1, false, 10>(cn::LinearArgs)"
-        _timer.stop(key, e0, sum(b[1] for b in built), sum(b[2] for b in built))
-    else:
-        _lib.check(lib.cn_linear_chain(arr, n, _stream()), "cn_linear_chain")
-    return layers[-1][0][4]
 
 
 WGRAD_MODES = {"fp32": 0, "bf16": 1, "bf16x6": 2}
@@ -468,24 +366,17 @@ def wgrad(Y0, X0, N, K, dW, *, db=None, Y1=None, X1=None, accumulate=False, mode
     return dW
 
 
-# COPENERF_WGRAD_BATCH=0 (benchmarking aid): every weight gradient its own cn_wgrad launch
-WGRAD_BATCH = os.environ.get("COPENERF_WGRAD_BATCH", "1") != "0"
-
-
 class WgradQueue(object):
     """Collects a backward pass's 256x256 stage-ring weight gradients and runs them with ONE
     cn_wgrad_batch call at flush(): one launch and one slab reduction instead of a launch, a
     full-chip slab write and a reduction each (other tile classes launch at add()).  The
     queue holds the operand tensors, so their memory stays allocated until the flush; the
-    gradients are written by the flush (call it before anything reads them).  With
-    COPENERF_WGRAD_BATCH=0, add() launches at once."""
+    gradients are written by the flush (call it before anything reads them)."""
 
     def __init__(self):
         self.jobs = []
 
     def add(self, Y0, X0, N, K, dW, *, db=None, Y1=None, X1=None, mode="fp32"):
-        if not WGRAD_BATCH:
-            return wgrad(Y0, X0, N, K, dW, db=db, Y1=Y1, X1=X1, mode=mode)
         d, ws = _wgrad_desc(Y0, X0, N, K, dW, db, Y1, X1, False, mode)
         if "WgradBatch" not in kernel_name(_lib.load().cn_wgrad_kernel_name, d):
             # not a stage-ring job (e.g. K = 64 first layers): nothing to share, launch it now

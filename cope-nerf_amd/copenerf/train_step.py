@@ -35,7 +35,6 @@ single-GPU gradient of the loss over all ranks' rays.
 """
 from __future__ import annotations
 
-import os
 
 import numpy as np
 import torch
@@ -48,8 +47,6 @@ from .motion import (MotionNetwork, affine_points, flow_rgb_loss, masked_chain, 
                      scene_flow_loss, stage1_terms_fused)
 from .rays import PoseRetriever, get_patch_indices, intrinsics_ndc, inv4x4, pixels_from_indices, world_rays
 from .renderer import NeuSRenderer
-
-FUSED_ADAM = os.environ.get("COPENERF_FUSED_ADAM", "1") != "0"
 
 SDF_CFG = dict(d_in=4, d_out=257, d_hidden=256, n_layers=8, skip_in=[4], multires=6, bias=0.5, scale=1.0,
                geometric_init=True, weight_norm=True)
@@ -177,7 +174,7 @@ class SyntheticTrainer:
     def __init__(self, device, rays=4096, H=540, W=960, patch=4, seed=678, depth_range=(0.01, 5.0),
                  cos_anneal_ratio=0.5, schedule="fixed", start_it=0, distributed=False, group=None,
                  sdf_cfg=None, col_cfg=None, ren_cfg=None, joint_pose=False, stage1=False, n_images=10,
-                 capturable=False, mfma_dtype="fp32", train_cfg=None):
+                 capturable=False, mfma_dtype="fp32", train_cfg=None, stage1_fused=True):
         if schedule not in ("fixed", "reference"):
             raise ValueError(f"schedule must be 'fixed' or 'reference' (got {schedule!r})")
         self.device = torch.device(device)
@@ -196,9 +193,9 @@ class SyntheticTrainer:
         self.renderer.expose_sdf_pack = stage1  # the stage-1 SDF re-query reuses the step's weight images
         self.params = list(self.sdf.parameters()) + list(self.var.parameters()) + list(self.col.parameters())
         self.joint_pose, self.stage1 = joint_pose, stage1
-        # stage-1 per-sample terms in the fused HIP pass; COPENERF_STAGE1_FUSED=0 keeps the
-        # torch expressions (device ops too; for A/B measurement and parity tests)
-        self.stage1_fused = os.environ.get("COPENERF_STAGE1_FUSED", "1") != "0"
+        # stage-1 per-sample terms in the fused HIP pass; stage1_fused=False keeps the torch
+        # expressions (device ops too: the parity test's reference, tests/test_gpu_stage1_fused.py)
+        self.stage1_fused = stage1_fused
         self.n_images = n_images
         self.nst = self.cfg["nb_sample_timestep"]
         wi = self.cfg["world_idx"]
@@ -229,9 +226,8 @@ class SyntheticTrainer:
             self.chain_steps = torch.arange(max(self.cfg["random_ref_interval"]), device=self.device)
         self.all_params = [p for g in groups for p in g["params"]]
         # torch's fused multi-tensor Adam: one kernel chain per step instead of the foreach
-        # implementation's ~8 launches (same update rule, training.py:552-558 / train.py:57-60);
-        # COPENERF_FUSED_ADAM=0 restores foreach
-        self.opt = torch.optim.Adam(groups, lr=lr, capturable=capturable, fused=True if FUSED_ADAM else None)
+        # implementation's ~8 launches (same update rule, training.py:552-558 / train.py:57-60)
+        self.opt = torch.optim.Adam(groups, lr=lr, capturable=capturable, fused=True)
         # data: rank-independent (every rank sees the same frames); sampling: per rank
         gdata = torch.Generator(device=self.device).manual_seed(seed)
         self.images = torch.rand(n_images, 3, H, W, device=self.device, generator=gdata)
@@ -356,7 +352,7 @@ class SyntheticTrainer:
                                                          vel, cw2, self.world_time_step, pose_grad, group=grp)
             flows = project_flow_sums(pbar, wbar, w2c, self.camera_mats.index_select(0, refc), self.I, batch["pixn"],
                                       (self.H, self.W))
-        else:  # the same terms as torch expressions (A/B and tests: COPENERF_STAGE1_FUSED=0)
+        else:  # the same terms as torch expressions (the parity test's reference: stage1_fused=False)
             sdf_loss = scene_flow_loss(pts, out["normals"], out["sdf_flows"], out["weights"], omega, vel, group=grp)
             flows = project_flow(pts, out["weights"], w2c, self.camera_mats.index_select(0, refc), self.I,
                                  batch["pixn"], (self.H, self.W))

@@ -24,16 +24,6 @@
 
 namespace cn {
 
-constexpr int kChainMax = 8;
-constexpr int kEpiReluMask = 9;  // internal: RELU that also writes the sign bits (cn_linear_desc.out_mask)
-struct ChainLayer {  // the per-layer part of a chained SOFTPLUS launch (the rest is shared)
-    const float* B;
-    const float* bias;
-    float* out0;
-    int N, nzero;
-    float inv_odiv;
-};
-
 struct LinearArgs {
     const float* A;
     const float* A2;
@@ -52,29 +42,16 @@ struct LinearArgs {
     float inv_adiv, inv_odiv, beta, threshold;
     float aux_c;       // -aux_beta * log2(e): sigma = 1 - 2^(aux_c * aux0)
     float aux2_scale;  // BWD_SOFTPLUS second-order term scale
-    int stagger;       // odd workgroups start this many s_sleep(127) later (epilogue / main-loop desync)
     const float* head_w;  // SOFTPLUS_HEAD: row-dot weights [N], bias [1], output, destination rows
     const float* head_b;
     float* head_out;
     const int* head_idx;
     int flags;
-    // MODE >= 4: A is the SDF encoding of the points emb_x (cn_linear_desc.emb_*): gload fetches one
-    // point per row, lstore encodes it; the N-tile-0 workgroups also write the encoding (emb_u0) and
-    // the skip input's tail (emb_u4, divided by emb_u4_div)
-    const float* emb_x;
-    float* emb_u0;
-    float* emb_u4;
-    int ld_emb_x, ld_emb_u0, ld_emb_u4, emb_L;
-    float emb_scale, emb_u4_div;
-    // MODE & 8: a layer chain (cn_linear_chain) -- one 256-row block goes through every layer in the
-    // same workgroup: layer j's A is layer j-1's out0 rows, just written (L2 / memory-side cache)
-    ChainLayer chain[kChainMax];
-    int nchain;
-    // RELU: the sign bits of the output (bit c of word c / 32 of a row: out > 0), written beside it;
-    // BWD_RELU: the same bits read instead of the stored activation (4 bytes per 32 columns, not 128)
-    unsigned* mask_out;
-    const unsigned* mask_in;
-    int ld_mask;
+    // bf16 images of the outputs (the operands of the GEMMs that consume them, rounded as their
+    // staging would round them): out0 / out1 values, RNE, same columns (NULL: none)
+    bf16_t* out0_b;
+    bf16_t* out1_b;
+    int ld_out0_b, ld_out1_b;
 };
 
 
@@ -101,36 +78,17 @@ struct LinearArgs {
 //         the fp32 image's geometry (conflict-free fragment reads, and the C tile
 //         parks in one slab).
 // The accumulator layout of the two MFMAs is the same, so the epilogue is shared.
-#ifndef X6_EXP
-#define X6_EXP 0  // benchmark-only ablations of the bf16x6 main loop (tools/x6_ablation.sh)
-#endif
-#ifndef DIRECT_EPI
-#define DIRECT_EPI 1  // aux-free epilogues of main tiles store from the MFMA layout (no LDS park)
-#endif
-#ifndef EPI_EXP
-#define EPI_EXP 0  // benchmark-only: 1 = epilogue without its global stores (tools/ab_libs.sh)
-#endif
-#ifndef LIN_SEG
-#define LIN_SEG 1  // pinned MFMA / staging segments on the 256x256 bf16x6 tile (see kSeg)
-#endif
-#ifndef LSTORE_ALWAYS
-#define LSTORE_ALWAYS 0  // 1: branch-free staging (measured: main loop -1.5 %, epilogue variants +2-3 %)
-#endif
 constexpr int kTblCols = 512;  // widest N with a bias / colv (the LDS column table)
 
 template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int EPI, bool ROWV, int MODE_>
 __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel(LinearArgs p) {
     constexpr int MODE = MODE_ & 3;         // the GEMM mode (0 fp32, 1 bf16, 2 bf16x6)
-    constexpr bool EMB = (MODE_ & 4) != 0;  // A generated from the points (the first SDF layer)
-    constexpr bool CHAIN = (MODE_ & 8) != 0;  // a layer chain (p.chain): row block through every layer
     constexpr int NT = 64 * WM * WN;
-    // the per-layer operands (CHAIN: updated per layer from p.chain; p itself stays the read-only kernarg)
-    const float* cA = p.A;
-    const float* cB = p.B;
-    const float* cBias = p.bias;
-    float* cOut0 = p.out0;
-    int cN = p.N, cNzero = p.nzero;
-    float cInvOdiv = p.inv_odiv;
+    const float* const cA = p.A;
+    const float* const cB = p.B;
+    float* const cOut0 = p.out0;
+    const int cN = p.N, cNzero = p.nzero;
+    const float cInvOdiv = p.inv_odiv;
     constexpr int BM = 32 * TM * WM;
     constexpr int BN = 32 * TN * WN;
     constexpr bool BF = MODE != 0;               // bf16 MFMA (modes 1, 2)
@@ -150,11 +108,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     constexpr int ESZB = BF ? 2 : 4;             // bytes per B element
     constexpr int PIECES_PL = BK / 8;            // MODE 2: 16-byte pieces per plane of a staged row
     constexpr int CS = BN + 4;
-    // kB1: the two-per-CU 128x256 bf16x6 tile (BWD_SOFTPLUS: every workgroup owns whole 256-wide rows, so A
-    // is read once, and the partner workgroup hides the epilogue's aux streams) fits two workgroups in the
-    // LDS only with ONE B stage buffer: A stays double-buffered, B is re-staged between two barriers
-    constexpr bool kB1 = MODE == 2 && OCC == 2 && TM * TN >= 8;
-    constexpr int LDS_FLOATS = 2 * BM * LS + (kB1 ? 1 : 2) * BN * LS;
+    constexpr int LDS_FLOATS = 2 * BM * LS + 2 * BN * LS;
     // the epilogue parks the C tile in the staging LDS, in NPART row slabs if it does not fit
     constexpr int NPART = (BM * CS <= LDS_FLOATS) ? 1 : ((BM / 2) * CS <= LDS_FLOATS ? 2 : 4);
     static_assert((BM / NPART) * CS <= LDS_FLOATS, "C tile slab must fit in the staging LDS");
@@ -167,7 +121,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     // pass -- each pass waited for the previous pass's stores)
     // (SOFTPLUS_HEAD: + the head weights and bias; its rows fit one tile, N <= 256)
     constexpr bool kHead = EPI == CN_EPI_SOFTPLUS_HEAD;
-    constexpr bool kBias = EPI == CN_EPI_STORE || EPI == CN_EPI_SOFTPLUS || EPI == CN_EPI_RELU || EPI == kEpiReluMask || kHead;
+    constexpr bool kBias = EPI == CN_EPI_STORE || EPI == CN_EPI_SOFTPLUS || EPI == CN_EPI_RELU || kHead;
     constexpr bool kColv = ROWV || kHead;
     constexpr int TBLC = kHead ? 256 : kTblCols;
     constexpr int TBL = (kBias ? TBLC : 0) + (kColv ? TBLC : 0) + (kHead ? TBLC + 4 : 0);
@@ -217,7 +171,6 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     const int lds_b = srowb * LS + scb * 4;
 
     floatx4 ra[DEPTH][ALD], rb[DEPTH][BLD];
-    int egrp[DEPTH], erow[DEPTH], erows[DEPTH];  // EMB: encoding group, side-output tile row (-1: none), rows
     // Straight-line staging: every call issues exactly ALD + BLD loads (an empty
     // view when `valid` is false, reads return zero) with no data-dependent branch,
     // so the compiler tracks vmcnt precisely and the LDS writes of one register
@@ -226,76 +179,29 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         const int k0 = kc * BK;
         const int rows = valid ? min(BM, p.M - m0) : 0;
         const bool second = k0 >= p.K1;  // wave-uniform: A2 half of a virtual concat
-#if X6_EXP == 6  // benchmark only: every tile reads A rows [0, 4096) (L2-resident: no HBM A traffic)
-        const int ma = m0 & 4095;
-#else
-        const int ma = m0;
-#endif
-        if constexpr (EMB) {
-            // the rows' points (lstore encodes them: this thread's columns are encoding group
-            // k0 / 4 + sc4); rows past M read zero, their outputs are dropped
-            const rsrc_t rX = make_view(p.emb_x + (int64_t)ma * p.ld_emb_x, rows * p.ld_emb_x * 4);
-#pragma unroll
-            for (int q = 0; q < ALD; ++q) ra[set][q] = bload4(rX, (srow + q * RSTEP) * p.ld_emb_x * 4, 0);
-            egrp[set] = (k0 >> 2) + sc4;
-            erow[set] = (valid && n0 == 0) ? m0 : -1;
-            erows[set] = rows;
-        } else {
-        const float* abase = second ? p.A2 + (int64_t)ma * p.lda2 : cA + (int64_t)ma * p.lda;
+        const float* abase = second ? p.A2 + (int64_t)m0 * p.lda2 : cA + (int64_t)m0 * p.lda;
         const int ald = second ? p.lda2 : p.lda;
         const int ak = second ? k0 - p.K1 : k0;
         const rsrc_t rA = make_view(abase, rows * ald * 4);
 #pragma unroll
-        for (int q = 0; q < ALD; ++q) {
-#if X6_EXP == 4
-            if (MODE == 2) { ra[set][q] = floatx4{(float)k0, (float)rows, (float)q, 1.0f}; continue; }
-#endif
-            ra[set][q] = bload4(rA, second ? voA2[q] : voA[q], ak * 4);
-        }
-        }
+        for (int q = 0; q < ALD; ++q) ra[set][q] = bload4(rA, second ? voA2[q] : voA[q], ak * 4);
         // MODE 2: chunk kc of the image is [ldb rows][48 bf16]; the tile's BN rows are 96 * BN contiguous bytes
         const int64_t bofs = MODE == 2 ? ((int64_t)kc * (BK / 16) * p.ldb + n0) * 96 : (int64_t)n0 * p.ldb * ESZB;
         const rsrc_t rB = make_view(reinterpret_cast<const float*>(reinterpret_cast<const char*>(cB) + bofs),
                                     valid ? (MODE == 2 ? ((BK / 16 - 1) * p.ldb + BN) * 96 : BN * p.ldb * ESZB) : 0);
 #pragma unroll
-        for (int q = 0; q < BLD; ++q) {
-#if X6_EXP == 4 || X6_EXP == 5
-            if (MODE == 2) { rb[set][q] = floatx4{(float)k0, (float)n0, (float)q, 1.0f}; continue; }
-#endif
-            rb[set][q] = bload4(rB, voB[q], MODE == 2 ? 0 : k0 * ESZB);
-        }
+        for (int q = 0; q < BLD; ++q) rb[set][q] = bload4(rB, voB[q], MODE == 2 ? 0 : k0 * ESZB);
     };
     // piece < 0: the whole stage; piece q < ALD: A row q only; piece ALD: B only
     auto lstore = [&](int set, int buf, int piece = -1) {
         float* a = sA + buf * BM * LS + lds_a;
-        float* b = sB + (kB1 ? 0 : buf) * BN * LS + lds_b;
+        float* b = sB + buf * BN * LS + lds_b;
 #pragma unroll
         for (int q = 0; q < ALD; ++q) {
             if (piece >= 0 && piece != q) continue;
-            if constexpr (EMB) {
-                const int g = egrp[set];
-                const floatx4 e = sdf_embed_group(ra[set][q], g, p.emb_L, p.emb_scale);
-                ra[set][q] = e;
-                if (erow[set] >= 0) {  // the encoding itself and the skip input's tail, once per row
-                    const int r = srow + q * RSTEP;
-                    const rsrc_t rU = make_view(p.emb_u0 + (int64_t)erow[set] * p.ld_emb_u0, p.emb_u0 ? erows[set] * p.ld_emb_u0 * 4 : 0);
-                    bstore4(rU, (r * p.ld_emb_u0 + 4 * g) * 4, 0, e);
-                    if (g < 1 + 2 * p.emb_L) {
-                        floatx4 h;
-#pragma unroll
-                        for (int c = 0; c < 4; ++c) h[c] = e[c] / p.emb_u4_div;
-                        const rsrc_t r4 = make_view(p.emb_u4 + (int64_t)erow[set] * p.ld_emb_u4, p.emb_u4 ? erows[set] * p.ld_emb_u4 * 4 : 0);
-                        bstore4(r4, (r * p.ld_emb_u4 + 4 * g) * 4, 0, h);
-                    }
-                }
-            }
             if constexpr (MODE == 2) {
                 bf16x4 x0, x1, x2;
-#if X6_EXP == 1
-                x0 = x1 = x2 = __builtin_convertvector(ra[set][q], bf16x4);
-#else
                 split3(ra[set][q], x0, x1, x2);
-#endif
                 *reinterpret_cast<bf16x4*>(a + q * RSTEP * LS) = x0;
                 *reinterpret_cast<bf16x4*>(a + q * RSTEP * LS + BK / 2) = x1;
                 *reinterpret_cast<bf16x4*>(a + q * RSTEP * LS + BK) = x2;
@@ -310,7 +216,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             if constexpr (MODE == 2) {
                 const int idx = tid + q * NT;
                 if (BN * KCB % NT == 0 || idx < BN * KCB)  // wave-uniform (NT, BN*KCB multiples of 64)
-                    *reinterpret_cast<floatx4*>(sB + (kB1 ? 0 : buf) * BN * LS + ldsB[q]) = rb[set][q];
+                    *reinterpret_cast<floatx4*>(sB + buf * BN * LS + ldsB[q]) = rb[set][q];
             } else {
                 *reinterpret_cast<floatx4*>(b + q * RSTEPB * LS) = rb[set][q];
             }
@@ -333,8 +239,8 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     };
 
     // pinned compute/staging segments: the 256x256 bf16x6 tile (one workgroup per CU, so no
-    // partner workgroup's MFMAs cover a trailing staging block; LIN_SEG=0: compiler's order)
-    constexpr bool kSeg = LIN_SEG && MODE == 2 && TM * TN >= 8 && TN > ALD && DEPTH == 2 && OCC == 1 && BK == 16;
+    // partner workgroup's MFMAs cover a trailing staging block)
+    constexpr bool kSeg = MODE == 2 && TM * TN >= 8 && TN > ALD && DEPTH == 2 && OCC == 1 && BK == 16;
     const int arow = wm * TM * 32 + (lane & 31);
     const int brow = wn * TN * 32 + (lane & 31);
     const int kofs = (BK / 2) * (lane >> 5);
@@ -363,22 +269,8 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 
     int vt = next_valid(blockIdx.x);
     if (vt >= ntiles) return;
-    int jl = 0;  // CHAIN: the layer of the current unit
-    bool first_unit = true;
-    const float* const chain_A = cA;
-    auto set_layer = [&](int j) {  // layer j's operands / outputs (shared: K, lda = ld_out0, tiling)
-        const ChainLayer& L = p.chain[j];
-        cA = j == 0 ? chain_A : p.chain[j - 1].out0;
-        cB = L.B;
-        cBias = L.bias;
-        cOut0 = L.out0;
-        cN = L.N;
-        cNzero = L.nzero;
-        cInvOdiv = L.inv_odiv;
-    };
-    if constexpr (CHAIN) set_layer(0);
     if constexpr (TBL > 0) {  // visible after the first tile's staging barrier
-        const rsrc_t rbias = make_view(cBias, kBias && cBias ? cN * 4 : 0);
+        const rsrc_t rbias = make_view(p.bias, kBias && p.bias ? cN * 4 : 0);
         const rsrc_t rcolv = make_view(p.colv, kColv && p.colv ? cN * 4 : 0);
         const rsrc_t rhw = make_view(p.head_w, kHead ? cN * 4 : 0);
         for (int i = tid; i < TBLC / 4; i += NT) {
@@ -388,10 +280,6 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         }
         if (kHead && tid == 0) sHeadW[TBLC] = p.head_b[0];
     }
-    // stagger: with 2 workgroups per CU, the second resident one (block ids past the first
-    // gridDim / 2 fill the CUs' second slots) starts later; with 1 per CU, the odd ones
-    if (OCC >= 2 ? (blockIdx.x >= gridDim.x / 2) : (blockIdx.x & 1))
-        for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
     int tm, tn;
     coords(vt, tm, tn);
     // the first DEPTH chunks of a tile are in the register sets when its loop starts (the next
@@ -409,18 +297,6 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 
     while (vt < ntiles) {
         const int m0 = tm * BM, n0 = tn * BN;
-        if constexpr (CHAIN) {
-            // a unit = (row block, layer): nothing of it could be prefetched during the previous unit
-            // (its A rows were being written), so its first chunks are fetched here, and the layer's
-            // bias table is re-read (the previous unit's readers passed the barrier that ended it)
-            if (!first_unit) {
-                set_layer(jl);
-#pragma unroll
-                for (int d = 0; d < DEPTH; ++d) gload(d, d, m0, n0, true);
-                const rsrc_t rbias = make_view(cBias, cBias ? cN * 4 : 0);
-                for (int i = tid; i < TBLC / 4; i += NT) *reinterpret_cast<floatx4*>(sBias + 4 * i) = bload4(rbias, 16 * i, 0);
-            }
-        }
         const int vt_next = next_valid(vt + gridDim.x);
         int tm_next = 0, tn_next = 0;
         if (vt_next < ntiles) coords(vt_next, tm_next, tn_next);
@@ -442,7 +318,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         auto compute = [&](int cur, auto side) {
             if constexpr (MODE == 2) {
                 const float* a_base = sA + cur * BM * LS + arow * LS + 4 * (lane >> 5);
-                const float* b_base = sB + (kB1 ? 0 : cur) * BN * LS + brow * LS + 4 * (lane >> 5);
+                const float* b_base = sB + cur * BN * LS + brow * LS + 4 * (lane >> 5);
                 if constexpr (TM * TN >= 8) {
                     // 64x128 wave tiles: the B fragments of one column block at a time (12 VGPRs
                     // instead of 48 live); a single accumulation chain issues back to back
@@ -481,13 +357,6 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                     bf16x8 af[3][TM], bf[3][TN];
 #pragma unroll
                     for (int t = 0; t < 3; ++t) {
-#if X6_EXP == 3
-                        if (t > 0) {
-                            for (int i = 0; i < TM; ++i) af[t][i] = af[0][i];
-                            for (int j = 0; j < TN; ++j) bf[t][j] = bf[0][j];
-                            continue;
-                        }
-#endif
 #pragma unroll
                         for (int i = 0; i < TM; ++i)
                             af[t][i] = *reinterpret_cast<const bf16x8*>(a_base + i * 32 * LS + t * (BK / 2) + ks * 8);
@@ -500,7 +369,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                     constexpr int TA[6] = {0, 1, 0, 2, 1, 0};
                     constexpr int TB[6] = {0, 0, 1, 0, 1, 2};
 #pragma unroll
-                    for (int u = 0; u < (X6_EXP == 2 ? 3 : 6); ++u)
+                    for (int u = 0; u < 6; ++u)
 #pragma unroll
                         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -512,7 +381,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             } else if constexpr (BF) {
                 // lane half h holds k = 8h + j of each 16-deep MFMA step (8 bf16 = 4 dwords)
                 const float* a_base = sA + cur * BM * LS + arow * LS + 4 * (lane >> 5);
-                const float* b_base = sB + (kB1 ? 0 : cur) * BN * LS + brow * LS + 4 * (lane >> 5);
+                const float* b_base = sB + cur * BN * LS + brow * LS + 4 * (lane >> 5);
 #pragma unroll
                 for (int ks = 0; ks < BK / 16; ++ks) {
                     bf16x8 af[TM], bf[TN];
@@ -531,7 +400,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 return;
             }
             const float* a_base = sA + cur * BM * LS + arow * LS + kofs;
-            const float* b_base = sB + (kB1 ? 0 : cur) * BN * LS + brow * LS + kofs;
+            const float* b_base = sB + cur * BN * LS + brow * LS + kofs;
 #pragma unroll
             for (int q4 = 0; q4 < BK / 8; ++q4) {
                 floatx4 af[TM], bf[TN];
@@ -558,9 +427,9 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 const int cur = kc & 1;
                 // chunk kc+1 of this tile, or the next tile's first chunk (consumed after the epilogue)
                 const bool more = kc + 1 < nk;
-                gload(0, more ? kc + 1 : 0, more ? m0 : m_next, more ? n0 : n_next, more || (!CHAIN && has_next));
+                gload(0, more ? kc + 1 : 0, more ? m0 : m_next, more ? n0 : n_next, more || has_next);
                 compute(cur, [](int) {});
-                if (LSTORE_ALWAYS || more) lstore(0, cur ^ 1);
+                if (more) lstore(0, cur ^ 1);
                 __syncthreads();
             }
         } else {
@@ -575,7 +444,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                     const bool here = cn < nk;
                     // past this tile: chunk cn - nk of the next one, issued before this tile's
                     // epilogue stores, so the next tile's first DEPTH stagings never wait for them
-                    gload(j, here ? cn : cn - nk, here ? m0 : m_next, here ? n0 : n_next, here || (!CHAIN && has_next));
+                    gload(j, here ? cn : cn - nk, here ? m0 : m_next, here ? n0 : n_next, here || has_next);
                     if constexpr (kSeg) {
                         // the next stage's staging (unconditional: after a tile's last chunk it
                         // stages the next tile's first chunk, or zeros, into the free buffer,
@@ -588,23 +457,12 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         continue;
                     }
                     compute(j & 1, [](int) {});
-                    if constexpr (kB1) {  // A into the free buffer; B after every wave is done reading it
-                        const bool more = LSTORE_ALWAYS || kc + j + 1 < nk;
-                        if (more) {
-#pragma unroll
-                            for (int q = 0; q < ALD; ++q) lstore((j + 1) % DEPTH, (j + 1) & 1, q);
-                        }
-                        __syncthreads();
-                        if (more) lstore((j + 1) % DEPTH, 0, ALD);
-                        __syncthreads();
-                        continue;
-                    }
                     // unconditional (branch-free: compute and the next stage's staging share a
                     // basic block, so the scheduler can interleave the split VALU / LDS writes
                     // with the MFMAs).  After the last chunk this stages the next tile's first
                     // chunk (or zeros) into the free buffer: harmless, the epilogue parks over it
                     // and the next tile stages it again.
-                    if (LSTORE_ALWAYS || kc + j + 1 < nk) lstore((j + 1) % DEPTH, (j + 1) & 1);
+                    if (kc + j + 1 < nk) lstore((j + 1) % DEPTH, (j + 1) & 1);
                     __syncthreads();
                 }
             }
@@ -620,20 +478,6 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             for (int q = 0; q < ALD; ++q) asm volatile("" : "+v"(ra[d][q]));
 #pragma unroll
             for (int q = 0; q < BLD; ++q) asm volatile("" : "+v"(rb[d][q]));
-        }
-        if constexpr (EPI == 7) {  // benchmark only: main loop alone, keep every accumulator live
-            float sum = 0.0f;
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) sum += acc[i][j][r];
-            cOut0[(int64_t)(m0 + (tid & 127)) * p.ld_out0 + n0 + (tid >> 7)] = sum;
-            vt = vt_next;
-            tm = tm_next;
-            tn = tn_next;
-            continue;
         }
         // Epilogue: park the accumulator tile (or a slab of PROWS rows of it) in the
         // now free staging LDS, then process it row-wise with 16-byte coalesced
@@ -796,10 +640,6 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         }
                         if constexpr (MAIN) {
                             main_vals(v, slot, q, o0);
-                            if (EPI_EXP == 1) {  // keep the values live without a global store
-                                asm volatile("" ::"v"(o0));
-                                continue;
-                            }
                             bstore4(view_at(tO0, lrow), voO0, 0, o0);
                         } else if (region == 0) {
                             main_vals(v, slot, q, o0);
@@ -825,14 +665,14 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         // the same way: their aux rows are read in the MFMA layout too (dword loads, two 128-byte
         // row segments per instruction), RG accumulator rows at a time, double-buffered (group
         // g+1's loads issued before group g's stores, so each wait skips those stores)
-        constexpr bool kDirectAux = DIRECT_EPI && TM * TN >= 8 && !ROWV &&
+        constexpr bool kDirectAux = TM * TN >= 8 && !ROWV &&
                                     (EPI == CN_EPI_MUL || EPI == CN_EPI_TANGENT || EPI == CN_EPI_BWD_SOFTPLUS ||
                                      EPI == CN_EPI_BWD_RELU);
-        constexpr bool kDirect = DIRECT_EPI && ((!kAnyAux && EPI != 7) || kDirectAux);
+        constexpr bool kDirect = !kAnyAux || kDirectAux;
         // SOFTPLUS_HEAD on the 64x128 wave tiles: the activation, the ∇-pass seed and the sdf row-dot
         // from the MFMA layout too (row sums: butterfly over the 32 lanes of a row, then the two
         // column waves' partials through LDS)
-        constexpr bool kDirectHead = DIRECT_EPI && kHead && TM * TN >= 8;
+        constexpr bool kDirectHead = kHead && TM * TN >= 8;
         // 64x128 wave tiles are dispatched only where one tile spans all columns (128 < N <= 256, no
         // rowv: host-checked), so their kernels carry no LDS-park path (and its registers)
         constexpr bool kDirectOnly = (kDirect || kDirectHead) && TM * TN >= 8;
@@ -873,12 +713,6 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             constexpr int RG = kAux1 ? 2 : 4;          // accumulator rows r per group
             constexpr int NGD = TM * 16 / RG;          // groups per tile
             float xa[2][RG][TN], xb[2][RG][TN], xc[2][RG][TN];
-            // BWD_RELU from sign bits: every lane of a half-wave loads its row's word of the column block
-            // (one dword per 32 columns) and takes bit lane % 32
-            const bool use_mask = EPI == CN_EPI_BWD_RELU && p.mask_in != nullptr;
-            const TileView tMk = {reinterpret_cast<const float*>(p.mask_in) + (int64_t)m0 * p.ld_mask, p.ld_mask,
-                                  use_mask ? min(BM, p.M - m0) * p.ld_mask * 4 : 0};
-            const int vmk = (lrow * p.ld_mask + (n0 >> 5) + wn * TN) * 4;
             auto dload = [&](int g, int sl) {
                 const int i = g / (16 / RG), r0 = (g % (16 / RG)) * RG;
 #pragma unroll
@@ -886,7 +720,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                     const int r = r0 + q, row = i * 32 + (r & 3) + 8 * (r >> 2);
 #pragma unroll
                     for (int j = 0; j < TN; ++j) {
-                        xa[sl][q][j] = use_mask ? bload1(view_at(tMk, row), vmk, 4 * j) : bload1(view_at(tX0, row), v0, 128 * j);
+                        xa[sl][q][j] = bload1(view_at(tX0, row), v0, 128 * j);
                         if (kAux1) xb[sl][q][j] = bload1(view_at(tX1, row), v1, 128 * j);
                         if (kAux1) xc[sl][q][j] = bload1(view_at(tX2, row), v2, 128 * j);
                     }
@@ -916,9 +750,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         const float sg = EPI == CN_EPI_BWD_RELU ? 0.0f : sigma_from_act(xa[sl][q][j], p.aux_c);
                         float o;
                         if constexpr (EPI == CN_EPI_BWD_RELU) {
-                            const bool pos = use_mask ? ((__float_as_uint(xa[sl][q][j]) >> (lane & 31)) & 1u) != 0
-                                                      : xa[sl][q][j] > 0.0f;
-                            o = pos ? u : 0.0f;
+                            o = xa[sl][q][j] > 0.0f ? u : 0.0f;
                         } else if constexpr (EPI == CN_EPI_MUL) {
                             o = u * sg;
                         } else if constexpr (EPI == CN_EPI_TANGENT) {
@@ -942,29 +774,19 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             float bj[TN];
 #pragma unroll
             for (int j = 0; j < TN; ++j) bj[j] = kBias ? sBias[min(n0 + lcol + 32 * j, kTblCols - 1)] : 0.0f;
-            const TileView tMo = {reinterpret_cast<const float*>(p.mask_out) + (int64_t)m0 * p.ld_mask, p.ld_mask,
-                                  EPI == kEpiReluMask ? min(BM, p.M - m0) * p.ld_mask * 4 : 0};
-            const int vmo = ((wm * TM * 32 + 4 * (lane >> 5)) * p.ld_mask + (n0 >> 5) + wn * TN) * 4;
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const rsrc_t vw = view_at(tO0, i * 32 + (r & 3) + 8 * (r >> 2));
-                    const rsrc_t vmr = view_at(tMo, i * 32 + (r & 3) + 8 * (r >> 2));  // (kEpiReluMask only)
 #pragma unroll
                     for (int j = 0; j < TN; ++j) {
                         const float z = acc[i][j][r] * p.inv_adiv + bj[j];
                         float o;
                         if constexpr (EPI == CN_EPI_SOFTPLUS) o = softplus_hw(z, c_exp, c_thr, c_log) * cInvOdiv;
-                        else if constexpr (EPI == CN_EPI_RELU || EPI == kEpiReluMask) o = z > 0.0f ? z : 0.0f;
+                        else if constexpr (EPI == CN_EPI_RELU) o = z > 0.0f ? z : 0.0f;
                         else o = z;
                         bstore1(vw, voj[j], 0, live[j] ? o : 0.0f);
-                        if constexpr (EPI == kEpiReluMask) {
-                            // lanes 0-31 hold row R, 32-63 row R + 4 of this column block: one word each
-                            const unsigned long long bal = __ballot(live[j] && o > 0.0f);
-                            const unsigned word = lane < 32 ? (unsigned)bal : (unsigned)(bal >> 32);
-                            if ((lane & 31) == 0) bstore1(vmr, vmo, 4 * j, __uint_as_float(word));
-                        }
                     }
                 }
         };
@@ -1029,15 +851,6 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 else passes(std::false_type{});
                 __syncthreads();  // sC is the next tile's staging buffer
             }
-        }
-        if constexpr (CHAIN) {
-            first_unit = false;
-            // this layer's rows are the next layer's A, read back by other waves of this workgroup:
-            // stores complete (workgroup scope: the CU's L1 is shared, write-through) before the barrier
-            __threadfence_block();
-            __syncthreads();
-            if (++jl < p.nchain) continue;  // same row block, next layer
-            jl = 0;
         }
         vt = vt_next;
         tm = tm_next;
@@ -1363,59 +1176,18 @@ __global__ void __launch_bounds__(256) colsum_kernel(int M, int K, const float* 
 
 using namespace cn;
 
-// Kernel variant (benchmarking aid, process-wide): 0 = 2-deep register prefetch
-// when K % 64 == 0 (else 1-deep), 1 = always 1-deep, 2 = BK 16 at 3 workgroups/CU; bf16x6:
-// 0 = 256x128 tiles when K % 64 == 0, 3 = 128x128 tiles only, 4 = 128x128 with a 4-deep prefetch.
-static int g_linear_variant = [] {
-    const char* e = getenv("COPENERF_LINEAR_VARIANT");
-    return e ? atoi(e) : 0;
-}();
-// bf16x6 epilogues that run on the 256x128 one-workgroup-per-CU tile (bit e = cn_epilogue e;
-// benchmarking aid: COPENERF_WIDE_EPIS).  Default: the epilogues that read at most one aux
-// stream (STORE, SOFTPLUS, RELU, MUL, TANGENT).
-static int g_wide_min_k = [] {  // measured: K = 64 launches 3-7 % faster on the 2-per-CU tile
-    const char* e = getenv("COPENERF_WIDE_MINK");
-    return e ? atoi(e) : 128;
-}();
-static int g_stagger = [] {  // benchmarking aid: COPENERF_STAGGER (units of s_sleep 127 = 8128 cycles)
-    const char* e = getenv("COPENERF_STAGGER");
-    return e ? atoi(e) : 0;
-}();
-// bf16x6 epilogues on the 128x256 tile (bit e = cn_epilogue e; benchmarking aid: COPENERF_X6_TALL).
-// Default MUL and TANGENT (one aux stream: -6 / -10 us per C2 layer launch); BWD_SOFTPLUS measured
-// +10-20 us on it, the light epilogues equal.
-static int g_x6_tall = [] {
-    const char* e = getenv("COPENERF_X6_TALL");
-    return e ? (int)strtol(e, nullptr, 0) : 0x18;
-}();
-// bf16x6 epilogues on the 256x256 tile (bit e = cn_epilogue e; COPENERF_X6_SQ): 8 waves of 64x128,
-// 16-deep stages; a workgroup owns whole 256-wide rows (A read and split once) and every staged
-// fragment feeds more MFMAs (0.375 vs 0.5 KiB of LDS reads per MFMA on the 256x128 tile).  Main
-// loop 316-320 vs 374 us at C2's layer shape; with the epilogue (tools/sq_check.py, bitwise equal
-// outputs): SOFTPLUS 445 vs 480-509, STORE 467 vs 491, RELU 385 vs 408-420, MUL / TANGENT 443-451 vs
-// 470 (their aux rows read in the MFMA layout); BWD_RELU 455-463 vs 477-479; BWD_SOFTPLUS 667 vs 614
-// (stays on 128x128); SOFTPLUS_HEAD (round 3) and MUL with a split output too.  Only for 128 < N <= 256: one tile spans every column
-// and takes the direct (MFMA-layout) epilogue, columns >= N masked (zero fill up to nzero).
-static int g_x6_sq = [] {
-    const char* e = getenv("COPENERF_X6_SQ");
-    return e ? (int)strtol(e, nullptr, 0) : 0x15f;  // bit e: epilogue e (SOFTPLUS_HEAD = 8 since round 3)
-}();
-static int g_x6_t2w = [] {  // epilogues on the 128x256 two-per-CU tile (COPENERF_X6_T2W)
-    const char* e = getenv("COPENERF_X6_T2W");
-    return e ? (int)strtol(e, nullptr, 0) : 0;
-}();
-static bool g_sq_nosplit = [] {  // COPENERF_SQ_NOSPLIT=1: MUL with a split output on the 128x256 tile
-    const char* e = getenv("COPENERF_SQ_NOSPLIT");
-    return e && atoi(e) != 0;
-}();
-static int g_x6_sq_min_m = [] {  // smallest M for the 256x256 tile (COPENERF_X6_SQ_MINM)
-    const char* e = getenv("COPENERF_X6_SQ_MINM");
-    return e ? atoi(e) : 0;
-}();
-static int g_wide_epis = [] {
-    const char* e = getenv("COPENERF_WIDE_EPIS");
-    return e ? (int)strtol(e, nullptr, 0) : 0x1f;
-}();
+// The CU count of the current device (cached per device: the launches size their persistent
+// grids from it).
+static int device_cus() {
+    static thread_local int cached_dev = -1, cached_cus = 256;
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && dev != cached_dev) {
+        int v = 0;
+        cached_cus = (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
+        cached_dev = dev;
+    }
+    return cached_cus;
+}
 
 template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int MODE = 0>
 static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_t s) {
@@ -1427,38 +1199,8 @@ static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_
     a.n_tiles_m = cdiv(d->M, BM);
     a.n_tiles_n = cdiv(d->N, BN);
     const int ntiles = cdiv(a.n_tiles_m, 8) * 8 * a.n_tiles_n;
-    static thread_local int cached_dev = -1, cached_cus = 256;  // per-launch attribute query avoided
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) {
-        if (dev != cached_dev) {
-            int v = 0;
-            cached_cus = (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
-            cached_dev = dev;
-        }
-        cus = cached_cus;
-    }
-    const int grid = std::min(ntiles, OCC * cus);  // OCC resident workgroups per CU
+    const int grid = std::min(ntiles, OCC * device_cus());  // OCC resident workgroups per CU
     dim3 block(64 * WM * WN);
-    if (a.emb_x) {  // the fused-encoding first layer: SOFTPLUS or STORE on the 128x128 tiles (host-checked)
-        if constexpr ((WM == 2 && WN == 2 && TM == 2 && TN == 2 && OCC <= 2) ||
-                      (MODE == 2 && WM == 4 && WN == 2 && TM == 2 && TN == 4 && BK == 16)) {
-            if (d->epilogue == CN_EPI_SOFTPLUS)
-                linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, CN_EPI_SOFTPLUS, false, MODE + 4><<<grid, block, 0, s>>>(a);
-            else
-                linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, CN_EPI_STORE, false, MODE + 4><<<grid, block, 0, s>>>(a);
-            return check_launch("cn_linear");
-        }
-        set_error("cn_linear: no fused-encoding kernel for this tile");
-        return CN_ERR_UNSUPPORTED;
-    }
-    if (a.mask_out) {  // RELU + sign bits: the 256x256 tile's direct epilogue only (host-checked)
-        if constexpr (MODE == 2 && TM * TN >= 8 && OCC == 1 && BK == 16) {
-            linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, kEpiReluMask, false, MODE><<<grid, block, 0, s>>>(a);
-            return check_launch("cn_linear");
-        }
-        set_error("cn_linear: out_mask needs the bf16x6 256x256 tile");
-        return CN_ERR_UNSUPPORTED;
-    }
     switch (d->epilogue) {
 #define CN_EPI_CASE(E)                                                                     \
         case E:                                                                            \
@@ -1474,7 +1216,6 @@ static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_
         CN_EPI_CASE(CN_EPI_BWD_RELU)
         CN_EPI_CASE(CN_EPI_SOFTPLUS_HEAD)
 #undef CN_EPI_CASE
-        case 7: linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, 7, false, MODE><<<grid, block, 0, s>>>(a); break;
         default: set_error("cn_linear: bad epilogue %d", d->epilogue); return CN_ERR_ARG;
     }
     return check_launch("cn_linear");
@@ -1484,9 +1225,20 @@ static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_
 // The kernel instance cn_linear launches for a descriptor: ONE function decides it, for the
 // launch and for cn_linear_kernel_name (a profiler's name of the launch), so the two cannot
 // disagree.  X-macro rows: (tile, WM, WN, TM, TN, BK, OCC, DEPTH, MODE).
-enum LinearTile { LT_BF_T0, LT_BF_T1, LT_X6_SQ, LT_X6_TALL, LT_X6_WIDE, LT_X6_T128, LT_X6_T1, LT_X6_T2W, LT_F_V2, LT_F_T0_D2,
+//   bf16x6 tiles (measured at C2's layer shape, M = 524,288, N = K = 256):
+//   * SQ 256x256, 8 waves of 64x128, 1 / CU, 16-deep stages: whole 256-wide rows per workgroup (A
+//     read and split once), direct epilogues (STORE / SOFTPLUS / RELU / MUL incl. the split output /
+//     TANGENT / BWD_RELU / SOFTPLUS_HEAD) for 128 < N <= 256, K >= 128.  Main loop 316-320 us vs 374
+//     on 256x128; SOFTPLUS 445 vs 480-509, RELU 385 vs 408-420, MUL / TANGENT 443-451 vs 470.
+//   * TALL 128x256 (1 / CU): SOFTPLUS_HEAD / MUL / TANGENT where SQ does not apply.
+//   * WIDE 256x128 (1 / CU, 32-deep): STORE / SOFTPLUS / RELU / MUL / TANGENT at K % 64 == 0.
+//   * T128 128x128 (2 / CU): BWD_SOFTPLUS (its three aux streams need the partner workgroup's main
+//     loop to hide: 614 vs 667 us on SQ), first layers (K < 128), edge shapes.
+//   bf16 (config C3) tiles: SQ 256x256 (1 / CU, 32-deep) for 128 < N <= 256, else 128x128 / 128x64.
+enum LinearTile { LT_BF_SQ, LT_BF_T0, LT_BF_T1, LT_X6_SQ, LT_X6_TALL, LT_X6_WIDE, LT_X6_T128, LT_X6_T1, LT_F_T0_D2,
                   LT_F_T0_D1, LT_F_T1_D2, LT_F_T1_D1 };
 #define CN_LINEAR_TILES(X)                 \
+    X(LT_BF_SQ, 4, 2, 2, 4, 32, 1, 2, 1)   \
     X(LT_BF_T0, 2, 2, 2, 2, 64, 2, 1, 1)   \
     X(LT_BF_T1, 4, 1, 1, 2, 64, 2, 1, 1)   \
     X(LT_X6_SQ, 4, 2, 2, 4, 16, 1, 2, 2)   \
@@ -1494,116 +1246,70 @@ enum LinearTile { LT_BF_T0, LT_BF_T1, LT_X6_SQ, LT_X6_TALL, LT_X6_WIDE, LT_X6_T1
     X(LT_X6_WIDE, 4, 2, 2, 2, 32, 1, 2, 2) \
     X(LT_X6_T128, 2, 2, 2, 2, 16, 2, 2, 2) \
     X(LT_X6_T1, 4, 1, 1, 2, 16, 2, 2, 2)   \
-    X(LT_X6_T2W, 2, 2, 2, 4, 16, 2, 2, 2)  \
-    X(LT_F_V2, 2, 2, 2, 2, 16, 3, 2, 0)    \
     X(LT_F_T0_D2, 2, 2, 2, 2, 32, 2, 2, 0) \
     X(LT_F_T0_D1, 2, 2, 2, 2, 32, 2, 1, 0) \
     X(LT_F_T1_D2, 4, 1, 1, 2, 32, 2, 2, 0) \
     X(LT_F_T1_D1, 4, 1, 1, 2, 32, 2, 1, 0)
 
 static LinearTile choose_linear_tile(const cn_linear_desc* d) {
-    const bool head = d->epilogue == CN_EPI_SOFTPLUS_HEAD;
-    if (d->mfma_dtype == CN_MFMA_BF16) return d->tile == 0 ? LT_BF_T0 : LT_BF_T1;
-    if (d->emb_x) {  // the fused-encoding first layer (K <= 64): the 2-per-CU 128x128 tiles
-        // (COPENERF_EMB_SQ=1: the 256x256 tile, every row encoded once instead of per N-tile)
-        static const bool emb_sq = [] {
-            const char* e = getenv("COPENERF_EMB_SQ");
-            return e && atoi(e) != 0;
-        }();
-        if (d->mfma_dtype == CN_MFMA_F32_BF16X6) return emb_sq && d->N > 128 && d->N <= 256 ? LT_X6_SQ : LT_X6_T128;
-        return (d->K % 64) == 0 && g_linear_variant == 0 ? LT_F_T0_D2 : LT_F_T0_D1;
+    const int e = d->epilogue;
+    const bool head = e == CN_EPI_SOFTPLUS_HEAD;
+    // one tile spans every column (the 64x128 wave tiles' direct epilogues), no rank-1 term
+    const bool wide_n = d->tile == 0 && d->N > 128 && d->N <= 256 && !d->rowv;
+    const bool longk = d->K >= 128;  // a first layer's two-chunk main loop cannot hide a 1 / CU epilogue
+    if (d->mfma_dtype == CN_MFMA_BF16) {
+        if (wide_n && (longk || head)) return LT_BF_SQ;
+        return d->tile == 1 ? LT_BF_T1 : LT_BF_T0;
     }
     if (d->mfma_dtype == CN_MFMA_F32_BF16X6) {
-        // K % 64 == 0, STORE / SOFTPLUS / RELU: 256x128 tiles of 8 waves, one workgroup per CU,
-        // 32-deep stages (whole 128-byte A row segments per load, half the barriers per K; main
-        // loop 366 vs 385 us at C2's layer shape); else 128x128 tiles of 16-deep chunks (K % 32
-        // == 0: an even number of chunks for the 2-deep prefetch)
-        if (d->tile != 0) return LT_X6_T1;
-        // (the wide tile only for the light epilogues: with one workgroup per CU an aux-reading
-        // epilogue no longer overlaps a partner workgroup's main loop, measured slower)
-        const bool light = (g_wide_epis >> d->epilogue) & 1;
-        // 128x256 ("tall-N") tiles: one workgroup owns whole 256-wide output rows, so A is
-        // read from HBM once (the two N-tiles of the 256x128 tiling re-fetch 30-50 % of it,
-        // PMC) and split once per row
-        const bool tall = ((g_x6_tall >> d->epilogue) & 1) || (head && d->N > 128);
-        // short K (a first layer): the main loop is two chunks, so the one-workgroup-per-CU tiles
-        // cannot hide their epilogue; the 2-per-CU 128x128 tile overlaps it with the partner's
-        // (COPENERF_WIDE_MINK: the smallest K for the 1-per-CU tiles)
-        const bool longk = d->K >= g_wide_min_k;
-        // (the epilogues with a direct form: STORE, SOFTPLUS, RELU, MUL, TANGENT, BWD_SOFTPLUS, BWD_RELU)
-        // (MUL with a split output too: the direct epilogue writes the split columns raw)
-        const bool sq = (g_x6_sq >> d->epilogue & 1) && d->N > 128 && d->N <= 256 && !d->rowv &&
-                        d->M >= g_x6_sq_min_m && !(g_sq_nosplit && d->epilogue == CN_EPI_MUL && d->out_split &&
-                                                   d->nsplit < d->N);
-        if (d->K % 32 == 0 && sq && d->ldb >= 256 && g_linear_variant == 0 && (longk || head)) return LT_X6_SQ;
-        // 128x256, two per CU (single-buffered B): the epilogues with aux streams whose partner-workgroup
-        // overlap matters (COPENERF_X6_T2W: bit e = epilogue e)
-        if ((g_x6_t2w >> d->epilogue & 1) && d->K % 32 == 0 && d->N > 128 && d->N <= 256 && !d->rowv &&
-            d->ldb >= 256 && g_linear_variant == 0 && !(d->epilogue == CN_EPI_MUL && d->out_split && d->nsplit < d->N))
-            return LT_X6_T2W;
-        if (d->K % 64 == 0 && tall && d->N > 128 && d->ldb >= 256 && g_linear_variant == 0 && (longk || head))
-            return LT_X6_TALL;
-        if (d->K % 64 == 0 && g_linear_variant == 0 && light && longk) return LT_X6_WIDE;
+        if (d->tile == 1) return LT_X6_T1;
+        if (d->tile == 2) return LT_X6_T128;
+        if (wide_n && d->K % 32 == 0 && d->ldb >= 256 && e != CN_EPI_BWD_SOFTPLUS && (longk || head)) return LT_X6_SQ;
+        const bool tall = e == CN_EPI_MUL || e == CN_EPI_TANGENT || head;
+        if (d->K % 64 == 0 && tall && d->N > 128 && d->ldb >= 256 && (longk || head)) return LT_X6_TALL;
+        // (an aux-reading epilogue with one workgroup per CU no longer overlaps a partner's main loop)
+        const bool light = e == CN_EPI_STORE || e == CN_EPI_SOFTPLUS || e == CN_EPI_RELU || e == CN_EPI_MUL ||
+                           e == CN_EPI_TANGENT;
+        if (d->K % 64 == 0 && light && longk) return LT_X6_WIDE;
         return LT_X6_T128;
     }
     const bool even = (d->K % 64) == 0;  // DEPTH-2 prefetch consumes K in pairs of 32-chunks
-    if (d->tile == 0) {
-        if (g_linear_variant == 2) return LT_F_V2;
-        return even && g_linear_variant == 0 ? LT_F_T0_D2 : LT_F_T0_D1;
-    }
-    return even && g_linear_variant == 0 ? LT_F_T1_D2 : LT_F_T1_D1;
+    if (d->tile == 1) return even ? LT_F_T1_D2 : LT_F_T1_D1;
+    return even ? LT_F_T0_D2 : LT_F_T0_D1;
 }
 
 // Validates a descriptor and builds its kernel arguments (a.M == 0: nothing to launch).
 static int linear_plan(const cn_linear_desc* d, LinearArgs& a) {
     CN_REQUIRE(d, CN_ERR_ARG, "cn_linear: null desc");
     const bool head = d->epilogue == CN_EPI_SOFTPLUS_HEAD;
-    const bool emb = d->emb_x != nullptr;
-    if (emb) {
-        CN_REQUIRE(!d->A && !d->A2 && !d->rowv && d->tile == 0 &&
-                       (d->epilogue == CN_EPI_SOFTPLUS || d->epilogue == CN_EPI_STORE),
-                   CN_ERR_ARG, "cn_linear: emb_x replaces A (no A / A2 / rowv, tile 0, SOFTPLUS or STORE)");
-        CN_REQUIRE(d->emb_multires >= 0 && d->emb_multires < 16 && 4 * (1 + 2 * d->emb_multires) <= d->K && d->K <= 64,
-                   CN_ERR_SHAPE, "cn_linear: emb_multires=%d does not fit K=%d (<= 64)", d->emb_multires, d->K);
-        CN_REQUIRE(al16(d->emb_x) && d->ld_emb_x % 4 == 0 && d->ld_emb_x >= 4 && d->ld_emb_x < (1 << 20) &&
-                       (!d->emb_u0 || (al16(d->emb_u0) && d->ld_emb_u0 % 4 == 0 && d->ld_emb_u0 >= d->K && d->ld_emb_u0 < (1 << 20))) &&
-                       (!d->emb_u4 || (al16(d->emb_u4) && d->ld_emb_u4 % 4 == 0 && d->ld_emb_u4 < (1 << 20))),
-                   CN_ERR_ALIGN, "cn_linear: emb_x / emb_u0 / emb_u4 alignment or leading dimensions");
-    }
-    CN_REQUIRE((d->A || emb) && d->B && (d->out0 || head), CN_ERR_ARG, "cn_linear: A, B and out0 are required");
+    CN_REQUIRE(d->A && d->B && (d->out0 || d->out0_b || head), CN_ERR_ARG, "cn_linear: A, B and out0 (or out0_b) are required");
     CN_REQUIRE(d->M >= 0 && d->N > 0 && d->K > 0, CN_ERR_SHAPE, "cn_linear: bad M/N/K %d/%d/%d", d->M, d->N, d->K);
     CN_REQUIRE(d->mfma_dtype == CN_MFMA_F32 || d->mfma_dtype == CN_MFMA_BF16 || d->mfma_dtype == CN_MFMA_F32_BF16X6,
                CN_ERR_ARG, "cn_linear: bad mfma_dtype %d", d->mfma_dtype);
     const bool bf = d->mfma_dtype == CN_MFMA_BF16;
     const bool x6 = d->mfma_dtype == CN_MFMA_F32_BF16X6;
     CN_REQUIRE(d->K % (bf ? 64 : 32) == 0, CN_ERR_SHAPE, "cn_linear: K=%d must be a multiple of %d", d->K, bf ? 64 : 32);
-    CN_REQUIRE(d->tile == 0 || d->tile == 1, CN_ERR_ARG, "cn_linear: bad tile %d", d->tile);
+    CN_REQUIRE(d->tile >= 0 && d->tile <= 2, CN_ERR_ARG, "cn_linear: bad tile %d", d->tile);
+    CN_REQUIRE(!d->a_bf16 && !d->aux0_bf16 && !d->out0_b && !d->out1_b, CN_ERR_UNSUPPORTED,
+               "cn_linear: bf16 operand images are not built yet");
     const int K1 = d->A2 ? d->K1 : d->K;
     CN_REQUIRE(K1 > 0 && K1 <= d->K && K1 % (bf ? 64 : 32) == 0, CN_ERR_SHAPE, "cn_linear: bad K1=%d", K1);
-    CN_REQUIRE(emb || (d->lda >= K1 && d->lda % 4 == 0 && al16(d->A)), CN_ERR_ALIGN,
+    CN_REQUIRE(d->lda >= K1 && d->lda % 4 == 0 && al16(d->A), CN_ERR_ALIGN,
                "cn_linear: A must be 16B aligned with lda>=K1, lda%%4==0");
     if (d->A2) CN_REQUIRE(d->lda2 >= d->K - K1 && d->lda2 % 4 == 0 && al16(d->A2), CN_ERR_ALIGN, "cn_linear: bad A2/lda2");
+    const int bn = d->tile == 1 ? 64 : 128;
     if (x6)  // ldb = rows of the chunk-major term image
-        CN_REQUIRE(d->ldb >= cdiv(d->N, d->tile == 0 ? 128 : 64) * (d->tile == 0 ? 128 : 64) && al16(d->B), CN_ERR_ALIGN,
+        CN_REQUIRE(d->ldb >= cdiv(d->N, bn) * bn && al16(d->B), CN_ERR_ALIGN,
                    "cn_linear: bf16x6 B image rows (ldb=%lld) must cover the N tiles", (long long)d->ldb);
     else
         CN_REQUIRE(d->ldb >= d->K && d->ldb % (bf ? 8 : 4) == 0 && al16(d->B), CN_ERR_ALIGN, "cn_linear: bad B/ldb");
     const int nzero = std::max(d->nzero, d->N);
-    const int bn = d->tile == 0 ? 128 : 64;
     CN_REQUIRE(nzero <= cdiv(d->N, bn) * bn, CN_ERR_SHAPE,
                "cn_linear: nzero=%d beyond the column tiles covering N=%d (tile width %d)", nzero, d->N, bn);
     CN_REQUIRE(!d->out0 || d->ld_out0 >= nzero, CN_ERR_SHAPE, "cn_linear: ld_out0=%lld < nzero=%d",
                (long long)d->ld_out0, nzero);
     const int e = d->epilogue;
-    if (d->out_mask || d->aux_mask) {  // sign bits: RELU writes them, BWD_RELU reads them (256x256 tile only)
-        CN_REQUIRE((d->out_mask ? e == CN_EPI_RELU : e == CN_EPI_BWD_RELU) && !(d->out_mask && d->aux_mask) &&
-                       choose_linear_tile(d) == LT_X6_SQ,
-                   CN_ERR_UNSUPPORTED, "cn_linear: out_mask (RELU) / aux_mask (BWD_RELU) need the bf16x6 256x256 tile");
-        CN_REQUIRE(al16(d->out_mask ? (const void*)d->out_mask : (const void*)d->aux_mask) &&
-                       d->ld_mask >= (d->N + 31) / 32 && d->ld_mask < (1 << 20),
-                   CN_ERR_ALIGN, "cn_linear: mask rows need ld_mask >= ceil(N / 32) words");
-    }
-    if (e == CN_EPI_MUL || e == CN_EPI_TANGENT || e == CN_EPI_BWD_SOFTPLUS || (e == CN_EPI_BWD_RELU && !d->aux_mask))
+    if (e == CN_EPI_MUL || e == CN_EPI_TANGENT || e == CN_EPI_BWD_SOFTPLUS || e == CN_EPI_BWD_RELU)
         CN_REQUIRE(d->aux0 && d->ld_aux0 >= d->N, CN_ERR_ARG, "cn_linear: epilogue %d needs aux0", e);
     if (e == CN_EPI_MUL || e == CN_EPI_TANGENT || e == CN_EPI_BWD_SOFTPLUS)
         CN_REQUIRE(d->aux_beta > 0.0f, CN_ERR_ARG, "cn_linear: epilogue %d needs aux_beta > 0 (sigma from aux0)", e);
@@ -1647,20 +1353,16 @@ static int linear_plan(const cn_linear_desc* d, LinearArgs& a) {
                    d->ld_out0 < kMaxLd && d->ld_out1 < kMaxLd && d->ld_split < kMaxLd,
                CN_ERR_SHAPE, "cn_linear: leading dimensions must be < 2^20");
     a = LinearArgs{};
-    a.A = d->A; a.A2 = d->A2; a.B = d->B; a.bias = d->bias; a.rowv = d->rowv; a.colv = d->colv;
-    a.aux0 = d->aux0; a.aux1 = d->aux1; a.aux2 = d->aux2; a.out0 = d->out0; a.out1 = d->out1; a.out_split = d->out_split;
+    a.A = static_cast<const float*>(d->A); a.A2 = static_cast<const float*>(d->A2); a.B = d->B;
+    a.bias = d->bias; a.rowv = d->rowv; a.colv = d->colv;
+    a.aux0 = static_cast<const float*>(d->aux0); a.aux1 = d->aux1; a.aux2 = d->aux2;
+    a.out0 = d->out0; a.out1 = d->out1; a.out_split = d->out_split;
     a.lda = (int)d->lda; a.lda2 = (int)d->lda2; a.ldb = (int)d->ldb;
     a.ld_aux0 = (int)d->ld_aux0; a.ld_aux1 = (int)d->ld_aux1; a.ld_aux2 = (int)d->ld_aux2;
     a.aux_c = -d->aux_beta * 1.44269504088896341f;
     a.aux2_scale = d->aux2_scale;
-    a.stagger = g_stagger;
     a.head_w = d->head_w; a.head_b = d->head_b; a.head_out = d->head_out; a.head_idx = d->head_idx;
     a.flags = d->flags;
-    a.emb_x = d->emb_x; a.emb_u0 = d->emb_u0; a.emb_u4 = d->emb_u4;
-    a.ld_emb_x = (int)d->ld_emb_x; a.ld_emb_u0 = (int)d->ld_emb_u0; a.ld_emb_u4 = (int)d->ld_emb_u4;
-    a.emb_L = d->emb_multires;
-    a.emb_scale = d->emb_scale;
-    a.emb_u4_div = d->emb_u4_div == 0.0f ? 1.0f : d->emb_u4_div;
     a.ld_out0 = (int)d->ld_out0; a.ld_out1 = (int)d->ld_out1; a.ld_split = (int)d->ld_split;
     a.M = d->M; a.N = d->N; a.K = d->K; a.K1 = K1; a.nzero = nzero;
     a.nsplit = (e == CN_EPI_MUL && d->out_split) ? d->nsplit : d->N;
@@ -1670,9 +1372,6 @@ static int linear_plan(const cn_linear_desc* d, LinearArgs& a) {
     a.inv_odiv = 1.0f / odiv;
     a.beta = d->beta;
     a.threshold = d->threshold;
-    a.mask_out = reinterpret_cast<unsigned*>(d->out_mask);
-    a.mask_in = reinterpret_cast<const unsigned*>(d->aux_mask);
-    a.ld_mask = (int)d->ld_mask;
     return CN_OK;
 }
 
@@ -1691,62 +1390,16 @@ extern "C" int cn_linear(const cn_linear_desc* d, cn_stream_t stream) {
     return CN_ERR_UNSUPPORTED;
 }
 
-// A chain of SOFTPLUS layers (the SDF's hidden layers 1..6, neus_fields.py:273-282) in one launch of the
-// 256x256 bf16x6 tile: each workgroup takes a 256-row block through every layer (layer j's A = layer j-1's
-// out0), so the chain's A operands come back from L2 / the memory-side cache and the launches' boundaries
-// go.  Every descriptor must be a valid cn_linear on that tile with the same M, K, leading dimensions and
-// tile order; outputs / biases / weights / N / nzero / odiv may differ per layer.
-extern "C" int cn_linear_chain(const cn_linear_desc* descs, int32_t n, cn_stream_t stream) {
-    CN_REQUIRE(descs && n >= 1 && n <= kChainMax, CN_ERR_ARG, "cn_linear_chain: %d layers (1..%d)", n, kChainMax);
-    LinearArgs a;
-    int rc = linear_plan(descs, a);
-    if (rc) return rc;
-    for (int j = 0; j < n; ++j) {
-        const cn_linear_desc* d = descs + j;
-        LinearArgs t;
-        rc = j ? linear_plan(d, t) : CN_OK;
-        if (rc) return rc;
-        CN_REQUIRE(d->epilogue == CN_EPI_SOFTPLUS && d->mfma_dtype == CN_MFMA_F32_BF16X6 && !d->A2 && !d->rowv &&
-                       !d->emb_x && choose_linear_tile(d) == LT_X6_SQ,
-                   CN_ERR_UNSUPPORTED, "cn_linear_chain: layer %d is not a bf16x6 SOFTPLUS on the 256x256 tile", j);
-        CN_REQUIRE(d->M == descs->M && d->K == descs->K && d->lda == descs->lda && d->ld_out0 == descs->lda &&
-                       d->ldb == descs->ldb && d->flags == descs->flags && d->beta == descs->beta &&
-                       d->threshold == descs->threshold && (d->adiv == descs->adiv) &&
-                       (j == 0 || d->A == descs[j - 1].out0),
-                   CN_ERR_ARG, "cn_linear_chain: layer %d does not continue the chain (A = the previous out0, same M, "
-                   "K, lda = ld_out0, ldb, flags, softplus)", j);
-        const float odiv = d->odiv == 0.0f ? 1.0f : d->odiv;
-        a.chain[j] = ChainLayer{d->B, d->bias, d->out0, d->N, std::max(d->nzero, d->N), 1.0f / odiv};
-    }
-    a.nchain = n;
-    if (descs->M == 0) return CN_OK;
-    hipStream_t s = (hipStream_t)stream;
-    a.n_tiles_m = cdiv(descs->M, 256);
-    a.n_tiles_n = 1;
-    const int ntiles = cdiv(a.n_tiles_m, 8) * 8;
-    static thread_local int cached_dev = -1, cached_cus = 256;
-    int dev = 0;
-    if (hipGetDevice(&dev) == hipSuccess && dev != cached_dev) {
-        int v = 0;
-        cached_cus = (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
-        cached_dev = dev;
-    }
-    const int grid = std::min(ntiles, cached_cus);
-    linear_kernel<4, 2, 2, 4, 16, 1, 2, CN_EPI_SOFTPLUS, false, 2 + 8><<<grid, 512, 0, s>>>(a);
-    return check_launch("cn_linear_chain");
-}
-
 extern "C" int cn_linear_kernel_name(const cn_linear_desc* d, char* buf, int32_t len) {
     CN_REQUIRE(d && buf && len > 0, CN_ERR_ARG, "cn_linear_kernel_name: null desc / buffer");
     const char* args = "";
+    int mode = 0;
     switch (choose_linear_tile(d)) {
 #define CN_TILE_NAME(T, WM, WN, TM, TN, BK, OCC, DEPTH, MODE) \
-        case T: args = #WM ", " #WN ", " #TM ", " #TN ", " #BK ", " #OCC ", " #DEPTH; break;
+        case T: args = #WM ", " #WN ", " #TM ", " #TN ", " #BK ", " #OCC ", " #DEPTH; mode = MODE; break;
         CN_LINEAR_TILES(CN_TILE_NAME)
 #undef CN_TILE_NAME
     }
-    const int mode = (d->mfma_dtype == CN_MFMA_F32_BF16X6 ? 2 : d->mfma_dtype == CN_MFMA_BF16 ? 1 : 0) +
-                     (d->emb_x ? 4 : 0);  // (MODE + 4: the fused-encoding first layer)
     const int n = snprintf(buf, (size_t)len, "void cn::linear_kernel<%s, %d, %s, %d>(cn::LinearArgs)", args,
                            d->epilogue, d->rowv ? "true" : "false", mode);
     CN_REQUIRE(n < len, CN_ERR_SHAPE, "cn_linear_kernel_name: buffer of %d bytes too small (%d)", len, n + 1);

@@ -8,12 +8,6 @@
 #include <cstdlib>
 #include <type_traits>
 
-#ifndef WGRAD_EXP
-#define WGRAD_EXP 0  // benchmark-only ablations (1: L2-resident operands)
-#endif
-#ifndef WGRAD_SGB
-#define WGRAD_SGB 1  // sched_barrier segments of the stage-ring weight gradient (0: compiler's own order)
-#endif
 
 namespace cn {
 
@@ -390,13 +384,8 @@ __global__ void __launch_bounds__(128 * WM, 2) wgrad_x6_kernel(WgradArgs p) {
         const int ly = pair ? p.ldy1 : p.ldy0;
         const int lx = pair ? p.ldx1 : p.ldx0;
         const int nrows = min(MC, mend - mrow);
-#if WGRAD_EXP == 1  // benchmark only: every chunk reads rows [0, 4096) (L2-resident operands)
-        const int mr = mrow & 4095;
-#else
-        const int mr = mrow;
-#endif
-        const rsrc_t vY = make_view(Y + (int64_t)mr * ly + n0, (nrows * ly - n0) * 4);
-        const rsrc_t vX = make_view(X + (int64_t)mr * lx + k0, (nrows * lx - k0) * 4);
+        const rsrc_t vY = make_view(Y + (int64_t)mrow * ly + n0, (nrows * ly - n0) * 4);
+        const rsrc_t vX = make_view(X + (int64_t)mrow * lx + k0, (nrows * lx - k0) * 4);
 #pragma unroll
         for (int r = 0; r < 4; ++r) ry[r] = bload4(vY, ((mq * 4 + r) * ly + cg * 4) * 4, 0);
         if (XT == NT || tid < XT) {
@@ -507,10 +496,10 @@ __global__ void __launch_bounds__(128 * WM, 2) wgrad_x6_kernel(WgradArgs p) {
 // tools/probes/mfma_bf16_valu_probe.hip; sched_group_barrier patterns were not followed).
 // Waves 0-3 stage Y, waves 4-7 stage X (thread: m-quad t % 4 of column group t / 4,
 // t = tid % 256).  v_mfma_f32_32x32x16_bf16, 2x4 accumulators of 32x32 per wave (64 n x
-// 128 k).  Measured against wgrad_x6_kernel<4, 4> (tools/wgrad_ab.sh): 767-772 vs 790-794
-// us per 2-pair C2-shape call on random data, 641-644 vs 666-676 with L2-resident operands
-// (WGRAD_EXP=1: the kernel is not HBM-bound); 16x16x32 MFMAs (higher clock, more cycles)
-// and a register-held split of the next 32-row chunk measured equal to the old kernel.
+// 128 k).  Measured (round 3) against the 32-row one-buffer form of wgrad_x6_kernel<4, 4>:
+// 767-772 vs 790-794 us per 2-pair C2-shape call on random data, 641-644 vs 666-676 with
+// L2-resident operands (the kernel is not HBM-bound); 16x16x32 MFMAs (higher clock, more
+// cycles) and a register-held split of the next 32-row chunk measured equal to the old kernel.
 template <int NRAW>
 __global__ void __launch_bounds__(512, 2) wgrad_x6r_kernel(WgradBatch batch) {
     constexpr int BNo = 256, MC = 16, PL = 8, LSB = 3 * PL + 4;  // 28 dwords per LDS row
@@ -554,13 +543,8 @@ __global__ void __launch_bounds__(512, 2) wgrad_x6r_kernel(WgradBatch batch) {
         const float* src = sx ? (pair ? p.X1 : p.X0) : (pair ? p.Y1 : p.Y0);
         const int ld = sx ? (pair ? p.ldx1 : p.ldx0) : (pair ? p.ldy1 : p.ldy0);
         const int nrows = valid ? min(MC, mend - mrow) : 0;
-#if WGRAD_EXP == 1
-        const int mr = mrow & 4095;
-#else
-        const int mr = mrow;
-#endif
         const int col0 = sx ? k0 : n0;
-        const rsrc_t v = make_view(src + (int64_t)mr * ld + col0, (nrows * ld - col0) * 4);
+        const rsrc_t v = make_view(src + (int64_t)mrow * ld + col0, (nrows * ld - col0) * 4);
 #pragma unroll
         for (int r = 0; r < 4; ++r) r4[r] = bload4(v, ((mq * 4 + r) * ld + cg * 4) * 4, 0);
     };
@@ -618,9 +602,7 @@ __global__ void __launch_bounds__(512, 2) wgrad_x6r_kernel(WgradBatch batch) {
                 for (int i = 0; i < 2; ++i)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[TA[u]][i], bj[j & 1][TB[u]], acc[i][j], 0, 0, 0);
             side(j);
-#if WGRAD_SGB
             __builtin_amdgcn_sched_barrier(0);
-#endif
         }
     };
 
@@ -761,9 +743,7 @@ __global__ void __launch_bounds__(512, 4) wgrad_x6n_kernel(WgradArgs p) {  // 2 
                 acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[TA[u]], bj[TB[u]], acc[j], 0, 0, 0);
             side(2 * j);
             side(2 * j + 1);
-#if WGRAD_SGB
             __builtin_amdgcn_sched_barrier(0);
-#endif
         }
     };
     const bool ybias = do_bias & sy;
@@ -908,29 +888,15 @@ int launch_slab_reduce(const float* part, int nslab, int64_t stride, int rows, i
 
 // ---------------------------------------------------------------------------
 // tile 0: 128x128 output tiles, 1: 128x64, 2 (bf16x6, operand rows at least 256-padded):
-// 256x256 tiles of 512-thread workgroups, one per CU (half the workgroup target).  Padding
-// columns of Y / X only feed output rows / columns past n_out / k_out, which the slab
-// reduction never reads.
-static bool wgrad_wide_on() {
-    static const bool on = [] {  // benchmarking aid: COPENERF_WGRAD_WIDE=0 keeps the 128x128 tiles
-        const char* e = getenv("COPENERF_WGRAD_WIDE");
-        return e ? atoi(e) != 0 : true;
-    }();
-    return on;
-}
-// 3 (bf16x6, K <= 64, Y rows 256-padded): 256x64 tiles of 512-thread workgroups on the stage ring
-// (wgrad_x6n_kernel; COPENERF_WGRAD_NARROW=0: the 128x64 tiles of wgrad_x6_kernel<2, 1>).
+// 256x256 tiles of 512-thread workgroups on the stage ring, one per CU, 3 (bf16x6, K <= 64, Y
+// rows 256-padded): 256x64 tiles on the narrow stage ring.  Padding columns of Y / X only feed
+// output rows / columns past n_out / k_out, which the slab reduction never reads.
 // Returns the wide mode: 0 none, 1 = 256x256, 2 = 256x64.
 static int wgrad_wide(const cn_wgrad_desc* d) {
-    static const bool narrow = [] {  // COPENERF_WGRAD_NARROW=0: the 128x64 tiles for K <= 64
-        const char* e = getenv("COPENERF_WGRAD_NARROW");
-        return e ? atoi(e) != 0 : true;
-    }();
     const int64_t np = (int64_t)cdiv(d->N, 256) * 256, kp = (int64_t)cdiv(d->K, 256) * 256;
-    if (!wgrad_wide_on() || d->mfma_dtype != CN_MFMA_F32_BF16X6 || d->ldy0 < np || (d->npairs == 2 && d->ldy1 < np))
-        return 0;
+    if (d->mfma_dtype != CN_MFMA_F32_BF16X6 || d->ldy0 < np || (d->npairs == 2 && d->ldy1 < np)) return 0;
     if (d->ldx0 >= kp && (d->npairs == 1 || d->ldx1 >= kp)) return 1;
-    return narrow && d->K <= 64 ? 2 : 0;
+    return d->K <= 64 ? 2 : 0;
 }
 
 // budget: workgroups this weight gradient may use (< 0: the default target; cn_wgrad_batch hands
@@ -943,11 +909,8 @@ static void wgrad_geometry(int M, int N, int K, int wide, int* tile, int* Npad, 
     *Npad = cdiv(N, BNo) * BNo;
     *Kpad = cdiv(K, BKo) * BKo;
     const int tiles = (*Npad / BNo) * (*Kpad / BKo);
-    static const int kTarget = [] {  // workgroups per cn_wgrad (benchmarking aid: COPENERF_WGRAD_BLOCKS)
-        const char* e = getenv("COPENERF_WGRAD_BLOCKS");
-        return e ? atoi(e) : 512;
-    }();
-    const int target = budget >= 0 ? budget : (t == 2 ? kTarget / 2 : kTarget);  // (t 2: 1 workgroup per CU)
+    constexpr int kTarget = 512;  // workgroups per cn_wgrad (two per CU; the 256x256 tiles one per CU)
+    const int target = budget >= 0 ? budget : (t == 2 ? kTarget / 2 : kTarget);
     int ns = std::max(1, target / tiles);
     ns = std::min(ns, std::max(1, cdiv(M, 512)));
     int rps = cdiv(cdiv(M, ns), 64) * 64;  // whole 32-row (fp32) / 64-row (bf16) chunks
@@ -956,14 +919,22 @@ static void wgrad_geometry(int M, int N, int K, int wide, int* tile, int* Npad, 
     *rows_per_slice = rps;
 }
 
+// The CU count of the current device, cached per device (the batch's slice layout -- and so the
+// fixed summation order of dW -- follows it).
+static int wgrad_device_cus() {
+    static thread_local int cached_dev = -1, cached_cus = 256;
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && dev != cached_dev) {
+        int v = 0;
+        cached_cus = (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
+        cached_dev = dev;
+    }
+    return cached_cus;
+}
+
 }  // namespace cn
 
 using namespace cn;
-
-static const int g_wgrad_variant = [] {  // benchmarking aid: COPENERF_WGRAD_KERNEL=1 (32-row kernel)
-    const char* e = getenv("COPENERF_WGRAD_KERNEL");
-    return e ? atoi(e) : 0;
-}();
 
 // The split-M kernel cn_wgrad launches for a descriptor (its fixed-order slab reduction,
 // cn::slab_reduce_kernel, follows it), decided by the same geometry as the launch.
@@ -973,23 +944,23 @@ extern "C" int cn_wgrad_kernel_name(const cn_wgrad_desc* d, char* buf, int32_t l
     wgrad_geometry(std::max(d->M, 1), d->N, d->K, wgrad_wide(d), &tile, &Npad, &Kpad, &ns, &rps);
     const char* k = "";
     if (d->mfma_dtype == CN_MFMA_F32_BF16X6)
-        k = tile == 2 ? (g_wgrad_variant == 1 ? "wgrad_x6_kernel<4, 4>" : "wgrad_x6r_kernel<2>")
-            : tile == 3 ? "wgrad_x6n_kernel<3>" : tile == 0 ? "wgrad_x6_kernel<2, 2>" : "wgrad_x6_kernel<2, 1>";
+        k = tile == 2 ? "wgrad_x6r_kernel<2>" : tile == 3 ? "wgrad_x6n_kernel<3>" : tile == 0 ? "wgrad_x6_kernel<2, 2>"
+                                                                                       : "wgrad_x6_kernel<2, 1>";
     else if (d->mfma_dtype == CN_MFMA_BF16)
         k = tile == 0 ? "wgrad_bf16_kernel<2, 2, 2, 2>" : "wgrad_bf16_kernel<2, 2, 2, 1>";
     else
         k = tile == 0 ? "wgrad_kernel<2, 2, 2, 2>" : "wgrad_kernel<2, 2, 2, 1>";
-    const bool ring = d->mfma_dtype == CN_MFMA_F32_BF16X6 && tile == 2 && g_wgrad_variant != 1;
+    const bool ring = d->mfma_dtype == CN_MFMA_F32_BF16X6 && tile == 2;
     const int n = snprintf(buf, (size_t)len, "void cn::%s(cn::%s)", k, ring ? "WgradBatch" : "WgradArgs");
     CN_REQUIRE(n < len, CN_ERR_SHAPE, "cn_wgrad_kernel_name: buffer of %d bytes too small (%d)", len, n + 1);
     return n;
 }
 
 extern "C" size_t cn_wgrad_workspace_bytes(int32_t M, int32_t N, int32_t K) {
-    size_t need = 0;  // the larger of the two tilings (the call's mfma_dtype picks one)
+    size_t need = 0;  // the largest of the tilings (the call's mfma_dtype and leading dimensions pick one)
     for (int w = 0; w < 3; ++w) {
         int tile, Npad, Kpad, ns, rps;
-        wgrad_geometry(std::max(M, 1), N, K, wgrad_wide_on() ? w : 0, &tile, &Npad, &Kpad, &ns, &rps);
+        wgrad_geometry(std::max(M, 1), N, K, w, &tile, &Npad, &Kpad, &ns, &rps);
         need = std::max(need, sizeof(float) * ((size_t)ns * Npad * Kpad + (size_t)ns * Npad));
     }
     return need;
@@ -1006,6 +977,7 @@ static int wgrad_plan(const cn_wgrad_desc* d, int budget, WgradArgs* a, int* til
                "cn_wgrad: bad shape M=%d N=%d K=%d (K must be a multiple of 64)", d->M, d->N, d->K);
     CN_REQUIRE(d->mfma_dtype == CN_MFMA_F32 || d->mfma_dtype == CN_MFMA_BF16 || d->mfma_dtype == CN_MFMA_F32_BF16X6,
                CN_ERR_ARG, "cn_wgrad: bad mfma_dtype %d", d->mfma_dtype);
+    CN_REQUIRE(!d->y_bf16 && !d->x_bf16, CN_ERR_UNSUPPORTED, "cn_wgrad: bf16 operand images are not built yet");
     int tile, Npad, Kpad, ns, rps;
     wgrad_geometry(std::max(d->M, 1), d->N, d->K, wgrad_wide(d), &tile, &Npad, &Kpad, &ns, &rps, budget);
     CN_REQUIRE(d->n_out <= Npad && d->k_out <= Kpad && d->n_out > 0 && d->k_out > 0, CN_ERR_SHAPE, "cn_wgrad: bad n_out/k_out");
@@ -1018,7 +990,8 @@ static int wgrad_plan(const cn_wgrad_desc* d, int budget, WgradArgs* a, int* til
                "cn_wgrad: leading dimensions must be < 2^20");
     const size_t need = cn_wgrad_workspace_bytes(d->M, d->N, d->K);  // covers every budget (ns <= the default's)
     CN_REQUIRE((size_t)d->workspace_bytes >= need, CN_ERR_SHAPE, "cn_wgrad: workspace %lld < %zu", (long long)d->workspace_bytes, need);
-    a->Y0 = d->Y0; a->X0 = d->X0; a->Y1 = d->Y1; a->X1 = d->X1;
+    a->Y0 = static_cast<const float*>(d->Y0); a->X0 = static_cast<const float*>(d->X0);
+    a->Y1 = static_cast<const float*>(d->Y1); a->X1 = static_cast<const float*>(d->X1);
     a->part = d->workspace;
     a->bpart = d->db ? d->workspace + (size_t)ns * Npad * Kpad : nullptr;
     a->ldy0 = (int)d->ldy0; a->ldx0 = (int)d->ldx0; a->ldy1 = (int)d->ldy1; a->ldx1 = (int)d->ldx1;
@@ -1044,25 +1017,18 @@ extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
     hipStream_t s = (hipStream_t)stream;
     if (d->mfma_dtype == CN_MFMA_F32_BF16X6) {
         if (tile == 2) {
-            // the stage ring (one barrier per 16 rows, split and LDS writes beside the MFMAs): C2
-            // step 145.0-145.3k vs 142.1-143.3k rays/s with the 32-row single-buffer kernel
-            // (COPENERF_WGRAD_KERNEL=1, benchmarking aid; tools/env_ab.sh, same box)
-            if (g_wgrad_variant == 1) {
-                wgrad_x6_kernel<4, 4><<<grid, 512, 0, s>>>(a);
-            } else {
-                WgradBatch b{};
-                b.job[0] = a;
-                b.blocks[0] = grid;
-                b.njobs = 1;
-                wgrad_x6r_kernel<2><<<grid, 512, 0, s>>>(b);
-            }
-        }
-        else if (tile == 3)
+            WgradBatch b{};
+            b.job[0] = a;
+            b.blocks[0] = grid;
+            b.njobs = 1;
+            wgrad_x6r_kernel<2><<<grid, 512, 0, s>>>(b);
+        } else if (tile == 3) {
             wgrad_x6n_kernel<3><<<grid, 512, 0, s>>>(a);
-        else if (tile == 0)
+        } else if (tile == 0) {
             wgrad_x6_kernel<2, 2><<<grid, 256, 0, s>>>(a);
-        else
+        } else {
             wgrad_x6_kernel<2, 1><<<grid, 256, 0, s>>>(a);
+        }
     } else if (d->mfma_dtype == CN_MFMA_BF16) {
         if (tile == 0)
             wgrad_bf16_kernel<2, 2, 2, 2><<<grid, 256, 0, s>>>(a);
@@ -1079,7 +1045,7 @@ extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
 
 // Whether cn_wgrad_batch runs a descriptor inside its shared stage-ring launch.
 static bool wgrad_batchable(const cn_wgrad_desc* d) {
-    return d->mfma_dtype == CN_MFMA_F32_BF16X6 && g_wgrad_variant != 1 && wgrad_wide(d) == 1;
+    return d->mfma_dtype == CN_MFMA_F32_BF16X6 && wgrad_wide(d) == 1;
 }
 
 extern "C" int cn_wgrad_batch(const cn_wgrad_desc* descs, int32_t n, cn_stream_t stream) {
@@ -1093,7 +1059,7 @@ extern "C" int cn_wgrad_batch(const cn_wgrad_desc* descs, int32_t n, cn_stream_t
     double total = 0.0;
     for (int i = 0; i < n; ++i) {
         const cn_wgrad_desc* d = descs + i;
-        if (!d || !wgrad_batchable(d) || nb == kWgradBatchMax) {
+        if (!wgrad_batchable(d) || nb == kWgradBatchMax) {
             int rc = cn_wgrad(d, stream);  // another tile class (or a full batch): its own launch
             if (rc) return rc;
             continue;
@@ -1104,11 +1070,7 @@ extern "C" int cn_wgrad_batch(const cn_wgrad_desc* descs, int32_t n, cn_stream_t
         idx[nb++] = i;
     }
     if (nb == 0) return CN_OK;
-    static const int kCUs = [] {
-        int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        return cus > 0 ? cus : 256;
-    }();
+    const int cus = wgrad_device_cus();
     WgradBatch b{};
     SlabJob js[2 * kWgradBatchMax];
     int grid = 0;
@@ -1116,7 +1078,7 @@ extern "C" int cn_wgrad_batch(const cn_wgrad_desc* descs, int32_t n, cn_stream_t
         const cn_wgrad_desc* d = descs + idx[q];
         const int tiles = cdiv(d->N, 256) * cdiv(d->K, 256);
         // floor of the proportional share: the slices of all jobs never exceed one workgroup per CU
-        const int budget = std::max(tiles, (int)(kCUs * work[q] / total) / tiles * tiles);
+        const int budget = std::max(tiles, (int)(cus * work[q] / total) / tiles * tiles);
         int tile, g;
         int rc = wgrad_plan(d, budget, &b.job[q], &tile, &g, &js[2 * q], &js[2 * q + 1]);
         if (rc) return rc;

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define CN_ABI_VERSION 9
+#define CN_ABI_VERSION 10
 
 typedef void* cn_stream_t; /* hipStream_t */
 
@@ -83,13 +83,13 @@ typedef enum cn_epilogue {
 } cn_epilogue;
 
 typedef struct cn_linear_desc {
-    const float* A;
-    const float* A2;
+    const void* A;       /* fp32, or bf16 when a_bf16 (A2 likewise) */
+    const void* A2;
     const float* B;
     const float* bias;   /* [N] or NULL (N <= 512 with a bias or colv) */
     const float* rowv;   /* [M] or NULL : rank-1 term rowv[m]*colv[n] added to v */
     const float* colv;   /* [N] or NULL */
-    const float* aux0;
+    const void* aux0;    /* fp32, or bf16 when aux0_bf16 */
     const float* aux1;
     float* out0;
     float* out1;         /* SOFTPLUS_HEAD only (else NULL) */
@@ -98,7 +98,8 @@ typedef struct cn_linear_desc {
     int32_t M, N, K, K1;
     int32_t nzero, nsplit;
     int32_t epilogue;    /* cn_epilogue */
-    int32_t tile;        /* 0: 128x128 block tile, 1: 128x64 */
+    int32_t tile;        /* 0: the library's tile choice (up to 256x256), 1: 128x64, 2: 128x128 only
+                            (tests compare the tiles: every tile gives the same bits) */
     float adiv, odiv;    /* divisors applied to A·Bᵀ and to the activation (0 means 1),
                             applied as multiplies by their fp32 reciprocals */
     float beta, threshold; /* Softplus(beta, threshold) of neus_fields.py:266 */
@@ -123,40 +124,26 @@ typedef struct cn_linear_desc {
     const float* head_b;
     float* head_out;           /* [M] (or indexed by head_idx) */
     const int32_t* head_idx;   /* [M] destination rows or NULL */
-    /* ABI v9 -- the first SDF layer with the positional encoding fused into its operand load
-       (neus_embedder.py:6-51 feeding neus_fields.py:268-272): when emb_x != NULL, A must be NULL and
-       row m of A is the encoding of emb_scale * emb_x[m][0:4] (column group 0: the scaled point, groups
-       1 + 2k / 2 + 2k: sin / cos(2^k x') for k < emb_multires, zero up to K <= 64), computed while the
-       tile is staged; SOFTPLUS or STORE, tile 0.  Optional side outputs, written once per row: emb_u0
-       = the encoding [M][K] (what cn_sdf_embed writes), emb_u4 = its first 4 (1 + 2 emb_multires)
-       columns divided by emb_u4_div (0 means 1: the skip input's tail, neus_fields.py:276-277). */
-    const float* emb_x;
-    int64_t ld_emb_x;
-    int32_t emb_multires;
-    float emb_scale;
-    float* emb_u0;
-    int64_t ld_emb_u0;
-    float* emb_u4;
-    int64_t ld_emb_u4;
-    float emb_u4_div;
-    /* ABI v9 -- ReLU sign bits (the colour network, neus_fields.py:364-373): RELU may write out_mask[m][c / 32]
-       bit c % 32 = (out[m][c] > 0); BWD_RELU may read aux_mask instead of the stored activation aux0 (the same
-       result, 4 bytes per 32 columns).  bf16x6 on the 256x256 tile only; ld_mask >= ceil(N / 32) words. */
-    uint32_t* out_mask;
-    const uint32_t* aux_mask;
-    int64_t ld_mask;
+    /* ABI v10 -- bf16 operand images (CN_MFMA_BF16 only, config C3's bf16 MLP MFMA): a GEMM operand
+       is rounded to bf16 (RNE) when it is staged, so a tensor whose consumers are GEMM operands can be
+       stored as that rounded image (2 bytes instead of 4) with bitwise-identical results.
+       a_bf16: A and A2 are bf16 row-major (lda / lda2 in bf16 elements, multiples of 8).
+       aux0_bf16: BWD_RELU's aux0 is bf16 (the sign test of the bf16 value: bf16 RNE keeps the sign,
+       and a positive value rounds to 0 only below 2^-133).
+       out0_b (ld_out0_b): the bf16 image of every value written to out0 (columns [0, nzero),
+       including the zero fill); out0 itself may then be NULL.  out1_b: the same for SOFTPLUS_HEAD's
+       out1.  Leading dimensions in bf16 elements, multiples of 8; 16-byte aligned. */
+    int32_t a_bf16;
+    int32_t aux0_bf16;
+    void* out0_b;
+    int64_t ld_out0_b;
+    void* out1_b;
+    int64_t ld_out1_b;
 } cn_linear_desc;
 
 enum cn_mfma_dtype { CN_MFMA_F32 = 0, CN_MFMA_BF16 = 1, CN_MFMA_F32_BF16X6 = 2 };
 
 int cn_linear(const cn_linear_desc* d, cn_stream_t stream);
-/* ABI v9: a chain of n <= 8 SOFTPLUS layers (the SDF's hidden layers, neus_fields.py:273-282) in one launch:
- * each workgroup takes a 256-row block through every layer, so layer j's A (= layer j-1's out0) is read back
- * from L2 / the memory-side cache instead of HBM and the launches' boundaries go.  Each descriptor must be a
- * valid cn_linear, bf16x6, on the 256x256 tile (128 < N <= 256, K a multiple of 32, no A2 / rowv / emb_x),
- * with the same M, K, lda == every ld_out0, ldb, flags, beta, threshold, adiv; descs[j].A == descs[j-1].out0.
- * Results equal the n cn_linear calls' bitwise. */
-int cn_linear_chain(const cn_linear_desc* descs, int32_t n, cn_stream_t stream);
 
 /* The rocprofv3 symbol of the kernel cn_linear would launch for *d (no launch, no device
  * access; the tile choice is the launch's own function): NUL-terminated into buf[len].
@@ -217,10 +204,10 @@ int cn_weight_norm(const cn_wn_job* jobs, int32_t njobs, int32_t backward, cn_st
  * every Linear above, including the create_graph term of neus_fields.py:296.
  * ------------------------------------------------------------------------ */
 typedef struct cn_wgrad_desc {
-    const float* Y0;
-    const float* X0;
-    const float* Y1;     /* NULL when npairs == 1 */
-    const float* X1;
+    const void* Y0;      /* fp32, or bf16 when y_bf16 (Y1 likewise) */
+    const void* X0;      /* fp32, or bf16 when x_bf16 (X1 likewise) */
+    const void* Y1;      /* NULL when npairs == 1 */
+    const void* X1;
     float* workspace;    /* cn_wgrad_workspace_bytes() */
     float* dW;           /* [n_out][k_out] (ld_dw) */
     float* db;           /* [n_out] or NULL */
@@ -235,6 +222,11 @@ typedef struct cn_wgrad_desc {
                             db is summed from the fp32 values either way;
                             CN_MFMA_F32_BF16X6: fp32 gradient from three bf16 terms per operand
                             (six products) */
+    /* ABI v10 (CN_MFMA_BF16 only): the Y side (Y0, Y1) / the X side (X0, X1) are bf16 operand images
+       (see cn_linear_desc.a_bf16; leading dimensions in bf16 elements, multiples of 8): the products
+       are the same bits as from the fp32 tensors they round; db then sums the bf16 values of Y0. */
+    int32_t y_bf16;
+    int32_t x_bf16;
 } cn_wgrad_desc;
 
 size_t cn_wgrad_workspace_bytes(int32_t M, int32_t N, int32_t K);

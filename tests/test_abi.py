@@ -66,10 +66,6 @@ def test_argument_validation_without_gpu():
     ws2 = (_lib.WgradDesc * 2)()
     assert lib.cn_wgrad_batch(ws2, 2, None) == -1  # checked before anything launches
     assert lib.cn_wgrad_batch(ws2, 0, None) == 0
-    assert lib.cn_linear_chain(None, 2, None) == -1
-    ld2 = (_lib.LinearDesc * 2)()
-    assert lib.cn_linear_chain(ld2, 9, None) == -1  # at most 8 layers
-    assert lib.cn_linear_chain(ld2, 2, None) == -1  # (layer 0: no A / B / out0)
     assert lib.cn_wgrad_workspace_bytes(524288, 256, 256) >= 4 * 256 * 256
     ws = lib.cn_train_loss_workspace_bytes(4096, 4)
     assert ws >= 8 * (4096 // 16 // 256)

@@ -45,8 +45,6 @@ def test_linear_tile_order_does_not_change_results():
     """cn_linear_desc.flags bit 0 (reverse M-tile walk, alternated launch to launch by
     ops.linear): both walks give bitwise identical outputs, edge tiles included."""
     ops = _ops()
-    if not ops.ALTERNATE_TILE_ORDER:
-        pytest.skip("COPENERF_ALT_ORDER=0")
     M, N, K = 70001, 256, 256
     A = _rnd(M, K, seed=51)
     W = _rnd(N, K, seed=52, scale=0.05)

@@ -88,15 +88,15 @@ def test_stage1_terms_bitwise_reproducible_and_empty():
     assert num.item() == 0.0 and sumw.item() == 0.0 and ray.shape == (0, 4)
 
 
-def test_trainer_stage1_fused_matches_torch_expressions(monkeypatch):
+def test_trainer_stage1_fused_matches_torch_expressions():
     """The trainer's stage-1 terms through the fused pass and through the torch
-    expressions (COPENERF_STAGE1_FUSED=0) on the same step: losses and gradients."""
+    expressions (stage1_fused=False) on the same step: losses and gradients."""
     from copenerf.train_step import SyntheticTrainer
     res = []
-    for fused in ("1", "0"):
-        monkeypatch.setenv("COPENERF_STAGE1_FUSED", fused)
+    for fused in (True, False):
         tr = SyntheticTrainer(DEV, rays=256, seed=5, stage1=True, joint_pose=True, n_images=8, start_it=3000,
-                              mfma_dtype="fp32", train_cfg={"sdf_consistency_enable_pose_grad": True})
+                              mfma_dtype="fp32", train_cfg={"sdf_consistency_enable_pose_grad": True},
+                              stage1_fused=fused)
         tr.begin_iteration()
         batch = tr.make_batch()
         torch.manual_seed(0)

@@ -210,41 +210,6 @@ def test_wgrad_batch_matches_single_calls():
         assert torch.equal(dW, dW2) and torch.equal(db, db2)
 
 
-@pytest.mark.parametrize("mode", ["fp32", "bf16x6", "bf16"])
-def test_fused_encoding_first_layer_bitwise(mode):
-    """The first SDF layer with the positional encoding computed in its operand load (cn_linear
-    emb_x, COPENERF_FUSE_EMB) against the cn_sdf_embed pass + GEMM: the encoding is one device
-    function and the GEMM tile is the same, so sdf, ∇ₓsdf, the feature, every parameter gradient
-    and the stored encoding / skip tail are bitwise equal -- on the grad path (U0 stored) and on
-    the sampler path (keep=False: no U0 at all).  A ragged M exercises the rows past the end."""
-    from copenerf import SDFNetwork, fields
-    from helpers import SDF_CFG
-    torch.manual_seed(5)
-    net = SDFNetwork(**SDF_CFG).to(DEV)
-    net.mfma_dtype = mode
-    x = (torch.rand(5001, 4, device=DEV) * 2 - 1)
-    res = {}
-    saved = fields.FUSE_EMB
-    try:
-        for fuse in (False, True):
-            fields.FUSE_EMB = fuse
-            sdf, feat, g = net.field(x)
-            loss = ((g.norm(dim=-1) - 1) ** 2).mean() + sdf.abs().mean() + 1e-2 * feat.square().mean()
-            grads = torch.autograd.grad(loss, list(net.parameters()))
-            Ws, bs, pk = net.params_and_pack()
-            st = fields.sdf_forward(net.layout(), pk, x, want_feat=False, want_grad=False, keep=False)
-            stk = fields.sdf_forward(net.layout(), pk, x, want_feat=False, want_grad=False, keep=True)
-            res[fuse] = (sdf.detach(), feat.detach(), g.detach(), grads, st["sdf"], stk["U"][0], stk["U"][1],
-                         stk["U"][net.layout().skip])
-    finally:
-        fields.FUSE_EMB = saved
-    a, b = res[False], res[True]
-    assert all(torch.equal(u, v) for u, v in zip(a[:3], b[:3]))
-    assert all(torch.equal(u, v) for u, v in zip(a[3], b[3]))
-    for u, v in zip(a[4:], b[4:]):
-        assert torch.equal(u, v)
-
-
 def test_linear_x6_mul_split_on_the_wide_tile():
     """The skip layer's ∇-pass MUL with a split output (neus_fields.py:276-277: the input adjoint's
     embedding columns go out raw) on the 256x256 tile's direct epilogue: columns < nsplit are
@@ -271,64 +236,3 @@ def test_linear_x6_mul_split_on_the_wide_tile():
     assert torch.all(out[:, 204:] == 0)
     torch.testing.assert_close(split[:, :52], v[:, 204:].float(), rtol=2e-5, atol=2e-6)
     assert torch.isnan(split[:, 52:]).all()
-
-
-def test_layer_chain_bitwise():
-    """cn_linear_chain (COPENERF_LAYER_CHAIN): the SDF's SOFTPLUS hidden layers 1..6 in one launch, each
-    workgroup taking a 256-row block through every layer, against one cn_linear per layer: every stored
-    activation (incl. the skip input assembled in place), the sdf, ∇ₓsdf and every parameter gradient are
-    bitwise equal (same tile, same K order), on the grad path and the sampler path; ragged M."""
-    from copenerf import SDFNetwork, fields
-    from helpers import SDF_CFG
-    torch.manual_seed(9)
-    net = SDFNetwork(**SDF_CFG).to(DEV)
-    net.mfma_dtype = "bf16x6"
-    x = (torch.rand(70001, 4, device=DEV) * 2 - 1)
-    res = {}
-    saved = fields.LAYER_CHAIN
-    try:
-        for chain in (False, True):
-            fields.LAYER_CHAIN = chain
-            Ws, bs, pk = net.params_and_pack()
-            assert bool(fields._chain_layers(net.layout(), pk, fields._fuse_head(net.layout(), pk))) == chain
-            sdf, feat, g = net.field(x)
-            loss = ((g.norm(dim=-1) - 1) ** 2).mean() + sdf.abs().mean() + 1e-2 * feat.square().mean()
-            grads = torch.autograd.grad(loss, list(net.parameters()))
-            st = fields.sdf_forward(net.layout(), pk, x, want_feat=False, want_grad=False, keep=False)
-            stk = fields.sdf_forward(net.layout(), pk, x, want_feat=False, want_grad=False, keep=True)
-            res[chain] = ([sdf.detach(), feat.detach(), g.detach(), st["sdf"]] + list(grads) +
-                          [u for u in stk["U"] if u is not None])
-    finally:
-        fields.LAYER_CHAIN = saved
-    for a, b in zip(res[False], res[True]):
-        assert torch.equal(a, b)
-
-
-def test_relu_sign_bit_masks_bitwise():
-    """COPENERF_RELU_MASK: the colour network's forward RELUs write the sign bits of their outputs and the
-    backward's BWD_RELU reads them instead of the stored activations -- rgb and every gradient (parameters,
-    points, normals, directions, feature) bitwise equal to the activation-reading backward; ragged M."""
-    from copenerf import RenderingNetwork, fields
-    torch.manual_seed(11)
-    from copenerf.train_step import COL_CFG
-    net = RenderingNetwork(**COL_CFG).to(DEV)
-    net.mfma_dtype = "bf16x6"
-    M = 5003
-    pts = torch.rand(M, 4, device=DEV, requires_grad=True)
-    nrm = torch.randn(M, 4, device=DEV, requires_grad=True)
-    dirs = torch.randn(M, 3, device=DEV, requires_grad=True)
-    feat = (0.1 * torch.randn(M, 256, device=DEV)).requires_grad_(True)
-    res = {}
-    saved = fields.RELU_MASK
-    try:
-        for on in (False, True):
-            fields.RELU_MASK = on
-            rgb = net(pts, nrm, dirs, feat)
-            loss = (rgb * torch.linspace(0.5, 1.5, 3, device=DEV)).square().sum()
-            grads = torch.autograd.grad(loss, [pts, nrm, dirs, feat] + list(net.parameters()), allow_unused=True)
-            res[on] = [rgb.detach()] + [g for g in grads if g is not None]
-    finally:
-        fields.RELU_MASK = saved
-    assert len(res[False]) == len(res[True])
-    for a, b in zip(res[False], res[True]):
-        assert torch.equal(a, b)

@@ -53,14 +53,12 @@ def main():
                           ("mul", ops.EPI_MUL, sg),
                           ("tangent", ops.EPI_TANGENT, sg),
                           ("bwd_softplus", ops.EPI_BWD_SOFTPLUS, so),
-                          ("relu", ops.EPI_RELU, dict(bias=bias)),
-                          ("main loop only (bench)", 7, {})):
+                          ("relu", ops.EPI_RELU, dict(bias=bias))):
         bench(res, "cn_linear " + name, lambda: ops.linear(A, B, N, K, o0, epi, **kw))
     Bb = B.bfloat16().contiguous()
     for name, epi, kw in (("store", ops.EPI_STORE, dict(bias=bias)),
                           ("softplus", ops.EPI_SOFTPLUS, dict(bias=bias)),
-                          ("tangent", ops.EPI_TANGENT, sg),
-                          ("main loop only (bench)", 7, {})):
+                          ("tangent", ops.EPI_TANGENT, sg)):
         bench(res, "cn_linear bf16 " + name, lambda: ops.linear(A, Bb, N, K, o0, epi, **kw))
     Bs = ops.split_bf16x3(B)
     for name, epi, kw in (("store", ops.EPI_STORE, dict(bias=bias)),
@@ -68,8 +66,7 @@ def main():
                           ("relu", ops.EPI_RELU, dict(bias=bias)),
                           ("mul", ops.EPI_MUL, sg),
                           ("tangent", ops.EPI_TANGENT, sg),
-                          ("bwd_softplus", ops.EPI_BWD_SOFTPLUS, so),
-                          ("main loop only (bench)", 7, {})):
+                          ("bwd_softplus", ops.EPI_BWD_SOFTPLUS, so)):
         bench(res, "cn_linear x6 " + name, lambda: ops.linear(A, Bs, N, K, o0, epi, **kw))
     bench(res, "torch.matmul bf16 (hipBLASLt)", lambda: torch.matmul(A.bfloat16(), Bb.t()))
     dW = torch.empty(N, K, device=dev)

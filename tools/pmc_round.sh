@@ -1,7 +1,7 @@
 #!/bin/bash
 # Counter round on the C2 bench (GPU box): kernel-trace stats, two SQ/GRBM passes
 # (MFMA busy, issue/wait split, instruction mix, clock), FETCH_SIZE and WRITE_SIZE in
-# separate passes, plus kernel-trace stats of the weight-gradient microbenchmark.
+# separate passes.
 # Every pass is its own rocprofv3 run under a time limit; counters the box does not
 # list are dropped before a pass runs.  Usage: bash tools/pmc_round.sh TAG [bench args]
 set -eo pipefail
@@ -25,9 +25,4 @@ timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $O/pf -o run --output-format c
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $O/pw -o run --output-format csv -- $B > /dev/null
 python3 $R/tools/sq_summary.py $O/p1/p1_counter_collection.csv $O/p2/p2_counter_collection.csv > $O/sq_summary.txt
 python3 $R/tools/pmc_summary.py $O/pf/run_counter_collection.csv $O/pw/run_counter_collection.csv $O/pmc.json
-for v in ${WGRAD_VARIANTS:-0 1}; do
-  COPENERF_WGRAD_KERNEL=$v timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/wab$v -o run --output-format csv -- python3 $R/tools/wgrad_ab.py > $O/wab$v.json
-  COPENERF_WGRAD_KERNEL=$v timeout -s KILL 200 rocprofv3 --pmc $P1 -d $O/wabp$v -o p1 --output-format csv -- python3 $R/tools/wgrad_ab.py > /dev/null
-  python3 $R/tools/sq_summary.py $O/wabp$v/p1_counter_collection.csv > $O/wab${v}_sq.txt
-done
 echo done
