@@ -88,19 +88,21 @@ SIGNATURES = {
     "cn_wgrad_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32]),
     "cn_wgrad": (c_i32, [ctypes.POINTER(WgradDesc), c_ptr]),
     "cn_wgrad_batch": (c_i32, [ctypes.POINTER(WgradDesc), c_i32, c_ptr]),
+    "cn_wgrad_batch_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(WgradDesc), c_i32, c_ptr]),
     "cn_pack_weights": (c_i32, [ctypes.POINTER(PackJob), c_i32, c_ptr]),
     "cn_row_head": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i32, c_i32, c_ptr, c_i64,
                             c_ptr, c_ptr]),
     "cn_softplus_adjoint_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32]),
     "cn_softplus_adjoint": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_f32, c_ptr, c_ptr, c_ptr, c_i64,
-                                    c_ptr, c_i64, c_f32, c_ptr, c_i64, c_ptr, c_ptr, c_f32, c_ptr, c_i64, c_ptr]),
+                                    c_ptr, c_i64, c_f32, c_ptr, c_i64, c_i32, c_ptr, c_ptr, c_f32, c_ptr, c_i64,
+                                    c_ptr]),
     "cn_scale_cols": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_i64, c_f32, c_ptr]),
     "cn_sdf_embed": (c_i32, [c_i32, c_ptr, c_i64, c_i32, c_f32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_f32,
-                             c_ptr]),
+                             c_i32, c_ptr]),
     "cn_sdf_grad_assemble": (c_i32, [c_i32, c_i32, c_f32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr,
                                      c_i64, c_ptr]),
     "cn_sdf_tangent_prep": (c_i32, [c_i32, c_i32, c_f32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64,
-                                    c_ptr, c_i64, c_f32, c_ptr]),
+                                    c_ptr, c_i64, c_f32, c_i32, c_ptr]),
     "cn_color_extras": (c_i32, [c_i32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_i32, c_i32, c_i32, c_ptr,
                                 c_i64, c_ptr]),
     "cn_rgb_head_bwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32]),

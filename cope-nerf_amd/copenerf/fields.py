@@ -177,14 +177,16 @@ def pack_sdf(lay: SDFLayout, Ws, bs, mfma_dtype: str = "fp32") -> SDFPack:
 def _fuse_head(lay: SDFLayout, pk: SDFPack) -> bool:
     """The last hidden layer computes the sdf head in its epilogue (EPI_SOFTPLUS_HEAD)
     when one GEMM tile spans its whole output row: N <= 128 in every mode, N <= 256
-    with the bf16x6 128x256 tile."""
+    with the 256-wide bf16x6 and bf16 tiles."""
     L8 = lay.n_lin - 1
     N = lay.out_dim[L8 - 1]
     if lay.in_dim[L8] != N or N % 4 or L8 == lay.skip or L8 - 1 == 0:
         return False
     B = pk.Bf[L8 - 1]
     x6 = B.dim() == 3
-    return N <= 128 or (x6 and N <= 256 and B.shape[1] >= 256 and rup(lay.in_dim[L8 - 1], 32) % 64 == 0)
+    bf = B.dtype == torch.bfloat16 and not x6
+    return N <= 128 or (x6 and N <= 256 and B.shape[1] >= 256 and rup(lay.in_dim[L8 - 1], 32) % 64 == 0) or \
+        (bf and N <= 256 and B.shape[0] >= 256)
 
 
 def sig_beta(lay: SDFLayout, l: int) -> float:
@@ -192,6 +194,18 @@ def sig_beta(lay: SDFLayout, l: int) -> float:
     (c = √2 for the layer feeding the skip concat, neus_fields.py:276-277):
     σ_l = 1 - exp(-β c U[l+1])."""
     return lay.beta * (SQRT2 if (l + 1) == lay.skip else 1.0)
+
+
+def _img_mode(pk) -> bool:
+    """bf16 MFMA mode (config C3): activations whose consumers are GEMM operands are stored as bf16
+    operand images -- the bits the GEMM staging would round them to -- beside (or instead of) the fp32
+    values the epilogues read."""
+    B = pk.Bf[0]
+    return B.dtype == torch.bfloat16 and B.dim() == 2
+
+
+def _empty_b(M, n, dev):
+    return torch.empty(M, n, device=dev, dtype=torch.bfloat16)
 
 
 def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool, want_grad: bool, keep: bool,
@@ -205,42 +219,59 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
     want_feat="hidden": no feature head -- the caller consumes the last hidden
     activation U[L8] directly (the renderer folds the feature head into the
     colour network's first layer, NeuSRenderer._folded_color_pack).
+    bf16 mode (_img_mode): Ub / Sb hold the bf16 operand images of the hidden activations and ∇-pass
+    adjoints (layers 1..7), which the next GEMMs and the weight gradients read; the fp32 U / S are
+    kept only for the epilogues that recover σ from them (not at all on the sampler path).
     """
     M, dev = x.shape[0], x.device
     nl, sk, HL, KE = lay.n_lin, lay.skip, lay.HL, lay.KE
     keep_u = keep or want_grad
-    U = [None] * nl
-    U[0] = _empty(M, KE, dev)
-    Usk, e_view = None, None
-    if sk >= 0:
-        Usk = _empty(M, HL, dev)
-        o = lay.out_dim[sk - 1]
-        e_view = Usk[:, o:o + lay.E]
-    ops.sdf_embed(x, lay.multires, lay.scale, U[0], e_view, SQRT2)
+    img = _img_mode(pk)
     L8 = nl - 1
+    U, Ub = [None] * nl, [None] * nl
+    U[0] = _empty(M, KE, dev)
+    Usk, Usk_b, e_view = None, None, None
+    if sk >= 0:
+        o = lay.out_dim[sk - 1]
+        if img and 1 <= sk < L8:
+            Usk_b = _empty_b(M, HL, dev)  # the skip input's operand image, its tail written by the embedding
+            Usk = _empty(M, HL, dev) if keep_u else None
+            e_view = Usk_b[:, o:o + lay.E]
+        else:
+            Usk = _empty(M, HL, dev)
+            e_view = Usk[:, o:o + lay.E]
+    ops.sdf_embed(x, lay.multires, lay.scale, U[0], e_view, SQRT2)
     sdf = sdf_out if sdf_out is not None else _empty(M, 1, dev)
     fuse = _fuse_head(lay, pk)
-    S7 = None
+    S7, S7b = None, None
     for l in range(nl - 1):
         into = (l + 1) == sk
         K = KE if l == 0 else rup(lay.in_dim[l], 32)
+        A = Ub[l] if Ub[l] is not None else U[l]
         if l == L8 - 1 and fuse:
             # the sdf head (and the ∇-pass seed s_7 = w80 ⊙ softplus'_7) in the layer's epilogue;
             # the activation itself is stored only when a consumer needs it (not on the sampler path)
             out = _empty(M, HL, dev) if (keep_u or want_feat is not False) else None
             S7 = _empty(M, HL, dev) if want_grad else None
-            ops.linear(U[l], pk.Bf[l], lay.out_dim[l], K, out, EPI_SOFTPLUS_HEAD, bias=pk.b[l], nzero=HL, beta=lay.beta,
+            S7b = _empty_b(M, HL, dev) if (want_grad and img) else None
+            ops.linear(A, pk.Bf[l], lay.out_dim[l], K, out, EPI_SOFTPLUS_HEAD, bias=pk.b[l], nzero=HL, beta=lay.beta,
                        threshold=lay.threshold, kalg=lay.in_dim[l], out1=S7, colv=pk.w80p if want_grad else None,
                        aux_beta=sig_beta(lay, l) if want_grad else 0.0, head_w=pk.w80[0], head_b=pk.b80, head_out=sdf,
-                       head_idx=dst, M=M)
+                       head_idx=dst, M=M, out1_b=S7b)
+            U[l + 1] = out
         else:
-            out = Usk if into else _empty(M, HL, dev)
-            ops.linear(U[l], pk.Bf[l], lay.out_dim[l], K, out, EPI_SOFTPLUS, bias=pk.b[l],
+            ob = None
+            if img and l + 1 < L8:  # the next layer's operand image (+ the fp32 values when kept)
+                ob = Usk_b if into else _empty_b(M, HL, dev)
+                out = (Usk if into else _empty(M, HL, dev)) if keep_u else None
+            else:
+                out = Usk if into else _empty(M, HL, dev)
+            ops.linear(A, pk.Bf[l], lay.out_dim[l], K, out, EPI_SOFTPLUS, bias=pk.b[l],
                        nzero=lay.out_dim[l] if into else HL, odiv=SQRT2 if into else 1.0, beta=lay.beta,
-                       threshold=lay.threshold, kalg=lay.in_dim[l])
-        U[l + 1] = out
+                       threshold=lay.threshold, kalg=lay.in_dim[l], out0_b=ob)
+            U[l + 1], Ub[l + 1] = out, ob
         if not keep_u and l >= 1 and (l != sk):
-            U[l] = None  # free as we go on the no-grad sampler path
+            U[l] = Ub[l] = None  # free as we go on the no-grad sampler path
     if not fuse:
         ops.row_head(U[L8], lay.in_dim[L8], pk.w80, pk.b80, 1, 0, sdf, dst_index=dst)
     feat = None
@@ -248,10 +279,10 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
         feat = _empty(M, rup(lay.H_feat, 128), dev)
         ops.linear(U[L8], pk.Bf8, lay.H_feat, rup(lay.in_dim[L8], 32), feat, EPI_STORE, bias=pk.bf8,
                    nzero=feat.shape[1])
-    G, S = None, None
+    G, S, Sb = None, None, None
     if want_grad:
-        S = [None] * (nl - 1)
-        S[L8 - 1] = S7
+        S, Sb = [None] * (nl - 1), [None] * (nl - 1)
+        S[L8 - 1], Sb[L8 - 1] = S7, S7b
         if S7 is None:
             S[L8 - 1] = _empty(M, HL, dev)
             ops.scale_cols(U[L8], HL, pk.w80p, S[L8 - 1], act_beta=sig_beta(lay, L8 - 1))
@@ -259,17 +290,20 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
         for l in range(L8 - 1, 0, -1):
             Kl = rup(lay.out_dim[l], 32)
             S[l - 1] = _empty(M, HL, dev)
+            Sb[l - 1] = _empty_b(M, HL, dev) if (img and l - 1 >= 1) else None
+            A = Sb[l] if Sb[l] is not None else S[l]
             if l == sk:
-                ops.linear(S[l], pk.Bt[l], lay.in_dim[l], Kl, S[l - 1], EPI_MUL, aux0=U[l], aux_beta=sig_beta(lay, l - 1),
-                           nsplit=lay.out_dim[l - 1], out_split=QE, nzero=HL, adiv=SQRT2, kalg=lay.out_dim[l])
+                ops.linear(A, pk.Bt[l], lay.in_dim[l], Kl, S[l - 1], EPI_MUL, aux0=U[l], aux_beta=sig_beta(lay, l - 1),
+                           nsplit=lay.out_dim[l - 1], out_split=QE, nzero=HL, adiv=SQRT2, kalg=lay.out_dim[l],
+                           out0_b=Sb[l - 1])
             else:
-                ops.linear(S[l], pk.Bt[l], lay.out_dim[l - 1], Kl, S[l - 1], EPI_MUL, aux0=U[l],
-                           aux_beta=sig_beta(lay, l - 1), nzero=HL, kalg=lay.out_dim[l])
+                ops.linear(A, pk.Bt[l], lay.out_dim[l - 1], Kl, S[l - 1], EPI_MUL, aux0=U[l],
+                           aux_beta=sig_beta(lay, l - 1), nzero=HL, kalg=lay.out_dim[l], out0_b=Sb[l - 1])
         Q0 = _empty(M, KE, dev)
         ops.linear(S[0], pk.Bt[0], lay.E, rup(lay.out_dim[0], 32), Q0, EPI_STORE, nzero=KE, kalg=lay.out_dim[0])
         G = _empty(M, 4, dev)
         ops.sdf_grad_assemble(lay.multires, lay.scale, U[0], Q0, QE, G)
-    return {"U": U, "S": S, "sdf": sdf, "feat": feat, "G": G}
+    return {"U": U, "Ub": Ub, "S": S, "Sb": Sb, "sdf": sdf, "feat": feat, "G": G}
 
 
 def sdf_input_grad(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dh=None):
@@ -340,27 +374,41 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
     M, dev = U[0].shape[0], U[0].device
     nl, sk, HL, KE = lay.n_lin, lay.skip, lay.HL, lay.KE
     L8 = nl - 1
+    img = _img_mode(pk)
+    Ub = st.get("Ub") or [None] * nl
+    Sb = st.get("Sb") or [None] * (nl - 1)
     second = dG is not None
     if second and S is None:
         raise RuntimeError("SDF double backward needs the ∇ pass buffers (want_grad=True in forward)")
-    Ud = None
+    Ud, Udb = None, [None] * nl
     if second:
         Ud = [None] * nl
         Ud[0] = _empty(M, KE, dev)
-        Usk_d, e_view = None, None
+        Usk_d, Usk_db, e_view = None, None, None
         if sk >= 0:
-            Usk_d = _empty(M, HL, dev)
             o = lay.out_dim[sk - 1]
-            e_view = Usk_d[:, o:o + lay.E]
+            Usk_d = _empty(M, HL, dev)
+            if img and 1 <= sk < L8:  # the tangent's skip input as an operand image (tail from the prep)
+                Usk_db = _empty_b(M, HL, dev)
+                e_view = Usk_db[:, o:o + lay.E]
+            else:
+                e_view = Usk_d[:, o:o + lay.E]
         ops.sdf_tangent_prep(lay.multires, lay.scale, U[0], dG, Ud[0], e_view, SQRT2)
         for l in range(nl - 1):
             into = (l + 1) == sk
             out = Usk_d if into else _empty(M, HL, dev)
+            ob = (Usk_db if into else _empty_b(M, HL, dev)) if (img and l + 1 < L8) else None
             K = KE if l == 0 else rup(lay.in_dim[l], 32)
-            ops.linear(Ud[l], pk.Bf[l], lay.out_dim[l], K, out, EPI_TANGENT, aux0=U[l + 1], aux_beta=sig_beta(lay, l),
+            A = Udb[l] if Udb[l] is not None else Ud[l]
+            ops.linear(A, pk.Bf[l], lay.out_dim[l], K, out, EPI_TANGENT, aux0=U[l + 1], aux_beta=sig_beta(lay, l),
                        nzero=lay.out_dim[l] if into else HL, odiv=SQRT2 if into else 1.0, beta=lay.beta,
-                       kalg=lay.in_dim[l])
-            Ud[l + 1] = out
+                       kalg=lay.in_dim[l], out0_b=ob)
+            Ud[l + 1], Udb[l + 1] = out, ob
+
+    def z_img(l):
+        """Z_l as a bf16 operand image only (its consumers: the next adjoint GEMM and the weight
+        gradient, whose second pair's Y is S_l: that must have an image too)."""
+        return img and 1 <= l < L8 and (not second or Sb[l] is not None) and Ub[l] is not None
 
     i8, o8 = lay.in_dim[L8], lay.out_dim[L8]
     dW8 = torch.empty(o8, i8, device=dev)
@@ -393,7 +441,7 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
             return {}
         return dict(aux1=S[l], aux2=Ud[l + 1], aux2_scale=lay.beta * (SQRT2 if (l + 1) == sk else 1.0))
 
-    Z = _empty(M, HL, dev)
+    Z = _empty_b(M, HL, dev) if (z_img(L8 - 1) and (dh is not None or (sdf_only and fused_cs))) else _empty(M, HL, dev)
     if dh is not None:  # Z_7 = (dh + dsdf w80) σ_7 + the second-order term: elementwise
         so = second_order(L8 - 1)
         ops.softplus_adjoint(U[L8], HL, Z, act_beta=sig_beta(lay, L8 - 1), D=dh, rowv=dsdf_flat,
@@ -423,22 +471,28 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
     for l in range(L8 - 1, -1, -1):
         Zl = Z
         if l > 0:
-            Z = _empty(M, HL, dev)
+            zb = z_img(l - 1)  # Z_{l-1} as an operand image only
+            Z = _empty_b(M, HL, dev) if zb else _empty(M, HL, dev)
+            zo = dict(out0_b=Z) if zb else {}
             if share and l == sk:  # + the embedding columns of the skip input (sdf_input_grad's PE)
-                ops.linear(Zl, pk.Bt[l], lay.in_dim[l], rup(lay.out_dim[l], 32), Z, EPI_MUL, aux0=U[l],
-                           aux_beta=sig_beta(lay, l - 1), nsplit=lay.out_dim[l - 1], out_split=PE, nzero=HL,
-                           adiv=SQRT2, kalg=lay.out_dim[l])
+                ops.linear(Zl, pk.Bt[l], lay.in_dim[l], rup(lay.out_dim[l], 32), None if zb else Z, EPI_MUL,
+                           aux0=U[l], aux_beta=sig_beta(lay, l - 1), nsplit=lay.out_dim[l - 1], out_split=PE,
+                           nzero=HL, adiv=SQRT2, kalg=lay.out_dim[l], **zo)
             else:
                 # first order only (no second-order term): Z = (W̃ᵀZ)σ is the MUL epilogue, which runs on
                 # the 256x256 tile (BWD_SOFTPLUS would add an all-zero term on the 128x128 tile)
-                ops.linear(Zl, pk.Bt[l], lay.out_dim[l - 1], rup(lay.out_dim[l], 32), Z,
+                ops.linear(Zl, pk.Bt[l], lay.out_dim[l - 1], rup(lay.out_dim[l], 32), None if zb else Z,
                            EPI_BWD_SOFTPLUS if second else EPI_MUL,
                            aux0=U[l], aux_beta=sig_beta(lay, l - 1), nzero=HL, adiv=SQRT2 if l == sk else 1.0,
-                           kalg=lay.out_dim[l], **second_order(l - 1))
+                           kalg=lay.out_dim[l], **second_order(l - 1), **zo)
         dW = torch.empty(lay.out_dim[l], lay.in_dim[l], device=dev)
         db = torch.empty(lay.out_dim[l], device=dev)
-        wq.add(Zl, U[l], lay.out_dim[l], lay.in_dim[l], dW, db=db,
-               Y1=S[l] if second else None, X1=Ud[l] if second else None, mode=wmode)
+        # the operands in one format per side: the images where Z_l is one (Y) / where U_l has one (X)
+        yb = Zl.dtype == torch.bfloat16
+        xb = Ub[l] is not None and (not second or Udb[l] is not None)
+        wq.add(Zl, Ub[l] if xb else U[l], lay.out_dim[l], lay.in_dim[l], dW, db=db,
+               Y1=(Sb[l] if yb else S[l]) if second else None, X1=(Udb[l] if xb else Ud[l]) if second else None,
+               mode=wmode)
         dWs[l], dbs[l] = dW, db
     wq.flush()
     if not want_dx:
@@ -687,11 +741,19 @@ class _ColorFieldFn(torch.autograd.Function):
         ext = _empty(M, lay.KX, dev)
         ops.color_extras(G, pts, dirs, dir_div, lay.multires_view, ext)
         H = []
+        img = _img_mode(pk)
         A, A2, K1, K = feat, ext, lay.F, lay.F + lay.KX
         for l in range(lay.n_lin - 1):
-            out = _empty(M, lay.HL, dev)
-            ops.linear(A, pk.Bf[l], lay.out_dim[l], K, out, EPI_RELU, bias=pk.b[l], A2=A2, K1=K1, nzero=lay.HL,
-                       kalg=lay.in_dim[l])
+            # bf16 mode: the hidden activations but the last are read only as GEMM operands (the next
+            # layer, the weight gradient) and for ReLU's sign (BWD_RELU): bf16 operand images only
+            if img and l < lay.n_lin - 2:
+                out = _empty_b(M, lay.HL, dev)
+                ops.linear(A, pk.Bf[l], lay.out_dim[l], K, None, EPI_RELU, bias=pk.b[l], A2=A2, K1=K1, nzero=lay.HL,
+                           kalg=lay.in_dim[l], out0_b=out)
+            else:
+                out = _empty(M, lay.HL, dev)
+                ops.linear(A, pk.Bf[l], lay.out_dim[l], K, out, EPI_RELU, bias=pk.b[l], A2=A2, K1=K1, nzero=lay.HL,
+                           kalg=lay.in_dim[l])
             H.append(out)
             A, A2, K1, K = out, None, None, rup(lay.out_dim[l], 32)
         rgb = _empty(M, 3, dev)
@@ -724,9 +786,14 @@ class _ColorFieldFn(torch.autograd.Function):
             db = torch.empty(lay.out_dim[l], device=dev)
             wq.add(dZ, H[l - 1], lay.out_dim[l], lay.in_dim[l], dW, db=db, mode=wmode)
             dWs[l], dbs[l] = dW, db
-            dZp = _empty(M, lay.HL, dev)
-            ops.linear(dZ, pk.Bt[l], lay.out_dim[l - 1], rup(lay.out_dim[l], 32), dZp, EPI_BWD_RELU, aux0=H[l - 1],
-                       nzero=lay.HL)
+            if _img_mode(pk) and l - 1 >= 1:  # dZ_{l-1}: read by the next adjoint GEMM and a weight gradient only
+                dZp = _empty_b(M, lay.HL, dev)
+                ops.linear(dZ, pk.Bt[l], lay.out_dim[l - 1], rup(lay.out_dim[l], 32), None, EPI_BWD_RELU,
+                           aux0=H[l - 1], nzero=lay.HL, out0_b=dZp)
+            else:
+                dZp = _empty(M, lay.HL, dev)
+                ops.linear(dZ, pk.Bt[l], lay.out_dim[l - 1], rup(lay.out_dim[l], 32), dZp, EPI_BWD_RELU,
+                           aux0=H[l - 1], nzero=lay.HL)
             dZ = dZp
         o0 = lay.out_dim[0]
         dWf = torch.empty(o0, lay.F, device=dev)

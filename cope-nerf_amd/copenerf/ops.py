@@ -218,7 +218,7 @@ def _tile_tag(name, tile):
 def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None, colv=None, aux0=None,
            aux1=None, aux2=None, out_split=None, nsplit=None, nzero=None, adiv=1.0, odiv=1.0, beta=100.0,
            threshold=20.0, aux_beta=0.0, aux2_scale=0.0, tile=None, M=None, kalg=None, out1=None, head_w=None,
-           head_b=None, head_out=None, head_idx=None):
+           head_b=None, head_out=None, head_idx=None, out0_b=None, out1_b=None):
     """out = epilogue((A|A2) @ B[:N].T / adiv) -- cn_linear.  MUL / TANGENT /
     BWD_SOFTPLUS read softplus' as sg = 1 - exp(-aux_beta * aux0) from the stored
     softplus output aux0 (include/copenerf.h).  kalg: the unpadded
@@ -230,19 +230,31 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     EPI_SOFTPLUS_HEAD (the last SDF hidden layer): out0 = softplus activation (or
     None: not stored), out1 = colv * softplus' (or None), head_out[head_idx[m] or m]
     = out0[m] · head_w + head_b.
-    tile: None (the library's choice), 1 (128x64), 2 (128x128 only: tests compare the tiles)."""
+    tile: None (the library's choice), 1 (128x64), 2 (128x128 only: tests compare the tiles).
+    bf16 operand images (bf16 MFMA mode only, ABI v10): A (with A2) may be bfloat16 -- the rounded
+    operand itself, read instead of rounded on load; aux0 may be bfloat16 for BWD_RELU (its sign);
+    out0_b / out1_b (bfloat16, or None) receive the RNE bf16 image of every value written to out0 /
+    out1, and out0 may then be None."""
     x6 = B.dim() == 3
     if x6 and (B.dtype != torch.bfloat16 or B.shape[2] != 48 or not B.is_contiguous()):
         raise RuntimeError(f"cn_linear: a 3-D B must be split_bf16x3's [K/16, N, 48] bfloat16 image (got "
                            f"{tuple(B.shape)}, {B.dtype}, strides {B.stride()})")
-    if out0 is None and epilogue != EPI_SOFTPLUS_HEAD:
-        raise RuntimeError("cn_linear: out0 is required")
-    for t, n in ((A, "A"), (A2, "A2"), (B, "B"), (out0, "out0"), (aux0, "aux0"), (aux1, "aux1"), (aux2, "aux2"),
-                 (out_split, "out_split"), (out1, "out1")):
-        _need(t, n, ndim=3 if (x6 and t is B) else 2)
-        if t is not None and t is not B and t.dtype == torch.bfloat16:
-            raise RuntimeError(f"cn_linear: {n} must be float32 (only B may be bfloat16)")
+    if out0 is None and out0_b is None and epilogue != EPI_SOFTPLUS_HEAD:
+        raise RuntimeError("cn_linear: out0 (or out0_b) is required")
     bf = B.dtype == torch.bfloat16 and not x6
+    for t, n in ((A, "A"), (A2, "A2"), (B, "B"), (out0, "out0"), (aux0, "aux0"), (aux1, "aux1"), (aux2, "aux2"),
+                 (out_split, "out_split"), (out1, "out1"), (out0_b, "out0_b"), (out1_b, "out1_b")):
+        _need(t, n, ndim=3 if (x6 and t is B) else 2)
+        if t is None or t is B:
+            continue
+        want_b = n in ("out0_b", "out1_b")
+        may_b = bf and (n in ("A", "A2") or (n == "aux0" and epilogue == EPI_BWD_RELU))
+        if (t.dtype == torch.bfloat16) != want_b and not (may_b and t.dtype == torch.bfloat16):
+            raise RuntimeError(f"cn_linear: {n} has dtype {t.dtype} (bfloat16 images: A / A2, BWD_RELU's aux0 "
+                               f"and out0_b / out1_b, in the bf16 MFMA mode only)")
+    a_b = A.dtype == torch.bfloat16
+    if A2 is not None and (A2.dtype == torch.bfloat16) != a_b:
+        raise RuntimeError("cn_linear: A and A2 must have the same dtype")
     if bf:
         K = rup(K, 64)
         K1 = rup(K1, 64) if K1 is not None else None
@@ -258,8 +270,8 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     b_rows, b_k = (B.shape[1], 16 * B.shape[0]) if x6 else (B.shape[0], B.shape[1])
     if b_rows < rup(N, bn) or b_k < K:
         raise RuntimeError(f"cn_linear: B {tuple(B.shape)} too small for N={N}, K={K} (tile {tile})")
-    if (out0 is not None and out0.shape[0] < M) or (out1 is not None and out1.shape[0] < M):
-        raise RuntimeError("cn_linear: out0 / out1 has fewer rows than A")
+    if any(t is not None and t.shape[0] < M for t in (out0, out1, out0_b, out1_b)):
+        raise RuntimeError("cn_linear: an output has fewer rows than A")
     if epilogue == EPI_SOFTPLUS_HEAD:
         _need(head_w, "head_w", ndim=1)
         _need(head_b, "head_b", ndim=1)
@@ -289,6 +301,9 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     d.epilogue, d.tile = epilogue, tile
     d.adiv, d.odiv, d.beta, d.threshold = adiv, odiv, beta, threshold
     d.mfma_dtype = 2 if x6 else (1 if bf else 0)
+    d.a_bf16 = 1 if a_b else 0
+    d.aux0_bf16 = 1 if (aux0 is not None and aux0.dtype == torch.bfloat16) else 0
+    d.out0_b, d.ld_out0_b, d.out1_b, d.ld_out1_b = _ptr(out0_b), _ld(out0_b), _ptr(out1_b), _ld(out1_b)
     global _flip
     _flip ^= 1  # consecutive launches walk the rows in opposite directions
     d.flags = _flip
@@ -297,14 +312,14 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
         _lib.check(_lib.load().cn_linear(d, _stream()), "cn_linear")
         name = kernel_name(_lib.load().cn_linear_kernel_name, d)
         tag = _tile_tag(name, tile) if (x6 or bf) else tile
-        key = ("linear", tag, EPI_NAMES[epilogue] + ("+rowv" if rowv is not None else "")) + \
-            (("bf16",) if bf else ("x6",) if x6 else ())
+        key = ("linear", tag, EPI_NAMES[epilogue] + ("+rowv" if rowv is not None else "") +
+               ("+imgA" if a_b else "")) + (("bf16",) if bf else ("x6",) if x6 else ())
         _timer.symbols[key] = name
         ka = kalg or K
         # algorithmic HBM bytes: A (unpadded K) and every aux row read once, each output
         # element written once, the weight image once (bf16x6: 3 bf16 terms per weight)
-        nb = 4.0 * M * ka + (6.0 if x6 else 2.0 if bf else 4.0) * N * ka
-        nb += 4.0 * M * N * sum(t is not None for t in (out0, out1, aux0, aux1, aux2))
+        nb = (2.0 if a_b else 4.0) * M * ka + (6.0 if x6 else 2.0 if bf else 4.0) * N * ka
+        nb += M * N * sum(t.element_size() for t in (out0, out1, aux0, aux1, aux2, out0_b, out1_b) if t is not None)
         nb += 4.0 * M * ((rowv is not None) + (head_out is not None) + (head_idx is not None))
         _timer.stop(key + ((M, N, K),) if _timer.detail else key, e0, 2.0 * M * N * ka, nb)
     else:
@@ -315,27 +330,43 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
 WGRAD_MODES = {"fp32": 0, "bf16": 1, "bf16x6": 2}
 
 
-def _wgrad_desc(Y0, X0, N, K, dW, db, Y1, X1, accumulate, mode):
-    """The cn_wgrad descriptor of one weight gradient and the workspace it points into."""
+def _wgrad_desc(Y0, X0, N, K, dW, db, Y1, X1, accumulate, mode, workspace=True):
+    """The cn_wgrad descriptor of one weight gradient and the workspace it points into (workspace=False:
+    none yet -- cn_wgrad_batch callers carve every job's slabs out of one buffer).  A bfloat16 Y0 / X0
+    (with Y1 / X1 of the same dtype) is a bf16 operand image (bf16 mode)."""
     if mode not in WGRAD_MODES:
         raise ValueError(f"wgrad: mode must be one of {tuple(WGRAD_MODES)} (got {mode!r})")
     for t, n in ((Y0, "Y0"), (X0, "X0"), (Y1, "Y1"), (X1, "X1"), (dW, "dW")):
         _need(t, n)
+    yb, xb = Y0.dtype == torch.bfloat16, X0.dtype == torch.bfloat16
+    if (Y1 is not None and (Y1.dtype == torch.bfloat16) != yb) or (X1 is not None and (X1.dtype == torch.bfloat16) != xb):
+        raise RuntimeError("wgrad: Y0 / Y1 and X0 / X1 must have the same dtype")
+    if (yb or xb) and mode != "bf16":
+        raise RuntimeError("wgrad: bfloat16 operand images only in the bf16 mode")
     M = Y0.shape[0]
     lib = _lib.load()
-    nbytes = lib.cn_wgrad_workspace_bytes(M, N, K)
-    ws = torch.empty(nbytes // 4 + 1, device=Y0.device, dtype=torch.float32)
+    ws = None
     d = _lib.WgradDesc()
+    if workspace:
+        nbytes = lib.cn_wgrad_workspace_bytes(M, N, K)
+        ws = torch.empty(nbytes // 4 + 1, device=Y0.device, dtype=torch.float32)
+        d.workspace, d.workspace_bytes = _ptr(ws), ws.numel() * 4
     d.Y0, d.X0, d.Y1, d.X1 = _ptr(Y0), _ptr(X0), _ptr(Y1), _ptr(X1)
-    d.workspace, d.dW, d.db = _ptr(ws), _ptr(dW), _ptr(db)
+    d.dW, d.db = _ptr(dW), _ptr(db)
     d.ldy0, d.ldx0, d.ldy1, d.ldx1, d.ld_dw = _ld(Y0), _ld(X0), _ld(Y1), _ld(X1), _ld(dW)
-    d.workspace_bytes = ws.numel() * 4
     d.M, d.N, d.K = M, N, rup(K, 64)
     d.npairs = 2 if Y1 is not None else 1
     d.n_out, d.k_out = dW.shape[0], dW.shape[1]
     d.accumulate = 1 if accumulate else 0
     d.mfma_dtype = WGRAD_MODES[mode]
+    d.y_bf16, d.x_bf16 = int(yb), int(xb)
     return d, ws
+
+
+def _wgrad_bytes(d, ops_):
+    """Algorithmic HBM bytes of a weight gradient: every operand row read once."""
+    Y0, X0 = ops_[0], ops_[1]
+    return float(d.npairs * d.M * (d.n_out * Y0.element_size() + d.k_out * X0.element_size()))
 
 
 def _wgrad_key(d, mode):
@@ -351,7 +382,7 @@ def wgrad(Y0, X0, N, K, dW, *, db=None, Y1=None, X1=None, accumulate=False, mode
     """dW[:n_out, :k_out] (+)= Y0ᵀX0 (+ Y1ᵀX1), db = colsum(Y0) -- cn_wgrad.
     mode: "fp32" (exact fp32 MFMA), "bf16x6" (fp32 from three bf16 terms per
     operand on the bf16 MFMA) or "bf16" (operands rounded to bf16 on load,
-    config C3's reduced-precision mode)."""
+    config C3's reduced-precision mode; Y / X may then be bfloat16 operand images)."""
     d, ws = _wgrad_desc(Y0, X0, N, K, dW, db, Y1, X1, accumulate, mode)
     lib = _lib.load()
     if _timer is not None:
@@ -360,7 +391,7 @@ def wgrad(Y0, X0, N, K, dW, *, db=None, Y1=None, X1=None, accumulate=False, mode
         key = _wgrad_key(d, mode)
         M = d.M
         _timer.stop(key + ((M, d.n_out, d.k_out),) if _timer.detail else key, e0,
-                    2.0 * M * d.n_out * d.k_out * d.npairs, 4.0 * d.npairs * M * (d.n_out + d.k_out))
+                    2.0 * M * d.n_out * d.k_out * d.npairs, _wgrad_bytes(d, (Y0, X0)))
     else:
         _lib.check(lib.cn_wgrad(d, _stream()), "cn_wgrad")
     return dW
@@ -371,17 +402,19 @@ class WgradQueue(object):
     cn_wgrad_batch call at flush(): one launch and one slab reduction instead of a launch, a
     full-chip slab write and a reduction each (other tile classes launch at add()).  The
     queue holds the operand tensors, so their memory stays allocated until the flush; the
-    gradients are written by the flush (call it before anything reads them)."""
+    gradients are written by the flush (call it before anything reads them).  Every job's slabs
+    come out of one workspace allocated at the flush, sized by the batch's own layout
+    (cn_wgrad_batch_workspace_bytes: each job's share of the slices, not a full launch's)."""
 
     def __init__(self):
         self.jobs = []
 
     def add(self, Y0, X0, N, K, dW, *, db=None, Y1=None, X1=None, mode="fp32"):
-        d, ws = _wgrad_desc(Y0, X0, N, K, dW, db, Y1, X1, False, mode)
+        d, _ = _wgrad_desc(Y0, X0, N, K, dW, db, Y1, X1, False, mode, workspace=False)
         if "WgradBatch" not in kernel_name(_lib.load().cn_wgrad_kernel_name, d):
             # not a stage-ring job (e.g. K = 64 first layers): nothing to share, launch it now
             return wgrad(Y0, X0, N, K, dW, db=db, Y1=Y1, X1=X1, mode=mode)
-        self.jobs.append((d, mode, (Y0, X0, Y1, X1, ws)))
+        self.jobs.append((d, mode, (Y0, X0, Y1, X1)))
         return dW
 
     def flush(self):
@@ -390,13 +423,20 @@ class WgradQueue(object):
         lib = _lib.load()
         n = len(self.jobs)
         arr = (_lib.WgradDesc * n)(*[d for d, _, _ in self.jobs])
+        offs = (ctypes.c_int64 * n)()
+        total = lib.cn_wgrad_batch_workspace_bytes(arr, n, offs)
+        ws = torch.empty(total // 4 + 1, device=self.jobs[0][2][0].device, dtype=torch.float32)
+        base = ws.data_ptr()
+        for i in range(n):
+            arr[i].workspace = base + offs[i]
+            arr[i].workspace_bytes = total - offs[i]
         if _timer is not None:
             # the batch's time goes to the class of its first job; the FLOPs of all of them
             e0 = _timer.start()
             _lib.check(lib.cn_wgrad_batch(arr, n, _stream()), "cn_wgrad_batch")
             key = _wgrad_key(self.jobs[0][0], self.jobs[0][1])
             fl = sum(2.0 * d.M * d.n_out * d.k_out * d.npairs for d, _, _ in self.jobs)
-            nb = sum(4.0 * d.npairs * d.M * (d.n_out + d.k_out) for d, _, _ in self.jobs)
+            nb = sum(_wgrad_bytes(d, t) for d, _, t in self.jobs)
             _timer.stop(key + (("batch", n),) if _timer.detail else key, e0, fl, nb)
         else:
             _lib.check(lib.cn_wgrad_batch(arr, n, _stream()), "cn_wgrad_batch")
@@ -435,6 +475,8 @@ def softplus_adjoint(act, N, out, *, act_beta, D=None, rowv=None, colv=None, aux
     rs_out[0] = Σ_m rowv[m] / cs_div (its bias gradient)."""
     for t, n in ((act, "act"), (out, "out"), (D, "D"), (aux1, "aux1"), (aux2, "aux2")):
         _need(t, n)
+        if t is not None and t is not out and t.dtype != torch.float32:
+            raise RuntimeError(f"softplus_adjoint: {n} must be float32")
     if rowv is not None and (not rowv.is_contiguous() or rowv.numel() != act.shape[0]):
         raise RuntimeError("softplus_adjoint: rowv must be a contiguous [M] tensor")
     M = act.shape[0]
@@ -447,7 +489,7 @@ def softplus_adjoint(act, N, out, *, act_beta, D=None, rowv=None, colv=None, aux
         ws = torch.empty(lib.cn_softplus_adjoint_workspace_bytes(M, N) // 4 + 1, device=act.device, dtype=torch.float32)
     _lib.call("cn_softplus_adjoint", M, N, _ptr(D), _ld(D), _ptr(act), _ld(act), float(act_beta),
               _ptr(rowv), _ptr(colv), _ptr(aux1), _ld(aux1), _ptr(aux2), _ld(aux2), float(aux2_scale), _ptr(out),
-              _ld(out), _ptr(cs_out), _ptr(rs_out if cs_out is not None else None), float(cs_div), _ptr(ws),
+              _ld(out), int(out.dtype == torch.bfloat16), _ptr(cs_out), _ptr(rs_out if cs_out is not None else None), float(cs_div), _ptr(ws),
               0 if ws is None else ws.numel() * 4, _stream())
     return out
 
@@ -463,10 +505,12 @@ def colsum(X, K, out, *, w=None, wdiv=1.0, accumulate=False):
 
 
 def sdf_embed(x, multires, scale, U0, U4e=None, u4div=1.0):
+    """U0 = the encoding of x; U4e (fp32, or a bfloat16 operand image) = its first columns / u4div."""
     _need(x, "x")
     _need(U0, "U0")
+    _need(U4e, "U4e")
     _lib.call("cn_sdf_embed", x.shape[0], _ptr(x), _ld(x), multires, scale, U0.shape[1], _ptr(U0), _ld(U0),
-              _ptr(U4e), _ld(U4e), u4div, _stream())
+              _ptr(U4e), _ld(U4e), u4div, int(U4e is not None and U4e.dtype == torch.bfloat16), _stream())
     return U0
 
 
@@ -477,9 +521,12 @@ def sdf_grad_assemble(multires, scale, U0, Q0, QE, G):
 
 
 def sdf_tangent_prep(multires, scale, U0, v, T0, T4e=None, t4div=1.0):
+    """T0 = the tangent of the encoding along v; T4e (fp32, or a bfloat16 image) = its first columns / t4div."""
     _need(v, "v")
+    _need(T4e, "T4e")
     _lib.call("cn_sdf_tangent_prep", U0.shape[0], multires, scale, T0.shape[1], _ptr(U0), _ld(U0), _ptr(v),
-              _ld(v), _ptr(T0), _ld(T0), _ptr(T4e), _ld(T4e), t4div, _stream())
+              _ld(v), _ptr(T0), _ld(T0), _ptr(T4e), _ld(T4e), t4div, int(T4e is not None and T4e.dtype == torch.bfloat16),
+              _stream())
     return T0
 
 

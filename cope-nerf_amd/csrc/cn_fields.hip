@@ -14,9 +14,17 @@ namespace cn {
 
 __device__ __forceinline__ floatx4 ld4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
 __device__ __forceinline__ void st4(float* p, floatx4 v) { *reinterpret_cast<floatx4*>(p) = v; }
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+// 4 values into row m, columns 4g.. of a tail buffer: fp32, or (bf16) the RNE bf16 operand image
+__device__ __forceinline__ void st4_tail(void* base, bool bf16, int64_t m, int64_t ld, int g, floatx4 v) {
+    if (bf16)
+        *reinterpret_cast<bf16x4_t*>(static_cast<__bf16*>(base) + m * ld + 4 * g) = __builtin_convertvector(v, bf16x4_t);
+    else
+        st4(static_cast<float*>(base) + m * ld + 4 * g, v);
+}
 
 __global__ void sdf_embed_kernel(int M, const float* __restrict__ x, int64_t ldx, int L, float scale, int G,
-                                 float* U0, int64_t ld_u0, float* U4e, int64_t ld_u4, float u4div) {
+                                 float* U0, int64_t ld_u0, void* U4e, int64_t ld_u4, float u4div, bool u4b) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t m = idx / G;
     const int g = idx % G;
@@ -27,7 +35,7 @@ __global__ void sdf_embed_kernel(int M, const float* __restrict__ x, int64_t ldx
     if (U4e && g < ng) {
         floatx4 q;
         for (int c = 0; c < 4; ++c) q[c] = o[c] / u4div;
-        st4(U4e + m * ld_u4 + 4 * g, q);
+        st4_tail(U4e, u4b, m, ld_u4, g, q);
     }
 }
 
@@ -72,7 +80,7 @@ __global__ void sdf_grad_assemble_kernel(int M, int L, float scale, int G, const
 // encoding along v = dL/d(gradient) (double backward of neus_fields.py:296).
 __global__ void sdf_tangent_prep_kernel(int M, int L, float scale, int G, const float* __restrict__ U0,
                                         int64_t ld_u0, const float* __restrict__ v, int64_t ld_v, float* T0,
-                                        int64_t ld_t0, float* T4e, int64_t ld_t4, float t4div) {
+                                        int64_t ld_t0, void* T4e, int64_t ld_t4, float t4div, bool t4b) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t m = idx / G;
     const int g = idx % G;
@@ -100,7 +108,7 @@ __global__ void sdf_tangent_prep_kernel(int M, int L, float scale, int G, const 
     if (T4e && g < ng) {
         floatx4 q4;
         for (int q = 0; q < 4; ++q) q4[q] = o[q] / t4div;
-        st4(T4e + m * ld_t4 + 4 * g, q4);
+        st4_tail(T4e, t4b, m, ld_t4, g, q4);
     }
 }
 
@@ -189,17 +197,18 @@ static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 using namespace cn;
 
 extern "C" int cn_sdf_embed(int32_t M, const float* x, int64_t ldx, int32_t multires, float scale, int32_t kpad,
-                            float* U0, int64_t ld_u0, float* U4e, int64_t ld_u4, float u4_scale, cn_stream_t stream) {
+                            float* U0, int64_t ld_u0, void* U4e, int64_t ld_u4, float u4_scale, int32_t u4_bf16,
+                            cn_stream_t stream) {
     CN_REQUIRE(x && U0, CN_ERR_ARG, "cn_sdf_embed: null pointer");
     CN_REQUIRE(multires >= 0 && 4 * (1 + 2 * multires) <= kpad && kpad % 4 == 0 && ld_u0 >= kpad && multires < 16,
                CN_ERR_SHAPE, "cn_sdf_embed: multires=%d kpad=%d ld_u0=%lld", multires, kpad, (long long)ld_u0);
-    CN_REQUIRE(al16(x) && al16(U0) && ldx % 4 == 0 && ld_u0 % 4 == 0 && (!U4e || (al16(U4e) && ld_u4 % 4 == 0)),
+    CN_REQUIRE(al16(x) && al16(U0) && ldx % 4 == 0 && ld_u0 % 4 == 0 && (!U4e || (((uintptr_t)U4e & 7) == 0 && ld_u4 % 4 == 0)),
                CN_ERR_ALIGN, "cn_sdf_embed: alignment");
     if (M == 0) return CN_OK;
     const int G = kpad / 4;
     const int64_t tot = (int64_t)M * G;
     sdf_embed_kernel<<<(int)((tot + 255) / 256), 256, 0, (hipStream_t)stream>>>(
-        M, x, ldx, multires, scale, G, U0, ld_u0, U4e, ld_u4, u4_scale == 0.f ? 1.f : u4_scale);
+        M, x, ldx, multires, scale, G, U0, ld_u0, U4e, ld_u4, u4_scale == 0.f ? 1.f : u4_scale, u4_bf16 != 0);
     return check_launch("cn_sdf_embed");
 }
 
@@ -221,18 +230,20 @@ extern "C" int cn_sdf_grad_assemble(int32_t M, int32_t multires, float scale, co
 }
 
 extern "C" int cn_sdf_tangent_prep(int32_t M, int32_t multires, float scale, int32_t kpad, const float* U0,
-                                   int64_t ld_u0, const float* v, int64_t ld_v, float* T0, int64_t ld_t0, float* T4e,
-                                   int64_t ld_t4, float t4_scale, cn_stream_t stream) {
+                                   int64_t ld_u0, const float* v, int64_t ld_v, float* T0, int64_t ld_t0, void* T4e,
+                                   int64_t ld_t4, float t4_scale, int32_t t4_bf16, cn_stream_t stream) {
     CN_REQUIRE(U0 && v && T0, CN_ERR_ARG, "cn_sdf_tangent_prep: null pointer");
     CN_REQUIRE(4 * (1 + 2 * multires) <= kpad && kpad % 4 == 0 && ld_t0 >= kpad, CN_ERR_SHAPE,
                "cn_sdf_tangent_prep: kpad");
-    CN_REQUIRE(al16(U0) && al16(v) && al16(T0) && (!T4e || al16(T4e)) && ld_v % 4 == 0 && ld_t0 % 4 == 0,
+    CN_REQUIRE(al16(U0) && al16(v) && al16(T0) && (!T4e || (((uintptr_t)T4e & 7) == 0 && ld_t4 % 4 == 0)) &&
+                   ld_v % 4 == 0 && ld_t0 % 4 == 0,
                CN_ERR_ALIGN, "cn_sdf_tangent_prep: alignment");
     if (M == 0) return CN_OK;
     const int G = kpad / 4;
     const int64_t tot = (int64_t)M * G;
     sdf_tangent_prep_kernel<<<(int)((tot + 255) / 256), 256, 0, (hipStream_t)stream>>>(
-        M, multires, scale, G, U0, ld_u0, v, ld_v, T0, ld_t0, T4e, ld_t4, t4_scale == 0.f ? 1.f : t4_scale);
+        M, multires, scale, G, U0, ld_u0, v, ld_v, T0, ld_t0, T4e, ld_t4, t4_scale == 0.f ? 1.f : t4_scale,
+        t4_bf16 != 0);
     return check_launch("cn_sdf_tangent_prep");
 }
 

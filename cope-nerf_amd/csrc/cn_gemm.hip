@@ -78,11 +78,16 @@ struct LinearArgs {
 //         the fp32 image's geometry (conflict-free fragment reads, and the C tile
 //         parks in one slab).
 // The accumulator layout of the two MFMAs is the same, so the epilogue is shared.
+// MODE_ bit 2 (MODE 1 only): A / A2 are bf16 operand images (16-byte pieces of 8 values land on
+//         the LDS rows as they are: no conversion); bit 3: aux0 is a bf16 image (BWD_RELU).
 constexpr int kTblCols = 512;  // widest N with a bias / colv (the LDS column table)
 
 template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int EPI, bool ROWV, int MODE_>
 __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel(LinearArgs p) {
     constexpr int MODE = MODE_ & 3;         // the GEMM mode (0 fp32, 1 bf16, 2 bf16x6)
+    constexpr bool ABF = (MODE_ & 4) != 0;  // A, A2 bf16 images
+    constexpr bool AUXB = (MODE_ & 8) != 0; // aux0 a bf16 image
+    static_assert(!ABF || MODE == 1, "bf16 A images only in the bf16 MFMA mode");
     constexpr int NT = 64 * WM * WN;
     const float* const cA = p.A;
     const float* const cB = p.B;
@@ -96,7 +101,9 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     // padded LDS row in dwords: 36 in every mode (BK = 32 f32 / 64 bf16 / 16 split: 3 x 8 + 12 pad)
     // (BK = 32 split: 3 x 16 + 4 pad = 52, conflict-free like wgrad_x6_kernel's rows)
     constexpr int LS = (BF ? NPL * BK / 2 : BK) + (MODE == 2 && BK == 16 ? 12 : 4);
-    constexpr int KC4 = BK / 4;                  // A: fp32 float4 per staged row
+    constexpr int EPA = ABF ? 8 : 4;             // A elements per 16-byte staging piece
+    constexpr int ESA = ABF ? 2 : 4;             // bytes per A element
+    constexpr int KC4 = BK / EPA;                // A: 16-byte pieces per staged row
     static_assert(NT % KC4 == 0, "staging rows");
     constexpr int RSTEP = NT / KC4;  // staged A rows per load instruction
     constexpr int KCB = BF ? NPL * BK / 8 : BK / 4;  // B: 16-byte pieces per staged row (all planes)
@@ -141,7 +148,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     const int ntiles = ((p.n_tiles_m + 7) / 8) * 8 * T;
     const int nk = p.K / BK;
 
-    // staging: thread tid loads A rows tid/KC4 + q*RSTEP (fp32 float4 column tid%KC4)
+    // staging: thread tid loads A rows tid/KC4 + q*RSTEP (16-byte piece tid%KC4: 4 fp32 or 8 bf16)
     // and B rows tid/KCB + q*RSTEPB (16-byte piece tid%KCB)
     const int srow = tid / KC4, sc4 = tid % KC4;
     const int srowb = tid / KCB, scb = tid % KCB;
@@ -149,8 +156,8 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     int ldsB[BLD];                      // MODE 2: LDS dword offset of B piece q within a buffer
 #pragma unroll
     for (int q = 0; q < ALD; ++q) {
-        voA[q] = ((srow + q * RSTEP) * p.lda + sc4 * 4) * 4;
-        voA2[q] = ((srow + q * RSTEP) * p.lda2 + sc4 * 4) * 4;
+        voA[q] = ((srow + q * RSTEP) * p.lda + sc4 * EPA) * ESA;
+        voA2[q] = ((srow + q * RSTEP) * p.lda2 + sc4 * EPA) * ESA;
     }
 #pragma unroll
     for (int q = 0; q < BLD; ++q) {
@@ -166,8 +173,9 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             voB[q] = (srowb + q * RSTEPB) * p.ldb * ESZB + scb * 16;
         }
     }
-    // LDS write offsets in dwords: A as fp32 float4 (4 dwords) or bf16x4 (2 dwords); B 16-byte pieces
-    const int lds_a = srow * LS + sc4 * (BF ? 2 : 4);
+    // LDS write offsets in dwords: A as fp32 float4 (4 dwords), bf16x4 (2 dwords) or a bf16x8 piece
+    // (4 dwords); B 16-byte pieces
+    const int lds_a = srow * LS + sc4 * (ABF || !BF ? 4 : 2);
     const int lds_b = srowb * LS + scb * 4;
 
     floatx4 ra[DEPTH][ALD], rb[DEPTH][BLD];
@@ -179,12 +187,13 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         const int k0 = kc * BK;
         const int rows = valid ? min(BM, p.M - m0) : 0;
         const bool second = k0 >= p.K1;  // wave-uniform: A2 half of a virtual concat
-        const float* abase = second ? p.A2 + (int64_t)m0 * p.lda2 : cA + (int64_t)m0 * p.lda;
+        const char* abase = second ? reinterpret_cast<const char*>(p.A2) + (int64_t)m0 * p.lda2 * ESA
+                                   : reinterpret_cast<const char*>(cA) + (int64_t)m0 * p.lda * ESA;
         const int ald = second ? p.lda2 : p.lda;
         const int ak = second ? k0 - p.K1 : k0;
-        const rsrc_t rA = make_view(abase, rows * ald * 4);
+        const rsrc_t rA = make_view(reinterpret_cast<const float*>(abase), rows * ald * ESA);
 #pragma unroll
-        for (int q = 0; q < ALD; ++q) ra[set][q] = bload4(rA, second ? voA2[q] : voA[q], ak * 4);
+        for (int q = 0; q < ALD; ++q) ra[set][q] = bload4(rA, second ? voA2[q] : voA[q], ak * ESA);
         // MODE 2: chunk kc of the image is [ldb rows][48 bf16]; the tile's BN rows are 96 * BN contiguous bytes
         const int64_t bofs = MODE == 2 ? ((int64_t)kc * (BK / 16) * p.ldb + n0) * 96 : (int64_t)n0 * p.ldb * ESZB;
         const rsrc_t rB = make_view(reinterpret_cast<const float*>(reinterpret_cast<const char*>(cB) + bofs),
@@ -205,7 +214,9 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 *reinterpret_cast<bf16x4*>(a + q * RSTEP * LS) = x0;
                 *reinterpret_cast<bf16x4*>(a + q * RSTEP * LS + BK / 2) = x1;
                 *reinterpret_cast<bf16x4*>(a + q * RSTEP * LS + BK) = x2;
-            } else if constexpr (BF)
+            } else if constexpr (ABF)
+                *reinterpret_cast<floatx4*>(a + q * RSTEP * LS) = ra[set][q];  // 8 bf16 as they are
+            else if constexpr (BF)
                 *reinterpret_cast<bf16x4*>(a + q * RSTEP * LS) = __builtin_convertvector(ra[set][q], bf16x4);
             else
                 *reinterpret_cast<floatx4*>(a + q * RSTEP * LS) = ra[set][q];
@@ -263,6 +274,9 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     const int voX1 = (rr * p.ld_aux1 + 4 * c4) * 4;
     const int voX2 = (rr * p.ld_aux2 + 4 * c4) * 4;
     const int voS = (rr * p.ld_split + 4 * c4) * 4;
+    const int voX0b = (rr * p.ld_aux0 + 4 * c4) * 2;  // (AUXB) bf16 aux0
+    const int voO0b = (rr * p.ld_out0_b + 4 * c4) * 2;  // bf16 images of out0 / out1
+    const int voO1b = (rr * p.ld_out1_b + 4 * c4) * 2;
     const float c_exp = p.beta * 1.44269504088896341f;        // beta log2(e)
     const float c_thr = p.threshold * 1.44269504088896341f;   // threshold in the log2 domain
     const float c_log = 0.693147180559945309f / p.beta;       // ln(2) / beta
@@ -488,7 +502,14 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         // per-tile views, re-based on the pass's first row by SALU arithmetic (view_at)
         const TileView tO0 = {cOut0 + (int64_t)m0 * p.ld_out0 + n0, p.ld_out0, cOut0 ? (rows * p.ld_out0 - n0) * 4 : 0};
         const TileView tO1 = {p.out1 + (int64_t)m0 * p.ld_out1 + n0, p.ld_out1, p.out1 ? (rows * p.ld_out1 - n0) * 4 : 0};
-        const TileView tX0 = {p.aux0 + (int64_t)m0 * p.ld_aux0 + n0, p.ld_aux0, p.aux0 ? (rows * p.ld_aux0 - n0) * 4 : 0};
+        const TileView tX0 = AUXB ? tile_view_b16(p.aux0, p.ld_aux0, m0, n0, rows)
+                                  : TileView{p.aux0 + (int64_t)m0 * p.ld_aux0 + n0, p.ld_aux0,
+                                             p.aux0 ? (rows * p.ld_aux0 - n0) * 4 : 0};
+        // bf16 images of out0 / out1 (MODE 1; empty views when absent)
+        const TileView tO0b = tile_view_b16(p.out0_b, p.ld_out0_b, m0, n0, rows);
+        const TileView tO1b = tile_view_b16(p.out1_b, p.ld_out1_b, m0, n0, rows);
+        const bool has_b0 = MODE == 1 && p.out0_b != nullptr;  // wave-uniform
+        const bool has_b1 = MODE == 1 && p.out1_b != nullptr;
         const TileView tX1 = {p.aux1 + (int64_t)m0 * p.ld_aux1 + n0, p.ld_aux1, p.aux1 ? (rows * p.ld_aux1 - n0) * 4 : 0};
         const TileView tX2 = {p.aux2 + (int64_t)m0 * p.ld_aux2 + n0, p.ld_aux2, p.aux2 ? (rows * p.ld_aux2 - n0) * 4 : 0};
         const TileView tR = {p.rowv + m0, 1, ROWV ? rows * 4 : 0};
@@ -522,7 +543,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 const int lrow = part * PROWS + (g * GROUP + q) * RPP;  // wave-uniform slab row of the pass
                 // unconditional: the views make reads past a row (columns >= N) or
                 // past the last row harmless, and only region-0 lanes use the values
-                if (kAux0) x0[slot][q] = bload4(view_at(tX0, lrow), voX0, 0);
+                if (kAux0) x0[slot][q] = AUXB ? bload_b16x4(view_at(tX0, lrow), voX0b, 0) : bload4(view_at(tX0, lrow), voX0, 0);
                 if (kAux1) x1[slot][q] = bload4(view_at(tX1, lrow), voX1, 0);
                 if (kAux1) x2[slot][q] = bload4(view_at(tX2, lrow), voX2, 0);
                 if (ROWV) rv[slot][q] = bload1(view_at(tR, lrow), rr * 4, 0);
@@ -612,11 +633,20 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         const int lrow = part * PROWS + (pb + q) * RPP;
                         const floatx4 v = *reinterpret_cast<const floatx4*>(sC + (rr + (pb + q) * RPP) * CS + 4 * c4);
                         floatx4 o0;
+                        // the bf16 images of the values stored to out0 / out1 (MODE 1)
+                        auto sb0 = [&](const floatx4& w) {
+                            if (has_b0) bstore_b16x4(view_at(tO0b, lrow), voO0b, 0, w);
+                        };
+                        auto sb1 = [&](const floatx4& w) {
+                            if (has_b1) bstore_b16x4(view_at(tO1b, lrow), voO1b, 0, w);
+                        };
+                        const floatx4 zero4 = {0.f, 0.f, 0.f, 0.f};
                         if constexpr (kHead) {  // the row's activation, the ∇-pass seed, the head row-dot
                             float part = 0.0f;
                             if (MAIN || region == 0) {
                                 main_vals(v, slot, q, o0);
                                 bstore4(view_at(tO0, lrow), voO0, 0, o0);  // (out0 NULL: empty view)
+                                sb0(o0);
                                 floatx4 s1;
 #pragma unroll
                                 for (int e = 0; e < 4; ++e) {
@@ -624,9 +654,12 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                                     s1[e] = colv[e] * sigma_from_act(o0[e], p.aux_c);
                                 }
                                 bstore4(view_at(tO1, lrow), voO1, 0, s1);  // (out1 NULL: empty view)
+                                sb1(s1);
                             } else if (region == 2) {
-                                bstore4(view_at(tO0, lrow), voO0, 0, floatx4{0.f, 0.f, 0.f, 0.f});
-                                bstore4(view_at(tO1, lrow), voO1, 0, floatx4{0.f, 0.f, 0.f, 0.f});
+                                bstore4(view_at(tO0, lrow), voO0, 0, zero4);
+                                bstore4(view_at(tO1, lrow), voO1, 0, zero4);
+                                sb0(zero4);
+                                sb1(zero4);
                             }
                             // row sum over the C4 lanes holding the row (fixed butterfly order)
 #pragma unroll
@@ -641,16 +674,22 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         if constexpr (MAIN) {
                             main_vals(v, slot, q, o0);
                             bstore4(view_at(tO0, lrow), voO0, 0, o0);
+                            sb0(o0);
                         } else if (region == 0) {
                             main_vals(v, slot, q, o0);
                             bstore4(view_at(tO0, lrow), voO0, 0, o0);
+                            sb0(o0);
                         } else if (region == 1) {  // EPI_MUL split columns: raw (A·Bᵀ)/adiv
 #pragma unroll
                             for (int e = 0; e < 4; ++e) o0[e] = v[e] * p.inv_adiv;
                             bstore4(view_at(tS, lrow), voS, 0, o0);
-                            if (col < cNzero) bstore4(view_at(tO0, lrow), voO0, 0, floatx4{0.f, 0.f, 0.f, 0.f});
+                            if (col < cNzero) {
+                                bstore4(view_at(tO0, lrow), voO0, 0, zero4);
+                                sb0(zero4);
+                            }
                         } else if (region == 2) {  // zero fill (region 3: past nzero, untouched)
-                            bstore4(view_at(tO0, lrow), voO0, 0, floatx4{0.f, 0.f, 0.f, 0.f});
+                            bstore4(view_at(tO0, lrow), voO0, 0, zero4);
+                            sb0(zero4);
                         }
                     }
                 }
@@ -689,16 +728,34 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 live[j] = col < cN;
             }
         };
+        // bf16 images from the MFMA layout (MODE 1): lanes 2c and 2c + 1 hold columns 2c, 2c + 1 of
+        // accumulator rows r (even) and r + 1; they swap one value (DPP) so the even lane writes
+        // (row r: 2c, 2c + 1) and the odd lane (row r + 1: 2c, 2c + 1), one dword each.  Per column
+        // block j the lane's byte offset (row r + 1 for odd lanes), or one past any view for
+        // columns >= nzero (the pair's columns are both below or both past it: nzero % 4 == 0).
+        const bool odd = lane & 1;
+        auto bimg_cols = [&](int ld, int lrow, int lcol, int* vbj) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int c = lcol - (odd ? 1 : 0) + 32 * j;
+                vbj[j] = n0 + c < cNzero ? ((lrow + (odd ? 1 : 0)) * ld + c) * 2 : (1 << 30);
+            }
+        };
+        auto bimg_pair = [&](const TileView& t, int rowi, int vb, float o_r, float o_r1) {
+            const float recv = lane_xor1(odd ? o_r : o_r1);
+            bstore_b16x2(view_at(t, rowi), vb, 0, odd ? recv : o_r, odd ? o_r1 : recv);
+        };
         auto direct_aux = [&]() {
             const int lrow = wm * TM * 32 + 4 * (lane >> 5);
             const int lcol = wn * TN * 32 + (lane & 31);
             const int vo = (lrow * p.ld_out0 + lcol) * 4;
-            const int v0 = (lrow * p.ld_aux0 + lcol) * 4;
+            const int v0 = (lrow * p.ld_aux0 + lcol) * (AUXB ? 2 : 4);
             const int v1 = (lrow * p.ld_aux1 + lcol) * 4;
             const int v2 = (lrow * p.ld_aux2 + lcol) * 4;
-            int voj[TN];
+            int voj[TN], vbj[TN];
             bool live[TN];
             direct_cols(vo, lcol, voj, live);
+            if (has_b0) bimg_cols(p.ld_out0_b, lrow, lcol, vbj);
             // EPI_MUL with a split output (the skip layer's ∇ pass: columns [nsplit, N) are the
             // embedding's adjoint, written raw (A·Bᵀ)/adiv to out_split while out0 is zero-filled
             // there; p.nsplit = N without a split)
@@ -710,8 +767,9 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 spl[j] = EPI == CN_EPI_MUL && c >= p.nsplit && c < cN;
                 vsj[j] = (lrow * p.ld_split + lcol + 32 * j) * 4;
             }
-            constexpr int RG = kAux1 ? 2 : 4;          // accumulator rows r per group
+            constexpr int RG = kAux1 ? 2 : 4;          // accumulator rows r per group (even: bf16 pairs)
             constexpr int NGD = TM * 16 / RG;          // groups per tile
+            constexpr int ASTEP = AUXB ? 64 : 128;     // bytes per 32-column block of aux0
             float xa[2][RG][TN], xb[2][RG][TN], xc[2][RG][TN];
             auto dload = [&](int g, int sl) {
                 const int i = g / (16 / RG), r0 = (g % (16 / RG)) * RG;
@@ -720,7 +778,8 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                     const int r = r0 + q, row = i * 32 + (r & 3) + 8 * (r >> 2);
 #pragma unroll
                     for (int j = 0; j < TN; ++j) {
-                        xa[sl][q][j] = bload1(view_at(tX0, row), v0, 128 * j);
+                        xa[sl][q][j] = AUXB ? bload_b16(view_at(tX0, row), v0, ASTEP * j)
+                                            : bload1(view_at(tX0, row), v0, ASTEP * j);
                         if (kAux1) xb[sl][q][j] = bload1(view_at(tX1, row), v1, 128 * j);
                         if (kAux1) xc[sl][q][j] = bload1(view_at(tX2, row), v2, 128 * j);
                     }
@@ -732,11 +791,13 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 const int sl = g & 1;
                 if (g + 1 < NGD) dload(g + 1, sl ^ 1);
                 const int i = g / (16 / RG), r0 = (g % (16 / RG)) * RG;
+                float prev[TN];  // row r - 1's stored values (bf16 pairs)
 #pragma unroll
                 for (int q = 0; q < RG; ++q) {
                     const int r = r0 + q;
                     const int rowi = i * 32 + (r & 3) + 8 * (r >> 2);
                     const rsrc_t vw = view_at(tO0, rowi);
+                    float ov[TN];
 #pragma unroll
                     for (int j = 0; j < TN; ++j) {
                         const float u = acc[i][j][r] * p.inv_adiv;
@@ -744,6 +805,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                             if (spl[j]) {
                                 bstore1(view_at(tS, rowi), vsj[j], 0, u);
                                 bstore1(vw, voj[j], 0, 0.0f);
+                                ov[j] = 0.0f;
                                 continue;
                             }
                         }
@@ -759,7 +821,17 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                             const float rr2 = sg > 0.0f ? (1.0f - sg) * __builtin_amdgcn_rcpf(sg) : 0.0f;
                             o = u * sg + xb[sl][q][j] * xc[sl][q][j] * (p.aux2_scale * rr2);
                         }
-                        bstore1(vw, voj[j], 0, live[j] ? o : 0.0f);
+                        ov[j] = live[j] ? o : 0.0f;
+                        bstore1(vw, voj[j], 0, ov[j]);
+                    }
+                    if (has_b0) {
+                        if (r & 1) {
+#pragma unroll
+                            for (int j = 0; j < TN; ++j) bimg_pair(tO0b, rowi - 1, vbj[j], prev[j], ov[j]);
+                        } else {
+#pragma unroll
+                            for (int j = 0; j < TN; ++j) prev[j] = ov[j];
+                        }
                     }
                 }
             }
@@ -768,17 +840,21 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             const int lrow = wm * TM * 32 + 4 * (lane >> 5);
             const int lcol = wn * TN * 32 + (lane & 31);
             const int vo = (lrow * p.ld_out0 + lcol) * 4;
-            int voj[TN];
+            int voj[TN], vbj[TN];
             bool live[TN];
             direct_cols(vo, lcol, voj, live);
+            if (has_b0) bimg_cols(p.ld_out0_b, lrow, lcol, vbj);
             float bj[TN];
 #pragma unroll
             for (int j = 0; j < TN; ++j) bj[j] = kBias ? sBias[min(n0 + lcol + 32 * j, kTblCols - 1)] : 0.0f;
+            float prev[TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const rsrc_t vw = view_at(tO0, i * 32 + (r & 3) + 8 * (r >> 2));
+                    const int rowi = i * 32 + (r & 3) + 8 * (r >> 2);
+                    const rsrc_t vw = view_at(tO0, rowi);
+                    float ov[TN];
 #pragma unroll
                     for (int j = 0; j < TN; ++j) {
                         const float z = acc[i][j][r] * p.inv_adiv + bj[j];
@@ -786,16 +862,28 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         if constexpr (EPI == CN_EPI_SOFTPLUS) o = softplus_hw(z, c_exp, c_thr, c_log) * cInvOdiv;
                         else if constexpr (EPI == CN_EPI_RELU) o = z > 0.0f ? z : 0.0f;
                         else o = z;
-                        bstore1(vw, voj[j], 0, live[j] ? o : 0.0f);
+                        ov[j] = live[j] ? o : 0.0f;
+                        bstore1(vw, voj[j], 0, ov[j]);
+                    }
+                    if (has_b0) {
+                        if (r & 1) {
+#pragma unroll
+                            for (int j = 0; j < TN; ++j) bimg_pair(tO0b, rowi - 1, vbj[j], prev[j], ov[j]);
+                        } else {
+#pragma unroll
+                            for (int j = 0; j < TN; ++j) prev[j] = ov[j];
+                        }
                     }
                 }
         };
         auto direct_head = [&]() {
             const int lrow = wm * TM * 32 + 4 * (lane >> 5);
             const int lcol = wn * TN * 32 + (lane & 31);
-            int voj[TN], vo1[TN];
+            int voj[TN], vo1[TN], vbj[TN], vb1[TN];
             bool live[TN];
             direct_cols((lrow * p.ld_out0 + lcol) * 4, lcol, voj, live);
+            if (has_b0) bimg_cols(p.ld_out0_b, lrow, lcol, vbj);
+            if (has_b1) bimg_cols(p.ld_out1_b, lrow, lcol, vb1);
             float bj[TN], cj[TN], hj[TN];
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
@@ -806,6 +894,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 vo1[j] = voj[j] == (1 << 30) ? voj[j] : (lrow * p.ld_out1 + lcol + 32 * j) * 4;
             }
             float* sRed = sA + BM * LS;  // staging buffer 1 is free after the main loop (its last reader)
+            float prev0[TN], prev1[TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -814,13 +903,31 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                     const rsrc_t vw = view_at(tO0, rowi);
                     const rsrc_t vw1 = view_at(tO1, rowi);
                     float part = 0.0f;
+                    float ov0[TN], ov1[TN];
 #pragma unroll
                     for (int j = 0; j < TN; ++j) {
                         const float a = softplus_hw(acc[i][j][r] * p.inv_adiv + bj[j], c_exp, c_thr, c_log) * cInvOdiv;
                         const float o = live[j] ? a : 0.0f;
+                        ov0[j] = o;
+                        ov1[j] = live[j] ? cj[j] * sigma_from_act(a, p.aux_c) : 0.0f;
                         bstore1(vw, voj[j], 0, o);  // (out0 NULL: empty view)
-                        bstore1(vw1, vo1[j], 0, live[j] ? cj[j] * sigma_from_act(a, p.aux_c) : 0.0f);
+                        bstore1(vw1, vo1[j], 0, ov1[j]);
                         part += o * hj[j];
+                    }
+                    if (has_b0 || has_b1) {
+                        if (r & 1) {
+#pragma unroll
+                            for (int j = 0; j < TN; ++j) {
+                                if (has_b0) bimg_pair(tO0b, rowi - 1, vbj[j], prev0[j], ov0[j]);
+                                if (has_b1) bimg_pair(tO1b, rowi - 1, vb1[j], prev1[j], ov1[j]);
+                            }
+                        } else {
+#pragma unroll
+                            for (int j = 0; j < TN; ++j) {
+                                prev0[j] = ov0[j];
+                                prev1[j] = ov1[j];
+                            }
+                        }
                     }
                     // the 32 lanes holding this row (lane >> 5 fixed), fixed butterfly order
 #pragma unroll
@@ -948,6 +1055,14 @@ __global__ void __launch_bounds__(256) scale_cols_kernel(int M, int N4, const fl
     }
 }
 
+// 4 values at element offset i of an fp32 output, or of its bf16 operand image (ob)
+__device__ __forceinline__ void store_row4(void* out, bool ob, int64_t i, floatx4 v) {
+    if (ob)
+        *reinterpret_cast<bf16x4*>(static_cast<bf16_t*>(out) + i) = __builtin_convertvector(v, bf16x4);
+    else
+        *reinterpret_cast<floatx4*>(static_cast<float*>(out) + i) = v;
+}
+
 // Adjoint of a softplus layer without a GEMM, when the upstream gradient of its output
 // is already at hand (the SDF's last hidden layer once the feature head is folded into
 // the colour network):  out = (D + rowv (x) colv) * sg + aux1 * aux2 * c2 * (1 - sg) / sg,
@@ -958,7 +1073,7 @@ __global__ void __launch_bounds__(256) softplus_adjoint_kernel(int M, int N4, co
                                                                const float* __restrict__ colv,
                                                                const float* __restrict__ aux1, int64_t ld1,
                                                                const float* __restrict__ aux2, int64_t ld2, float c2,
-                                                               float* out, int64_t ldo) {
+                                                               void* out, int64_t ldo, bool ob) {
     const int64_t tot = (int64_t)M * N4;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += stride) {
@@ -979,7 +1094,7 @@ __global__ void __launch_bounds__(256) softplus_adjoint_kernel(int M, int N4, co
             const float rr = sg > 0.0f ? (1.0f - sg) * __builtin_amdgcn_rcpf(sg) : 0.0f;
             o[e] = g[e] * sg + s1[e] * s2[e] * (c2 * rr);
         }
-        *reinterpret_cast<floatx4*>(out + m * ldo + n) = o;
+        store_row4(out, ob, m * ldo + n, o);
     }
 }
 
@@ -995,8 +1110,8 @@ __global__ void __launch_bounds__(256) softplus_adjoint_cs_kernel(int M, int N4,
                                                                   const float* __restrict__ colv,
                                                                   const float* __restrict__ aux1, int64_t ld1,
                                                                   const float* __restrict__ aux2, int64_t ld2,
-                                                                  float c2, float* out, int64_t ldo, float* part,
-                                                                  float* rpart) {
+                                                                  float c2, void* out, int64_t ldo, bool ob,
+                                                                  float* part, float* rpart) {
     __shared__ floatx4 red[256];
     __shared__ float redr[256];
     const int c = threadIdx.x % N4;
@@ -1024,7 +1139,7 @@ __global__ void __launch_bounds__(256) softplus_adjoint_cs_kernel(int M, int N4,
             const float rr = sg > 0.0f ? (1.0f - sg) * __builtin_amdgcn_rcpf(sg) : 0.0f;
             o[e] = g[e] * sg + s1[e] * s2[e] * (c2 * rr);
         }
-        *reinterpret_cast<floatx4*>(out + (int64_t)m * ldo + n) = o;
+        store_row4(out, ob, (int64_t)m * ldo + n, o);
         cs = cs + rv * a + s2;
         rs += rv;
     };
@@ -1189,8 +1304,8 @@ static int device_cus() {
     return cached_cus;
 }
 
-template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int MODE = 0>
-static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_t s) {
+template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int MODE_>
+static int launch_linear_tile_m(const cn_linear_desc* d, LinearArgs& a, hipStream_t s) {
     constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
     if (d->epilogue == CN_EPI_SOFTPLUS_HEAD && d->N > BN) {
         set_error("cn_linear: SOFTPLUS_HEAD with N=%d needs a tile of >= N columns (this mode / tile: %d)", d->N, BN);
@@ -1201,11 +1316,16 @@ static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_
     const int ntiles = cdiv(a.n_tiles_m, 8) * 8 * a.n_tiles_n;
     const int grid = std::min(ntiles, OCC * device_cus());  // OCC resident workgroups per CU
     dim3 block(64 * WM * WN);
+    // (a bf16 aux0 -- MODE_ bit 3 -- only for BWD_RELU, without a rank-1 term: host-checked)
     switch (d->epilogue) {
-#define CN_EPI_CASE(E)                                                                     \
-        case E:                                                                            \
-            if (d->rowv) linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, E, true, MODE><<<grid, block, 0, s>>>(a); \
-            else linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, E, false, MODE><<<grid, block, 0, s>>>(a);        \
+#define CN_EPI_CASE(E)                                                                                   \
+        case E:                                                                                          \
+            if constexpr ((MODE_ & 8) == 0 || E == CN_EPI_BWD_RELU) {                                     \
+                if (d->rowv && (MODE_ & 8) == 0)                                                         \
+                    linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, E, (MODE_ & 8) == 0, MODE_><<<grid, block, 0, s>>>(a); \
+                else                                                                                     \
+                    linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, E, false, MODE_><<<grid, block, 0, s>>>(a); \
+            }                                                                                            \
             break;
         CN_EPI_CASE(CN_EPI_STORE)
         CN_EPI_CASE(CN_EPI_SOFTPLUS)
@@ -1219,6 +1339,25 @@ static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_
         default: set_error("cn_linear: bad epilogue %d", d->epilogue); return CN_ERR_ARG;
     }
     return check_launch("cn_linear");
+}
+
+// The template MODE_ of a descriptor on a tile of GEMM mode MODE: + 4 for bf16 A images, + 8 for a
+// bf16 aux0 (MODE 1 only).
+static int linear_mode_bits(const cn_linear_desc* d, int mode) {
+    return mode == 1 ? mode + (d->a_bf16 ? 4 : 0) + (d->aux0_bf16 ? 8 : 0) : mode;
+}
+
+template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int MODE = 0>
+static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_t s) {
+    if constexpr (MODE == 1) {
+        switch (linear_mode_bits(d, MODE)) {
+            case 5: return launch_linear_tile_m<WM, WN, TM, TN, BK, OCC, DEPTH, 5>(d, a, s);
+            case 9: return launch_linear_tile_m<WM, WN, TM, TN, BK, OCC, DEPTH, 9>(d, a, s);
+            case 13: return launch_linear_tile_m<WM, WN, TM, TN, BK, OCC, DEPTH, 13>(d, a, s);
+            default: break;
+        }
+    }
+    return launch_linear_tile_m<WM, WN, TM, TN, BK, OCC, DEPTH, MODE>(d, a, s);
 }
 
 
@@ -1290,8 +1429,20 @@ static int linear_plan(const cn_linear_desc* d, LinearArgs& a) {
     const bool x6 = d->mfma_dtype == CN_MFMA_F32_BF16X6;
     CN_REQUIRE(d->K % (bf ? 64 : 32) == 0, CN_ERR_SHAPE, "cn_linear: K=%d must be a multiple of %d", d->K, bf ? 64 : 32);
     CN_REQUIRE(d->tile >= 0 && d->tile <= 2, CN_ERR_ARG, "cn_linear: bad tile %d", d->tile);
-    CN_REQUIRE(!d->a_bf16 && !d->aux0_bf16 && !d->out0_b && !d->out1_b, CN_ERR_UNSUPPORTED,
-               "cn_linear: bf16 operand images are not built yet");
+    if (d->a_bf16 || d->aux0_bf16 || d->out0_b || d->out1_b) {  // bf16 operand images (ABI v10)
+        CN_REQUIRE(bf, CN_ERR_UNSUPPORTED, "cn_linear: bf16 operand images need mfma_dtype CN_MFMA_BF16");
+        CN_REQUIRE(!d->a_bf16 || (d->lda % 8 == 0 && (!d->A2 || d->lda2 % 8 == 0)), CN_ERR_ALIGN,
+                   "cn_linear: bf16 A / A2 need lda, lda2 multiples of 8");
+        CN_REQUIRE(!d->aux0_bf16 || (d->epilogue == CN_EPI_BWD_RELU && !d->rowv && d->ld_aux0 % 8 == 0),
+                   CN_ERR_UNSUPPORTED, "cn_linear: a bf16 aux0 is for BWD_RELU (no rowv, ld_aux0 % 8 == 0)");
+        CN_REQUIRE(!d->out0_b || (al16(d->out0_b) && d->ld_out0_b % 8 == 0 && d->ld_out0_b < (1 << 20) &&
+                                  d->ld_out0_b >= std::max(d->nzero, d->N)),
+                   CN_ERR_ALIGN, "cn_linear: out0_b needs 16-byte alignment and ld_out0_b >= nzero, % 8 == 0");
+        CN_REQUIRE(!d->out1_b || (d->epilogue == CN_EPI_SOFTPLUS_HEAD && d->out1 && al16(d->out1_b) &&
+                                  d->ld_out1_b % 8 == 0 && d->ld_out1_b < (1 << 20) &&
+                                  d->ld_out1_b >= std::max(d->nzero, d->N)),
+                   CN_ERR_ARG, "cn_linear: out1_b is SOFTPLUS_HEAD's image of out1 (16-byte aligned, ld % 8 == 0)");
+    }
     const int K1 = d->A2 ? d->K1 : d->K;
     CN_REQUIRE(K1 > 0 && K1 <= d->K && K1 % (bf ? 64 : 32) == 0, CN_ERR_SHAPE, "cn_linear: bad K1=%d", K1);
     CN_REQUIRE(d->lda >= K1 && d->lda % 4 == 0 && al16(d->A), CN_ERR_ALIGN,
@@ -1372,6 +1523,10 @@ static int linear_plan(const cn_linear_desc* d, LinearArgs& a) {
     a.inv_odiv = 1.0f / odiv;
     a.beta = d->beta;
     a.threshold = d->threshold;
+    a.out0_b = static_cast<bf16_t*>(d->out0_b);
+    a.out1_b = static_cast<bf16_t*>(d->out1_b);
+    a.ld_out0_b = (int)d->ld_out0_b;
+    a.ld_out1_b = (int)d->ld_out1_b;
     return CN_OK;
 }
 
@@ -1396,12 +1551,12 @@ extern "C" int cn_linear_kernel_name(const cn_linear_desc* d, char* buf, int32_t
     int mode = 0;
     switch (choose_linear_tile(d)) {
 #define CN_TILE_NAME(T, WM, WN, TM, TN, BK, OCC, DEPTH, MODE) \
-        case T: args = #WM ", " #WN ", " #TM ", " #TN ", " #BK ", " #OCC ", " #DEPTH; mode = MODE; break;
+        case T: args = #WM ", " #WN ", " #TM ", " #TN ", " #BK ", " #OCC ", " #DEPTH; mode = linear_mode_bits(d, MODE); break;
         CN_LINEAR_TILES(CN_TILE_NAME)
 #undef CN_TILE_NAME
     }
     const int n = snprintf(buf, (size_t)len, "void cn::linear_kernel<%s, %d, %s, %d>(cn::LinearArgs)", args,
-                           d->epilogue, d->rowv ? "true" : "false", mode);
+                           d->epilogue, d->rowv && !d->aux0_bf16 ? "true" : "false", mode);
     CN_REQUIRE(n < len, CN_ERR_SHAPE, "cn_linear_kernel_name: buffer of %d bytes too small (%d)", len, n + 1);
     return n;
 }
@@ -1440,9 +1595,9 @@ extern "C" size_t cn_softplus_adjoint_workspace_bytes(int32_t M, int32_t N) {
 
 extern "C" int cn_softplus_adjoint(int32_t M, int32_t N, const float* D, int64_t ldd, const float* act, int64_t lda,
                                    float act_beta, const float* rowv, const float* colv, const float* aux1,
-                                   int64_t ld1, const float* aux2, int64_t ld2, float aux2_scale, float* out,
-                                   int64_t ld_out, float* cs_out, float* rs_out, float cs_div, float* workspace,
-                                   int64_t workspace_bytes, cn_stream_t stream) {
+                                   int64_t ld1, const float* aux2, int64_t ld2, float aux2_scale, void* out,
+                                   int64_t ld_out, int32_t out_bf16, float* cs_out, float* rs_out, float cs_div,
+                                   float* workspace, int64_t workspace_bytes, cn_stream_t stream) {
     CN_REQUIRE(act && out && act_beta > 0.0f, CN_ERR_ARG, "cn_softplus_adjoint: act, out and act_beta > 0 required");
     CN_REQUIRE((rowv == nullptr) == (colv == nullptr) && (aux1 == nullptr) == (aux2 == nullptr), CN_ERR_ARG,
                "cn_softplus_adjoint: rowv/colv and aux1/aux2 go together");
@@ -1465,7 +1620,7 @@ extern "C" int cn_softplus_adjoint(int32_t M, int32_t N, const float* D, int64_t
         float* rpart = rs_out ? workspace + (size_t)nblk * N : nullptr;
         softplus_adjoint_cs_kernel<<<nblk, 256, 0, s>>>(M, N / 4, D, ldd, act, lda, -act_beta * 1.44269504088896341f,
                                                         rowv, colv, aux1, ld1, aux2, ld2, aux2_scale, out, ld_out,
-                                                        workspace, rpart);
+                                                        out_bf16 != 0, workspace, rpart);
         int rc = check_launch("cn_softplus_adjoint");
         if (rc) return rc;
         const float dv = cs_div == 0.f ? 1.f : cs_div;
@@ -1477,7 +1632,8 @@ extern "C" int cn_softplus_adjoint(int32_t M, int32_t N, const float* D, int64_t
     const int blocks = (int)std::min<int64_t>((tot + 255) / 256, 8192);
     softplus_adjoint_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(M, N / 4, D, ldd, act, lda,
                                                                      -act_beta * 1.44269504088896341f, rowv, colv,
-                                                                     aux1, ld1, aux2, ld2, aux2_scale, out, ld_out);
+                                                                     aux1, ld1, aux2, ld2, aux2_scale, out, ld_out,
+                                                                     out_bf16 != 0);
     return check_launch("cn_softplus_adjoint");
 }
 

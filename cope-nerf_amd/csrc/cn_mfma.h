@@ -52,6 +52,42 @@ __device__ __forceinline__ void bstore4(rsrc_t r, int voff, int soff, floatx4 v)
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, soff, 0);
 }
 
+// bf16 operand images (ABI v10): a tile's rows of a bf16 tensor (ld in bf16 elements, a
+// multiple of 8) as the float-typed TileView over the same bytes (rows ld / 2 floats apart), so
+// view_at works unchanged; voffsets into it are byte offsets, as for fp32 views.
+__device__ __forceinline__ TileView tile_view_b16(const void* base, int ld, int64_t row0, int col0, int rows) {
+    const char* b = static_cast<const char*>(base) + (row0 * ld + col0) * 2;
+    return TileView{reinterpret_cast<const float*>(b), ld / 2, base ? (rows * ld - col0) * 2 : 0};
+}
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+// one bf16 read as the fp32 value it represents
+__device__ __forceinline__ float bload_b16(rsrc_t r, int voff, int soff) {
+    const unsigned short h = __builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, 0);
+    return __builtin_bit_cast(float, (unsigned)h << 16);
+}
+// four bf16 (8 bytes) as fp32 values
+__device__ __forceinline__ floatx4 bload_b16x4(rsrc_t r, int voff, int soff) {
+    const u32x2_t w = __builtin_bit_cast(u32x2_t, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+    return floatx4{__builtin_bit_cast(float, w[0] << 16), __builtin_bit_cast(float, w[0] & 0xffff0000u),
+                   __builtin_bit_cast(float, w[1] << 16), __builtin_bit_cast(float, w[1] & 0xffff0000u)};
+}
+// RNE bf16 of two / four fp32 values (v_cvt_pk_bf16_f32: the rounding the GEMM staging applies)
+__device__ __forceinline__ void bstore_b16x2(rsrc_t r, int voff, int soff, float a, float b) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const bf16x2_t h = __builtin_convertvector((f2){a, b}, bf16x2_t);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, h), r, voff, soff, 0);
+}
+__device__ __forceinline__ void bstore_b16x4(rsrc_t r, int voff, int soff, floatx4 v) {
+    typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+    const b4 h = __builtin_convertvector(v, b4);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, h), r, voff, soff, 0);
+}
+// the value of the neighbouring lane (lane ^ 1): DPP quad_perm [1, 0, 3, 2]
+__device__ __forceinline__ float lane_xor1(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, true));
+}
+
 // torch.nn.Softplus(beta, threshold) on the hardware transcendentals: e = 2^(z beta
 // log2 e), a = log2(1 + e) ln2 / beta; the linear branch (beta z > threshold) exactly
 // as torch.  Absolute error of a is ~1e-9 (log2 of the rounded 1 + e; v_exp/v_log

@@ -22,6 +22,7 @@ struct WgradArgs {
     float* bpart;  // [nslices][Npad]
     int ldy0, ldx0, ldy1, ldx1;
     int M, Npad, Kpad, npairs, rows_per_slice, n_tiles_n, n_tiles_k, nslices;
+    int yb, xb;  // wgrad_b16r_kernel: the Y / X side are bf16 operand images
 };
 
 // Several independent weight gradients in one launch of the stage-ring kernel (cn_wgrad_batch):
@@ -656,6 +657,181 @@ __global__ void __launch_bounds__(512, 2) wgrad_x6r_kernel(WgradBatch batch) {
     }
 }
 
+// Whole-layer (256x256) bf16 weight gradient (config C3's bf16 MLP MFMA) on a stage ring: the
+// wgrad_x6r_kernel structure with one bf16 term per operand.  The products are the bf16 roundings
+// of Y and X (RNE while staging, or read as bf16 operand images: the same bits), so dW equals
+// wgrad_bf16_kernel's up to the fp32 summation order.  A stage is 32 sample rows: two buffers of
+// [256 Y rows | 256 X rows] x (16 dwords of 32 bf16 + 4 pad) = 2 x 40 KB (conflict-free fragment
+// reads), NRAW register sets of raw rows in flight, ONE barrier per stage; every wave does 16
+// v_mfma_f32_32x32x16_bf16 per stage (2x4 accumulators of 32x32: 64 n x 128 k).  This shape is
+// HBM-bound (32 KB of fp32 operands per stage for 256 MFMA cycles per SIMD), so what matters is
+// the bytes in flight and reading each operand once: waves 0-3 stage Y, waves 4-7 X, each side fp32
+// (m-quad t % 8 of the 4-column groups t / 8 and t / 8 + 32) or a bf16 image (m-quad t % 8 of the
+// 8-column group t / 8), decided per job and side (WgradArgs::yb / xb: wave-uniform branches).
+template <int NRAW>
+__global__ void __launch_bounds__(512, 2) wgrad_b16r_kernel(WgradBatch batch) {
+    constexpr int BNo = 256, MC = 32, PL = MC / 2, LSB = PL + 4;  // 20 dwords per LDS row
+    constexpr int IMG = 2 * BNo * LSB;                              // one buffer: Y rows then X rows
+    __shared__ __attribute__((aligned(16))) float smem[2 * IMG];
+
+    int ji = 0, b = (int)blockIdx.x;
+    while (ji + 1 < batch.njobs && b >= batch.blocks[ji]) b -= batch.blocks[ji++];
+    const WgradArgs& p = batch.job[ji];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int T = p.n_tiles_n * p.n_tiles_k;
+    const int tile = batch.njobs > 1 ? b % T : (b >> 3) % T;
+    const int slice = batch.njobs > 1 ? b / T : (b & 7) + 8 * ((b >> 3) / T);
+    if (slice >= p.nslices) return;
+    const int n0 = (tile / p.n_tiles_k) * BNo;
+    const int k0 = (tile % p.n_tiles_k) * BNo;
+    const int mbeg = slice * p.rows_per_slice;
+    const int mend = min(p.M, mbeg + p.rows_per_slice);
+    const int nch = mend > mbeg ? cdiv(mend - mbeg, MC) : 0;
+    const int total = nch * p.npairs;
+    const bool do_bias = k0 == 0 && p.bpart != nullptr;
+
+    const bool sx = wave >= 4;                  // wave-uniform: this wave stages X
+    const bool bfs = sx ? p.xb != 0 : p.yb != 0;  // wave-uniform: this side is a bf16 image
+    const int t = tid & 255, mq = t & 7, cg = t >> 3;  // m-quad, column group (4 fp32 / 8 bf16 columns)
+    floatx4 raw[NRAW][8];
+    float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    auto gload = [&](int c, floatx4 (&r8)[8]) {
+        const bool valid = c < total;
+        const int cc = valid ? c : 0;
+        const int pair = cc >= nch;
+        const int mrow = mbeg + (cc - pair * nch) * MC;
+        const float* src = sx ? (pair ? p.X1 : p.X0) : (pair ? p.Y1 : p.Y0);
+        const int ld = sx ? (pair ? p.ldx1 : p.ldx0) : (pair ? p.ldy1 : p.ldy0);
+        const int nrows = valid ? min(MC, mend - mrow) : 0;
+        const int col0 = sx ? k0 : n0;
+        if (bfs) {  // 4 rows x 8 bf16 columns
+            const char* base = reinterpret_cast<const char*>(src) + ((int64_t)mrow * ld + col0) * 2;
+            const rsrc_t v = make_view(reinterpret_cast<const float*>(base), (nrows * ld - col0) * 2);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) r8[r] = bload4(v, ((mq * 4 + r) * ld + cg * 8) * 2, 0);
+        } else {  // 4 rows x (4 columns of group cg, 4 of group cg + 32)
+            const rsrc_t v = make_view(src + (int64_t)mrow * ld + col0, (nrows * ld - col0) * 4);
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) r8[4 * h + r] = bload4(v, ((mq * 4 + r) * ld + (cg + 32 * h) * 4) * 4, 0);
+        }
+    };
+    // the stage image of a register set: column c's 4 values of this m-quad as one bf16x4 at row c
+    auto stage = [&](const floatx4 (&r8)[8], int buf, bool bias) {
+        float* img = smem + buf * IMG + (sx ? BNo * LSB : 0) + mq * 2;
+        if (bfs) {
+            // rows r0..r3 as 4 dwords each (8 bf16): column 2d is the low halves of dword d, 2d + 1 the high
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const unsigned w0 = __builtin_bit_cast(unsigned, r8[0][d]), w1 = __builtin_bit_cast(unsigned, r8[1][d]);
+                const unsigned w2 = __builtin_bit_cast(unsigned, r8[2][d]), w3 = __builtin_bit_cast(unsigned, r8[3][d]);
+                const u32x2_t lo = {__builtin_amdgcn_perm(w1, w0, 0x05040100u), __builtin_amdgcn_perm(w3, w2, 0x05040100u)};
+                const u32x2_t hi = {__builtin_amdgcn_perm(w1, w0, 0x07060302u), __builtin_amdgcn_perm(w3, w2, 0x07060302u)};
+                *reinterpret_cast<u32x2_t*>(img + (cg * 8 + 2 * d) * LSB) = lo;
+                *reinterpret_cast<u32x2_t*>(img + (cg * 8 + 2 * d + 1) * LSB) = hi;
+                if (bias) {
+                    bsum[2 * d] += (__builtin_bit_cast(float, w0 << 16) + __builtin_bit_cast(float, w1 << 16)) +
+                                   (__builtin_bit_cast(float, w2 << 16) + __builtin_bit_cast(float, w3 << 16));
+                    bsum[2 * d + 1] += (__builtin_bit_cast(float, w0 & 0xffff0000u) + __builtin_bit_cast(float, w1 & 0xffff0000u)) +
+                                       (__builtin_bit_cast(float, w2 & 0xffff0000u) + __builtin_bit_cast(float, w3 & 0xffff0000u));
+                }
+            }
+        } else {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const floatx4 col = {r8[4 * h][e], r8[4 * h + 1][e], r8[4 * h + 2][e], r8[4 * h + 3][e]};
+                    if (bias) bsum[4 * h + e] += (col[0] + col[1]) + (col[2] + col[3]);
+                    *reinterpret_cast<bf16x4*>(img + ((cg + 32 * h) * 4 + e) * LSB) = __builtin_convertvector(col, bf16x4);
+                }
+        }
+    };
+
+    floatx16 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+    const int frow = lane & 31, fh = lane >> 5;
+    auto compute = [&](int buf) {
+        const float* ya = smem + buf * IMG + (wm * 64 + frow) * LSB + 4 * fh;
+        const float* xa = smem + buf * IMG + BNo * LSB + (wn * 128 + frow) * LSB + 4 * fh;
+#pragma unroll
+        for (int ks = 0; ks < MC / 16; ++ks) {
+            bf16x8 af[2], bf[4];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) af[i] = *reinterpret_cast<const bf16x8*>(ya + i * 32 * LSB + ks * 8);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const bf16x8*>(xa + j * 32 * LSB + ks * 8);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
+    };
+
+    const bool ybias = do_bias & !sx;
+    auto bias_of = [&](int c) { return ybias & (c < nch); };
+#pragma unroll
+    for (int s = 0; s < NRAW; ++s) gload(s, raw[s]);
+    stage(raw[0], 0, bias_of(0));
+    __syncthreads();
+    for (int c0 = 0; c0 < total; c0 += NRAW) {
+#pragma unroll
+        for (int k = 0; k < NRAW; ++k) {
+            const int c = c0 + k;
+            gload(c + NRAW, raw[k]);  // set k held stage c (staged in the previous stage)
+            compute(c & 1);
+            stage(raw[(k + 1) % NRAW], (c + 1) & 1, bias_of(c + 1));
+            __syncthreads();  // stage c+1 written, stage c's buffer free
+        }
+    }
+    __syncthreads();  // LDS is reused for the bias partials
+
+    const rsrc_t vP = make_view(p.part + (int64_t)slice * p.Npad * p.Kpad, p.Npad * p.Kpad * 4);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int col = k0 + wn * 128 + j * 32 + (lane & 31);
+            const int rbase = n0 + wm * 64 + i * 32 + 4 * (lane >> 5);
+            const int vo = (rbase * p.Kpad + col) * 4;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) bstore1(vP, vo, ((r & 3) + 8 * (r >> 2)) * p.Kpad * 4, acc[i][j][r]);
+        }
+    }
+    if (do_bias) {  // reduce the Y threads' column partials over the 8 m-quads (fixed order)
+        float* red = smem;  // [8][BNo]
+        if (!sx) {
+            if (p.yb) {
+#pragma unroll
+                for (int c = 0; c < 8; ++c) red[mq * BNo + cg * 8 + c] = bsum[c];
+            } else {
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) red[mq * BNo + (cg + 32 * h) * 4 + e] = bsum[4 * h + e];
+            }
+        }
+        __syncthreads();
+        if (tid < BNo) {
+            float tot = 0.0f;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) tot += red[q * BNo + tid];
+            p.bpart[(int64_t)slice * p.Npad + n0 + tid] = tot;
+        }
+    }
+}
+
 // 256 x 64 weight gradient (the K = 64 first layers: the SDF's dW0 = Z_0ᵀ U0 + S_0ᵀ U̇_0 and the colour
 // network's extras columns, neus_fields.py:268-272, 364-366) on the stage ring of wgrad_x6r_kernel:
 // 16 sample rows per stage, two split-image buffers (2 x 35 KB: 256 Y rows + 64 X rows of 28 dwords),
@@ -892,11 +1068,14 @@ int launch_slab_reduce(const float* part, int nslab, int64_t stride, int rows, i
 // rows 256-padded): 256x64 tiles on the narrow stage ring.  Padding columns of Y / X only feed
 // output rows / columns past n_out / k_out, which the slab reduction never reads.
 // Returns the wide mode: 0 none, 1 = 256x256, 2 = 256x64.
+// bf16 (CN_MFMA_BF16): 256x256 tiles on the bf16 stage ring (wgrad_b16r_kernel) when the operand
+// rows are 256-padded, else the 128x128 / 128x64 tiles of wgrad_bf16_kernel (fp32 operands).
 static int wgrad_wide(const cn_wgrad_desc* d) {
     const int64_t np = (int64_t)cdiv(d->N, 256) * 256, kp = (int64_t)cdiv(d->K, 256) * 256;
-    if (d->mfma_dtype != CN_MFMA_F32_BF16X6 || d->ldy0 < np || (d->npairs == 2 && d->ldy1 < np)) return 0;
+    const bool x6 = d->mfma_dtype == CN_MFMA_F32_BF16X6, bf = d->mfma_dtype == CN_MFMA_BF16;
+    if (!(x6 || bf) || d->ldy0 < np || (d->npairs == 2 && d->ldy1 < np)) return 0;
     if (d->ldx0 >= kp && (d->npairs == 1 || d->ldx1 >= kp)) return 1;
-    return d->K <= 64 ? 2 : 0;
+    return x6 && d->K <= 64 ? 2 : 0;
 }
 
 // budget: workgroups this weight gradient may use (< 0: the default target; cn_wgrad_batch hands
@@ -947,10 +1126,10 @@ extern "C" int cn_wgrad_kernel_name(const cn_wgrad_desc* d, char* buf, int32_t l
         k = tile == 2 ? "wgrad_x6r_kernel<2>" : tile == 3 ? "wgrad_x6n_kernel<3>" : tile == 0 ? "wgrad_x6_kernel<2, 2>"
                                                                                        : "wgrad_x6_kernel<2, 1>";
     else if (d->mfma_dtype == CN_MFMA_BF16)
-        k = tile == 0 ? "wgrad_bf16_kernel<2, 2, 2, 2>" : "wgrad_bf16_kernel<2, 2, 2, 1>";
+        k = tile == 2 ? "wgrad_b16r_kernel<2>" : tile == 0 ? "wgrad_bf16_kernel<2, 2, 2, 2>" : "wgrad_bf16_kernel<2, 2, 2, 1>";
     else
         k = tile == 0 ? "wgrad_kernel<2, 2, 2, 2>" : "wgrad_kernel<2, 2, 2, 1>";
-    const bool ring = d->mfma_dtype == CN_MFMA_F32_BF16X6 && tile == 2;
+    const bool ring = (d->mfma_dtype == CN_MFMA_F32_BF16X6 || d->mfma_dtype == CN_MFMA_BF16) && tile == 2;
     const int n = snprintf(buf, (size_t)len, "void cn::%s(cn::%s)", k, ring ? "WgradBatch" : "WgradArgs");
     CN_REQUIRE(n < len, CN_ERR_SHAPE, "cn_wgrad_kernel_name: buffer of %d bytes too small (%d)", len, n + 1);
     return n;
@@ -966,6 +1145,13 @@ extern "C" size_t cn_wgrad_workspace_bytes(int32_t M, int32_t N, int32_t K) {
     return need;
 }
 
+// The workspace one weight gradient needs with a workgroup budget (its slabs of dW and db).
+static size_t wgrad_need(const cn_wgrad_desc* d, int budget) {
+    int tile, Npad, Kpad, ns, rps;
+    wgrad_geometry(std::max(d->M, 1), d->N, d->K, wgrad_wide(d), &tile, &Npad, &Kpad, &ns, &rps, budget);
+    return sizeof(float) * ((size_t)ns * Npad * Kpad + (size_t)ns * Npad);
+}
+
 // Checks a descriptor and lays out its launch: kernel arguments, the tile class, the grid and
 // the slab reductions of dW and db.  budget as in wgrad_geometry.
 static int wgrad_plan(const cn_wgrad_desc* d, int budget, WgradArgs* a, int* tile_out, int* grid_out, SlabJob* jw,
@@ -977,9 +1163,13 @@ static int wgrad_plan(const cn_wgrad_desc* d, int budget, WgradArgs* a, int* til
                "cn_wgrad: bad shape M=%d N=%d K=%d (K must be a multiple of 64)", d->M, d->N, d->K);
     CN_REQUIRE(d->mfma_dtype == CN_MFMA_F32 || d->mfma_dtype == CN_MFMA_BF16 || d->mfma_dtype == CN_MFMA_F32_BF16X6,
                CN_ERR_ARG, "cn_wgrad: bad mfma_dtype %d", d->mfma_dtype);
-    CN_REQUIRE(!d->y_bf16 && !d->x_bf16, CN_ERR_UNSUPPORTED, "cn_wgrad: bf16 operand images are not built yet");
     int tile, Npad, Kpad, ns, rps;
     wgrad_geometry(std::max(d->M, 1), d->N, d->K, wgrad_wide(d), &tile, &Npad, &Kpad, &ns, &rps, budget);
+    if (d->y_bf16 || d->x_bf16)  // bf16 operand images (ABI v10): the bf16 stage ring only
+        CN_REQUIRE(d->mfma_dtype == CN_MFMA_BF16 && tile == 2 && (!d->y_bf16 || (d->ldy0 % 8 == 0 && d->ldy1 % 8 == 0)) &&
+                       (!d->x_bf16 || (d->ldx0 % 8 == 0 && d->ldx1 % 8 == 0)),
+                   CN_ERR_UNSUPPORTED, "cn_wgrad: bf16 operand images need CN_MFMA_BF16, 256-padded operand rows and "
+                   "leading dimensions % 8 == 0");
     CN_REQUIRE(d->n_out <= Npad && d->k_out <= Kpad && d->n_out > 0 && d->k_out > 0, CN_ERR_SHAPE, "cn_wgrad: bad n_out/k_out");
     CN_REQUIRE(d->ldy0 >= Npad && d->ldx0 >= Kpad && d->ldy0 % 4 == 0 && d->ldx0 % 4 == 0 && al16(d->Y0) && al16(d->X0),
                CN_ERR_ALIGN, "cn_wgrad: Y0/X0 must be 16B aligned with ld >= padded tile (%d, %d)", Npad, Kpad);
@@ -988,7 +1178,7 @@ static int wgrad_plan(const cn_wgrad_desc* d, int budget, WgradArgs* a, int* til
                    CN_ERR_ALIGN, "cn_wgrad: Y1/X1 alignment");
     CN_REQUIRE(d->ldy0 < (1 << 20) && d->ldx0 < (1 << 20) && d->ldy1 < (1 << 20) && d->ldx1 < (1 << 20), CN_ERR_SHAPE,
                "cn_wgrad: leading dimensions must be < 2^20");
-    const size_t need = cn_wgrad_workspace_bytes(d->M, d->N, d->K);  // covers every budget (ns <= the default's)
+    const size_t need = wgrad_need(d, budget);  // <= cn_wgrad_workspace_bytes (ns <= the default's)
     CN_REQUIRE((size_t)d->workspace_bytes >= need, CN_ERR_SHAPE, "cn_wgrad: workspace %lld < %zu", (long long)d->workspace_bytes, need);
     a->Y0 = static_cast<const float*>(d->Y0); a->X0 = static_cast<const float*>(d->X0);
     a->Y1 = static_cast<const float*>(d->Y1); a->X1 = static_cast<const float*>(d->X1);
@@ -1000,6 +1190,8 @@ static int wgrad_plan(const cn_wgrad_desc* d, int budget, WgradArgs* a, int* til
     a->n_tiles_k = Kpad / BKo;
     a->n_tiles_n = Npad / BNo;
     a->nslices = ns;
+    a->yb = d->y_bf16 ? 1 : 0;
+    a->xb = d->x_bf16 ? 1 : 0;
     *tile_out = tile;
     *grid_out = cdiv(ns, 8) * 8 * a->n_tiles_n * a->n_tiles_k;
     // dW and db (when asked for) in one reduction launch
@@ -1030,7 +1222,13 @@ extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
             wgrad_x6_kernel<2, 1><<<grid, 256, 0, s>>>(a);
         }
     } else if (d->mfma_dtype == CN_MFMA_BF16) {
-        if (tile == 0)
+        if (tile == 2) {
+            WgradBatch b{};
+            b.job[0] = a;
+            b.blocks[0] = grid;
+            b.njobs = 1;
+            wgrad_b16r_kernel<2><<<grid, 512, 0, s>>>(b);
+        } else if (tile == 0)
             wgrad_bf16_kernel<2, 2, 2, 2><<<grid, 256, 0, s>>>(a);
         else
             wgrad_bf16_kernel<2, 2, 2, 1><<<grid, 256, 0, s>>>(a);
@@ -1043,44 +1241,53 @@ extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
     return rc ? rc : launch_slab_batch(js, 2, s);
 }
 
-// Whether cn_wgrad_batch runs a descriptor inside its shared stage-ring launch.
-static bool wgrad_batchable(const cn_wgrad_desc* d) {
-    return d->mfma_dtype == CN_MFMA_F32_BF16X6 && wgrad_wide(d) == 1;
+// Whether cn_wgrad_batch runs a descriptor inside a shared stage-ring launch (1: bf16x6, 2: bf16).
+static int wgrad_batchable(const cn_wgrad_desc* d) {
+    if (wgrad_wide(d) != 1) return 0;
+    return d->mfma_dtype == CN_MFMA_F32_BF16X6 ? 1 : d->mfma_dtype == CN_MFMA_BF16 ? 2 : 0;
 }
 
-extern "C" int cn_wgrad_batch(const cn_wgrad_desc* descs, int32_t n, cn_stream_t stream) {
-    CN_REQUIRE(descs && n >= 0, CN_ERR_ARG, "cn_wgrad_batch: null descs / n < 0");
-    hipStream_t s = (hipStream_t)stream;
-    // the stage-ring (256x256) jobs share one launch of one workgroup per CU: each takes a share of
-    // the workgroups proportional to its work (rows x pairs x output tiles), so they end together
-    double work[kWgradBatchMax];
-    int idx[kWgradBatchMax];
-    int nb = 0;
-    double total = 0.0;
+// The batch layout of cn_wgrad_batch: the stage-ring descriptors of each kind (1: bf16x6, 2: bf16,
+// at most kWgradBatchMax each) share one launch, each with a share of the device's workgroups
+// proportional to its work (rows x pairs x output tiles), so they end together; budget[i] = -1:
+// descriptor i runs alone (cn_wgrad).  kind[i] as wgrad_batchable.
+static void wgrad_batch_layout(const cn_wgrad_desc* descs, int n, int* kind, int* budget) {
+    double total[2] = {0.0, 0.0};
+    int cnt[2] = {0, 0};
     for (int i = 0; i < n; ++i) {
         const cn_wgrad_desc* d = descs + i;
-        if (!wgrad_batchable(d) || nb == kWgradBatchMax) {
-            int rc = cn_wgrad(d, stream);  // another tile class (or a full batch): its own launch
-            if (rc) return rc;
+        kind[i] = wgrad_batchable(d);
+        budget[i] = -1;
+        if (kind[i] == 0 || cnt[kind[i] - 1] == kWgradBatchMax) {
+            kind[i] = 0;
             continue;
         }
-        const int tiles = cdiv(d->N, 256) * cdiv(d->K, 256);
-        work[nb] = (double)std::max(d->M, 1) * d->npairs * tiles;
-        total += work[nb];
-        idx[nb++] = i;
+        cnt[kind[i] - 1]++;
+        total[kind[i] - 1] += (double)std::max(d->M, 1) * d->npairs * cdiv(d->N, 256) * cdiv(d->K, 256);
     }
-    if (nb == 0) return CN_OK;
     const int cus = wgrad_device_cus();
+    for (int i = 0; i < n; ++i) {
+        if (kind[i] == 0) continue;
+        const cn_wgrad_desc* d = descs + i;
+        const int tiles = cdiv(d->N, 256) * cdiv(d->K, 256);
+        const double work = (double)std::max(d->M, 1) * d->npairs * tiles;
+        // floor of the proportional share: the slices of all jobs never exceed one workgroup per CU
+        budget[i] = std::max(tiles, (int)(cus * work / total[kind[i] - 1]) / tiles * tiles);
+    }
+}
+
+// One shared launch of a stage-ring kernel (kind 1: bf16x6, 2: bf16) over the descriptors idx[0..nb)
+// with their budgets, then one slab reduction.
+static int wgrad_ring_batch(const cn_wgrad_desc* descs, const int* idx, const int* budgets, int nb, int kind,
+                            hipStream_t s) {
+    if (nb == 0) return CN_OK;
     WgradBatch b{};
     SlabJob js[2 * kWgradBatchMax];
     int grid = 0;
     for (int q = 0; q < nb; ++q) {
         const cn_wgrad_desc* d = descs + idx[q];
-        const int tiles = cdiv(d->N, 256) * cdiv(d->K, 256);
-        // floor of the proportional share: the slices of all jobs never exceed one workgroup per CU
-        const int budget = std::max(tiles, (int)(cus * work[q] / total) / tiles * tiles);
         int tile, g;
-        int rc = wgrad_plan(d, budget, &b.job[q], &tile, &g, &js[2 * q], &js[2 * q + 1]);
+        int rc = wgrad_plan(d, budgets[idx[q]], &b.job[q], &tile, &g, &js[2 * q], &js[2 * q + 1]);
         if (rc) return rc;
         g = b.job[q].nslices * b.job[q].n_tiles_n * b.job[q].n_tiles_k;  // dense (see the kernel)
         b.blocks[q] = g;
@@ -1088,7 +1295,44 @@ extern "C" int cn_wgrad_batch(const cn_wgrad_desc* descs, int32_t n, cn_stream_t
     }
     b.njobs = nb;
     if (nb == 1) b.blocks[0] = grid = cdiv(b.job[0].nslices, 8) * 8 * b.job[0].n_tiles_n * b.job[0].n_tiles_k;
-    wgrad_x6r_kernel<2><<<grid, 512, 0, s>>>(b);
+    if (kind == 1)
+        wgrad_x6r_kernel<2><<<grid, 512, 0, s>>>(b);
+    else
+        wgrad_b16r_kernel<2><<<grid, 512, 0, s>>>(b);
     int rc = check_launch("cn_wgrad_batch");
     return rc ? rc : launch_slab_batch(js, 2 * nb, s);
+}
+
+extern "C" size_t cn_wgrad_batch_workspace_bytes(const cn_wgrad_desc* descs, int32_t n, int64_t* offsets) {
+    if (!descs || n <= 0 || n > 4 * kWgradBatchMax) return 0;
+    int kind[4 * kWgradBatchMax], budget[4 * kWgradBatchMax];
+    wgrad_batch_layout(descs, n, kind, budget);
+    size_t off = 0;
+    for (int i = 0; i < n; ++i) {
+        if (offsets) offsets[i] = (int64_t)off;
+        off += (wgrad_need(descs + i, budget[i]) + 255) / 256 * 256;
+    }
+    return off;
+}
+
+extern "C" int cn_wgrad_batch(const cn_wgrad_desc* descs, int32_t n, cn_stream_t stream) {
+    CN_REQUIRE(descs && n >= 0 && n <= 4 * kWgradBatchMax, CN_ERR_ARG, "cn_wgrad_batch: null descs / n outside [0, %d]",
+               4 * kWgradBatchMax);
+    hipStream_t s = (hipStream_t)stream;
+    int kind[4 * kWgradBatchMax], budget[4 * kWgradBatchMax];
+    wgrad_batch_layout(descs, n, kind, budget);
+    int idx[2][kWgradBatchMax], nb[2] = {0, 0};
+    for (int i = 0; i < n; ++i) {
+        if (kind[i] == 0) {
+            int rc = cn_wgrad(descs + i, stream);  // another tile class (or a full batch): its own launch
+            if (rc) return rc;
+            continue;
+        }
+        idx[kind[i] - 1][nb[kind[i] - 1]++] = i;
+    }
+    for (int k = 1; k <= 2; ++k) {
+        int rc = wgrad_ring_batch(descs, idx[k - 1], budget, nb[k - 1], k, s);
+        if (rc) return rc;
+    }
+    return CN_OK;
 }

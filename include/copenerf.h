@@ -233,13 +233,18 @@ size_t cn_wgrad_workspace_bytes(int32_t M, int32_t N, int32_t K);
 int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream);
 /* As cn_linear_kernel_name for cn_wgrad's split-M kernel (cn::slab_reduce_kernel follows it). */
 int cn_wgrad_kernel_name(const cn_wgrad_desc* d, char* buf, int32_t len);
-/* Several independent weight gradients (ABI v9).  The descriptors that cn_wgrad would run on the
- * 256x256 bf16x6 stage-ring kernel share ONE launch of it (each takes a share of the workgroups
+/* Several independent weight gradients (ABI v9).  The descriptors that cn_wgrad would run on a
+ * 256x256 stage-ring kernel (bf16x6, or bf16 since ABI v10) share ONE launch of it (each takes a share of the workgroups
  * proportional to its rows x pairs x output tiles, its own M-slices and slabs in its own
  * workspace) and ONE cn::slab_reduce_kernel launch; any other descriptor is run as by cn_wgrad.
  * Results equal cn_wgrad's up to the slice count (fixed-order sums: bitwise reproducible).
  * Replaces the per-layer dW of neus_fields.py:291-303 (SDF) and 364-373 (colour) as one call. */
 int cn_wgrad_batch(const cn_wgrad_desc* descs, int32_t n, cn_stream_t stream);
+/* ABI v10: the workspace a cn_wgrad_batch call over descs[0..n) needs (n <= 64), and each
+ * descriptor's byte offset into one buffer of that size (offsets may be NULL): a batched job takes
+ * only its share of the slabs, so this is less than the sum of cn_wgrad_workspace_bytes.  The
+ * layout follows the CU count of the current device: query and launch on the same device. */
+size_t cn_wgrad_batch_workspace_bytes(const cn_wgrad_desc* descs, int32_t n, int64_t* offsets);
 
 /* ------------------------------------------------------------------------ *
  * Per-row heads (neus_fields.py:279-283 last Linear row 0 = sdf;
@@ -277,9 +282,10 @@ int cn_scale_cols(int32_t M, int32_t N, const float* X, int64_t ldx, const float
  *   rs_out[0] = (sum_m rowv[m]) / cs_div (the sdf head's bias gradient; rs_out may be NULL),
  * fixed-order slab reductions through workspace (cn_softplus_adjoint_workspace_bytes). */
 size_t cn_softplus_adjoint_workspace_bytes(int32_t M, int32_t N);
+/* out_bf16 (ABI v10): out is written as its bf16 operand image (RNE; ld_out in bf16 elements, % 4 == 0). */
 int cn_softplus_adjoint(int32_t M, int32_t N, const float* D, int64_t ldd, const float* act, int64_t lda,
                         float act_beta, const float* rowv, const float* colv, const float* aux1, int64_t ld1,
-                        const float* aux2, int64_t ld2, float aux2_scale, float* out, int64_t ld_out,
+                        const float* aux2, int64_t ld2, float aux2_scale, void* out, int64_t ld_out, int32_t out_bf16,
                         float* cs_out, float* rs_out, float cs_div, float* workspace, int64_t workspace_bytes,
                         cn_stream_t stream);
 
@@ -288,11 +294,13 @@ int cn_softplus_adjoint(int32_t M, int32_t N, const float* D, int64_t ldd, const
  * include_input, log-sampled bands 2^0..2^(multires-1), [sin, cos]; applied at
  * neus_fields.py:269-271 to x*scale):
  *   U0[m][0..4+8*multires) = embed(scale * x[m][0..4)),  zeros up to kpad.
- *   If U4e != NULL also U4e[m][j] = u4_scale * U0[m][j] (the skip-connection
- *   copy of neus_fields.py:276-277).
+ *   If U4e != NULL also U4e[m][j] = U0[m][j] / u4_scale (the skip-connection
+ *   copy of neus_fields.py:276-277); u4_bf16 (ABI v10): U4e is a bf16 operand
+ *   image (RNE; ld_u4 in bf16 elements, 8-byte aligned).
  * ------------------------------------------------------------------------ */
 int cn_sdf_embed(int32_t M, const float* x, int64_t ldx, int32_t multires, float scale, int32_t kpad,
-                 float* U0, int64_t ld_u0, float* U4e, int64_t ld_u4, float u4_scale, cn_stream_t stream);
+                 float* U0, int64_t ld_u0, void* U4e, int64_t ld_u4, float u4_scale, int32_t u4_bf16,
+                 cn_stream_t stream);
 
 /* ∇ₓSDF from the embedding adjoint: G[m][i] = scale * J_embed(x)ᵀ (Q0[m] + QE[m])
  * (neus_fields.py:291-303; the chain rule through neus_embedder.py:20-22). */
@@ -302,10 +310,11 @@ int cn_sdf_grad_assemble(int32_t M, int32_t multires, float scale, const float* 
 
 /* Tangent of the embedding along v = dL/d(∇ₓSDF) (forward-over-reverse form
  * of the double backward of neus_fields.py:296):
- *   T0[m] = scale * J_embed(x) v[m] (zeros up to kpad);  T4e[m] = t4_scale * T0[m]. */
+ *   T0[m] = scale * J_embed(x) v[m] (zeros up to kpad);  T4e[m] = T0[m] / t4_scale
+ *   (t4_bf16, ABI v10: T4e a bf16 operand image, as cn_sdf_embed's U4e). */
 int cn_sdf_tangent_prep(int32_t M, int32_t multires, float scale, int32_t kpad, const float* U0,
                         int64_t ld_u0, const float* v, int64_t ld_v, float* T0, int64_t ld_t0,
-                        float* T4e, int64_t ld_t4, float t4_scale, cn_stream_t stream);
+                        void* T4e, int64_t ld_t4, float t4_scale, int32_t t4_bf16, cn_stream_t stream);
 
 /* Colour-network input extras (neus_fields.py:346-356, mode 'idr'):
  *   ext[m] = [ G[m][0..4), pts[m][0..4), embed_view(dirs[m / dir_div]) (3+6*multires_view), 0... ]
