@@ -55,6 +55,26 @@ SAMPLES = 128
 GFLOP_PER_RAY_REF = 1.4809  # reference GEMM FLOPs per ray per train step (64+4x16)
 
 
+def rocprof_launch_ns(symbol, config):
+    """Average duration (ns) of `symbol` in the newest committed rocprofv3 kernel-stats summary of
+    this config's bench (profiles/<tag>_kernel_stats.csv for c2, <tag>_<config>_kernel_stats.csv
+    otherwise), and the file; (None, None) when no committed profile has the kernel."""
+    import csv
+    pat = "*_kernel_stats.csv" if config == "c2" else f"*_{config}_kernel_stats.csv"
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pat)))
+    if config == "c2":  # (another config's files carry its name before the suffix)
+        files = [f for f in files if not any(f.endswith(f"_{c}_kernel_stats.csv") for c in CONFIGS if c != "c2")]
+    for f in reversed(files):
+        try:
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    if row.get("Name") == symbol:
+                        return float(row["AverageNs"]), os.path.relpath(f, ROOT)
+        except (OSError, ValueError, KeyError):
+            continue
+    return None, None
+
+
 def pmc_traffic(symbol):
     """Per-launch HBM bytes of `symbol` from the newest committed counter pass."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
@@ -158,8 +178,12 @@ CONFIGS = {
               "(sampler + SDF + ∇SDF + colour + compositing), 65,536-ray chunks, fp32"),
     "c2bf16": (4096, {"mfma_dtype": "bf16"},
                "C2 workload (4096 rays x 128 samples, fixed poses) with bf16 MLP MFMA (fp32 accumulate)"),
-    "c4": (8192, {"mfma_dtype": "bf16x6"}, "C4: synthetic scene, 8192 rays x 128 samples per GPU, fp32, fixed poses, "
-                                            "data-parallel"),
+    # C4 = Co3D/skateboard (its stage-1 pose optimisation, as c3fp32) at 8192 rays per GPU, data-parallel:
+    # one process per GPU, the gradients and stage-1 normalisers all-reduced over RCCL
+    "c4": (8192, {"stage1": True, "mfma_dtype": "bf16x6", "start_it": 30000, "train_cfg": dict(C3_TRAIN)},
+           "C4: Co3D/skateboard stage 1 on a synthetic 10-frame scene (MotionNetwork pose optimisation, scene-flow SDF "
+           "loss, flow-RGB warp, SDF consistency with pose gradient), 8192 rays x 128 samples per GPU, fp32 (bf16x6), "
+           "data-parallel (RCCL all-reduce of the gradients and the stage-1 normalisers)"),
     "c5": (4096, {"ren_cfg": dict(n_samples=64, n_importance=128, n_outside=0, up_sample_steps=4, perturb=1.0,
                                   n_max_network_queries=64000, importance_sampling_start=0, naive_render=False),
                   "graph": True, "mfma_dtype": "bf16x6"},
@@ -270,7 +294,7 @@ def main():
         "roofline": None,
         "cpu_baseline": None,
     }
-    result.update(roofline_fields(timer, n_inst, rays_total / elapsed, mode))
+    result.update(roofline_fields(timer, n_inst, rays_total / elapsed, mode, args.config))
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
         result["cpu_baseline"] = cpu_baseline()
     if rank == 0:
@@ -279,7 +303,7 @@ def main():
         dist.destroy_process_group()
 
 
-def roofline_fields(timer, steps, rays_per_s, mode):
+def roofline_fields(timer, steps, rays_per_s, mode, config="c2"):
     agg = timer.summary()
     # the dominant launch class over every cn_linear and cn_wgrad class (a launch class is one
     # kernel instance, named by the library: cn_linear_kernel_name / cn_wgrad_kernel_name; a
@@ -295,10 +319,21 @@ def roofline_fields(timer, steps, rays_per_s, mode):
     symbol = timer.symbols[dom_key]
     traffic, traffic_src = pmc_traffic(symbol)
     kernels_ms = sum(a["ms"] for a in agg.values()) / steps
+    # the kernel's own duration from the committed rocprofv3 stats of this config (the HIP events
+    # bracket the library call: for a weight gradient also its slab reduction); the HIP-event
+    # figure of this run beside it
+    frac_ev = max(t_flop, t_byte) / avg_s
+    prof_ns, prof_src = rocprof_launch_ns(symbol, config)
+    kern_s = prof_ns * 1e-9 if prof_ns else avg_s
     roof = {"bound": "hbm" if hbm else "mfma",
-            "achieved": round(nbytes / avg_s / 1e9, 1) if hbm else round(flops / avg_s / 1e12, 2),
+            "achieved": round(nbytes / kern_s / 1e9, 1) if hbm else round(flops / kern_s / 1e12, 2),
             "peak": HBM_PEAK_GBS if hbm else round(peak_tf, 1), "unit": "GB/s" if hbm else "TFLOP/s",
-            "frac": round(max(t_flop, t_byte) / avg_s, 4), "traffic": traffic, "traffic_source": traffic_src,
+            "frac": round(max(t_flop, t_byte) / kern_s, 4),
+            "frac_source": (f"{prof_src}: the kernel's rocprofv3 average duration" if prof_src else
+                            "HIP events of this run (no committed rocprofv3 stats name this kernel)"),
+            "avg_launch_ms_rocprof": round(prof_ns * 1e-6, 4) if prof_ns else None,
+            "frac_hip_events": round(frac_ev, 4),
+            "traffic": traffic, "traffic_source": traffic_src,
             "kernel": symbol, "launch_class": "/".join(map(str, dom_key)),
             "timed_region": ("the cn_wgrad_batch call (a backward pass's 256x256 weight gradients in one launch): "
                              "this kernel + one cn::slab_reduce_kernel (every job's dW, db)"

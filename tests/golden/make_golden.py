@@ -24,6 +24,37 @@ import torch
 REF = os.environ.get("COPENERF_REFERENCE", "/root/reference")
 OUT = os.path.dirname(os.path.abspath(__file__))
 
+# The reference is untrusted public content: every source file this generator executes (imported
+# module, or a block AST-extracted from train.py / training.py) is pinned by its sha256, and nothing
+# runs if a file differs from the snapshot the fixtures were generated from.
+PINNED = {
+    "model/neus_embedder.py": "a949926f2c29c2ec1dd374505c2c994c1e822a60a6d6a165971a665bfe84739d",
+    "utils_poses/pose_pytorch3d.py": "6026fda1c4defbf2603b1140ec7e8a93e9ed6fdc35187cafd72e5262a0874705",
+    "model/neus_fields.py": "16292e97bde411fb7376294125ea03f31eee4fdc79145e9d0a63404ba75237c7",
+    "model/neus_renderer.py": "6b0642436284c2a188b9ca52701af133711e543bbc2d2d354f802c2c8d7a9da8",
+    "model/training.py": "3c99029d001d73e5864224b3a8bc6bec7ff90b9f7a3d401d5801ec799495319d",
+    "train.py": "145aa03d8103d27fd00ba9e6255fa03b1d78313da3a88b671373e162acc16ab6",
+    "model/checkpoints.py": "a0040bb837453b91baa4eb403962cfb1298130de463a6dbcebdb450483ad18fc",
+    "model/poses_retriever.py": "92881188beb3d744e224de2ecb4f30654f0ebb4e5e8242930e197ef71be19392",
+    "model/common.py": "09fc4fef0377091323e9a1a94e639ec434fed1df79af2f0befe2505f6131a656",
+}
+
+
+def _ref_text(rel):
+    """The text of a pinned reference source file (refuses a file whose hash differs)."""
+    import hashlib
+    path = os.path.join(REF, rel)
+    data = open(path, "rb").read()
+    got = hashlib.sha256(data).hexdigest()
+    if PINNED.get(rel) != got:
+        raise RuntimeError(f"{path}: sha256 {got} is not the pinned one; refusing to execute it")
+    return data.decode()
+
+
+def _ref_path(rel):
+    _ref_text(rel)
+    return os.path.join(REF, rel)
+
 SDF_CFG = dict(d_in=4, d_out=257, d_hidden=256, n_layers=8, skip_in=[4], multires=6, bias=0.5, scale=1.0,
                geometric_init=True, weight_norm=True)
 COL_CFG = dict(d_feature=256, mode="idr", d_in=11, d_out=3, d_hidden=256, n_layers=4, weight_norm=True,
@@ -44,7 +75,7 @@ def load_reference():
         sys.modules[pkg] = p
 
     def load(modname, rel):
-        spec = importlib.util.spec_from_file_location(modname, os.path.join(REF, rel))
+        spec = importlib.util.spec_from_file_location(modname, _ref_path(rel))
         mod = importlib.util.module_from_spec(spec)
         sys.modules[modname] = mod
         spec.loader.exec_module(mod)
@@ -315,7 +346,7 @@ def load_reference_trainer():
     load_reference()
 
     def load(modname, rel):
-        spec = importlib.util.spec_from_file_location(modname, os.path.join(REF, rel))
+        spec = importlib.util.spec_from_file_location(modname, _ref_path(rel))
         mod = importlib.util.module_from_spec(spec)
         sys.modules[modname] = mod
         spec.loader.exec_module(mod)
@@ -323,7 +354,7 @@ def load_reference_trainer():
 
     common = load("model.common", "model/common.py")
     poses = load("model.poses_retriever", "model/poses_retriever.py")
-    src = open(os.path.join(REF, "model", "training.py")).read()
+    src = _ref_text("model/training.py")
     tree = ast.parse(src)
     cls = next(n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == "Trainer")
     keep = {"__init__", "near_far_from_sphere", "get_cos_anneal_ratio", "get_patch_indices", "process_data_dict",
@@ -415,7 +446,7 @@ def load_reference_stage1_block():
     iteration's value (a loop local of Trainer.train); the first iteration on such a frame
     would raise UnboundLocalError."""
     import ast
-    src = open(os.path.join(REF, "train.py")).read()
+    src = _ref_text("train.py")
     tree = ast.parse(src)
     cls = next(n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == "Trainer")
     warp = next(f for f in cls.body if isinstance(f, ast.FunctionDef) and f.name == "warp_pixel")
@@ -546,7 +577,7 @@ def checkpoint_case(fields, rend):
     torch.load(weights_only=True) reads it)."""
     import json
     import tempfile
-    ckio = importlib.util.spec_from_file_location("model.checkpoints", os.path.join(REF, "model", "checkpoints.py"))
+    ckio = importlib.util.spec_from_file_location("model.checkpoints", _ref_path("model/checkpoints.py"))
     ckmod = importlib.util.module_from_spec(ckio)
     ckio.loader.exec_module(ckmod)
 

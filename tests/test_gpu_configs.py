@@ -73,11 +73,12 @@ def test_c2_full_size_bf16x6_against_oracle():
 
 
 def test_c4_8192_rays_step_and_ray_independence():
-    """C4's per-GPU batch (8192 rays x 128 samples): the training step runs, and a
-    ray's render does not depend on the batch it is in (8192 = two 4096 halves,
-    bitwise)."""
+    """C4's per-GPU workload (bench.py --config c4: Co3D/skateboard's stage 1 at 8192 rays x 128
+    samples): the training step runs with finite parameters, and a ray's render does not depend on
+    the batch it is in (8192 = two 4096 halves, bitwise)."""
     from copenerf.train_step import SyntheticTrainer
-    tr = SyntheticTrainer(DEV, rays=8192, mfma_dtype="bf16x6")
+    skateboard = dict(sdf_consistency_enable_pose_grad=True, rgb_weight=0.33333, end_sdf_weight_increase_iteration=-1)
+    tr = SyntheticTrainer(DEV, rays=8192, mfma_dtype="bf16x6", stage1=True, start_it=30000, train_cfg=skateboard)
     for _ in range(2):
         loss = tr.step()
     assert torch.isfinite(loss).item()

@@ -1,8 +1,10 @@
-"""Data parallel on the HIP path: 2 processes, each running the HIP
-renderer on cuda:0 on its half of the patches of one batch, with joint pose and
-the stage-1 losses on -- their global normalisers (Σw of the scene-flow loss,
-Σvalid of flow-RGB) all-reduced before the divide -- and the HIP gradients
-exchanged by train_step.flat_allreduce_mean (gloo here; RCCL on the bench).
+"""Data parallel on the HIP path: 2 or 4 processes, each running the HIP
+renderer on cuda:0 on its share of the patches of one batch, with the stage-1 losses on
+-- their global normalisers (Σw of the scene-flow loss, Σvalid of flow-RGB) all-reduced
+before the divide -- and the HIP gradients exchanged by train_step.flat_allreduce_mean
+(gloo here; RCCL on the bench).  Two workloads: joint pose + stage 1 on 2 ranks, and
+config C4's (bench.py --config c4): Co3D/skateboard's stage 1 (MotionNetwork, SDF
+consistency with the pose gradient, skateboard.yaml's loss options) on 4 ranks.
 Every rank must end with the single-process full-batch gradient."""
 import os
 import socket
@@ -13,8 +15,13 @@ import torch
 import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
-KW = dict(H=48, W=64, seed=21, joint_pose=True, stage1=True, n_images=6, start_it=30001, schedule="reference",
-          mfma_dtype="bf16x6", depth_range=(0.01, 3.0))
+BASE = dict(H=48, W=64, seed=21, stage1=True, n_images=6, start_it=30001, schedule="reference", mfma_dtype="bf16x6",
+            depth_range=(0.01, 3.0))
+# C3_TRAIN of bench.py: /root/reference configs/Co3D/skateboard.yaml:4,23,27 (sdf_consistency_enable_pose_grad,
+# rgb_weight, a fixed sdf_weight)
+SKATEBOARD = dict(sdf_consistency_enable_pose_grad=True, rgb_weight=0.33333, end_sdf_weight_increase_iteration=-1)
+WORKLOADS = {"joint_pose_stage1": dict(BASE, joint_pose=True),
+             "skateboard_c4": dict(BASE, train_cfg=SKATEBOARD)}
 R = 256  # 16 patches of 4x4
 
 
@@ -31,7 +38,7 @@ def _grads(tr):
             [("p%d" % i, p) for i, p in enumerate(tr.all_params)] if p.grad is not None}
 
 
-def _worker(rank, world, port, batch, q):
+def _worker(rank, world, port, batch, q, KW):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [os.path.join(root, "cope-nerf_amd"), root, os.path.join(root, "tests")]
@@ -51,9 +58,10 @@ def _worker(rank, world, port, batch, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_hip_data_parallel_equals_full_batch(world):
+@pytest.mark.parametrize("world,workload", [(2, "joint_pose_stage1"), (4, "skateboard_c4")])
+def test_hip_data_parallel_equals_full_batch(world, workload):
     from copenerf.train_step import SyntheticTrainer
+    KW = WORKLOADS[workload]
     from helpers import smooth_frames
     ref = SyntheticTrainer("cuda:0", rays=R, **KW)
     ref.images = smooth_frames(KW["n_images"], KW["H"], KW["W"], "cuda:0")
@@ -65,7 +73,7 @@ def test_hip_data_parallel_equals_full_batch(world):
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, batch_np, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, batch_np, q, KW)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict((r, g) for r, g, _ in (q.get(timeout=300) for _ in range(world)))

@@ -2,7 +2,8 @@
 newest profiled bench line names (cn_linear_kernel_name / cn_wgrad_kernel_name: the
 library's own tile choice) a kernel present in the rocprofv3 stats of the same run,
 and the bench's HIP-event launch time of the dominant kernel agrees with rocprof's
-(bench line and kernel stats come from the same profile round, tools/profile_round.sh)."""
+(bench line and kernel stats come from the same profile round, tools/profile_round.sh), and
+the line's roofline frac is the one its cited kernel stats give."""
 import csv
 import glob
 import json
@@ -36,3 +37,32 @@ def test_launch_classes_name_profiled_kernels():
     assert roof["kernel"] in stats
     avg_us = float(stats[roof["kernel"]]["AverageNs"]) / 1e3
     assert abs(avg_us - roof["avg_launch_ms"] * 1e3) <= 0.05 * avg_us, (avg_us, roof["avg_launch_ms"])
+
+
+def test_roofline_frac_follows_the_cited_kernel_stats():
+    """bench.py reports roofline.frac from the committed rocprofv3 average duration of the dominant
+    kernel (roofline.frac_source names the file): recomputed here from that file, within 1 %."""
+    from bench import BF16_MFMA_PEAK_TFLOPS, HBM_PEAK_GBS, MODE_PEAK_TFLOPS  # noqa: F401
+    checked = 0
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*bench*.json"))):
+        with open(f) as fh:
+            lines = [ln for ln in fh.read().strip().splitlines() if ln.startswith("{")]
+        if not lines:
+            continue
+        line = json.loads(lines[-1])
+        roof = line.get("roofline") or {}
+        src = roof.get("frac_source", "")
+        if not src.endswith("average duration"):
+            continue
+        path = os.path.join(ROOT, src.split(":")[0])
+        with open(path) as fh:
+            stats = {r["Name"]: r for r in csv.DictReader(fh)}
+        avg_s = float(stats[roof["kernel"]]["AverageNs"]) * 1e-9
+        flops = roof["algorithmic_gflop_per_launch"] * 1e9
+        nbytes = roof["algorithmic_mb_per_launch"] * 1e6
+        mode = {"bf16 MFMA dense": "bf16", "fp32 MFMA dense": "fp32"}.get(roof["peak_basis"].split(";")[0], "bf16x6")
+        peak_tf = MODE_PEAK_TFLOPS[mode]
+        frac = max(flops / (peak_tf * 1e12), nbytes / (HBM_PEAK_GBS * 1e9)) / avg_s
+        assert abs(frac - roof["frac"]) <= 0.01 * roof["frac"], (f, frac, roof["frac"])
+        checked += 1
+    assert checked >= 1, "no committed bench line cites rocprofv3 stats for its roofline"
