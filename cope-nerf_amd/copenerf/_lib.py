@@ -52,7 +52,7 @@ class LinearDesc(ctypes.Structure):
         ("mfma_dtype", c_i32), ("aux_beta", c_f32), ("aux2", c_ptr), ("ld_aux2", c_i64),
         ("aux2_scale", c_f32), ("flags", c_i32),
         ("head_w", c_ptr), ("head_b", c_ptr), ("head_out", c_ptr), ("head_idx", c_ptr),
-        ("a_bf16", c_i32), ("aux0_bf16", c_i32), ("out0_b", c_ptr), ("ld_out0_b", c_i64),
+        ("a_bf16", c_i32), ("aux0_bf16", c_i32), ("aux12_bf16", c_i32), ("out0_b", c_ptr), ("ld_out0_b", c_i64),
         ("out1_b", c_ptr), ("ld_out1_b", c_i64),
     ]
 

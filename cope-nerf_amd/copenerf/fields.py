@@ -220,8 +220,9 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
     activation U[L8] directly (the renderer folds the feature head into the
     colour network's first layer, NeuSRenderer._folded_color_pack).
     bf16 mode (_img_mode): Ub / Sb hold the bf16 operand images of the hidden activations and ∇-pass
-    adjoints (layers 1..7), which the next GEMMs and the weight gradients read; the fp32 U / S are
-    kept only for the epilogues that recover σ from them (not at all on the sampler path).
+    adjoints, which the next GEMMs, the weight gradients and (s) the adjoint's second-order term read;
+    fp32 is kept only where it is needed: U_l for the epilogues that recover σ from it (not on the
+    sampler path), s_0 and s_7 for the fp32 first-layer weight gradient / the elementwise last adjoint.
     """
     M, dev = x.shape[0], x.device
     nl, sk, HL, KE = lay.n_lin, lay.skip, lay.HL, lay.KE
@@ -289,8 +290,10 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
         QE = _empty(M, KE, dev) if sk >= 0 else None
         for l in range(L8 - 1, 0, -1):
             Kl = rup(lay.out_dim[l], 32)
-            S[l - 1] = _empty(M, HL, dev)
-            Sb[l - 1] = _empty_b(M, HL, dev) if (img and l - 1 >= 1) else None
+            # bf16 mode: s_l is read by the next ∇ GEMM, a weight gradient and the second-order term
+            # of the adjoint (all from its image); s_0 also by the first layer's fp32 weight gradient
+            Sb[l - 1] = _empty_b(M, HL, dev) if img else None
+            S[l - 1] = _empty(M, HL, dev) if (not img or l - 1 == 0) else None
             A = Sb[l] if Sb[l] is not None else S[l]
             if l == sk:
                 ops.linear(A, pk.Bt[l], lay.in_dim[l], Kl, S[l - 1], EPI_MUL, aux0=U[l], aux_beta=sig_beta(lay, l - 1),
@@ -300,7 +303,8 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
                 ops.linear(A, pk.Bt[l], lay.out_dim[l - 1], Kl, S[l - 1], EPI_MUL, aux0=U[l],
                            aux_beta=sig_beta(lay, l - 1), nzero=HL, kalg=lay.out_dim[l], out0_b=Sb[l - 1])
         Q0 = _empty(M, KE, dev)
-        ops.linear(S[0], pk.Bt[0], lay.E, rup(lay.out_dim[0], 32), Q0, EPI_STORE, nzero=KE, kalg=lay.out_dim[0])
+        ops.linear(Sb[0] if Sb[0] is not None else S[0], pk.Bt[0], lay.E, rup(lay.out_dim[0], 32), Q0, EPI_STORE,
+                   nzero=KE, kalg=lay.out_dim[0])
         G = _empty(M, 4, dev)
         ops.sdf_grad_assemble(lay.multires, lay.scale, U[0], Q0, QE, G)
     return {"U": U, "Ub": Ub, "S": S, "Sb": Sb, "sdf": sdf, "feat": feat, "G": G}
@@ -387,17 +391,21 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
         Usk_d, Usk_db, e_view = None, None, None
         if sk >= 0:
             o = lay.out_dim[sk - 1]
-            Usk_d = _empty(M, HL, dev)
             if img and 1 <= sk < L8:  # the tangent's skip input as an operand image (tail from the prep)
                 Usk_db = _empty_b(M, HL, dev)
                 e_view = Usk_db[:, o:o + lay.E]
             else:
+                Usk_d = _empty(M, HL, dev)
                 e_view = Usk_d[:, o:o + lay.E]
         ops.sdf_tangent_prep(lay.multires, lay.scale, U[0], dG, Ud[0], e_view, SQRT2)
         for l in range(nl - 1):
             into = (l + 1) == sk
-            out = Usk_d if into else _empty(M, HL, dev)
-            ob = (Usk_db if into else _empty_b(M, HL, dev)) if (img and l + 1 < L8) else None
+            # bf16 mode: u̇_{l+1} is read by the next tangent GEMM, a weight gradient and the adjoint's
+            # second-order term (all from its image); u̇_8 by the elementwise last adjoint (fp32)
+            if img and l + 1 < L8:
+                out, ob = None, (Usk_db if into else _empty_b(M, HL, dev))
+            else:
+                out, ob = (Usk_d if into else _empty(M, HL, dev)), None
             K = KE if l == 0 else rup(lay.in_dim[l], 32)
             A = Udb[l] if Udb[l] is not None else Ud[l]
             ops.linear(A, pk.Bf[l], lay.out_dim[l], K, out, EPI_TANGENT, aux0=U[l + 1], aux_beta=sig_beta(lay, l),
@@ -439,7 +447,9 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
     def second_order(l):  # BWD_SOFTPLUS inputs of β s_l (1-σ_l) ż_l, ż_l = u̇_{l+1} c_l / σ_l
         if not second:
             return {}
-        return dict(aux1=S[l], aux2=Ud[l + 1], aux2_scale=lay.beta * (SQRT2 if (l + 1) == sk else 1.0))
+        img2 = l < L8 - 1 and Sb[l] is not None and Udb[l + 1] is not None  # (bf16 mode: the images)
+        return dict(aux1=Sb[l] if img2 else S[l], aux2=Udb[l + 1] if img2 else Ud[l + 1],
+                    aux2_scale=lay.beta * (SQRT2 if (l + 1) == sk else 1.0))
 
     Z = _empty_b(M, HL, dev) if (z_img(L8 - 1) and (dh is not None or (sdf_only and fused_cs))) else _empty(M, HL, dev)
     if dh is not None:  # Z_7 = (dh + dsdf w80) σ_7 + the second-order term: elementwise

@@ -248,13 +248,16 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
         if t is None or t is B:
             continue
         want_b = n in ("out0_b", "out1_b")
-        may_b = bf and (n in ("A", "A2") or (n == "aux0" and epilogue == EPI_BWD_RELU))
+        may_b = bf and (n in ("A", "A2") or (n == "aux0" and epilogue == EPI_BWD_RELU) or
+                        (n in ("aux1", "aux2") and epilogue == EPI_BWD_SOFTPLUS))
         if (t.dtype == torch.bfloat16) != want_b and not (may_b and t.dtype == torch.bfloat16):
-            raise RuntimeError(f"cn_linear: {n} has dtype {t.dtype} (bfloat16 images: A / A2, BWD_RELU's aux0 "
-                               f"and out0_b / out1_b, in the bf16 MFMA mode only)")
+            raise RuntimeError(f"cn_linear: {n} has dtype {t.dtype} (bfloat16 images: A / A2, BWD_RELU's aux0, "
+                               f"BWD_SOFTPLUS's aux1 / aux2 and out0_b / out1_b, in the bf16 MFMA mode only)")
     a_b = A.dtype == torch.bfloat16
     if A2 is not None and (A2.dtype == torch.bfloat16) != a_b:
         raise RuntimeError("cn_linear: A and A2 must have the same dtype")
+    if aux1 is not None and aux2 is not None and aux1.dtype != aux2.dtype:
+        raise RuntimeError("cn_linear: aux1 and aux2 must have the same dtype")
     if bf:
         K = rup(K, 64)
         K1 = rup(K1, 64) if K1 is not None else None
@@ -303,6 +306,7 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     d.mfma_dtype = 2 if x6 else (1 if bf else 0)
     d.a_bf16 = 1 if a_b else 0
     d.aux0_bf16 = 1 if (aux0 is not None and aux0.dtype == torch.bfloat16) else 0
+    d.aux12_bf16 = 1 if (aux1 is not None and aux1.dtype == torch.bfloat16) else 0
     d.out0_b, d.ld_out0_b, d.out1_b, d.ld_out1_b = _ptr(out0_b), _ld(out0_b), _ptr(out1_b), _ld(out1_b)
     global _flip
     _flip ^= 1  # consecutive launches walk the rows in opposite directions

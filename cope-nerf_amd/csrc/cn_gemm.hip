@@ -79,14 +79,19 @@ struct LinearArgs {
 //         parks in one slab).
 // The accumulator layout of the two MFMAs is the same, so the epilogue is shared.
 // MODE_ bit 2 (MODE 1 only): A / A2 are bf16 operand images (16-byte pieces of 8 values land on
-//         the LDS rows as they are: no conversion); bit 3: aux0 is a bf16 image (BWD_RELU).
+//         the LDS rows as they are: no conversion); bit 3: BWD_RELU's aux0 / BWD_SOFTPLUS's aux1
+//         and aux2 are bf16 images.
 constexpr int kTblCols = 512;  // widest N with a bias / colv (the LDS column table)
 
 template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int EPI, bool ROWV, int MODE_>
 __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel(LinearArgs p) {
     constexpr int MODE = MODE_ & 3;         // the GEMM mode (0 fp32, 1 bf16, 2 bf16x6)
     constexpr bool ABF = (MODE_ & 4) != 0;  // A, A2 bf16 images
-    constexpr bool AUXB = (MODE_ & 8) != 0; // aux0 a bf16 image
+    // MODE_ bit 3: the value-read aux operands are bf16 images -- BWD_RELU's aux0 (its sign),
+    // BWD_SOFTPLUS's aux1 / aux2 (the second-order term); a σ source (aux0 of MUL / TANGENT /
+    // BWD_SOFTPLUS) stays fp32
+    constexpr bool AUX0B = (MODE_ & 8) != 0 && EPI == CN_EPI_BWD_RELU;
+    constexpr bool AUX12B = (MODE_ & 8) != 0 && EPI == CN_EPI_BWD_SOFTPLUS;
     static_assert(!ABF || MODE == 1, "bf16 A images only in the bf16 MFMA mode");
     constexpr int NT = 64 * WM * WN;
     const float* const cA = p.A;
@@ -271,10 +276,10 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     const int voO0 = (rr * p.ld_out0 + 4 * c4) * 4;
     const int voO1 = (rr * p.ld_out1 + 4 * c4) * 4;
     const int voX0 = (rr * p.ld_aux0 + 4 * c4) * 4;
-    const int voX1 = (rr * p.ld_aux1 + 4 * c4) * 4;
-    const int voX2 = (rr * p.ld_aux2 + 4 * c4) * 4;
+    const int voX1 = (rr * p.ld_aux1 + 4 * c4) * (AUX12B ? 2 : 4);
+    const int voX2 = (rr * p.ld_aux2 + 4 * c4) * (AUX12B ? 2 : 4);
     const int voS = (rr * p.ld_split + 4 * c4) * 4;
-    const int voX0b = (rr * p.ld_aux0 + 4 * c4) * 2;  // (AUXB) bf16 aux0
+    const int voX0b = (rr * p.ld_aux0 + 4 * c4) * 2;  // (AUX0B) bf16 aux0
     const int voO0b = (rr * p.ld_out0_b + 4 * c4) * 2;  // bf16 images of out0 / out1
     const int voO1b = (rr * p.ld_out1_b + 4 * c4) * 2;
     const float c_exp = p.beta * 1.44269504088896341f;        // beta log2(e)
@@ -502,7 +507,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         // per-tile views, re-based on the pass's first row by SALU arithmetic (view_at)
         const TileView tO0 = {cOut0 + (int64_t)m0 * p.ld_out0 + n0, p.ld_out0, cOut0 ? (rows * p.ld_out0 - n0) * 4 : 0};
         const TileView tO1 = {p.out1 + (int64_t)m0 * p.ld_out1 + n0, p.ld_out1, p.out1 ? (rows * p.ld_out1 - n0) * 4 : 0};
-        const TileView tX0 = AUXB ? tile_view_b16(p.aux0, p.ld_aux0, m0, n0, rows)
+        const TileView tX0 = AUX0B ? tile_view_b16(p.aux0, p.ld_aux0, m0, n0, rows)
                                   : TileView{p.aux0 + (int64_t)m0 * p.ld_aux0 + n0, p.ld_aux0,
                                              p.aux0 ? (rows * p.ld_aux0 - n0) * 4 : 0};
         // bf16 images of out0 / out1 (MODE 1; empty views when absent)
@@ -510,8 +515,12 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         const TileView tO1b = tile_view_b16(p.out1_b, p.ld_out1_b, m0, n0, rows);
         const bool has_b0 = MODE == 1 && p.out0_b != nullptr;  // wave-uniform
         const bool has_b1 = MODE == 1 && p.out1_b != nullptr;
-        const TileView tX1 = {p.aux1 + (int64_t)m0 * p.ld_aux1 + n0, p.ld_aux1, p.aux1 ? (rows * p.ld_aux1 - n0) * 4 : 0};
-        const TileView tX2 = {p.aux2 + (int64_t)m0 * p.ld_aux2 + n0, p.ld_aux2, p.aux2 ? (rows * p.ld_aux2 - n0) * 4 : 0};
+        const TileView tX1 = AUX12B ? tile_view_b16(p.aux1, p.ld_aux1, m0, n0, rows)
+                                    : TileView{p.aux1 + (int64_t)m0 * p.ld_aux1 + n0, p.ld_aux1,
+                                               p.aux1 ? (rows * p.ld_aux1 - n0) * 4 : 0};
+        const TileView tX2 = AUX12B ? tile_view_b16(p.aux2, p.ld_aux2, m0, n0, rows)
+                                    : TileView{p.aux2 + (int64_t)m0 * p.ld_aux2 + n0, p.ld_aux2,
+                                               p.aux2 ? (rows * p.ld_aux2 - n0) * 4 : 0};
         const TileView tR = {p.rowv + m0, 1, ROWV ? rows * 4 : 0};
         const int sh = n0 - p.nsplit;  // out_split column of this tile's first column
         const TileView tS = {p.out_split + (int64_t)m0 * p.ld_split + sh, p.ld_split,
@@ -543,9 +552,9 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 const int lrow = part * PROWS + (g * GROUP + q) * RPP;  // wave-uniform slab row of the pass
                 // unconditional: the views make reads past a row (columns >= N) or
                 // past the last row harmless, and only region-0 lanes use the values
-                if (kAux0) x0[slot][q] = AUXB ? bload_b16x4(view_at(tX0, lrow), voX0b, 0) : bload4(view_at(tX0, lrow), voX0, 0);
-                if (kAux1) x1[slot][q] = bload4(view_at(tX1, lrow), voX1, 0);
-                if (kAux1) x2[slot][q] = bload4(view_at(tX2, lrow), voX2, 0);
+                if (kAux0) x0[slot][q] = AUX0B ? bload_b16x4(view_at(tX0, lrow), voX0b, 0) : bload4(view_at(tX0, lrow), voX0, 0);
+                if (kAux1) x1[slot][q] = AUX12B ? bload_b16x4(view_at(tX1, lrow), voX1, 0) : bload4(view_at(tX1, lrow), voX1, 0);
+                if (kAux1) x2[slot][q] = AUX12B ? bload_b16x4(view_at(tX2, lrow), voX2, 0) : bload4(view_at(tX2, lrow), voX2, 0);
                 if (ROWV) rv[slot][q] = bload1(view_at(tR, lrow), rr * 4, 0);
                 if (kHead) hidx[slot][q] = __builtin_bit_cast(int, bload1(view_at(tI, lrow), rr * 4, 0));
             }
@@ -749,9 +758,9 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             const int lrow = wm * TM * 32 + 4 * (lane >> 5);
             const int lcol = wn * TN * 32 + (lane & 31);
             const int vo = (lrow * p.ld_out0 + lcol) * 4;
-            const int v0 = (lrow * p.ld_aux0 + lcol) * (AUXB ? 2 : 4);
-            const int v1 = (lrow * p.ld_aux1 + lcol) * 4;
-            const int v2 = (lrow * p.ld_aux2 + lcol) * 4;
+            const int v0 = (lrow * p.ld_aux0 + lcol) * (AUX0B ? 2 : 4);
+            const int v1 = (lrow * p.ld_aux1 + lcol) * (AUX12B ? 2 : 4);
+            const int v2 = (lrow * p.ld_aux2 + lcol) * (AUX12B ? 2 : 4);
             int voj[TN], vbj[TN];
             bool live[TN];
             direct_cols(vo, lcol, voj, live);
@@ -769,7 +778,8 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             }
             constexpr int RG = kAux1 ? 2 : 4;          // accumulator rows r per group (even: bf16 pairs)
             constexpr int NGD = TM * 16 / RG;          // groups per tile
-            constexpr int ASTEP = AUXB ? 64 : 128;     // bytes per 32-column block of aux0
+            constexpr int ASTEP = AUX0B ? 64 : 128;    // bytes per 32-column block of aux0
+            constexpr int XSTEP = AUX12B ? 64 : 128;   // ... of aux1 / aux2
             float xa[2][RG][TN], xb[2][RG][TN], xc[2][RG][TN];
             auto dload = [&](int g, int sl) {
                 const int i = g / (16 / RG), r0 = (g % (16 / RG)) * RG;
@@ -778,10 +788,12 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                     const int r = r0 + q, row = i * 32 + (r & 3) + 8 * (r >> 2);
 #pragma unroll
                     for (int j = 0; j < TN; ++j) {
-                        xa[sl][q][j] = AUXB ? bload_b16(view_at(tX0, row), v0, ASTEP * j)
+                        xa[sl][q][j] = AUX0B ? bload_b16(view_at(tX0, row), v0, ASTEP * j)
                                             : bload1(view_at(tX0, row), v0, ASTEP * j);
-                        if (kAux1) xb[sl][q][j] = bload1(view_at(tX1, row), v1, 128 * j);
-                        if (kAux1) xc[sl][q][j] = bload1(view_at(tX2, row), v2, 128 * j);
+                        if (kAux1) xb[sl][q][j] = AUX12B ? bload_b16(view_at(tX1, row), v1, XSTEP * j)
+                                                         : bload1(view_at(tX1, row), v1, XSTEP * j);
+                        if (kAux1) xc[sl][q][j] = AUX12B ? bload_b16(view_at(tX2, row), v2, XSTEP * j)
+                                                         : bload1(view_at(tX2, row), v2, XSTEP * j);
                     }
                 }
             };
@@ -1316,11 +1328,11 @@ static int launch_linear_tile_m(const cn_linear_desc* d, LinearArgs& a, hipStrea
     const int ntiles = cdiv(a.n_tiles_m, 8) * 8 * a.n_tiles_n;
     const int grid = std::min(ntiles, OCC * device_cus());  // OCC resident workgroups per CU
     dim3 block(64 * WM * WN);
-    // (a bf16 aux0 -- MODE_ bit 3 -- only for BWD_RELU, without a rank-1 term: host-checked)
+    // (bf16 aux images -- MODE_ bit 3 -- only for BWD_RELU / BWD_SOFTPLUS, without a rank-1 term: host-checked)
     switch (d->epilogue) {
 #define CN_EPI_CASE(E)                                                                                   \
         case E:                                                                                          \
-            if constexpr ((MODE_ & 8) == 0 || E == CN_EPI_BWD_RELU) {                                     \
+            if constexpr ((MODE_ & 8) == 0 || E == CN_EPI_BWD_RELU || E == CN_EPI_BWD_SOFTPLUS) {         \
                 if (d->rowv && (MODE_ & 8) == 0)                                                         \
                     linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, E, (MODE_ & 8) == 0, MODE_><<<grid, block, 0, s>>>(a); \
                 else                                                                                     \
@@ -1344,7 +1356,7 @@ static int launch_linear_tile_m(const cn_linear_desc* d, LinearArgs& a, hipStrea
 // The template MODE_ of a descriptor on a tile of GEMM mode MODE: + 4 for bf16 A images, + 8 for a
 // bf16 aux0 (MODE 1 only).
 static int linear_mode_bits(const cn_linear_desc* d, int mode) {
-    return mode == 1 ? mode + (d->a_bf16 ? 4 : 0) + (d->aux0_bf16 ? 8 : 0) : mode;
+    return mode == 1 ? mode + (d->a_bf16 ? 4 : 0) + (d->aux0_bf16 || d->aux12_bf16 ? 8 : 0) : mode;
 }
 
 template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int MODE = 0>
@@ -1429,12 +1441,16 @@ static int linear_plan(const cn_linear_desc* d, LinearArgs& a) {
     const bool x6 = d->mfma_dtype == CN_MFMA_F32_BF16X6;
     CN_REQUIRE(d->K % (bf ? 64 : 32) == 0, CN_ERR_SHAPE, "cn_linear: K=%d must be a multiple of %d", d->K, bf ? 64 : 32);
     CN_REQUIRE(d->tile >= 0 && d->tile <= 2, CN_ERR_ARG, "cn_linear: bad tile %d", d->tile);
-    if (d->a_bf16 || d->aux0_bf16 || d->out0_b || d->out1_b) {  // bf16 operand images (ABI v10)
+    if (d->a_bf16 || d->aux0_bf16 || d->aux12_bf16 || d->out0_b || d->out1_b) {  // bf16 operand images (ABI v10)
         CN_REQUIRE(bf, CN_ERR_UNSUPPORTED, "cn_linear: bf16 operand images need mfma_dtype CN_MFMA_BF16");
         CN_REQUIRE(!d->a_bf16 || (d->lda % 8 == 0 && (!d->A2 || d->lda2 % 8 == 0)), CN_ERR_ALIGN,
                    "cn_linear: bf16 A / A2 need lda, lda2 multiples of 8");
         CN_REQUIRE(!d->aux0_bf16 || (d->epilogue == CN_EPI_BWD_RELU && !d->rowv && d->ld_aux0 % 8 == 0),
                    CN_ERR_UNSUPPORTED, "cn_linear: a bf16 aux0 is for BWD_RELU (no rowv, ld_aux0 % 8 == 0)");
+        CN_REQUIRE(!d->aux12_bf16 || (d->epilogue == CN_EPI_BWD_SOFTPLUS && !d->rowv && d->aux1 && d->aux2 &&
+                                      d->ld_aux1 % 8 == 0 && d->ld_aux2 % 8 == 0),
+                   CN_ERR_UNSUPPORTED, "cn_linear: bf16 aux1 / aux2 are for BWD_SOFTPLUS (both set, no rowv, "
+                   "leading dimensions % 8 == 0)");
         CN_REQUIRE(!d->out0_b || (al16(d->out0_b) && d->ld_out0_b % 8 == 0 && d->ld_out0_b < (1 << 20) &&
                                   d->ld_out0_b >= std::max(d->nzero, d->N)),
                    CN_ERR_ALIGN, "cn_linear: out0_b needs 16-byte alignment and ld_out0_b >= nzero, % 8 == 0");
@@ -1556,7 +1572,7 @@ extern "C" int cn_linear_kernel_name(const cn_linear_desc* d, char* buf, int32_t
 #undef CN_TILE_NAME
     }
     const int n = snprintf(buf, (size_t)len, "void cn::linear_kernel<%s, %d, %s, %d>(cn::LinearArgs)", args,
-                           d->epilogue, d->rowv && !d->aux0_bf16 ? "true" : "false", mode);
+                           d->epilogue, d->rowv && (mode & 8) == 0 ? "true" : "false", mode);
     CN_REQUIRE(n < len, CN_ERR_SHAPE, "cn_linear_kernel_name: buffer of %d bytes too small (%d)", len, n + 1);
     return n;
 }

@@ -130,11 +130,15 @@ typedef struct cn_linear_desc {
        a_bf16: A and A2 are bf16 row-major (lda / lda2 in bf16 elements, multiples of 8).
        aux0_bf16: BWD_RELU's aux0 is bf16 (the sign test of the bf16 value: bf16 RNE keeps the sign,
        and a positive value rounds to 0 only below 2^-133).
+       aux12_bf16: BWD_SOFTPLUS's aux1 and aux2 (the second-order term's s and u') are bf16 (config
+       C3 stores the ∇-pass adjoints and the tangents, read only by GEMMs and by this term, in bf16;
+       the σ source aux0 stays fp32).
        out0_b (ld_out0_b): the bf16 image of every value written to out0 (columns [0, nzero),
        including the zero fill); out0 itself may then be NULL.  out1_b: the same for SOFTPLUS_HEAD's
        out1.  Leading dimensions in bf16 elements, multiples of 8; 16-byte aligned. */
     int32_t a_bf16;
     int32_t aux0_bf16;
+    int32_t aux12_bf16;
     void* out0_b;
     int64_t ld_out0_b;
     void* out1_b;

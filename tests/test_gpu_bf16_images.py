@@ -166,8 +166,10 @@ def test_wgrad_bf16_ring_images(M, pairs):
 
 def test_sdf_field_bf16_images_match_fp32_operand_path():
     """The SDF field in bf16 mode (every hidden activation / adjoint read as a bf16 image) against the
-    same field with the images' fp32 sources as operands (the kernels round those the same way):
-    sdf, ∇ₓsdf and every parameter gradient of a double-backward loss, bitwise."""
+    same field with the images' fp32 sources as operands (the kernels round those the same way): sdf,
+    feature and ∇ₓsdf bitwise; the parameter gradients of a double-backward loss within bf16 rounding
+    (the mode also stores the ∇-pass adjoints s and the tangents u̇ in bf16 for the adjoint's
+    second-order term, and db sums the bf16 adjoint images)."""
     from copenerf import SDFNetwork, fields
     from helpers import SDF_CFG
     torch.manual_seed(3)
@@ -187,11 +189,12 @@ def test_sdf_field_bf16_images_match_fp32_operand_path():
         fields._img_mode = saved
     names = ["sdf", "feat", "grad"] + [n for n, _ in net.named_parameters()]
     for n, a, b in zip(names, res[0], res[1]):
-        if n.endswith("bias") and not n.startswith("lin8"):
-            # db sums the bf16 image of Z_l (the adjoint is stored as an image): bf16-rounding noise
-            torch.testing.assert_close(a, b, rtol=1e-2, atol=1e-2 * b.abs().max().item() + 1e-6)
-        else:
+        if n in ("sdf", "feat", "grad"):
             assert torch.equal(a, b), n
+        else:
+            rel = ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+            print(f"{n}: relative L2 {rel:.2e}")
+            assert rel <= 2e-2, (n, rel)
 
 
 def test_color_bf16_images_match_fp32_operand_path():

@@ -20,7 +20,9 @@ if [ $TESTS = 1 ]; then
   [ $rc = 0 ] || exit $rc
 fi
 for c in ${@:-c2}; do
-  timeout -k 10 400 python3 -u bench.py --config $c --no-cpu-baseline > $O/bench_$c.json 2> $O/bench_$c.err
+  # <config>graph: the config replayed from a captured HIP graph
+  case $c in *graph) args="--config ${c%graph} --graph";; *) args="--config $c";; esac
+  timeout -k 10 400 python3 -u bench.py $args --no-cpu-baseline > $O/bench_$c.json 2> $O/bench_$c.err
   rc=$?
   [ $rc = 0 ] || { echo "bench $c failed rc=$rc"; tail -5 $O/bench_$c.err; exit $rc; }
   python3 -c "import json,sys; d=json.load(open('$O/bench_$c.json')); print('$c', d['value'], d['ms_per_step'], d['roofline']['launch_class'], d['roofline']['frac'])"
