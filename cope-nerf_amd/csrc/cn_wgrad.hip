@@ -713,6 +713,9 @@ __global__ void __launch_bounds__(512, 2) wgrad_b16r_kernel(WgradBatch batch) {
             const rsrc_t v = make_view(reinterpret_cast<const float*>(base), (nrows * ld - col0) * 2);
 #pragma unroll
             for (int r = 0; r < 4; ++r) r8[r] = bload4(v, ((mq * 4 + r) * ld + cg * 8) * 2, 0);
+            // defined on both paths: with sets 4..7 left unwritten here the ring went to scratch
+#pragma unroll
+            for (int r = 4; r < 8; ++r) r8[r] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
         } else {  // 4 rows x (4 columns of group cg, 4 of group cg + 32)
             const rsrc_t v = make_view(src + (int64_t)mrow * ld + col0, (nrows * ld - col0) * 4);
 #pragma unroll
@@ -728,8 +731,10 @@ __global__ void __launch_bounds__(512, 2) wgrad_b16r_kernel(WgradBatch batch) {
             // rows r0..r3 as 4 dwords each (8 bf16): column 2d is the low halves of dword d, 2d + 1 the high
 #pragma unroll
             for (int d = 0; d < 4; ++d) {
-                const unsigned w0 = __builtin_bit_cast(unsigned, r8[0][d]), w1 = __builtin_bit_cast(unsigned, r8[1][d]);
-                const unsigned w2 = __builtin_bit_cast(unsigned, r8[2][d]), w3 = __builtin_bit_cast(unsigned, r8[3][d]);
+                // values first: a bit cast of a vector-element lvalue reads the vector's first element
+                const float f0 = r8[0][d], f1 = r8[1][d], f2 = r8[2][d], f3 = r8[3][d];
+                const unsigned w0 = __builtin_bit_cast(unsigned, f0), w1 = __builtin_bit_cast(unsigned, f1);
+                const unsigned w2 = __builtin_bit_cast(unsigned, f2), w3 = __builtin_bit_cast(unsigned, f3);
                 const u32x2_t lo = {__builtin_amdgcn_perm(w1, w0, 0x05040100u), __builtin_amdgcn_perm(w3, w2, 0x05040100u)};
                 const u32x2_t hi = {__builtin_amdgcn_perm(w1, w0, 0x07060302u), __builtin_amdgcn_perm(w3, w2, 0x07060302u)};
                 *reinterpret_cast<u32x2_t*>(img + (cg * 8 + 2 * d) * LSB) = lo;
