@@ -1328,13 +1328,15 @@ static int launch_linear_tile_m(const cn_linear_desc* d, LinearArgs& a, hipStrea
     const int ntiles = cdiv(a.n_tiles_m, 8) * 8 * a.n_tiles_n;
     const int grid = std::min(ntiles, OCC * device_cus());  // OCC resident workgroups per CU
     dim3 block(64 * WM * WN);
-    // (bf16 aux images -- MODE_ bit 3 -- only for BWD_RELU / BWD_SOFTPLUS, without a rank-1 term: host-checked)
+    // (bf16 aux images -- MODE_ bit 3 -- only for BWD_RELU / BWD_SOFTPLUS, without a rank-1 term; the
+    // 64x128 wave tiles never take a rank-1 term: both host-checked, so those kernels are not built)
+    constexpr bool kRowv = (MODE_ & 8) == 0 && TM * TN < 8;
     switch (d->epilogue) {
 #define CN_EPI_CASE(E)                                                                                   \
         case E:                                                                                          \
             if constexpr ((MODE_ & 8) == 0 || E == CN_EPI_BWD_RELU || E == CN_EPI_BWD_SOFTPLUS) {         \
-                if (d->rowv && (MODE_ & 8) == 0)                                                         \
-                    linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, E, (MODE_ & 8) == 0, MODE_><<<grid, block, 0, s>>>(a); \
+                if (kRowv && d->rowv)                                                                    \
+                    linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, E, kRowv, MODE_><<<grid, block, 0, s>>>(a); \
                 else                                                                                     \
                     linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, E, false, MODE_><<<grid, block, 0, s>>>(a); \
             }                                                                                            \
