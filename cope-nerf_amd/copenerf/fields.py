@@ -208,6 +208,12 @@ def _empty_b(M, n, dev):
     return torch.empty(M, n, device=dev, dtype=torch.bfloat16)
 
 
+def _act(U, Ub, l):
+    """The stored activation U_l an epilogue recovers σ_{l-1} from: fp32, or (bf16 mode, hidden layers
+    1..7) its bf16 image -- the only copy kept there."""
+    return U[l] if U[l] is not None else Ub[l]
+
+
 def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool, want_grad: bool, keep: bool,
                 sdf_out: Optional[torch.Tensor] = None, dst: Optional[torch.Tensor] = None):
     """Forward of SDFNetwork (neus_fields.py:268-283) and, with want_grad, the
@@ -221,8 +227,10 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
     colour network's first layer, NeuSRenderer._folded_color_pack).
     bf16 mode (_img_mode): Ub / Sb hold the bf16 operand images of the hidden activations and ∇-pass
     adjoints, which the next GEMMs, the weight gradients and (s) the adjoint's second-order term read;
-    fp32 is kept only where it is needed: U_l for the epilogues that recover σ from it (not on the
-    sampler path), s_0 and s_7 for the fp32 first-layer weight gradient / the elementwise last adjoint.
+    fp32 is kept only where it is needed: the encoding U_0, the last hidden activation U_8 (the
+    elementwise last adjoint, the colour network's fold), s_0 and s_7 for the fp32 first-layer weight
+    gradient / the elementwise last adjoint.  The hidden activations U_1..U_7 are images only: the GEMMs
+    read them as A, the weight gradients as X, and MUL / TANGENT / BWD_SOFTPLUS recover σ from them.
     """
     M, dev = x.shape[0], x.device
     nl, sk, HL, KE = lay.n_lin, lay.skip, lay.HL, lay.KE
@@ -236,7 +244,6 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
         o = lay.out_dim[sk - 1]
         if img and 1 <= sk < L8:
             Usk_b = _empty_b(M, HL, dev)  # the skip input's operand image, its tail written by the embedding
-            Usk = _empty(M, HL, dev) if keep_u else None
             e_view = Usk_b[:, o:o + lay.E]
         else:
             Usk = _empty(M, HL, dev)
@@ -262,9 +269,9 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
             U[l + 1] = out
         else:
             ob = None
-            if img and l + 1 < L8:  # the next layer's operand image (+ the fp32 values when kept)
+            if img and l + 1 < L8:  # the next layer's operand image, the activation's only copy
                 ob = Usk_b if into else _empty_b(M, HL, dev)
-                out = (Usk if into else _empty(M, HL, dev)) if keep_u else None
+                out = None
             else:
                 out = Usk if into else _empty(M, HL, dev)
             ops.linear(A, pk.Bf[l], lay.out_dim[l], K, out, EPI_SOFTPLUS, bias=pk.b[l],
@@ -296,11 +303,11 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
             S[l - 1] = _empty(M, HL, dev) if (not img or l - 1 == 0) else None
             A = Sb[l] if Sb[l] is not None else S[l]
             if l == sk:
-                ops.linear(A, pk.Bt[l], lay.in_dim[l], Kl, S[l - 1], EPI_MUL, aux0=U[l], aux_beta=sig_beta(lay, l - 1),
-                           nsplit=lay.out_dim[l - 1], out_split=QE, nzero=HL, adiv=SQRT2, kalg=lay.out_dim[l],
-                           out0_b=Sb[l - 1])
+                ops.linear(A, pk.Bt[l], lay.in_dim[l], Kl, S[l - 1], EPI_MUL, aux0=_act(U, Ub, l),
+                           aux_beta=sig_beta(lay, l - 1), nsplit=lay.out_dim[l - 1], out_split=QE, nzero=HL,
+                           adiv=SQRT2, kalg=lay.out_dim[l], out0_b=Sb[l - 1])
             else:
-                ops.linear(A, pk.Bt[l], lay.out_dim[l - 1], Kl, S[l - 1], EPI_MUL, aux0=U[l],
+                ops.linear(A, pk.Bt[l], lay.out_dim[l - 1], Kl, S[l - 1], EPI_MUL, aux0=_act(U, Ub, l),
                            aux_beta=sig_beta(lay, l - 1), nzero=HL, kalg=lay.out_dim[l], out0_b=Sb[l - 1])
         Q0 = _empty(M, KE, dev)
         ops.linear(Sb[0] if Sb[0] is not None else S[0], pk.Bt[0], lay.E, rup(lay.out_dim[0], 32), Q0, EPI_STORE,
@@ -317,6 +324,7 @@ def sdf_input_grad(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dh=None):
     P_{l-1} = (W_lᵀ P_l) ⊙ σ_{l-1} from P_7 = (W_8fᵀ dfeat + dsdf w80) ⊙ σ_7, then
     dx = scale · J_emb(x)ᵀ (W_0ᵀ P_0 + skip-embedding part)."""
     U = st["U"]
+    Ub = st.get("Ub") or [None] * lay.n_lin
     M, dev = U[0].shape[0], U[0].device
     nl, sk, HL, KE = lay.n_lin, lay.skip, lay.HL, lay.KE
     L8 = nl - 1
@@ -339,11 +347,12 @@ def sdf_input_grad(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dh=None):
         Kl = rup(lay.out_dim[l], 32)
         Pn = _empty(M, HL, dev)
         if l == sk:
-            ops.linear(P, pk.Bt[l], lay.in_dim[l], Kl, Pn, EPI_MUL, aux0=U[l], aux_beta=sig_beta(lay, l - 1),
-                       nsplit=lay.out_dim[l - 1], out_split=PE, nzero=HL, adiv=SQRT2, kalg=lay.out_dim[l])
+            ops.linear(P, pk.Bt[l], lay.in_dim[l], Kl, Pn, EPI_MUL, aux0=_act(U, Ub, l),
+                       aux_beta=sig_beta(lay, l - 1), nsplit=lay.out_dim[l - 1], out_split=PE, nzero=HL, adiv=SQRT2,
+                       kalg=lay.out_dim[l])
         else:
-            ops.linear(P, pk.Bt[l], lay.out_dim[l - 1], Kl, Pn, EPI_MUL, aux0=U[l], aux_beta=sig_beta(lay, l - 1),
-                       nzero=HL, kalg=lay.out_dim[l])
+            ops.linear(P, pk.Bt[l], lay.out_dim[l - 1], Kl, Pn, EPI_MUL, aux0=_act(U, Ub, l),
+                       aux_beta=sig_beta(lay, l - 1), nzero=HL, kalg=lay.out_dim[l])
         P = Pn
     P0 = _empty(M, KE, dev)
     ops.linear(P, pk.Bt[0], lay.E, rup(lay.out_dim[0], 32), P0, EPI_STORE, nzero=KE, kalg=lay.out_dim[0])
@@ -408,7 +417,8 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
                 out, ob = (Usk_d if into else _empty(M, HL, dev)), None
             K = KE if l == 0 else rup(lay.in_dim[l], 32)
             A = Udb[l] if Udb[l] is not None else Ud[l]
-            ops.linear(A, pk.Bf[l], lay.out_dim[l], K, out, EPI_TANGENT, aux0=U[l + 1], aux_beta=sig_beta(lay, l),
+            ops.linear(A, pk.Bf[l], lay.out_dim[l], K, out, EPI_TANGENT, aux0=_act(U, Ub, l + 1),
+                       aux_beta=sig_beta(lay, l),
                        nzero=lay.out_dim[l] if into else HL, odiv=SQRT2 if into else 1.0, beta=lay.beta,
                        kalg=lay.in_dim[l], out0_b=ob)
             Ud[l + 1], Udb[l + 1] = out, ob
@@ -486,14 +496,15 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
             zo = dict(out0_b=Z) if zb else {}
             if share and l == sk:  # + the embedding columns of the skip input (sdf_input_grad's PE)
                 ops.linear(Zl, pk.Bt[l], lay.in_dim[l], rup(lay.out_dim[l], 32), None if zb else Z, EPI_MUL,
-                           aux0=U[l], aux_beta=sig_beta(lay, l - 1), nsplit=lay.out_dim[l - 1], out_split=PE,
+                           aux0=_act(U, Ub, l), aux_beta=sig_beta(lay, l - 1), nsplit=lay.out_dim[l - 1], out_split=PE,
                            nzero=HL, adiv=SQRT2, kalg=lay.out_dim[l], **zo)
             else:
                 # first order only (no second-order term): Z = (W̃ᵀZ)σ is the MUL epilogue, which runs on
                 # the 256x256 tile (BWD_SOFTPLUS would add an all-zero term on the 128x128 tile)
                 ops.linear(Zl, pk.Bt[l], lay.out_dim[l - 1], rup(lay.out_dim[l], 32), None if zb else Z,
                            EPI_BWD_SOFTPLUS if second else EPI_MUL,
-                           aux0=U[l], aux_beta=sig_beta(lay, l - 1), nzero=HL, adiv=SQRT2 if l == sk else 1.0,
+                           aux0=_act(U, Ub, l), aux_beta=sig_beta(lay, l - 1), nzero=HL,
+                           adiv=SQRT2 if l == sk else 1.0,
                            kalg=lay.out_dim[l], **second_order(l - 1), **zo)
         dW = torch.empty(lay.out_dim[l], lay.in_dim[l], device=dev)
         db = torch.empty(lay.out_dim[l], device=dev)

@@ -232,7 +232,9 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
     = out0[m] · head_w + head_b.
     tile: None (the library's choice), 1 (128x64), 2 (128x128 only: tests compare the tiles).
     bf16 operand images (bf16 MFMA mode only, ABI v10): A (with A2) may be bfloat16 -- the rounded
-    operand itself, read instead of rounded on load; aux0 may be bfloat16 for BWD_RELU (its sign);
+    operand itself, read instead of rounded on load; aux0 may be bfloat16 for BWD_RELU (its sign) and
+    for MUL / TANGENT / BWD_SOFTPLUS (the activation σ is recovered from), BWD_SOFTPLUS's aux1 / aux2
+    too (all three in one dtype);
     out0_b / out1_b (bfloat16, or None) receive the RNE bf16 image of every value written to out0 /
     out1, and out0 may then be None."""
     x6 = B.dim() == 3
@@ -248,16 +250,20 @@ def linear(A, B, N, K, out0, epilogue, *, bias=None, A2=None, K1=None, rowv=None
         if t is None or t is B:
             continue
         want_b = n in ("out0_b", "out1_b")
-        may_b = bf and (n in ("A", "A2") or (n == "aux0" and epilogue == EPI_BWD_RELU) or
+        may_b = bf and (n in ("A", "A2") or
+                        (n == "aux0" and epilogue in (EPI_BWD_RELU, EPI_MUL, EPI_TANGENT, EPI_BWD_SOFTPLUS)) or
                         (n in ("aux1", "aux2") and epilogue == EPI_BWD_SOFTPLUS))
         if (t.dtype == torch.bfloat16) != want_b and not (may_b and t.dtype == torch.bfloat16):
-            raise RuntimeError(f"cn_linear: {n} has dtype {t.dtype} (bfloat16 images: A / A2, BWD_RELU's aux0, "
-                               f"BWD_SOFTPLUS's aux1 / aux2 and out0_b / out1_b, in the bf16 MFMA mode only)")
+            raise RuntimeError(f"cn_linear: {n} has dtype {t.dtype} (bfloat16 images: A / A2, the aux0 of MUL / "
+                               f"TANGENT / BWD_SOFTPLUS / BWD_RELU, BWD_SOFTPLUS's aux1 / aux2 and out0_b / out1_b, "
+                               f"in the bf16 MFMA mode only)")
     a_b = A.dtype == torch.bfloat16
     if A2 is not None and (A2.dtype == torch.bfloat16) != a_b:
         raise RuntimeError("cn_linear: A and A2 must have the same dtype")
     if aux1 is not None and aux2 is not None and aux1.dtype != aux2.dtype:
         raise RuntimeError("cn_linear: aux1 and aux2 must have the same dtype")
+    if aux1 is not None and aux0 is not None and aux1.dtype != aux0.dtype:
+        raise RuntimeError("cn_linear: BWD_SOFTPLUS's aux0, aux1 and aux2 must have the same dtype")
     if bf:
         K = rup(K, 64)
         K1 = rup(K1, 64) if K1 is not None else None

@@ -90,7 +90,10 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     // MODE_ bit 3: the value-read aux operands are bf16 images -- BWD_RELU's aux0 (its sign),
     // BWD_SOFTPLUS's aux1 / aux2 (the second-order term); a σ source (aux0 of MUL / TANGENT /
     // BWD_SOFTPLUS) stays fp32
-    constexpr bool AUX0B = (MODE_ & 8) != 0 && EPI == CN_EPI_BWD_RELU;
+    // MODE_ bit 3: every aux operand of the epilogue is a bf16 image (aux0: σ's activation or
+    // BWD_RELU's sign source; BWD_SOFTPLUS's aux1 / aux2 too)
+    constexpr bool AUX0B = (MODE_ & 8) != 0 && (EPI == CN_EPI_BWD_RELU || EPI == CN_EPI_MUL || EPI == CN_EPI_TANGENT ||
+                                                EPI == CN_EPI_BWD_SOFTPLUS);
     constexpr bool AUX12B = (MODE_ & 8) != 0 && EPI == CN_EPI_BWD_SOFTPLUS;
     static_assert(!ABF || MODE == 1, "bf16 A images only in the bf16 MFMA mode");
     constexpr int NT = 64 * WM * WN;
@@ -1328,13 +1331,14 @@ static int launch_linear_tile_m(const cn_linear_desc* d, LinearArgs& a, hipStrea
     const int ntiles = cdiv(a.n_tiles_m, 8) * 8 * a.n_tiles_n;
     const int grid = std::min(ntiles, OCC * device_cus());  // OCC resident workgroups per CU
     dim3 block(64 * WM * WN);
-    // (bf16 aux images -- MODE_ bit 3 -- only for BWD_RELU / BWD_SOFTPLUS, without a rank-1 term; the
+    // (bf16 aux images -- MODE_ bit 3 -- only for MUL / TANGENT / BWD_SOFTPLUS / BWD_RELU, without a rank-1 term; the
     // 64x128 wave tiles never take a rank-1 term: both host-checked, so those kernels are not built)
     constexpr bool kRowv = (MODE_ & 8) == 0 && TM * TN < 8;
     switch (d->epilogue) {
 #define CN_EPI_CASE(E)                                                                                   \
         case E:                                                                                          \
-            if constexpr ((MODE_ & 8) == 0 || E == CN_EPI_BWD_RELU || E == CN_EPI_BWD_SOFTPLUS) {         \
+            if constexpr ((MODE_ & 8) == 0 || E == CN_EPI_BWD_RELU || E == CN_EPI_BWD_SOFTPLUS ||       \
+                          E == CN_EPI_MUL || E == CN_EPI_TANGENT) {                                      \
                 if (kRowv && d->rowv)                                                                    \
                     linear_kernel<WM, WN, TM, TN, BK, OCC, DEPTH, E, kRowv, MODE_><<<grid, block, 0, s>>>(a); \
                 else                                                                                     \
@@ -1447,12 +1451,18 @@ static int linear_plan(const cn_linear_desc* d, LinearArgs& a) {
         CN_REQUIRE(bf, CN_ERR_UNSUPPORTED, "cn_linear: bf16 operand images need mfma_dtype CN_MFMA_BF16");
         CN_REQUIRE(!d->a_bf16 || (d->lda % 8 == 0 && (!d->A2 || d->lda2 % 8 == 0)), CN_ERR_ALIGN,
                    "cn_linear: bf16 A / A2 need lda, lda2 multiples of 8");
-        CN_REQUIRE(!d->aux0_bf16 || (d->epilogue == CN_EPI_BWD_RELU && !d->rowv && d->ld_aux0 % 8 == 0),
-                   CN_ERR_UNSUPPORTED, "cn_linear: a bf16 aux0 is for BWD_RELU (no rowv, ld_aux0 % 8 == 0)");
-        CN_REQUIRE(!d->aux12_bf16 || (d->epilogue == CN_EPI_BWD_SOFTPLUS && !d->rowv && d->aux1 && d->aux2 &&
+        const int e = d->epilogue;
+        CN_REQUIRE(!d->aux0_bf16 || ((e == CN_EPI_BWD_RELU || e == CN_EPI_MUL || e == CN_EPI_TANGENT ||
+                                      e == CN_EPI_BWD_SOFTPLUS) && d->aux0 && !d->rowv && d->ld_aux0 % 8 == 0),
+                   CN_ERR_UNSUPPORTED, "cn_linear: a bf16 aux0 is for MUL / TANGENT / BWD_SOFTPLUS / BWD_RELU "
+                   "(no rowv, ld_aux0 % 8 == 0)");
+        CN_REQUIRE(!d->aux12_bf16 || (e == CN_EPI_BWD_SOFTPLUS && !d->rowv && d->aux1 && d->aux2 &&
                                       d->ld_aux1 % 8 == 0 && d->ld_aux2 % 8 == 0),
                    CN_ERR_UNSUPPORTED, "cn_linear: bf16 aux1 / aux2 are for BWD_SOFTPLUS (both set, no rowv, "
                    "leading dimensions % 8 == 0)");
+        // one kernel bit for the epilogue's aux operands: all bf16 or all fp32
+        CN_REQUIRE(e != CN_EPI_BWD_SOFTPLUS || !d->aux1 || (d->aux0_bf16 != 0) == (d->aux12_bf16 != 0),
+                   CN_ERR_UNSUPPORTED, "cn_linear: BWD_SOFTPLUS's aux0 and aux1 / aux2 are all bf16 images or all fp32");
         CN_REQUIRE(!d->out0_b || (al16(d->out0_b) && d->ld_out0_b % 8 == 0 && d->ld_out0_b < (1 << 20) &&
                                   d->ld_out0_b >= std::max(d->nzero, d->N)),
                    CN_ERR_ALIGN, "cn_linear: out0_b needs 16-byte alignment and ld_out0_b >= nzero, % 8 == 0");

@@ -128,11 +128,14 @@ typedef struct cn_linear_desc {
        is rounded to bf16 (RNE) when it is staged, so a tensor whose consumers are GEMM operands can be
        stored as that rounded image (2 bytes instead of 4) with bitwise-identical results.
        a_bf16: A and A2 are bf16 row-major (lda / lda2 in bf16 elements, multiples of 8).
-       aux0_bf16: BWD_RELU's aux0 is bf16 (the sign test of the bf16 value: bf16 RNE keeps the sign,
-       and a positive value rounds to 0 only below 2^-133).
+       aux0_bf16: aux0 is bf16 -- BWD_RELU's sign source (bf16 RNE keeps the sign, and a positive
+       value rounds to 0 only below 2^-133), or the activation MUL / TANGENT / BWD_SOFTPLUS recover
+       softplus' σ from (config C3 stores the SDF's hidden activations as bf16 images only; σ from
+       the bf16 activation is within the mode's bf16 operand rounding).
        aux12_bf16: BWD_SOFTPLUS's aux1 and aux2 (the second-order term's s and u') are bf16 (config
-       C3 stores the ∇-pass adjoints and the tangents, read only by GEMMs and by this term, in bf16;
-       the σ source aux0 stays fp32).
+       C3 stores the ∇-pass adjoints and the tangents, read only by GEMMs and by this term, in bf16).
+       BWD_SOFTPLUS with aux1 / aux2 takes all three aux operands in one format: aux0_bf16 ==
+       aux12_bf16.
        out0_b (ld_out0_b): the bf16 image of every value written to out0 (columns [0, nzero),
        including the zero fill); out0 itself may then be NULL.  out1_b: the same for SOFTPLUS_HEAD's
        out1.  Leading dimensions in bf16 elements, multiples of 8; 16-byte aligned. */

@@ -94,6 +94,34 @@ def test_bf16_operand_images_bitwise(tile):
     assert torch.equal(ob, ref.bfloat16())
 
 
+@pytest.mark.parametrize("tile", [0, 2])
+def test_bf16_aux_images_bitwise(tile):
+    """MUL / TANGENT / BWD_SOFTPLUS / BWD_RELU with every aux operand as a bf16 image equal the same
+    epilogues fed the image's values in fp32 (σ recovered from the same activation value, the
+    second-order term from the same s and u̇), with A and the outputs as images too."""
+    from copenerf import ops
+    M, N, K = 3001, 256, 256
+    A = _rnd(M, K, seed=23, scale=0.3)
+    Bb = _rnd(N, K, seed=24, scale=0.06).bfloat16().contiguous()
+    for name, epi, kw in _epi_cases(ops, M, N, 30):
+        if "aux0" not in kw:
+            continue
+        kr = {k: (v.bfloat16().float() if k in ("aux0", "aux1", "aux2") else v) for k, v in kw.items()}
+        ki = {k: (v.bfloat16() if k in ("aux0", "aux1", "aux2") else v) for k, v in kw.items()}
+        ref, _, s_ref = _run(ops, A, Bb, N, K, epi, kr, tile)
+        out, ob, s = _run(ops, A, Bb, N, K, epi, ki, tile, image=True, a_img=True)
+        assert torch.equal(out, ref), name
+        assert torch.equal(ob, ref.bfloat16()), name
+        if s is not None:
+            assert torch.equal(torch.nan_to_num(s, 7.0), torch.nan_to_num(s_ref, 7.0)), name
+    # one format for BWD_SOFTPLUS's three aux operands
+    kw = dict(_epi_cases(ops, M, N, 30)[5][2])
+    assert _epi_cases(ops, M, N, 30)[5][0] == "bwd_softplus"
+    kw["aux0"] = kw["aux0"].bfloat16()
+    with pytest.raises(RuntimeError):
+        _run(ops, A, Bb, N, K, ops.EPI_BWD_SOFTPLUS, kw, tile)
+
+
 def test_bf16_concat_image_and_head():
     """A virtual concat of two images (A | A2), and SOFTPLUS_HEAD's activation / ∇-pass seed images."""
     from copenerf import ops
