@@ -120,6 +120,10 @@ __device__ __forceinline__ floatx2 widen_bf16x2(unsigned p) {
     return floatx2{__builtin_bit_cast(float, p << 16), __builtin_bit_cast(float, p & 0xffff0000u)};
 }
 __device__ __forceinline__ void split3(floatx4 v, bf16x4& t0, bf16x4& t1, bf16x4& t2) {
+#ifdef CN_EXP_SPLIT1  // TEMPORARY measurement build: one rounding, the three terms equal (wrong numerics)
+    t0 = t1 = t2 = __builtin_convertvector(v, bf16x4);
+    return;
+#endif
     unsigned p0[2], p1[2], p2[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {

@@ -194,10 +194,11 @@ def test_wgrad_bf16_ring_images(M, pairs):
 
 def test_sdf_field_bf16_images_match_fp32_operand_path():
     """The SDF field in bf16 mode (every hidden activation / adjoint read as a bf16 image) against the
-    same field with the images' fp32 sources as operands (the kernels round those the same way): sdf,
-    feature and ∇ₓsdf bitwise; the parameter gradients of a double-backward loss within bf16 rounding
-    (the mode also stores the ∇-pass adjoints s and the tangents u̇ in bf16 for the adjoint's
-    second-order term, and db sums the bf16 adjoint images)."""
+    same field with the images' fp32 sources as operands (the kernels round those the same way): sdf
+    and feature bitwise; ∇ₓsdf and the parameter gradients of a double-backward loss within bf16
+    rounding: the mode keeps the hidden activations as images only, so σ is recovered from the bf16
+    activation, and it stores the ∇-pass adjoints s and the tangents u̇ in bf16 for the adjoint's
+    second-order term (db sums the bf16 adjoint images)."""
     from copenerf import SDFNetwork, fields
     from helpers import SDF_CFG
     torch.manual_seed(3)
@@ -217,8 +218,12 @@ def test_sdf_field_bf16_images_match_fp32_operand_path():
         fields._img_mode = saved
     names = ["sdf", "feat", "grad"] + [n for n, _ in net.named_parameters()]
     for n, a, b in zip(names, res[0], res[1]):
-        if n in ("sdf", "feat", "grad"):
+        if n in ("sdf", "feat"):
             assert torch.equal(a, b), n
+        elif n == "grad":
+            rel = ((a - b).norm() / b.norm()).item()
+            print(f"grad: relative L2 {rel:.2e}")
+            assert rel <= 5e-3, rel
         else:
             rel = ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
             print(f"{n}: relative L2 {rel:.2e}")
