@@ -837,6 +837,212 @@ __global__ void __launch_bounds__(512, 2) wgrad_b16r_kernel(WgradBatch batch) {
     }
 }
 
+// s_waitcnt that waits for this wave's vector-memory count to drop to N (expcnt, lgkmcnt untouched)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+
+// One MFMA operand (8 bf16 along the reduction) by two ds_read_b64_tr_b16 at rows r and r + 4 of a
+// 512-byte-row image (ks: + 16 rows); the caller waits lgkmcnt before using it.
+template <int OFF>
+__device__ __forceinline__ bf16x8 tr_read8(uint32_t addr, int ks) {
+    u32x2v lo, hi;
+    if (ks == 0) {
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(addr), "i"(OFF) : "memory");
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(addr), "i"(OFF + 4 * 512) : "memory");
+    } else {
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(addr), "i"(OFF + 16 * 512) : "memory");
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(addr), "i"(OFF + 20 * 512) : "memory");
+    }
+    return __builtin_bit_cast(bf16x8, (u32x4){lo[0], lo[1], hi[0], hi[1]});
+}
+
+// The bf16 weight gradient with BOTH operands bf16 images (config C3's SDF and colour backward
+// passes): the rows go HBM -> LDS by LDS-DMA (buffer_load ... lds, 16 bytes per lane), so the
+// bytes in flight do not live in registers -- wgrad_b16r_kernel's register ring holds two 32-row
+// stages at one workgroup per CU (~4.1 TB/s), this ring NS - 1 = 3 stages (96 KB per CU) -- and the
+// MFMA operands come out of the row-major images by the transposed read ds_read_b64_tr_b16 (lane i
+// of a 16-lane group gets column i of 4 rows).  A stage is 32 sample rows: [32][256] bf16 of Y then
+// of X, 512-byte rows whose 16-byte chunks are XOR-swizzled by (row & 3) << 2 (the DMA writes LDS
+// linearly; the swizzle is in the per-lane global address), so the four rows of a transposed read
+// land in four different bank quarters: conflict-free.  The m order of every MFMA operand is
+// wgrad_b16r_kernel's (m = 16 ks + 8 (lane >> 5) + e), so dW is bitwise equal to it; db sums the Y
+// fragments of pair 0 in the registers (waves of the first column block), a fixed order.
+template <int NS>
+__global__ void __launch_bounds__(512, 2) wgrad_b16d_kernel(WgradBatch batch) {
+    constexpr int BNo = 256, MC = 32, ROWB = 512;
+    constexpr int SIDE = MC * ROWB, STAGE = 2 * SIDE;
+    static_assert(NS >= 3 && MC == 32, "the ring keeps NS - 1 stages of two k-steps in flight");
+    __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
+
+    int ji = 0, b = (int)blockIdx.x;
+    while (ji + 1 < batch.njobs && b >= batch.blocks[ji]) b -= batch.blocks[ji++];
+    const WgradArgs& p = batch.job[ji];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int T = p.n_tiles_n * p.n_tiles_k;
+    const int tile = batch.njobs > 1 ? b % T : (b >> 3) % T;
+    const int slice = batch.njobs > 1 ? b / T : (b & 7) + 8 * ((b >> 3) / T);
+    if (slice >= p.nslices) return;  // (whole workgroup: no barrier is left waiting)
+    const int n0 = (tile / p.n_tiles_k) * BNo;
+    const int k0 = (tile % p.n_tiles_k) * BNo;
+    const int mbeg = slice * p.rows_per_slice;
+    const int mend = min(p.M, mbeg + p.rows_per_slice);
+    const int nch = mend > mbeg ? cdiv(mend - mbeg, MC) : 0;
+    const int total = nch * p.npairs;
+    const bool do_bias = k0 == 0 && p.bpart != nullptr;
+
+    // LDS-DMA: waves 0-3 stage Y, 4-7 X; wave w & 3 the stage rows 8 (w & 3) .. + 7, two rows
+    // (1 KB) per instruction: lane l -> row + (l >> 5), physical chunk l & 31
+    const bool sx = wave >= 4;
+    const int wq = wave & 3;
+    const int col0 = sx ? k0 : n0;
+    // the side's pair-0 / pair-1 rows of this slice from col0 (wave-uniform scalars: the DMA's buffer
+    // resource must sit in SGPRs)
+    auto ufirst = [](int64_t x) {
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x), hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+        return (int64_t)(((uint64_t)hi << 32) | lo);
+    };
+    const int ld0 = sx ? p.ldx0 : p.ldy0, ld1 = sx ? p.ldx1 : p.ldy1;
+    const int64_t src0 = ufirst(reinterpret_cast<int64_t>(reinterpret_cast<const bf16_t*>(sx ? p.X0 : p.Y0) +
+                                                          (int64_t)mbeg * ld0 + col0));
+    const int64_t src1 = p.npairs > 1 ? ufirst(reinterpret_cast<int64_t>(reinterpret_cast<const bf16_t*>(sx ? p.X1 : p.Y1) +
+                                                                         (int64_t)mbeg * ld1 + col0))
+                                      : src0;
+    const int bytes0 = mend > mbeg ? ((mend - mbeg) * ld0 - col0) * 2 : 0;
+    const int bytes1 = mend > mbeg && p.npairs > 1 ? ((mend - mbeg) * ld1 - col0) * 2 : 0;
+    const int drow = (lane >> 5), dch = lane & 31;
+    auto issue = [&](int c) {  // stage c (or zeros past the last: an empty view) into buffer c % NS
+        const bool valid = c < total;
+        const int pair = valid && c >= nch;
+        const int r0 = valid ? (c - pair * nch) * MC : 0;
+        const int ld = pair ? ld1 : ld0;
+        const int bytes = __builtin_amdgcn_readfirstlane(valid ? (pair ? bytes1 : bytes0) : 0);
+        const rsrc_t v = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(pair ? src1 : src0), 0, bytes,
+                                                           0x00020000);
+        char* dst = smem + (c % NS) * STAGE + (sx ? SIDE : 0) + wq * 8 * ROWB;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = wq * 8 + 2 * j + drow;
+            const int ch = dch ^ ((row & 3) << 2);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(v, (lds_void*)(dst + j * 1024), 16, (r0 + row) * ld * 2 + ch * 16,
+                                                     0, 0, 0);
+        }
+    };
+
+    // transposed-read addresses: lane 4q + p of its 16-lane group g supplies row (q) of the group's
+    // block, columns 4p .. 4p + 3 of its 16 (g & 1: the second 16 columns; g >> 1: rows + 8).  The
+    // reads are inline asm: the compiler would otherwise drain every LDS-DMA in flight (vmcnt(0))
+    // before each of them (it cannot tell the ring's buffers apart), so their lgkmcnt waits are
+    // explicit too.  Per lane six addresses (Y: i = 0, 1; X: j = 0..3) within a stage; rows + 4
+    // (the second half of the 8) and + 16 (ks = 1) keep row & 3, hence the swizzle: immediates.
+    const int g = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
+    auto tr_off = [&](int row, int col) {  // byte offset of (row, col) in a swizzled side image
+        return row * ROWB + (((col >> 3) ^ ((row & 3) << 2)) << 4) + (col & 7) * 2;
+    };
+    const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem);
+    uint32_t ya[2], xa[4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) ya[i] = lds0 + tr_off(8 * (g >> 1) + tq, wm * 64 + i * 32 + 16 * (g & 1) + 4 * tp);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        xa[j] = lds0 + SIDE + tr_off(8 * (g >> 1) + tq, wn * 128 + j * 32 + 16 * (g & 1) + 4 * tp);
+    floatx16 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+    const bool bias_wave = do_bias && wn == 0;  // wave-uniform
+    float bs[2] = {0.0f, 0.0f};
+    auto compute = [&](int buf, bool bias) {
+        const uint32_t sb = buf * STAGE;
+        // both k-steps' fragments requested up front: the second's reads land under the first's MFMAs
+        bf16x8 af[2][2], bf[2][4];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) af[ks][i] = tr_read8<0>(ya[i] + sb, ks);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bf[ks][j] = tr_read8<0>(xa[j] + sb, ks);
+        }
+        asm volatile("s_waitcnt lgkmcnt(12)"  // (LDS reads retire in order: the first k-step's 12)
+                     : "+v"(af[0][0]), "+v"(af[0][1]), "+v"(bf[0][0]), "+v"(bf[0][1]), "+v"(bf[0][2]), "+v"(bf[0][3]));
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][i], bf[0][j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);  // the first k-step's MFMAs issue before the second's wait
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(af[1][0]), "+v"(af[1][1]), "+v"(bf[1][0]), "+v"(bf[1][1]), "+v"(bf[1][2]), "+v"(bf[1][3]));
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][i], bf[1][j], acc[i][j], 0, 0, 0);
+        if (bias) {  // this lane's column of Y over its 16 rows of the stage, in m order
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                float sm = 0.0f;
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    const u32x4 w = __builtin_bit_cast(u32x4, af[ks][i]);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        sm += __builtin_bit_cast(float, w[e] << 16) + __builtin_bit_cast(float, w[e] & 0xffff0000u);
+                }
+                bs[i] += sm;
+            }
+        }
+    };
+
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s) issue(s);
+    for (int c = 0; c < total; ++c) {
+        wait_vmcnt<4 * (NS - 2)>();  // this wave's DMAs of stage c landed (NS - 2 later stages may fly)
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave's stage c landed; every wave is done with stage c - 1
+        asm volatile("" ::: "memory");
+        issue(c + NS - 1);  // into the buffer stage c - 1 used
+        compute(c % NS, bias_wave && c < nch);
+    }
+    wait_vmcnt<0>();
+    asm volatile("" ::: "memory");
+    __syncthreads();  // LDS is reused for the bias partials
+
+    const rsrc_t vP = make_view(p.part + (int64_t)slice * p.Npad * p.Kpad, p.Npad * p.Kpad * 4);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int col = k0 + wn * 128 + j * 32 + (lane & 31);
+            const int rbase = n0 + wm * 64 + i * 32 + 4 * (lane >> 5);
+            const int vo = (rbase * p.Kpad + col) * 4;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) bstore1(vP, vo, ((r & 3) + 8 * (r >> 2)) * p.Kpad * 4, acc[i][j][r]);
+        }
+    }
+    if (do_bias) {  // the two row halves of each column (lanes l, l + 32), fixed order
+        float* red = reinterpret_cast<float*>(smem);  // [2][BNo]
+        if (bias_wave) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) red[(lane >> 5) * BNo + wm * 64 + i * 32 + (lane & 31)] = bs[i];
+        }
+        __syncthreads();
+        if (tid < BNo) p.bpart[(int64_t)slice * p.Npad + n0 + tid] = red[tid] + red[BNo + tid];
+    }
+}
+
 // 256 x 64 weight gradient (the K = 64 first layers: the SDF's dW0 = Z_0ᵀ U0 + S_0ᵀ U̇_0 and the colour
 // network's extras columns, neus_fields.py:268-272, 364-366) on the stage ring of wgrad_x6r_kernel:
 // 16 sample rows per stage, two split-image buffers (2 x 35 KB: 256 Y rows + 64 X rows of 28 dwords),
@@ -1131,7 +1337,8 @@ extern "C" int cn_wgrad_kernel_name(const cn_wgrad_desc* d, char* buf, int32_t l
         k = tile == 2 ? "wgrad_x6r_kernel<2>" : tile == 3 ? "wgrad_x6n_kernel<3>" : tile == 0 ? "wgrad_x6_kernel<2, 2>"
                                                                                        : "wgrad_x6_kernel<2, 1>";
     else if (d->mfma_dtype == CN_MFMA_BF16)
-        k = tile == 2 ? "wgrad_b16r_kernel<2>" : tile == 0 ? "wgrad_bf16_kernel<2, 2, 2, 2>" : "wgrad_bf16_kernel<2, 2, 2, 1>";
+        k = tile == 2 ? (d->y_bf16 && d->x_bf16 ? "wgrad_b16d_kernel<4>" : "wgrad_b16r_kernel<2>")
+                      : tile == 0 ? "wgrad_bf16_kernel<2, 2, 2, 2>" : "wgrad_bf16_kernel<2, 2, 2, 1>";
     else
         k = tile == 0 ? "wgrad_kernel<2, 2, 2, 2>" : "wgrad_kernel<2, 2, 2, 1>";
     const bool ring = (d->mfma_dtype == CN_MFMA_F32_BF16X6 || d->mfma_dtype == CN_MFMA_BF16) && tile == 2;
@@ -1232,7 +1439,10 @@ extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
             b.job[0] = a;
             b.blocks[0] = grid;
             b.njobs = 1;
-            wgrad_b16r_kernel<2><<<grid, 512, 0, s>>>(b);
+            if (a.yb && a.xb)
+                wgrad_b16d_kernel<4><<<grid, 512, 0, s>>>(b);
+            else
+                wgrad_b16r_kernel<2><<<grid, 512, 0, s>>>(b);
         } else if (tile == 0)
             wgrad_bf16_kernel<2, 2, 2, 2><<<grid, 256, 0, s>>>(a);
         else
@@ -1246,19 +1456,23 @@ extern "C" int cn_wgrad(const cn_wgrad_desc* d, cn_stream_t stream) {
     return rc ? rc : launch_slab_batch(js, 2, s);
 }
 
-// Whether cn_wgrad_batch runs a descriptor inside a shared stage-ring launch (1: bf16x6, 2: bf16).
+// Whether cn_wgrad_batch runs a descriptor inside a shared stage-ring launch (1: bf16x6, 2: bf16,
+// 3: bf16 with both operands images -- wgrad_b16d_kernel).
+constexpr int kWgradKinds = 3;
 static int wgrad_batchable(const cn_wgrad_desc* d) {
     if (wgrad_wide(d) != 1) return 0;
-    return d->mfma_dtype == CN_MFMA_F32_BF16X6 ? 1 : d->mfma_dtype == CN_MFMA_BF16 ? 2 : 0;
+    if (d->mfma_dtype == CN_MFMA_F32_BF16X6) return 1;
+    if (d->mfma_dtype == CN_MFMA_BF16) return d->y_bf16 && d->x_bf16 ? 3 : 2;
+    return 0;
 }
 
-// The batch layout of cn_wgrad_batch: the stage-ring descriptors of each kind (1: bf16x6, 2: bf16,
-// at most kWgradBatchMax each) share one launch, each with a share of the device's workgroups
+// The batch layout of cn_wgrad_batch: the stage-ring descriptors of each kind (wgrad_batchable; at
+// most kWgradBatchMax each) share one launch, each with a share of the device's workgroups
 // proportional to its work (rows x pairs x output tiles), so they end together; budget[i] = -1:
 // descriptor i runs alone (cn_wgrad).  kind[i] as wgrad_batchable.
 static void wgrad_batch_layout(const cn_wgrad_desc* descs, int n, int* kind, int* budget) {
-    double total[2] = {0.0, 0.0};
-    int cnt[2] = {0, 0};
+    double total[kWgradKinds] = {};
+    int cnt[kWgradKinds] = {};
     for (int i = 0; i < n; ++i) {
         const cn_wgrad_desc* d = descs + i;
         kind[i] = wgrad_batchable(d);
@@ -1281,7 +1495,7 @@ static void wgrad_batch_layout(const cn_wgrad_desc* descs, int n, int* kind, int
     }
 }
 
-// One shared launch of a stage-ring kernel (kind 1: bf16x6, 2: bf16) over the descriptors idx[0..nb)
+// One shared launch of a stage-ring kernel (kind as wgrad_batchable) over the descriptors idx[0..nb)
 // with their budgets, then one slab reduction.
 static int wgrad_ring_batch(const cn_wgrad_desc* descs, const int* idx, const int* budgets, int nb, int kind,
                             hipStream_t s) {
@@ -1302,6 +1516,8 @@ static int wgrad_ring_batch(const cn_wgrad_desc* descs, const int* idx, const in
     if (nb == 1) b.blocks[0] = grid = cdiv(b.job[0].nslices, 8) * 8 * b.job[0].n_tiles_n * b.job[0].n_tiles_k;
     if (kind == 1)
         wgrad_x6r_kernel<2><<<grid, 512, 0, s>>>(b);
+    else if (kind == 3)
+        wgrad_b16d_kernel<4><<<grid, 512, 0, s>>>(b);
     else
         wgrad_b16r_kernel<2><<<grid, 512, 0, s>>>(b);
     int rc = check_launch("cn_wgrad_batch");
@@ -1326,7 +1542,7 @@ extern "C" int cn_wgrad_batch(const cn_wgrad_desc* descs, int32_t n, cn_stream_t
     hipStream_t s = (hipStream_t)stream;
     int kind[4 * kWgradBatchMax], budget[4 * kWgradBatchMax];
     wgrad_batch_layout(descs, n, kind, budget);
-    int idx[2][kWgradBatchMax], nb[2] = {0, 0};
+    int idx[kWgradKinds][kWgradBatchMax], nb[kWgradKinds] = {};
     for (int i = 0; i < n; ++i) {
         if (kind[i] == 0) {
             int rc = cn_wgrad(descs + i, stream);  // another tile class (or a full batch): its own launch
@@ -1335,7 +1551,7 @@ extern "C" int cn_wgrad_batch(const cn_wgrad_desc* descs, int32_t n, cn_stream_t
         }
         idx[kind[i] - 1][nb[kind[i] - 1]++] = i;
     }
-    for (int k = 1; k <= 2; ++k) {
+    for (int k = 1; k <= kWgradKinds; ++k) {
         int rc = wgrad_ring_batch(descs, idx[k - 1], budget, nb[k - 1], k, s);
         if (rc) return rc;
     }
