@@ -87,9 +87,6 @@ template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int EPI, b
 __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel(LinearArgs p) {
     constexpr int MODE = MODE_ & 3;         // the GEMM mode (0 fp32, 1 bf16, 2 bf16x6)
     constexpr bool ABF = (MODE_ & 4) != 0;  // A, A2 bf16 images
-    // MODE_ bit 3: the value-read aux operands are bf16 images -- BWD_RELU's aux0 (its sign),
-    // BWD_SOFTPLUS's aux1 / aux2 (the second-order term); a σ source (aux0 of MUL / TANGENT /
-    // BWD_SOFTPLUS) stays fp32
     // MODE_ bit 3: every aux operand of the epilogue is a bf16 image (aux0: σ's activation or
     // BWD_RELU's sign source; BWD_SOFTPLUS's aux1 / aux2 too)
     constexpr bool AUX0B = (MODE_ & 8) != 0 && (EPI == CN_EPI_BWD_RELU || EPI == CN_EPI_MUL || EPI == CN_EPI_TANGENT ||
@@ -140,10 +137,20 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     constexpr bool kColv = ROWV || kHead;
     constexpr int TBLC = kHead ? 256 : kTblCols;
     constexpr int TBL = (kBias ? TBLC : 0) + (kColv ? TBLC : 0) + (kHead ? TBLC + 4 : 0);
-    __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS + TBL];
+    // The 256x256 bf16 tile with bf16 A images stages A and B by LDS-DMA into a ring of DNS stages
+    // (no register staging: DNS - 1 = 3 stages, 96 KB, in flight per CU, across tile boundaries,
+    // under the epilogue too).  A stage is the BM A rows and BN B rows of one 32-deep chunk, 64-byte
+    // rows whose 16-byte chunks are XOR-swizzled by (row >> 2) & 3 (the DMA writes LDS linearly, the
+    // swizzle is in the per-lane global address): the ds_read_b128 lane groups of the MFMA operand
+    // reads ({0-3, 12-15, 20-27}, ...) then hit 16 distinct bank quads.  + 2 * BM floats: the
+    // SOFTPLUS_HEAD row partials (the ring is busy with the next tile's stages during the epilogue).
+    constexpr bool kDma = ABF && MODE == 1 && TM * TN >= 8 && BK == 32 && OCC == 1 && BM == 256 && BN == 256;
+    constexpr int DNS = 4, DROWB = BK * 2, DSIDEA = BM * DROWB, DSTAGE = (BM + BN) * DROWB;
+    constexpr int LDS_MAIN = kDma ? DNS * DSTAGE / 4 + 2 * BM : LDS_FLOATS;
+    __shared__ __attribute__((aligned(16))) float smem[LDS_MAIN + TBL];
     float* sA = smem;
     float* sB = smem + 2 * BM * LS;
-    float* sBias = smem + LDS_FLOATS;
+    float* sBias = smem + LDS_MAIN;
     float* sColv = sBias + (kBias ? TBLC : 0);
     float* sHeadW = sColv + (kColv ? TBLC : 0);
 
@@ -304,18 +311,86 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     }
     int tm, tn;
     coords(vt, tm, tn);
-    // the first DEPTH chunks of a tile are in the register sets when its loop starts (the next
-    // tile's are fetched during the current tile's last DEPTH chunks); see the end of the tile
-    // loop for the asm re-definition (the sets enter the loop as asm-defined values on both paths)
+
+    // ---- LDS-DMA ring (kDma): wave w < 4 fills A rows 64 w .. + 63, wave w >= 4 B rows 64 (w - 4) ..,
+    // four 1-KiB pieces of 16 rows each; lane l: row + (l >> 2), physical chunk l & 3
+    const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)smem);
+    const int dwave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool dsb = dwave >= 4;
+    const int drow = (dwave & 3) * 64 + (lane >> 2);
+    const int dch = (lane & 3) ^ ((lane >> 4) & 3);  // logical chunk of the lane's physical one
+    auto ufirst = [](const void* ptr) {
+        const uint64_t x = reinterpret_cast<uint64_t>(ptr);
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x), hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+        return reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+    };
+    // chunk kc of the tile at (m0, n0) into ring slot `slot` (valid false: zeros)
+    auto dma_issue = [&](int slot, int kc, int m0, int n0, bool valid) {
+        const int k0 = kc * BK;
+        const char* base;
+        int ld, bytes, kk;
+        if (!dsb) {
+            const bool second = k0 >= p.K1;  // wave-uniform: A2 half of a virtual concat
+            ld = second ? p.lda2 : p.lda;
+            kk = second ? k0 - p.K1 : k0;
+            base = reinterpret_cast<const char*>(second ? p.A2 : cA) + (int64_t)m0 * ld * 2;
+            bytes = valid ? min(BM, p.M - m0) * ld * 2 : 0;
+        } else {
+            ld = p.ldb;
+            kk = k0;
+            base = reinterpret_cast<const char*>(cB) + (int64_t)n0 * ld * 2;
+            bytes = valid ? BN * ld * 2 : 0;
+        }
+        const rsrc_t v = __builtin_amdgcn_make_buffer_rsrc(ufirst(base), 0, __builtin_amdgcn_readfirstlane(bytes),
+                                                           0x00020000);
+        char* dst = reinterpret_cast<char*>(smem) + slot * DSTAGE + (dsb ? DSIDEA : 0) + (dwave & 3) * 64 * DROWB;
 #pragma unroll
-    for (int d = 0; d < DEPTH; ++d) gload(d, d, tm * BM, tn * BN, true);
+        for (int j = 0; j < 4; ++j)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(v, (__attribute__((address_space(3))) void*)(dst + j * 1024), 16,
+                                                     (drow + 16 * j) * ld * 2 + (kk + dch * 8) * 2, 0, 0, 0);
+    };
+    // MFMA operand reads: lane l's row (l & 31) of each 32-row block, 16-byte chunk 2 ks + (l >> 5)
+    // at its swizzled place ((row >> 2) & 3 = ((l & 31) >> 2) & 3: the blocks start at multiples of 32)
+    const int dsw = ((lane & 31) >> 2) & 3;
+    uint32_t daoff[2], dboff[2];
 #pragma unroll
-    for (int d = 0; d < DEPTH; ++d) {
-#pragma unroll
-        for (int q = 0; q < ALD; ++q) asm volatile("" : "+v"(ra[d][q]));
-#pragma unroll
-        for (int q = 0; q < BLD; ++q) asm volatile("" : "+v"(rb[d][q]));
+    for (int ks = 0; ks < 2; ++ks) {
+        const int ch = ((2 * ks + (lane >> 5)) ^ dsw) << 4;
+        daoff[ks] = lds0 + (wm * TM * 32 + (lane & 31)) * DROWB + ch;
+        dboff[ks] = lds0 + DSIDEA + (wn * TN * 32 + (lane & 31)) * DROWB + ch;
     }
+    if constexpr (kDma) {
+        // the column tables are read into registers now (a table read beside the ring would wait
+        // for every DMA in flight); 128 < N <= 256: one N-tile, n0 = 0 on every tile
+        __syncthreads();
+#pragma unroll
+        for (int d = 0; d < DNS - 1; ++d) dma_issue(d, d, tm * BM, tn * BN, true);
+    } else {
+        // the first DEPTH chunks of a tile are in the register sets when its loop starts (the next
+        // tile's are fetched during the current tile's last DEPTH chunks); see the end of the tile
+        // loop for the asm re-definition (the sets enter the loop as asm-defined values on both paths)
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) gload(d, d, tm * BM, tn * BN, true);
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+#pragma unroll
+            for (int q = 0; q < ALD; ++q) asm volatile("" : "+v"(ra[d][q]));
+#pragma unroll
+            for (int q = 0; q < BLD; ++q) asm volatile("" : "+v"(rb[d][q]));
+        }
+    }
+    // (kDma) per-lane column-table values of the direct epilogues, n0 = 0
+    float tbias[TN], tcolv[TN], thw[TN];
+    float thb = 0.0f;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int c = min(wn * TN * 32 + (lane & 31) + 32 * j, TBLC - 1);
+        tbias[j] = kDma && kBias ? sBias[c] : 0.0f;
+        tcolv[j] = kDma && kColv ? sColv[c] : 0.0f;
+        thw[j] = kDma && kHead ? sHeadW[c] : 0.0f;
+    }
+    if (kDma && kHead) thb = sHeadW[TBLC];
+    int gs = 0;  // (kDma) ring slot of the current tile's chunk 0
 
     while (vt < ntiles) {
         const int m0 = tm * BM, n0 = tn * BN;
@@ -323,8 +398,10 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         int tm_next = 0, tn_next = 0;
         if (vt_next < ntiles) coords(vt_next, tm_next, tn_next);
 
-        lstore(0, 0);
-        __syncthreads();
+        if constexpr (!kDma) {
+            lstore(0, 0);
+            __syncthreads();
+        }
 
         floatx16 acc[TM][TN];
 #pragma unroll
@@ -444,7 +521,45 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 
         const int m_next = tm_next * BM, n_next = tn_next * BN;
         const bool has_next = vt_next < ntiles;
-        if constexpr (DEPTH == 1) {
+        if constexpr (kDma) {
+            // chunk kc is in slot (gs + kc) % DNS; the stage issued at kc (DNS - 1 ahead: this tile's
+            // chunk kc + DNS - 1 or the next tile's first ones) goes to the slot chunk kc - 1 used
+            for (int kc = 0; kc < nk; ++kc) {
+                wait_vmcnt<4 * (DNS - 2)>();  // this wave's pieces of chunk kc landed
+                asm volatile("" ::: "memory");
+                __builtin_amdgcn_s_barrier();  // every wave's pieces landed; chunk kc - 1 consumed
+                asm volatile("" ::: "memory");
+                const int cn = kc + DNS - 1;
+                const bool here = cn < nk;
+                dma_issue((gs + cn) % DNS, here ? cn : cn - nk, here ? m0 : m_next, here ? n0 : n_next, here || has_next);
+                const uint32_t sb = ((gs + kc) % DNS) * DSTAGE;
+                bf16x8 af[2][TM], bfr[2][TN];
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) af[ks][i] = __builtin_bit_cast(bf16x8, lds_read_b128<0>(daoff[ks] + sb + i * 32 * DROWB));
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) bfr[ks][j] = __builtin_bit_cast(bf16x8, lds_read_b128<0>(dboff[ks] + sb + j * 32 * DROWB));
+                }
+                static_assert(TM == 2 && TN == 4, "the lgkmcnt split below counts 6 reads per k-step");
+                asm volatile("s_waitcnt lgkmcnt(6)"
+                             : "+v"(af[0][0]), "+v"(af[0][1]), "+v"(bfr[0][0]), "+v"(bfr[0][1]), "+v"(bfr[0][2]), "+v"(bfr[0][3]));
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][i], bfr[0][j], acc[i][j], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_waitcnt lgkmcnt(0)"
+                             : "+v"(af[1][0]), "+v"(af[1][1]), "+v"(bfr[1][0]), "+v"(bfr[1][1]), "+v"(bfr[1][2]), "+v"(bfr[1][3]));
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][i], bfr[1][j], acc[i][j], 0, 0, 0);
+            }
+            gs = (gs + nk) % DNS;
+        } else if constexpr (DEPTH == 1) {
             for (int kc = 0; kc < nk; ++kc) {
                 const int cur = kc & 1;
                 // chunk kc+1 of this tile, or the next tile's first chunk (consumed after the epilogue)
@@ -494,12 +609,14 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         // set's, so the compiler drains them first).  Re-defining the register sets through
         // an empty asm tells it so: the next tile's staging of its prefetched first chunk then
         // waits for nothing, instead of for the epilogue's stores (one vmcnt, in issue order).
+        if constexpr (!kDma) {
 #pragma unroll
-        for (int d = 0; d < DEPTH; ++d) {
+            for (int d = 0; d < DEPTH; ++d) {
 #pragma unroll
-            for (int q = 0; q < ALD; ++q) asm volatile("" : "+v"(ra[d][q]));
+                for (int q = 0; q < ALD; ++q) asm volatile("" : "+v"(ra[d][q]));
 #pragma unroll
-            for (int q = 0; q < BLD; ++q) asm volatile("" : "+v"(rb[d][q]));
+                for (int q = 0; q < BLD; ++q) asm volatile("" : "+v"(rb[d][q]));
+            }
         }
         // Epilogue: park the accumulator tile (or a slab of PROWS rows of it) in the
         // now free staging LDS, then process it row-wise with 16-byte coalesced
@@ -771,13 +888,16 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             // EPI_MUL with a split output (the skip layer's ∇ pass: columns [nsplit, N) are the
             // embedding's adjoint, written raw (A·Bᵀ)/adiv to out_split while out0 is zero-filled
             // there; p.nsplit = N without a split)
+            const bool has_split = EPI == CN_EPI_MUL && p.nsplit < cN;  // wave-uniform
             bool spl[TN];
             int vsj[TN];
+            unsigned keep[TN];  // all ones where out0 takes the epilogue's value (else its zero fill)
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 const int c = n0 + lcol + 32 * j;
                 spl[j] = EPI == CN_EPI_MUL && c >= p.nsplit && c < cN;
                 vsj[j] = (lrow * p.ld_split + lcol + 32 * j) * 4;
+                keep[j] = live[j] && !spl[j] ? ~0u : 0u;
             }
             constexpr int RG = kAux1 ? 2 : 4;          // accumulator rows r per group (even: bf16 pairs)
             constexpr int NGD = TM * 16 / RG;          // groups per tile
@@ -805,6 +925,9 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             for (int g = 0; g < NGD; ++g) {
                 const int sl = g & 1;
                 if (g + 1 < NGD) dload(g + 1, sl ^ 1);
+                // the next group's loads stay ahead of this group's math (scheduled into it, a load
+                // could be followed by its own use and a vmcnt(0): the next tile's staging drained)
+                __builtin_amdgcn_sched_barrier(0);
                 const int i = g / (16 / RG), r0 = (g % (16 / RG)) * RG;
                 float prev[TN];  // row r - 1's stored values (bf16 pairs)
 #pragma unroll
@@ -816,14 +939,11 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 #pragma unroll
                     for (int j = 0; j < TN; ++j) {
                         const float u = acc[i][j][r] * p.inv_adiv;
-                        if constexpr (EPI == CN_EPI_MUL) {
-                            if (spl[j]) {
-                                bstore1(view_at(tS, rowi), vsj[j], 0, u);
-                                bstore1(vw, voj[j], 0, 0.0f);
-                                ov[j] = 0.0f;
-                                continue;
-                            }
-                        }
+                        // the split columns' raw values (a wave-uniform branch; the other lanes' stores
+                        // fall past the view), out0 zero-filled there below.  No per-lane branch: the
+                        // compiler would sink the aux load into it and drain vmcnt(0) there, the next
+                        // tile's staging loads included
+                        if (EPI == CN_EPI_MUL && has_split) bstore1(view_at(tS, rowi), spl[j] ? vsj[j] : (1 << 30), 0, u);
                         const float sg = EPI == CN_EPI_BWD_RELU ? 0.0f : sigma_from_act(xa[sl][q][j], p.aux_c);
                         float o;
                         if constexpr (EPI == CN_EPI_BWD_RELU) {
@@ -836,7 +956,8 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                             const float rr2 = sg > 0.0f ? (1.0f - sg) * __builtin_amdgcn_rcpf(sg) : 0.0f;
                             o = u * sg + xb[sl][q][j] * xc[sl][q][j] * (p.aux2_scale * rr2);
                         }
-                        ov[j] = live[j] ? o : 0.0f;
+                        // (a bit mask, not a select: the compiler made the select a branch per element)
+                        ov[j] = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, o) & keep[j]);
                         bstore1(vw, voj[j], 0, ov[j]);
                     }
                     if (has_b0) {
@@ -861,7 +982,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             if (has_b0) bimg_cols(p.ld_out0_b, lrow, lcol, vbj);
             float bj[TN];
 #pragma unroll
-            for (int j = 0; j < TN; ++j) bj[j] = kBias ? sBias[min(n0 + lcol + 32 * j, kTblCols - 1)] : 0.0f;
+            for (int j = 0; j < TN; ++j) bj[j] = kDma ? tbias[j] : kBias ? sBias[min(n0 + lcol + 32 * j, kTblCols - 1)] : 0.0f;
             float prev[TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
@@ -903,12 +1024,13 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 const int c = min(n0 + lcol + 32 * j, TBLC - 1);
-                bj[j] = sBias[c];
-                cj[j] = sColv[c];
-                hj[j] = sHeadW[c];  // zero past N (the table's view ends at N)
+                bj[j] = kDma ? tbias[j] : sBias[c];
+                cj[j] = kDma ? tcolv[j] : sColv[c];
+                hj[j] = kDma ? thw[j] : sHeadW[c];  // zero past N (the table's view ends at N)
                 vo1[j] = voj[j] == (1 << 30) ? voj[j] : (lrow * p.ld_out1 + lcol + 32 * j) * 4;
             }
-            float* sRed = sA + BM * LS;  // staging buffer 1 is free after the main loop (its last reader)
+            // staging buffer 1 is free after the main loop (its last reader); the DMA ring is not
+            float* sRed = kDma ? smem + DNS * DSTAGE / 4 : sA + BM * LS;
             float prev0[TN], prev1[TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
@@ -955,7 +1077,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 if (row < p.M) {
                     const float sum = sRed[tid * 2] + sRed[tid * 2 + 1];
                     const int dst = p.head_idx ? p.head_idx[row] : row;
-                    p.head_out[dst] = sum + sHeadW[TBLC];
+                    p.head_out[dst] = sum + (kDma ? thb : sHeadW[TBLC]);
                 }
             }
         };
@@ -978,6 +1100,8 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         tm = tm_next;
         tn = tn_next;
     }
+    // (kDma) the last stages (zeros) land in LDS before the workgroup ends
+    if constexpr (kDma) wait_vmcnt<0>();
 }
 
 
@@ -1415,7 +1539,8 @@ static LinearTile choose_linear_tile(const cn_linear_desc* d) {
     const bool wide_n = d->tile == 0 && d->N > 128 && d->N <= 256 && !d->rowv;
     const bool longk = d->K >= 128;  // a first layer's two-chunk main loop cannot hide a 1 / CU epilogue
     if (d->mfma_dtype == CN_MFMA_BF16) {
-        if (wide_n && (longk || head)) return LT_BF_SQ;
+        // (its LDS-DMA ring prefetches 3 chunks of 32: K >= 96)
+        if (wide_n && d->K >= 96 && (longk || head)) return LT_BF_SQ;
         return d->tile == 1 ? LT_BF_T1 : LT_BF_T0;
     }
     if (d->mfma_dtype == CN_MFMA_F32_BF16X6) {

@@ -120,10 +120,6 @@ __device__ __forceinline__ floatx2 widen_bf16x2(unsigned p) {
     return floatx2{__builtin_bit_cast(float, p << 16), __builtin_bit_cast(float, p & 0xffff0000u)};
 }
 __device__ __forceinline__ void split3(floatx4 v, bf16x4& t0, bf16x4& t1, bf16x4& t2) {
-#ifdef CN_EXP_SPLIT1  // TEMPORARY measurement build: one rounding, the three terms equal (wrong numerics)
-    t0 = t1 = t2 = __builtin_convertvector(v, bf16x4);
-    return;
-#endif
     unsigned p0[2], p1[2], p2[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -137,6 +133,24 @@ __device__ __forceinline__ void split3(floatx4 v, bf16x4& t0, bf16x4& t1, bf16x4
     t0 = __builtin_bit_cast(bf16x4, (u32x2){p0[0], p0[1]});
     t1 = __builtin_bit_cast(bf16x4, (u32x2){p1[0], p1[1]});
     t2 = __builtin_bit_cast(bf16x4, (u32x2){p2[0], p2[1]});
+}
+
+// s_waitcnt that waits for this wave's vector-memory count to drop to N (expcnt, lgkmcnt untouched).
+// The LDS-DMA rings wait with it: the compiler would otherwise drain every DMA in flight.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+// 16-byte LDS read as inline asm (the caller waits lgkmcnt): beside an LDS-DMA ring a compiled
+// LDS read would make the compiler drain every DMA in flight first (vmcnt(0)), since it cannot
+// tell the ring's buffers apart.
+template <int OFF>
+__device__ __forceinline__ u32x4 lds_read_b128(uint32_t addr) {
+    u32x4 r;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF) : "memory");
+    return r;
 }
 
 // Virtual tile vt -> (tm, tn).  XCD-aware: blocks b and b+8 are dispatched to

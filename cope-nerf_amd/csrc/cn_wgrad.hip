@@ -837,13 +837,6 @@ __global__ void __launch_bounds__(512, 2) wgrad_b16r_kernel(WgradBatch batch) {
     }
 }
 
-// s_waitcnt that waits for this wave's vector-memory count to drop to N (expcnt, lgkmcnt untouched)
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
-    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
-}
-
 typedef __attribute__((address_space(3))) void lds_void;
 typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
 
