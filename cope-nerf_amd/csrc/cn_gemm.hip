@@ -390,7 +390,9 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         thw[j] = kDma && kHead ? sHeadW[c] : 0.0f;
     }
     if (kDma && kHead) thb = sHeadW[TBLC];
-    int gs = 0;  // (kDma) ring slot of the current tile's chunk 0
+    const bool epi_big = !kHead || p.out0 || p.out1 || p.out0_b || p.out1_b;  // (kDma) see the main loop
+    int gs = 0;             // (kDma) ring slot of the current tile's chunk 0
+    bool gs_first = true;   // (kDma) the workgroup's first tile: no epilogue issued before its chunks
 
     while (vt < ntiles) {
         const int m0 = tm * BM, n0 = tn * BN;
@@ -525,7 +527,16 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             // chunk kc is in slot (gs + kc) % DNS; the stage issued at kc (DNS - 1 ahead: this tile's
             // chunk kc + DNS - 1 or the next tile's first ones) goes to the slot chunk kc - 1 used
             for (int kc = 0; kc < nk; ++kc) {
-                wait_vmcnt<4 * (DNS - 2)>();  // this wave's pieces of chunk kc landed
+                // this wave's pieces of chunk kc landed.  vmcnt retires in issue order, so the wait
+                // counts what was issued after them: DNS - 2 later chunks (4 pieces each), and for
+                // the first DNS - 1 chunks of a tile after the first, the previous tile's epilogue
+                // too (>= 64 loads / stores per thread -- epi_big: the aux epilogues read 128 values,
+                // the others store 128 fp32 values or 64 image dwords, SOFTPLUS_HEAD may store
+                // neither): vmcnt(63) then, so the epilogue's stores are not drained first
+                if (gs_first || !epi_big || kc >= DNS - 1)
+                    wait_vmcnt<4 * (DNS - 2)>();
+                else
+                    wait_vmcnt<63>();
                 asm volatile("" ::: "memory");
                 __builtin_amdgcn_s_barrier();  // every wave's pieces landed; chunk kc - 1 consumed
                 asm volatile("" ::: "memory");
@@ -559,6 +570,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][i], bfr[1][j], acc[i][j], 0, 0, 0);
             }
             gs = (gs + nk) % DNS;
+            gs_first = false;
         } else if constexpr (DEPTH == 1) {
             for (int kc = 0; kc < nk; ++kc) {
                 const int cur = kc & 1;
@@ -635,6 +647,9 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         const TileView tO1b = tile_view_b16(p.out1_b, p.ld_out1_b, m0, n0, rows);
         const bool has_b0 = MODE == 1 && p.out0_b != nullptr;  // wave-uniform
         const bool has_b1 = MODE == 1 && p.out1_b != nullptr;
+        // the direct epilogues skip the fp32 stores of an absent out0 / out1 (a wave-uniform branch:
+        // image-only outputs would otherwise issue two dropped stores per stored image dword)
+        const bool has_o0 = cOut0 != nullptr, has_o1 = p.out1 != nullptr;
         const TileView tX1 = AUX12B ? tile_view_b16(p.aux1, p.ld_aux1, m0, n0, rows)
                                     : TileView{p.aux1 + (int64_t)m0 * p.ld_aux1 + n0, p.ld_aux1,
                                                p.aux1 ? (rows * p.ld_aux1 - n0) * 4 : 0};
@@ -874,7 +889,13 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             const float recv = lane_xor1(odd ? o_r : o_r1);
             bstore_b16x2(view_at(t, rowi), vb, 0, odd ? recv : o_r, odd ? o_r1 : recv);
         };
-        auto direct_aux = [&]() {
+        // The direct epilogues take the wave-uniform choices (fp32 out0 stored, bf16 image of it, MUL's
+        // split output) as template flags: as branches inside the element loops they left the
+        // compiler's vmcnt bookkeeping unsure at every merge point, and it drained vmcnt(0) there --
+        // the next tile's staging loads included.
+        auto direct_aux = [&](auto o0_tag, auto b0_tag, auto spl_tag) {
+            constexpr bool O0 = decltype(o0_tag)::value, B0 = decltype(b0_tag)::value;
+            constexpr bool SPL = decltype(spl_tag)::value;
             const int lrow = wm * TM * 32 + 4 * (lane >> 5);
             const int lcol = wn * TN * 32 + (lane & 31);
             const int vo = (lrow * p.ld_out0 + lcol) * 4;
@@ -884,11 +905,10 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             int voj[TN], vbj[TN];
             bool live[TN];
             direct_cols(vo, lcol, voj, live);
-            if (has_b0) bimg_cols(p.ld_out0_b, lrow, lcol, vbj);
+            if (B0) bimg_cols(p.ld_out0_b, lrow, lcol, vbj);
             // EPI_MUL with a split output (the skip layer's ∇ pass: columns [nsplit, N) are the
             // embedding's adjoint, written raw (A·Bᵀ)/adiv to out_split while out0 is zero-filled
             // there; p.nsplit = N without a split)
-            const bool has_split = EPI == CN_EPI_MUL && p.nsplit < cN;  // wave-uniform
             bool spl[TN];
             int vsj[TN];
             unsigned keep[TN];  // all ones where out0 takes the epilogue's value (else its zero fill)
@@ -903,7 +923,11 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             constexpr int NGD = TM * 16 / RG;          // groups per tile
             constexpr int ASTEP = AUX0B ? 64 : 128;    // bytes per 32-column block of aux0
             constexpr int XSTEP = AUX12B ? 64 : 128;   // ... of aux1 / aux2
-            float xa[2][RG][TN], xb[2][RG][TN], xc[2][RG][TN];
+            // raw loaded bits (a bf16 image value is widened where it is used: a widening inside the
+            // prefetch would be a use, and the scheduling barrier below would wait for every load)
+            unsigned xa[2][RG][TN], xb[2][RG][TN], xc[2][RG][TN];
+            auto w0 = [&](unsigned r) { return __builtin_bit_cast(float, AUX0B ? r << 16 : r); };
+            auto w12 = [&](unsigned r) { return __builtin_bit_cast(float, AUX12B ? r << 16 : r); };
             auto dload = [&](int g, int sl) {
                 const int i = g / (16 / RG), r0 = (g % (16 / RG)) * RG;
 #pragma unroll
@@ -911,12 +935,12 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                     const int r = r0 + q, row = i * 32 + (r & 3) + 8 * (r >> 2);
 #pragma unroll
                     for (int j = 0; j < TN; ++j) {
-                        xa[sl][q][j] = AUX0B ? bload_b16(view_at(tX0, row), v0, ASTEP * j)
-                                            : bload1(view_at(tX0, row), v0, ASTEP * j);
-                        if (kAux1) xb[sl][q][j] = AUX12B ? bload_b16(view_at(tX1, row), v1, XSTEP * j)
-                                                         : bload1(view_at(tX1, row), v1, XSTEP * j);
-                        if (kAux1) xc[sl][q][j] = AUX12B ? bload_b16(view_at(tX2, row), v2, XSTEP * j)
-                                                         : bload1(view_at(tX2, row), v2, XSTEP * j);
+                        xa[sl][q][j] = AUX0B ? bload_u16(view_at(tX0, row), v0, ASTEP * j)
+                                            : __builtin_bit_cast(unsigned, bload1(view_at(tX0, row), v0, ASTEP * j));
+                        if (kAux1) xb[sl][q][j] = AUX12B ? bload_u16(view_at(tX1, row), v1, XSTEP * j)
+                                                         : __builtin_bit_cast(unsigned, bload1(view_at(tX1, row), v1, XSTEP * j));
+                        if (kAux1) xc[sl][q][j] = AUX12B ? bload_u16(view_at(tX2, row), v2, XSTEP * j)
+                                                         : __builtin_bit_cast(unsigned, bload1(view_at(tX2, row), v2, XSTEP * j));
                     }
                 }
             };
@@ -943,24 +967,24 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         // fall past the view), out0 zero-filled there below.  No per-lane branch: the
                         // compiler would sink the aux load into it and drain vmcnt(0) there, the next
                         // tile's staging loads included
-                        if (EPI == CN_EPI_MUL && has_split) bstore1(view_at(tS, rowi), spl[j] ? vsj[j] : (1 << 30), 0, u);
-                        const float sg = EPI == CN_EPI_BWD_RELU ? 0.0f : sigma_from_act(xa[sl][q][j], p.aux_c);
+                        if constexpr (EPI == CN_EPI_MUL && SPL) bstore1(view_at(tS, rowi), spl[j] ? vsj[j] : (1 << 30), 0, u);
+                        const float sg = EPI == CN_EPI_BWD_RELU ? 0.0f : sigma_from_act(w0(xa[sl][q][j]), p.aux_c);
                         float o;
                         if constexpr (EPI == CN_EPI_BWD_RELU) {
-                            o = xa[sl][q][j] > 0.0f ? u : 0.0f;
+                            o = w0(xa[sl][q][j]) > 0.0f ? u : 0.0f;
                         } else if constexpr (EPI == CN_EPI_MUL) {
                             o = u * sg;
                         } else if constexpr (EPI == CN_EPI_TANGENT) {
                             o = u * sg * cInvOdiv;
                         } else {  // BWD_SOFTPLUS, as main_vals
                             const float rr2 = sg > 0.0f ? (1.0f - sg) * __builtin_amdgcn_rcpf(sg) : 0.0f;
-                            o = u * sg + xb[sl][q][j] * xc[sl][q][j] * (p.aux2_scale * rr2);
+                            o = u * sg + w12(xb[sl][q][j]) * w12(xc[sl][q][j]) * (p.aux2_scale * rr2);
                         }
                         // (a bit mask, not a select: the compiler made the select a branch per element)
                         ov[j] = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, o) & keep[j]);
-                        bstore1(vw, voj[j], 0, ov[j]);
+                        if constexpr (O0) bstore1(vw, voj[j], 0, ov[j]);
                     }
-                    if (has_b0) {
+                    if constexpr (B0) {
                         if (r & 1) {
 #pragma unroll
                             for (int j = 0; j < TN; ++j) bimg_pair(tO0b, rowi - 1, vbj[j], prev[j], ov[j]);
@@ -972,14 +996,15 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 }
             }
         };
-        auto direct_plain = [&]() {
+        auto direct_plain = [&](auto o0_tag, auto b0_tag) {
+            constexpr bool O0 = decltype(o0_tag)::value, B0 = decltype(b0_tag)::value;
             const int lrow = wm * TM * 32 + 4 * (lane >> 5);
             const int lcol = wn * TN * 32 + (lane & 31);
             const int vo = (lrow * p.ld_out0 + lcol) * 4;
             int voj[TN], vbj[TN];
             bool live[TN];
             direct_cols(vo, lcol, voj, live);
-            if (has_b0) bimg_cols(p.ld_out0_b, lrow, lcol, vbj);
+            if (B0) bimg_cols(p.ld_out0_b, lrow, lcol, vbj);
             float bj[TN];
 #pragma unroll
             for (int j = 0; j < TN; ++j) bj[j] = kDma ? tbias[j] : kBias ? sBias[min(n0 + lcol + 32 * j, kTblCols - 1)] : 0.0f;
@@ -999,9 +1024,9 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         else if constexpr (EPI == CN_EPI_RELU) o = z > 0.0f ? z : 0.0f;
                         else o = z;
                         ov[j] = live[j] ? o : 0.0f;
-                        bstore1(vw, voj[j], 0, ov[j]);
+                        if constexpr (O0) bstore1(vw, voj[j], 0, ov[j]);
                     }
-                    if (has_b0) {
+                    if constexpr (B0) {
                         if (r & 1) {
 #pragma unroll
                             for (int j = 0; j < TN; ++j) bimg_pair(tO0b, rowi - 1, vbj[j], prev[j], ov[j]);
@@ -1047,8 +1072,8 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         const float o = live[j] ? a : 0.0f;
                         ov0[j] = o;
                         ov1[j] = live[j] ? cj[j] * sigma_from_act(a, p.aux_c) : 0.0f;
-                        bstore1(vw, voj[j], 0, o);  // (out0 NULL: empty view)
-                        bstore1(vw1, vo1[j], 0, ov1[j]);
+                        if (has_o0) bstore1(vw, voj[j], 0, o);
+                        if (has_o1) bstore1(vw1, vo1[j], 0, ov1[j]);
                         part += o * hj[j];
                     }
                     if (has_b0 || has_b1) {
@@ -1081,15 +1106,38 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 }
             }
         };
+        using T1 = std::true_type;
+        using F0 = std::false_type;
+        auto run_direct_plain = [&]() {
+            if (has_o0) {
+                if (has_b0) direct_plain(T1{}, T1{}); else direct_plain(T1{}, F0{});
+            } else {
+                if (has_b0) direct_plain(F0{}, T1{}); else direct_plain(F0{}, F0{});  // (out0_b required then)
+            }
+        };
+        auto run_direct_aux = [&]() {
+            auto go = [&](auto spl) {
+                if (has_o0) {
+                    if (has_b0) direct_aux(T1{}, T1{}, spl); else direct_aux(T1{}, F0{}, spl);
+                } else {
+                    if (has_b0) direct_aux(F0{}, T1{}, spl); else direct_aux(F0{}, F0{}, spl);
+                }
+            };
+            if constexpr (EPI == CN_EPI_MUL) {
+                if (p.nsplit < cN) go(T1{}); else go(F0{});
+            } else {
+                go(F0{});
+            }
+        };
         if constexpr (kDirectOnly) {
             if constexpr (kDirectHead) direct_head();
-            else if constexpr (kDirectAux) direct_aux();
-            else direct_plain();
+            else if constexpr (kDirectAux) run_direct_aux();
+            else run_direct_plain();
         } else {
             if (kDirectAux && tile_main) {
-                direct_aux();
+                run_direct_aux();
             } else if (kDirect && tile_main) {
-                direct_plain();
+                run_direct_plain();
             } else {
                 if (tile_main) passes(std::true_type{});
                 else passes(std::false_type{});

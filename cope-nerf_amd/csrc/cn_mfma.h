@@ -66,6 +66,10 @@ __device__ __forceinline__ float bload_b16(rsrc_t r, int voff, int soff) {
     const unsigned short h = __builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, 0);
     return __builtin_bit_cast(float, (unsigned)h << 16);
 }
+// one bf16 as its raw bits (zero-extended)
+__device__ __forceinline__ unsigned bload_u16(rsrc_t r, int voff, int soff) {
+    return __builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, 0);
+}
 // four bf16 (8 bytes) as fp32 values
 __device__ __forceinline__ floatx4 bload_b16x4(rsrc_t r, int voff, int soff) {
     const u32x2_t w = __builtin_bit_cast(u32x2_t, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));

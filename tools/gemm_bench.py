@@ -60,6 +60,18 @@ def main():
                           ("softplus", ops.EPI_SOFTPLUS, dict(bias=bias)),
                           ("tangent", ops.EPI_TANGENT, sg)):
         bench(res, "cn_linear bf16 " + name, lambda: ops.linear(A, Bb, N, K, o0, epi, **kw))
+    # bf16 mode with operand images (config C3): A, aux and the output as bf16 images
+    Ai, ob = A.bfloat16(), torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    sgi = dict(aux0=aux0.bfloat16(), aux_beta=100.0)
+    soi = dict(sgi, aux1=aux1.bfloat16(), aux2=aux2.bfloat16(), aux2_scale=100.0)
+    for name, epi, kw in (("store", ops.EPI_STORE, dict(bias=bias)),
+                          ("softplus", ops.EPI_SOFTPLUS, dict(bias=bias)),
+                          ("relu", ops.EPI_RELU, dict(bias=bias)),
+                          ("mul", ops.EPI_MUL, sgi),
+                          ("tangent", ops.EPI_TANGENT, sgi),
+                          ("bwd_softplus", ops.EPI_BWD_SOFTPLUS, soi),
+                          ("bwd_relu", ops.EPI_BWD_RELU, dict(aux0=aux1.bfloat16()))):
+        bench(res, "cn_linear img " + name, lambda: ops.linear(Ai, Bb, N, K, None, epi, out0_b=ob, **kw))
     Bs = ops.split_bf16x3(B)
     for name, epi, kw in (("store", ops.EPI_STORE, dict(bias=bias)),
                           ("softplus", ops.EPI_SOFTPLUS, dict(bias=bias)),
@@ -77,8 +89,13 @@ def main():
     bench(res, "cn_wgrad x6 2 pairs", lambda: ops.wgrad(A, A, N, K, dW, db=db, Y1=aux1, X1=aux0, mode="bf16x6"), 2)
     bench(res, "cn_wgrad bf16 2 pairs", lambda: ops.wgrad(A, A, N, K, dW, db=db, Y1=aux1, X1=aux0, mode="bf16"), 2)
     bench(res, "torch A^T A", lambda: torch.matmul(A.t(), A, out=dW))
+    naux = {"store": 0, "softplus": 0, "relu": 0, "mul": 1, "tangent": 1, "bwd_softplus": 3, "bwd_relu": 1}
     for k, ms in res.items():
-        print(f"{k:32s} {ms*1e3:9.1f} us  {fl / ms / 1e9:8.1f} TFLOP/s")
+        extra = ""
+        if k.startswith("cn_linear img "):  # A + aux streams + the output, 2 bytes each
+            nb = 2.0 * M * N * (2 + naux[k.split()[-1]])
+            extra = f"  {nb / ms / 1e9:7.0f} GB/s"
+        print(f"{k:32s} {ms*1e3:9.1f} us  {fl / ms / 1e9:8.1f} TFLOP/s{extra}")
 
 
 if __name__ == "__main__":
