@@ -94,7 +94,7 @@ def main():
         extra = ""
         if k.startswith("cn_linear img "):  # A + aux streams + the output, 2 bytes each
             nb = 2.0 * M * N * (2 + naux[k.split()[-1]])
-            extra = f"  {nb / ms / 1e9:7.0f} GB/s"
+            extra = f"  {nb / ms / 1e6:7.0f} GB/s"  # (ms in milliseconds)
         print(f"{k:32s} {ms*1e3:9.1f} us  {fl / ms / 1e9:8.1f} TFLOP/s{extra}")
 
 
