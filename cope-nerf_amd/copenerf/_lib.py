@@ -106,8 +106,8 @@ SIGNATURES = {
     "cn_color_extras": (c_i32, [c_i32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_i32, c_i32, c_i32, c_ptr,
                                 c_i64, c_ptr]),
     "cn_rgb_head_bwd_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32]),
-    "cn_rgb_head_bwd": (c_i32, [c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_ptr,
-                                c_ptr, c_i64, c_ptr]),
+    "cn_rgb_head_bwd": (c_i32, [c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_i32, c_ptr,
+                                c_ptr, c_ptr, c_i64, c_ptr]),
     "cn_colsum_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32]),
     "cn_colsum": (c_i32, [c_i32, c_i32, c_ptr, c_ptr, c_i64, c_f32, c_ptr, c_i32, c_ptr, c_i64, c_ptr]),
     "cn_patch_indices": (c_i32, [c_i32, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_ptr]),

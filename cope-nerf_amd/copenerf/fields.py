@@ -799,7 +799,9 @@ class _ColorFieldFn(torch.autograd.Function):
         dWs, dbs = [None] * n, [None] * n
         dWs[n - 1] = torch.empty(3, lay.in_dim[n - 1], device=dev)
         dbs[n - 1] = torch.empty(3, device=dev)
-        dZ = _empty(M, lay.HL, dev)
+        # bf16 mode: the last hidden layer's adjoint as an operand image (read by the next adjoint GEMM
+        # and a weight gradient only)
+        dZ = _empty_b(M, lay.HL, dev) if (_img_mode(pk) and n - 2 >= 1) else _empty(M, lay.HL, dev)
         ops.rgb_head_bwd(drgb, rgb, H[-1], lay.in_dim[n - 1], pk.W3, dZ, dWs[n - 1], dbs[n - 1])
         wq = ops.WgradQueue()  # the 256x256 weight gradients: one launch after the chain
         for l in range(n - 2, 0, -1):

@@ -553,7 +553,7 @@ def rgb_head_bwd(drgb, rgb, H3, K, W3, dZ2, dW3, db3):
     lib = _lib.load()
     ws = torch.empty(lib.cn_rgb_head_bwd_workspace_bytes(M, K) // 4 + 1, device=rgb.device, dtype=torch.float32)
     _lib.call("cn_rgb_head_bwd", M, K, _ptr(drgb), _ptr(rgb), _ptr(H3), _ld(H3), _ptr(W3), _ptr(dZ2), _ld(dZ2),
-              _ptr(dW3), _ptr(db3), _ptr(ws), ws.numel() * 4, _stream())
+              1 if dZ2.dtype == torch.bfloat16 else 0, _ptr(dW3), _ptr(db3), _ptr(ws), ws.numel() * 4, _stream())
 
 
 def patch_indices(h, w, ps, n_patches, key, out=None):

@@ -1363,8 +1363,8 @@ constexpr int kHeadRowsPerBlock = 256;
 __global__ void __launch_bounds__(256) rgb_head_bwd_kernel(int M, int K, const float* __restrict__ drgb,
                                                            const float* __restrict__ rgb,
                                                            const float* __restrict__ H3, int64_t ld_h,
-                                                           const float* __restrict__ W3, float* dZ2, int64_t ld_dz,
-                                                           float* part /*[nblk][4][K]*/) {
+                                                           const float* __restrict__ W3, void* dZ2, int64_t ld_dz,
+                                                           bool dz_bf16, float* part /*[nblk][4][K]*/) {
     __shared__ float sd[kHeadRowsPerBlock][3];
     __shared__ floatx4 red[4][64][3];
     __shared__ float redb[4][3];
@@ -1398,7 +1398,10 @@ __global__ void __launch_bounds__(256) rgb_head_bwd_kernel(int M, int K, const f
                 const float dh = d0 * w0[e] + d1 * w1[e] + d2 * w2[e];
                 dz[e] = h[e] > 0.0f ? dh : 0.0f;
             }
-            *reinterpret_cast<floatx4*>(dZ2 + (int64_t)m * ld_dz + k) = dz;
+            if (dz_bf16)  // (bf16 mode: dZ2's image, the operand of the next adjoint GEMM and a weight gradient)
+                *reinterpret_cast<bf16x4*>(static_cast<bf16_t*>(dZ2) + (int64_t)m * ld_dz + k) = __builtin_convertvector(dz, bf16x4);
+            else
+                *reinterpret_cast<floatx4*>(static_cast<float*>(dZ2) + (int64_t)m * ld_dz + k) = dz;
             a0 = a0 + d0 * h;
             a1 = a1 + d1 * h;
             a2 = a2 + d2 * h;
@@ -1594,7 +1597,11 @@ static LinearTile choose_linear_tile(const cn_linear_desc* d) {
     if (d->mfma_dtype == CN_MFMA_F32_BF16X6) {
         if (d->tile == 1) return LT_X6_T1;
         if (d->tile == 2) return LT_X6_T128;
+#ifndef CN_EXP_X6SQ_BWD
         if (wide_n && d->K % 32 == 0 && d->ldb >= 256 && e != CN_EPI_BWD_SOFTPLUS && (longk || head)) return LT_X6_SQ;
+#else  // TEMPORARY measurement build: BWD_SOFTPLUS on the 256x256 tile too
+        if (wide_n && d->K % 32 == 0 && d->ldb >= 256 && (longk || head)) return LT_X6_SQ;
+#endif
         const bool tall = e == CN_EPI_MUL || e == CN_EPI_TANGENT || head;
         if (d->K % 64 == 0 && tall && d->N > 128 && d->ldb >= 256 && (longk || head)) return LT_X6_TALL;
         // (an aux-reading epilogue with one workgroup per CU no longer overlaps a partner's main loop)
@@ -1843,16 +1850,16 @@ extern "C" size_t cn_rgb_head_bwd_workspace_bytes(int32_t M, int32_t K) {
 }
 
 extern "C" int cn_rgb_head_bwd(int32_t M, int32_t K, const float* drgb, const float* rgb, const float* H3,
-                               int64_t ld_h, const float* W3, float* dZ2, int64_t ld_dz, float* dW3, float* db3,
-                               float* workspace, int64_t workspace_bytes, cn_stream_t stream) {
+                               int64_t ld_h, const float* W3, void* dZ2, int64_t ld_dz, int32_t dz_bf16, float* dW3,
+                               float* db3, float* workspace, int64_t workspace_bytes, cn_stream_t stream) {
     CN_REQUIRE(drgb && rgb && H3 && W3 && dZ2 && dW3 && db3 && workspace, CN_ERR_ARG, "cn_rgb_head_bwd: null pointer");
     CN_REQUIRE(K > 0 && K <= 256, CN_ERR_UNSUPPORTED, "cn_rgb_head_bwd: K=%d", K);
-    CN_REQUIRE(K % 4 == 0 && ld_h % 4 == 0 && ld_dz % 4 == 0 && al16(H3) && al16(dZ2) && al16(W3), CN_ERR_ALIGN,
+    CN_REQUIRE(K % 4 == 0 && ld_h % 4 == 0 && ld_dz % 4 == 0 && al16(H3) && (dz_bf16 ? al8(dZ2) : al16(dZ2)) && al16(W3), CN_ERR_ALIGN,
                "cn_rgb_head_bwd: K, leading dimensions and H3 / dZ2 / W3 must be multiples of 4 floats");
     CN_REQUIRE((size_t)workspace_bytes >= cn_rgb_head_bwd_workspace_bytes(M, K), CN_ERR_SHAPE, "cn_rgb_head_bwd: workspace");
     const int nblk = std::max(1, cdiv(M, kHeadRowsPerBlock));
     hipStream_t s = (hipStream_t)stream;
-    rgb_head_bwd_kernel<<<nblk, 256, 0, s>>>(M, K, drgb, rgb, H3, ld_h, W3, dZ2, ld_dz, workspace);
+    rgb_head_bwd_kernel<<<nblk, 256, 0, s>>>(M, K, drgb, rgb, H3, ld_h, W3, dZ2, ld_dz, dz_bf16 != 0, workspace);
     int rc = check_launch("cn_rgb_head_bwd");
     if (rc) return rc;
     return launch_slab_jobs(slab_job(workspace, nblk, 4 * K, 3, K, K, dW3, K, 1.0f, 0),

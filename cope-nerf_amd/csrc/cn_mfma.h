@@ -168,6 +168,7 @@ __device__ __forceinline__ void tile_coords(int vt, int T, int& tm, int& tn) {
 }
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+inline bool al8(const void* p) { return ((uintptr_t)p & 7) == 0; }
 
 // Fixed-order sum of nslab fp32 slabs (cn_wgrad.hip): out[r*ldo + c] (+)= (sum_s part[s*stride + r*ldp + c]) / div.
 struct SlabJob {

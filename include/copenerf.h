@@ -345,8 +345,8 @@ int cn_color_extras_bwd(int32_t R, int32_t dir_div, const float* d_ext, int64_t 
  *   dW3 = sum_m dz3ᵀ H3, db3 = sum_m dz3 (fixed-order slab reduction). */
 size_t cn_rgb_head_bwd_workspace_bytes(int32_t M, int32_t K);
 int cn_rgb_head_bwd(int32_t M, int32_t K, const float* drgb, const float* rgb, const float* H3,
-                    int64_t ld_h, const float* W3, float* dZ2, int64_t ld_dz, float* dW3, float* db3,
-                    float* workspace, int64_t workspace_bytes, cn_stream_t stream);
+                    int64_t ld_h, const float* W3, void* dZ2, int64_t ld_dz, int32_t dz_bf16, float* dW3,
+                    float* db3, float* workspace, int64_t workspace_bytes, cn_stream_t stream);
 
 /* ------------------------------------------------------------------------ *
  * Patch sampling (model/training.py:413-436 on the device): idx[p*ps*ps + a*ps + b] =

@@ -438,6 +438,10 @@ def test_row_head_edge_cases_and_rgb_head_bwd():
     torch.testing.assert_close(dZ, gZ, rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(dW, gW, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(db, gb, rtol=1e-4, atol=1e-5)
+    # dZ as a bf16 operand image (bf16 mode): the RNE image of the same values, dW / db unchanged
+    dZb, dW2, db2 = torch.empty(M, K, device=DEV, dtype=torch.bfloat16), torch.empty_like(dW), torch.empty_like(db)
+    ops.rgb_head_bwd(drgb, rgb.detach().contiguous(), torch.relu(Z).detach(), K, W3.detach().contiguous(), dZb, dW2, db2)
+    assert torch.equal(dZb, dZ.bfloat16()) and torch.equal(dW2, dW) and torch.equal(db2, db)
     cs = torch.empty(K, device=DEV)
     ops.colsum(H3, K, cs)
     torch.testing.assert_close(cs, H3.double().sum(0).float(), rtol=1e-5, atol=1e-4)
