@@ -94,8 +94,8 @@ SIGNATURES = {
                             c_ptr, c_ptr]),
     "cn_softplus_adjoint_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32]),
     "cn_softplus_adjoint": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_f32, c_ptr, c_ptr, c_ptr, c_i64,
-                                    c_ptr, c_i64, c_f32, c_ptr, c_i64, c_i32, c_ptr, c_ptr, c_f32, c_ptr, c_i64,
-                                    c_ptr]),
+                                    c_ptr, c_i64, c_f32, c_ptr, c_i64, c_i32, c_i32, c_ptr, c_ptr, c_f32, c_ptr,
+                                    c_i64, c_ptr]),
     "cn_scale_cols": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_i64, c_f32, c_ptr]),
     "cn_sdf_embed": (c_i32, [c_i32, c_ptr, c_i64, c_i32, c_f32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_f32,
                              c_i32, c_ptr]),

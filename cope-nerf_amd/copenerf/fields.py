@@ -260,7 +260,9 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
             # the sdf head (and the ∇-pass seed s_7 = w80 ⊙ softplus'_7) in the layer's epilogue;
             # the activation itself is stored only when a consumer needs it (not on the sampler path)
             out = _empty(M, HL, dev) if (keep_u or want_feat is not False) else None
-            S7 = _empty(M, HL, dev) if want_grad else None
+            # bf16 mode with the folded feature head: s_7's consumers (the next ∇ GEMM, a weight
+            # gradient, the elementwise last adjoint's second-order term) all read its image
+            S7 = _empty(M, HL, dev) if (want_grad and not (img and want_feat is not True)) else None
             S7b = _empty_b(M, HL, dev) if (want_grad and img) else None
             ops.linear(A, pk.Bf[l], lay.out_dim[l], K, out, EPI_SOFTPLUS_HEAD, bias=pk.b[l], nzero=HL, beta=lay.beta,
                        threshold=lay.threshold, kalg=lay.in_dim[l], out1=S7, colv=pk.w80p if want_grad else None,
@@ -393,6 +395,14 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
     second = dG is not None
     if second and S is None:
         raise RuntimeError("SDF double backward needs the ∇ pass buffers (want_grad=True in forward)")
+    i8 = lay.in_dim[L8]
+    # dW8[0] = Σ_m dsdf U8 (+ Ud8) / scale: fused into the adjoint kernel on the folded-head path
+    # (also on the sdf-only first-order path, e.g. the consistency re-query: Z_7 = dsdf w80 σ_7)
+    sdf_only = dh is None and dfeat is None and not second and dsdf is not None
+    fused_cs = i8 == HL and ((dh is not None and (dsdf is not None or second)) or sdf_only)
+    # bf16 mode: the top tangent u̇_8 and s_7 reach the elementwise last adjoint (and its fused column
+    # sums) as images
+    top_img = img and second and dh is not None and fused_cs and Sb[L8 - 1] is not None
     Ud, Udb = None, [None] * nl
     if second:
         Ud = [None] * nl
@@ -411,7 +421,7 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
             into = (l + 1) == sk
             # bf16 mode: u̇_{l+1} is read by the next tangent GEMM, a weight gradient and the adjoint's
             # second-order term (all from its image); u̇_8 by the elementwise last adjoint (fp32)
-            if img and l + 1 < L8:
+            if img and (l + 1 < L8 or top_img):
                 out, ob = None, (Usk_db if into else _empty_b(M, HL, dev))
             else:
                 out, ob = (Usk_d if into else _empty(M, HL, dev)), None
@@ -428,7 +438,7 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
         gradient, whose second pair's Y is S_l: that must have an image too)."""
         return img and 1 <= l < L8 and (not second or Sb[l] is not None) and Ub[l] is not None
 
-    i8, o8 = lay.in_dim[L8], lay.out_dim[L8]
+    o8 = lay.out_dim[L8]
     dW8 = torch.empty(o8, i8, device=dev)
     db8 = torch.empty(o8, device=dev)
     if dfeat is not None and dh is None:
@@ -437,10 +447,6 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
         dW8[1:].zero_()
         db8[1:].zero_()
     dsdf_flat = None
-    # dW8[0] = Σ_m dsdf U8 (+ Ud8) / scale: fused into the adjoint kernel on the folded-head path
-    # (also on the sdf-only first-order path, e.g. the consistency re-query: Z_7 = dsdf w80 σ_7)
-    sdf_only = dh is None and dfeat is None and not second and dsdf is not None
-    fused_cs = i8 == HL and ((dh is not None and (dsdf is not None or second)) or sdf_only)
     if dsdf is not None:
         dsdf = dsdf.reshape(M, 1).contiguous()
         dsdf_flat = dsdf
@@ -457,7 +463,8 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
     def second_order(l):  # BWD_SOFTPLUS inputs of β s_l (1-σ_l) ż_l, ż_l = u̇_{l+1} c_l / σ_l
         if not second:
             return {}
-        img2 = l < L8 - 1 and Sb[l] is not None and Udb[l + 1] is not None  # (bf16 mode: the images)
+        # (bf16 mode: the images; the top layer's only on the elementwise path, top_img)
+        img2 = (l < L8 - 1 or top_img) and Sb[l] is not None and Udb[l + 1] is not None
         return dict(aux1=Sb[l] if img2 else S[l], aux2=Udb[l + 1] if img2 else Ud[l + 1],
                     aux2_scale=lay.beta * (SQRT2 if (l + 1) == sk else 1.0))
 

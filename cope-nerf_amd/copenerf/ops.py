@@ -485,8 +485,12 @@ def softplus_adjoint(act, N, out, *, act_beta, D=None, rowv=None, colv=None, aux
     rs_out[0] = Σ_m rowv[m] / cs_div (its bias gradient)."""
     for t, n in ((act, "act"), (out, "out"), (D, "D"), (aux1, "aux1"), (aux2, "aux2")):
         _need(t, n)
-        if t is not None and t is not out and t.dtype != torch.float32:
-            raise RuntimeError(f"softplus_adjoint: {n} must be float32")
+        if t is not None and t.dtype not in (torch.float32, torch.bfloat16):
+            raise RuntimeError(f"softplus_adjoint: {n} must be float32 or a bfloat16 operand image")
+    if aux1 is not None and aux2 is not None and aux1.dtype != aux2.dtype:
+        raise RuntimeError("softplus_adjoint: aux1 and aux2 must have the same dtype")
+    isb = lambda t: t is not None and t.dtype == torch.bfloat16  # noqa: E731
+    in_bf16 = (1 if isb(D) else 0) | (2 if isb(act) else 0) | (4 if isb(aux1) else 0)
     if rowv is not None and (not rowv.is_contiguous() or rowv.numel() != act.shape[0]):
         raise RuntimeError("softplus_adjoint: rowv must be a contiguous [M] tensor")
     M = act.shape[0]
@@ -499,7 +503,8 @@ def softplus_adjoint(act, N, out, *, act_beta, D=None, rowv=None, colv=None, aux
         ws = torch.empty(lib.cn_softplus_adjoint_workspace_bytes(M, N) // 4 + 1, device=act.device, dtype=torch.float32)
     _lib.call("cn_softplus_adjoint", M, N, _ptr(D), _ld(D), _ptr(act), _ld(act), float(act_beta),
               _ptr(rowv), _ptr(colv), _ptr(aux1), _ld(aux1), _ptr(aux2), _ld(aux2), float(aux2_scale), _ptr(out),
-              _ld(out), int(out.dtype == torch.bfloat16), _ptr(cs_out), _ptr(rs_out if cs_out is not None else None), float(cs_div), _ptr(ws),
+              _ld(out), int(out.dtype == torch.bfloat16), in_bf16, _ptr(cs_out),
+              _ptr(rs_out if cs_out is not None else None), float(cs_div), _ptr(ws),
               0 if ws is None else ws.numel() * 4, _stream())
     return out
 

@@ -1243,6 +1243,17 @@ __global__ void __launch_bounds__(256) scale_cols_kernel(int M, int N4, const fl
 }
 
 // 4 values at element offset i of an fp32 output, or of its bf16 operand image (ob)
+// four consecutive values of a row: fp32, or (B) a bf16 operand image widened
+template <bool B>
+__device__ __forceinline__ floatx4 load_row4(const void* p, int64_t i) {
+    if constexpr (B) {
+        const u32x2_t w = *reinterpret_cast<const u32x2_t*>(static_cast<const bf16_t*>(p) + i);
+        return floatx4{__builtin_bit_cast(float, w[0] << 16), __builtin_bit_cast(float, w[0] & 0xffff0000u),
+                       __builtin_bit_cast(float, w[1] << 16), __builtin_bit_cast(float, w[1] & 0xffff0000u)};
+    } else {
+        return *reinterpret_cast<const floatx4*>(static_cast<const float*>(p) + i);
+    }
+}
 __device__ __forceinline__ void store_row4(void* out, bool ob, int64_t i, floatx4 v) {
     if (ob)
         *reinterpret_cast<bf16x4*>(static_cast<bf16_t*>(out) + i) = __builtin_convertvector(v, bf16x4);
@@ -1254,25 +1265,27 @@ __device__ __forceinline__ void store_row4(void* out, bool ob, int64_t i, floatx
 // is already at hand (the SDF's last hidden layer once the feature head is folded into
 // the colour network):  out = (D + rowv (x) colv) * sg + aux1 * aux2 * c2 * (1 - sg) / sg,
 // sg = softplus' recovered from the activation (sigma_from_act); absent terms are 0.
-__global__ void __launch_bounds__(256) softplus_adjoint_kernel(int M, int N4, const float* __restrict__ D, int64_t ldd,
-                                                               const float* __restrict__ act, int64_t lda, float aux_c,
+// IB bit 0: D, bit 1: act, bit 2: aux1 / aux2 are bf16 operand images (config C3's bf16 mode)
+template <int IB>
+__global__ void __launch_bounds__(256) softplus_adjoint_kernel(int M, int N4, const void* __restrict__ D, int64_t ldd,
+                                                               const void* __restrict__ act, int64_t lda, float aux_c,
                                                                const float* __restrict__ rowv,
                                                                const float* __restrict__ colv,
-                                                               const float* __restrict__ aux1, int64_t ld1,
-                                                               const float* __restrict__ aux2, int64_t ld2, float c2,
+                                                               const void* __restrict__ aux1, int64_t ld1,
+                                                               const void* __restrict__ aux2, int64_t ld2, float c2,
                                                                void* out, int64_t ldo, bool ob) {
     const int64_t tot = (int64_t)M * N4;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += stride) {
         const int64_t m = idx / N4;
         const int n = (int)(idx - m * N4) * 4;
-        const floatx4 a = *reinterpret_cast<const floatx4*>(act + m * lda + n);
-        floatx4 g = D ? *reinterpret_cast<const floatx4*>(D + m * ldd + n) : floatx4{0.f, 0.f, 0.f, 0.f};
+        const floatx4 a = load_row4<(IB & 2) != 0>(act, m * lda + n);
+        floatx4 g = D ? load_row4<(IB & 1) != 0>(D, m * ldd + n) : floatx4{0.f, 0.f, 0.f, 0.f};
         if (rowv) g = g + rowv[m] * *reinterpret_cast<const floatx4*>(colv + n);
         floatx4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
         if (aux1) {
-            s1 = *reinterpret_cast<const floatx4*>(aux1 + m * ld1 + n);
-            s2 = *reinterpret_cast<const floatx4*>(aux2 + m * ld2 + n);
+            s1 = load_row4<(IB & 4) != 0>(aux1, m * ld1 + n);
+            s2 = load_row4<(IB & 4) != 0>(aux2, m * ld2 + n);
         }
         floatx4 o;
 #pragma unroll
@@ -1290,13 +1303,14 @@ __global__ void __launch_bounds__(256) softplus_adjoint_kernel(int M, int N4, co
 // columns), accumulates Σ_m rowv[m] act[m][n] + aux2[m][n] per thread in fp32, combines its
 // row lanes in a fixed order through LDS and writes one partial row per block.
 constexpr int kSaRows = 512;  // rows per block of the column-sum form
-__global__ void __launch_bounds__(256) softplus_adjoint_cs_kernel(int M, int N4, const float* __restrict__ D,
-                                                                  int64_t ldd, const float* __restrict__ act,
+template <int IB>
+__global__ void __launch_bounds__(256) softplus_adjoint_cs_kernel(int M, int N4, const void* __restrict__ D,
+                                                                  int64_t ldd, const void* __restrict__ act,
                                                                   int64_t lda, float aux_c,
                                                                   const float* __restrict__ rowv,
                                                                   const float* __restrict__ colv,
-                                                                  const float* __restrict__ aux1, int64_t ld1,
-                                                                  const float* __restrict__ aux2, int64_t ld2,
+                                                                  const void* __restrict__ aux1, int64_t ld1,
+                                                                  const void* __restrict__ aux2, int64_t ld2,
                                                                   float c2, void* out, int64_t ldo, bool ob,
                                                                   float* part, float* rpart) {
     __shared__ floatx4 red[256];
@@ -1310,14 +1324,14 @@ __global__ void __launch_bounds__(256) softplus_adjoint_cs_kernel(int M, int N4,
     floatx4 cs = {0.f, 0.f, 0.f, 0.f};
     float rs = 0.0f;  // Σ rowv over the rows of this lane (the head bias gradient), column-0 lanes
     auto row = [&](int m) {
-        const floatx4 a = *reinterpret_cast<const floatx4*>(act + (int64_t)m * lda + n);
-        floatx4 g = D ? *reinterpret_cast<const floatx4*>(D + (int64_t)m * ldd + n) : floatx4{0.f, 0.f, 0.f, 0.f};
+        const floatx4 a = load_row4<(IB & 2) != 0>(act, (int64_t)m * lda + n);
+        floatx4 g = D ? load_row4<(IB & 1) != 0>(D, (int64_t)m * ldd + n) : floatx4{0.f, 0.f, 0.f, 0.f};
         const float rv = rowv ? rowv[m] : 0.0f;
         g = g + rv * cv;
         floatx4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
         if (aux1) {
-            s1 = *reinterpret_cast<const floatx4*>(aux1 + (int64_t)m * ld1 + n);
-            s2 = *reinterpret_cast<const floatx4*>(aux2 + (int64_t)m * ld2 + n);
+            s1 = load_row4<(IB & 4) != 0>(aux1, (int64_t)m * ld1 + n);
+            s2 = load_row4<(IB & 4) != 0>(aux2, (int64_t)m * ld2 + n);
         }
         floatx4 o;
 #pragma unroll
@@ -1801,17 +1815,20 @@ extern "C" size_t cn_softplus_adjoint_workspace_bytes(int32_t M, int32_t N) {
     return sizeof(float) * (size_t)std::max(1, cdiv(M, kSaRows)) * (std::max(N, 4) + 1);
 }
 
-extern "C" int cn_softplus_adjoint(int32_t M, int32_t N, const float* D, int64_t ldd, const float* act, int64_t lda,
-                                   float act_beta, const float* rowv, const float* colv, const float* aux1,
-                                   int64_t ld1, const float* aux2, int64_t ld2, float aux2_scale, void* out,
-                                   int64_t ld_out, int32_t out_bf16, float* cs_out, float* rs_out, float cs_div,
-                                   float* workspace, int64_t workspace_bytes, cn_stream_t stream) {
+extern "C" int cn_softplus_adjoint(int32_t M, int32_t N, const void* D, int64_t ldd, const void* act, int64_t lda,
+                                   float act_beta, const float* rowv, const float* colv, const void* aux1,
+                                   int64_t ld1, const void* aux2, int64_t ld2, float aux2_scale, void* out,
+                                   int64_t ld_out, int32_t out_bf16, int32_t in_bf16, float* cs_out, float* rs_out,
+                                   float cs_div, float* workspace, int64_t workspace_bytes, cn_stream_t stream) {
     CN_REQUIRE(act && out && act_beta > 0.0f, CN_ERR_ARG, "cn_softplus_adjoint: act, out and act_beta > 0 required");
     CN_REQUIRE((rowv == nullptr) == (colv == nullptr) && (aux1 == nullptr) == (aux2 == nullptr), CN_ERR_ARG,
                "cn_softplus_adjoint: rowv/colv and aux1/aux2 go together");
-    CN_REQUIRE(N % 4 == 0 && lda % 4 == 0 && ld_out % 4 == 0 && al16(act) && al16(out) &&
-                   (!D || (ldd % 4 == 0 && al16(D))) && (!colv || al16(colv)) &&
-                   (!aux1 || (ld1 % 4 == 0 && ld2 % 4 == 0 && al16(aux1) && al16(aux2))),
+    CN_REQUIRE(in_bf16 >= 0 && in_bf16 < 8, CN_ERR_ARG, "cn_softplus_adjoint: in_bf16 is a 3-bit mask");
+    CN_REQUIRE(N % 4 == 0 && lda % 4 == 0 && ld_out % 4 == 0 && al8(act) && al8(out) &&
+                   (!D || (ldd % 4 == 0 && al8(D))) && (!colv || al16(colv)) &&
+                   (!aux1 || (ld1 % 4 == 0 && ld2 % 4 == 0 && al8(aux1) && al8(aux2))) &&
+                   ((in_bf16 & 2) || al16(act)) && (out_bf16 || al16(out)) && (!D || (in_bf16 & 1) || al16(D)) &&
+                   (!aux1 || (in_bf16 & 4) || (al16(aux1) && al16(aux2))),
                CN_ERR_ALIGN, "cn_softplus_adjoint: N, leading dimensions and pointers must be multiples of 4 floats");
     if (cs_out) {
         CN_REQUIRE(N >= 4 && N <= 1024 && workspace &&
@@ -1826,9 +1843,17 @@ extern "C" int cn_softplus_adjoint(int32_t M, int32_t N, const float* D, int64_t
         const int nblk = cdiv(M, kSaRows);
         hipStream_t s = (hipStream_t)stream;
         float* rpart = rs_out ? workspace + (size_t)nblk * N : nullptr;
-        softplus_adjoint_cs_kernel<<<nblk, 256, 0, s>>>(M, N / 4, D, ldd, act, lda, -act_beta * 1.44269504088896341f,
-                                                        rowv, colv, aux1, ld1, aux2, ld2, aux2_scale, out, ld_out,
-                                                        out_bf16 != 0, workspace, rpart);
+        switch (in_bf16) {
+#define CN_SA_CS(IB)                                                                                             \
+            case IB:                                                                                             \
+                softplus_adjoint_cs_kernel<IB><<<nblk, 256, 0, s>>>(M, N / 4, D, ldd, act, lda,                   \
+                                                                    -act_beta * 1.44269504088896341f, rowv, colv, \
+                                                                    aux1, ld1, aux2, ld2, aux2_scale, out, ld_out, \
+                                                                    out_bf16 != 0, workspace, rpart);            \
+                break;
+            CN_SA_CS(0) CN_SA_CS(1) CN_SA_CS(2) CN_SA_CS(3) CN_SA_CS(4) CN_SA_CS(5) CN_SA_CS(6) CN_SA_CS(7)
+#undef CN_SA_CS
+        }
         int rc = check_launch("cn_softplus_adjoint");
         if (rc) return rc;
         const float dv = cs_div == 0.f ? 1.f : cs_div;
@@ -1838,10 +1863,16 @@ extern "C" int cn_softplus_adjoint(int32_t M, int32_t N, const float* D, int64_t
     if ((int64_t)M * N == 0) return CN_OK;
     const int64_t tot = (int64_t)M * (N / 4);
     const int blocks = (int)std::min<int64_t>((tot + 255) / 256, 8192);
-    softplus_adjoint_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(M, N / 4, D, ldd, act, lda,
-                                                                     -act_beta * 1.44269504088896341f, rowv, colv,
-                                                                     aux1, ld1, aux2, ld2, aux2_scale, out, ld_out,
-                                                                     out_bf16 != 0);
+    switch (in_bf16) {
+#define CN_SA(IB)                                                                                                \
+        case IB:                                                                                                 \
+            softplus_adjoint_kernel<IB><<<blocks, 256, 0, (hipStream_t)stream>>>(                                \
+                M, N / 4, D, ldd, act, lda, -act_beta * 1.44269504088896341f, rowv, colv, aux1, ld1, aux2, ld2,  \
+                aux2_scale, out, ld_out, out_bf16 != 0);                                                         \
+            break;
+        CN_SA(0) CN_SA(1) CN_SA(2) CN_SA(3) CN_SA(4) CN_SA(5) CN_SA(6) CN_SA(7)
+#undef CN_SA
+    }
     return check_launch("cn_softplus_adjoint");
 }
 

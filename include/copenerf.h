@@ -289,12 +289,14 @@ int cn_scale_cols(int32_t M, int32_t N, const float* X, int64_t ldx, const float
  *   rs_out[0] = (sum_m rowv[m]) / cs_div (the sdf head's bias gradient; rs_out may be NULL),
  * fixed-order slab reductions through workspace (cn_softplus_adjoint_workspace_bytes). */
 size_t cn_softplus_adjoint_workspace_bytes(int32_t M, int32_t N);
-/* out_bf16 (ABI v10): out is written as its bf16 operand image (RNE; ld_out in bf16 elements, % 4 == 0). */
-int cn_softplus_adjoint(int32_t M, int32_t N, const float* D, int64_t ldd, const float* act, int64_t lda,
-                        float act_beta, const float* rowv, const float* colv, const float* aux1, int64_t ld1,
-                        const float* aux2, int64_t ld2, float aux2_scale, void* out, int64_t ld_out, int32_t out_bf16,
-                        float* cs_out, float* rs_out, float cs_div, float* workspace, int64_t workspace_bytes,
-                        cn_stream_t stream);
+/* out_bf16 (ABI v10): out is written as its bf16 operand image (RNE; ld_out in bf16 elements, % 4 == 0).
+ * in_bf16 (ABI v10): bit 0: D, bit 1: act, bit 2: aux1 and aux2 are bf16 operand images (config C3's
+ * bf16 mode; leading dimensions in bf16 elements, % 4 == 0, 8-byte aligned). */
+int cn_softplus_adjoint(int32_t M, int32_t N, const void* D, int64_t ldd, const void* act, int64_t lda,
+                        float act_beta, const float* rowv, const float* colv, const void* aux1, int64_t ld1,
+                        const void* aux2, int64_t ld2, float aux2_scale, void* out, int64_t ld_out, int32_t out_bf16,
+                        int32_t in_bf16, float* cs_out, float* rs_out, float cs_div, float* workspace,
+                        int64_t workspace_bytes, cn_stream_t stream);
 
 /* ------------------------------------------------------------------------ *
  * Positional encoding of the SDF input (neus_embedder.py:6-51 with
