@@ -82,6 +82,21 @@ def test_argument_validation_without_gpu():
     d.aux_beta, d.out1 = 100.0, 16
     assert lib.cn_linear(ctypes.byref(d), None) == -1
     assert b"out1" in lib.cn_last_error()
+    # ABI v10 bf16 images: BWD_SOFTPLUS takes its three aux operands in one format
+    d = _lib.LinearDesc()
+    d.A, d.B, d.out0_b, d.aux0, d.aux1, d.aux2 = 16, 16, 16, 16, 16, 16
+    d.M, d.N, d.K, d.lda, d.ldb, d.ld_out0_b, d.ld_aux0, d.ld_aux1, d.ld_aux2 = 8, 256, 256, 256, 256, 256, 256, 256, 256
+    d.epilogue, d.mfma_dtype, d.aux_beta, d.a_bf16, d.aux0_bf16 = _lib.EPI_BWD_SOFTPLUS, 1, 100.0, 1, 1
+    assert lib.cn_linear(ctypes.byref(d), None) == -5
+    assert b"all bf16 images or all fp32" in lib.cn_last_error()
+    d.mfma_dtype = 2  # images only in the bf16 MFMA mode
+    assert lib.cn_linear(ctypes.byref(d), None) == -5
+    assert b"CN_MFMA_BF16" in lib.cn_last_error()
+    # cn_softplus_adjoint's in_bf16 is a 3-bit mask; cn_rgb_head_bwd's bf16 dZ needs 8-byte alignment
+    assert lib.cn_softplus_adjoint(8, 256, None, 0, 16, 256, 100.0, None, None, None, 0, None, 0, 0.0, 16, 256,
+                                   1, 9, None, None, 1.0, None, 0, None) == -1
+    assert b"3-bit mask" in lib.cn_last_error()
+    assert lib.cn_rgb_head_bwd(8, 256, 16, 16, 16, 256, 16, 18, 256, 1, 16, 16, 16, 1 << 20, None) == -3
 
 
 def test_product_path_refuses_cpu_tensors():

@@ -1,4 +1,4 @@
-"""Where the small torch launches of a C2 step come from: every aten op on a
+"""Where the small torch launches of a train step (CONFIG: a bench.py config) come from: every aten op on a
 device tensor during one step, counted by the innermost repo (or torch.optim /
 autograd) source line that issued it."""
 import collections
@@ -39,10 +39,11 @@ class Origins(TorchDispatchMode):
 
 
 def main():
-    kw = dict(mfma_dtype=os.environ.get("MODE", "bf16x6"))
-    if os.environ.get("C3"):  # the c3fp32 bench config: joint pose + stage 1
-        kw.update(joint_pose=True, stage1=True, start_it=30000)
-    tr = SyntheticTrainer("cuda:0", rays=4096, **kw)
+    # CONFIG: a bench.py config (default c2)
+    from bench import CONFIGS
+    rays, kw, _ = CONFIGS[os.environ.get("CONFIG", "c2")]
+    kw = {k: v for k, v in kw.items() if k != "graph"}
+    tr = SyntheticTrainer("cuda:0", rays=rays, **kw)
     for _ in range(2):
         tr.step()
     torch.cuda.synchronize()

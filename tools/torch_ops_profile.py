@@ -10,10 +10,11 @@ from copenerf.train_step import SyntheticTrainer  # noqa: E402
 
 
 def main():
-    kw = dict(mfma_dtype=os.environ.get("MODE", "bf16x6"))
-    if os.environ.get("C3"):  # the c3fp32 bench config: joint pose + stage 1
-        kw.update(joint_pose=True, stage1=True, start_it=30000)
-    tr = SyntheticTrainer("cuda:0", rays=4096, **kw)
+    # CONFIG: a bench.py config (default c2)
+    from bench import CONFIGS
+    rays, kw, _ = CONFIGS[os.environ.get("CONFIG", "c2")]
+    kw = {k: v for k, v in kw.items() if k != "graph"}
+    tr = SyntheticTrainer("cuda:0", rays=rays, **kw)
     for _ in range(3):
         tr.step()
     torch.cuda.synchronize()
