@@ -420,7 +420,8 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
         for l in range(nl - 1):
             into = (l + 1) == sk
             # bf16 mode: u̇_{l+1} is read by the next tangent GEMM, a weight gradient and the adjoint's
-            # second-order term (all from its image); u̇_8 by the elementwise last adjoint (fp32)
+            # second-order term (all from its image); u̇_8 by the elementwise last adjoint (an image with
+            # top_img, else fp32)
             if img and (l + 1 < L8 or top_img):
                 out, ob = None, (Usk_db if into else _empty_b(M, HL, dev))
             else:
