@@ -1660,10 +1660,11 @@ static int linear_plan(const cn_linear_desc* d, LinearArgs& a) {
         CN_REQUIRE(!d->out0_b || (al16(d->out0_b) && d->ld_out0_b % 8 == 0 && d->ld_out0_b < (1 << 20) &&
                                   d->ld_out0_b >= std::max(d->nzero, d->N)),
                    CN_ERR_ALIGN, "cn_linear: out0_b needs 16-byte alignment and ld_out0_b >= nzero, % 8 == 0");
-        CN_REQUIRE(!d->out1_b || (d->epilogue == CN_EPI_SOFTPLUS_HEAD && d->out1 && al16(d->out1_b) &&
-                                  d->ld_out1_b % 8 == 0 && d->ld_out1_b < (1 << 20) &&
+        CN_REQUIRE(!d->out1_b || (d->epilogue == CN_EPI_SOFTPLUS_HEAD && d->colv && d->aux_beta > 0.0f &&
+                                  al16(d->out1_b) && d->ld_out1_b % 8 == 0 && d->ld_out1_b < (1 << 20) &&
                                   d->ld_out1_b >= std::max(d->nzero, d->N)),
-                   CN_ERR_ARG, "cn_linear: out1_b is SOFTPLUS_HEAD's image of out1 (16-byte aligned, ld % 8 == 0)");
+                   CN_ERR_ARG, "cn_linear: out1_b is SOFTPLUS_HEAD's image of out1 (colv, aux_beta > 0; 16-byte "
+                   "aligned, ld % 8 == 0; out1 itself may be NULL)");
     }
     const int K1 = d->A2 ? d->K1 : d->K;
     CN_REQUIRE(K1 > 0 && K1 <= d->K && K1 % (bf ? 64 : 32) == 0, CN_ERR_SHAPE, "cn_linear: bad K1=%d", K1);

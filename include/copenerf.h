@@ -138,7 +138,7 @@ typedef struct cn_linear_desc {
        aux12_bf16.
        out0_b (ld_out0_b): the bf16 image of every value written to out0 (columns [0, nzero),
        including the zero fill); out0 itself may then be NULL.  out1_b: the same for SOFTPLUS_HEAD's
-       out1.  Leading dimensions in bf16 elements, multiples of 8; 16-byte aligned. */
+       out1 (colv and aux_beta set; out1 may then be NULL).  Leading dimensions in bf16 elements, multiples of 8; 16-byte aligned. */
     int32_t a_bf16;
     int32_t aux0_bf16;
     int32_t aux12_bf16;

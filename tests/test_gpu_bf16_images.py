@@ -151,6 +151,12 @@ def test_bf16_concat_image_and_head():
     (a, s1, sdf, _, _), (a2, s2, sdf2, ab, sb) = res
     assert torch.equal(a, a2) and torch.equal(s1, s2) and torch.equal(sdf, sdf2)
     assert torch.equal(ab, a.bfloat16()) and torch.equal(sb, s1.bfloat16())
+    # the ∇-pass seed as an image only (out1 NULL): the same image
+    sb2 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    sdf3 = torch.empty(M, device=DEV)
+    ops.linear(o.bfloat16(), Bh, N, N, None, ops.EPI_SOFTPLUS_HEAD, bias=bias, colv=colv, aux_beta=100.0,
+               head_w=hw, head_b=hb, head_out=sdf3, out0_b=torch.empty_like(sb2), out1_b=sb2)
+    assert torch.equal(sb2, sb) and torch.equal(sdf3, sdf)
 
 
 @pytest.mark.parametrize("M,pairs", [(70001, 2), (4097, 1), (33, 2)])
