@@ -264,7 +264,7 @@ def test_color_bf16_images_match_fp32_operand_path():
         fields._img_mode = saved
     names = ["rgb", "pts", "nrm", "dirs", "feat"] + [n for n, _ in net.named_parameters()]
     for n, a, b in zip(names, res[0], res[1]):
-        if n in ("lin1.bias", "lin2.bias"):
+        if n in ("lin1.bias", "lin2.bias", "lin3.bias"):  # (the adjoints that are images: bias sums of bf16 values)
             torch.testing.assert_close(a, b, rtol=1e-2, atol=1e-2 * b.abs().max().item() + 1e-6)
         else:
             assert torch.equal(a, b), n
