@@ -1611,11 +1611,9 @@ static LinearTile choose_linear_tile(const cn_linear_desc* d) {
     if (d->mfma_dtype == CN_MFMA_F32_BF16X6) {
         if (d->tile == 1) return LT_X6_T1;
         if (d->tile == 2) return LT_X6_T128;
-#ifndef CN_EXP_X6SQ_BWD
+        // (BWD_SOFTPLUS on the 256x256 tile: re-measured in round 4 with the branch-free epilogue, equal or
+        // slower -- 4.25 vs 4.17 ms per C2 step, profiles/r4_ab.txt r4m)
         if (wide_n && d->K % 32 == 0 && d->ldb >= 256 && e != CN_EPI_BWD_SOFTPLUS && (longk || head)) return LT_X6_SQ;
-#else  // TEMPORARY measurement build: BWD_SOFTPLUS on the 256x256 tile too
-        if (wide_n && d->K % 32 == 0 && d->ldb >= 256 && (longk || head)) return LT_X6_SQ;
-#endif
         const bool tall = e == CN_EPI_MUL || e == CN_EPI_TANGENT || head;
         if (d->K % 64 == 0 && tall && d->N > 128 && d->ldb >= 256 && (longk || head)) return LT_X6_TALL;
         // (an aux-reading epilogue with one workgroup per CU no longer overlaps a partner's main loop)
