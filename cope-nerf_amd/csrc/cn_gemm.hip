@@ -873,11 +873,15 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             }
         };
         // bf16 images from the MFMA layout (MODE 1): lanes 2c and 2c + 1 hold columns 2c, 2c + 1 of
-        // accumulator rows r (even) and r + 1; they swap one value (DPP) so the even lane writes
-        // (row r: 2c, 2c + 1) and the odd lane (row r + 1: 2c, 2c + 1), one dword each.  Per column
-        // block j the lane's byte offset (row r + 1 for odd lanes), or one past any view for
-        // columns >= nzero (the pair's columns are both below or both past it: nzero % 4 == 0).
+        // accumulator rows r (even) and r + 1.  Each lane rounds its own (row r, row r + 1) pair to
+        // bf16 (one v_cvt_pk: the RNE of any other packing), the two lanes swap the packed dwords
+        // (DPP) and one v_perm picks row r's halves (even lane) or row r + 1's (odd lane): one dword
+        // store each, no per-element selects.  Per column block j the lane's byte offset (row r + 1
+        // for odd lanes), or one past any view for columns >= nzero (the pair's columns are both
+        // below or both past it: nzero % 4 == 0).
         const bool odd = lane & 1;
+        // v_perm byte selectors over {recv : own}: own.lo, recv.lo (even); recv.hi, own.hi (odd)
+        const unsigned psel = odd ? 0x03020706u : 0x05040100u;
         auto bimg_cols = [&](int ld, int lrow, int lcol, int* vbj) {
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
@@ -886,8 +890,9 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             }
         };
         auto bimg_pair = [&](const TileView& t, int rowi, int vb, float o_r, float o_r1) {
-            const float recv = lane_xor1(odd ? o_r : o_r1);
-            bstore_b16x2(view_at(t, rowi), vb, 0, odd ? recv : o_r, odd ? o_r1 : recv);
+            const unsigned own = pack_b16x2(o_r, o_r1);
+            const unsigned recv = __builtin_amdgcn_mov_dpp(own, 0xB1, 0xF, 0xF, true);  // lane ^ 1
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(recv, own, psel), view_at(t, rowi), vb, 0, 0);
         };
         // The direct epilogues take the wave-uniform choices (fp32 out0 stored, bf16 image of it, MUL's
         // split output) as template flags: as branches inside the element loops they left the

@@ -77,19 +77,17 @@ __device__ __forceinline__ floatx4 bload_b16x4(rsrc_t r, int voff, int soff) {
                    __builtin_bit_cast(float, w[1] << 16), __builtin_bit_cast(float, w[1] & 0xffff0000u)};
 }
 // RNE bf16 of two / four fp32 values (v_cvt_pk_bf16_f32: the rounding the GEMM staging applies)
-__device__ __forceinline__ void bstore_b16x2(rsrc_t r, int voff, int soff, float a, float b) {
+__device__ __forceinline__ unsigned pack_b16x2(float a, float b) {
     typedef float f2 __attribute__((ext_vector_type(2)));
-    const bf16x2_t h = __builtin_convertvector((f2){a, b}, bf16x2_t);
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, h), r, voff, soff, 0);
+    return __builtin_bit_cast(unsigned, __builtin_convertvector((f2){a, b}, bf16x2_t));
+}
+__device__ __forceinline__ void bstore_b16x2(rsrc_t r, int voff, int soff, float a, float b) {
+    __builtin_amdgcn_raw_buffer_store_b32(pack_b16x2(a, b), r, voff, soff, 0);
 }
 __device__ __forceinline__ void bstore_b16x4(rsrc_t r, int voff, int soff, floatx4 v) {
     typedef __bf16 b4 __attribute__((ext_vector_type(4)));
     const b4 h = __builtin_convertvector(v, b4);
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, h), r, voff, soff, 0);
-}
-// the value of the neighbouring lane (lane ^ 1): DPP quad_perm [1, 0, 3, 2]
-__device__ __forceinline__ float lane_xor1(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, true));
 }
 
 // torch.nn.Softplus(beta, threshold) on the hardware transcendentals: e = 2^(z beta
