@@ -250,6 +250,35 @@ def test_softplus_adjoint():
     assert torch.all(cs2 == 0)
 
 
+@pytest.mark.parametrize("img", [0, 1, 2, 4, 7])
+def test_softplus_adjoint_cs_images_strided(img):
+    """The column-sum form (buffer views of a block's rows, four rows in flight per lane) over
+    bf16 operand images (in_bf16 mask `img`, bf16 out when img) and column slices of wider
+    tensors (leading dimension > N): out bitwise equal to the plain form's, the sums within fp32
+    summation error of the fp64 reference, over ragged M (block tails, a lane's tail)."""
+    ops = _ops()
+    K, W = 256, 264
+    for M in (1029, 517, 3):
+        def t(seed, b):
+            x = _rnd(M, W, seed=seed)[:, 4:4 + K]
+            return x.to(torch.bfloat16) if b else x
+        act = _act(M, W, 41 + M)[:, 4:4 + K]
+        act = act.to(torch.bfloat16) if img & 2 else act
+        D, s1, s2 = t(42, img & 1), t(43, img & 4), t(44, img & 4)
+        rv, cv = _rnd(M, seed=45), _rnd(K, seed=46)
+        dt = torch.bfloat16 if img else torch.float32
+        ref_out = torch.full((M, W), float("nan"), device=DEV, dtype=dt)[:, :K]
+        out = torch.full((M, W), float("nan"), device=DEV, dtype=dt)[:, :K]
+        kw = dict(act_beta=100.0, D=D, rowv=rv, colv=cv, aux1=s1, aux2=s2, aux2_scale=0.7)
+        ops.softplus_adjoint(act, K, ref_out, **kw)
+        cs, rs = torch.empty(K, device=DEV), torch.empty(1, device=DEV)
+        ops.softplus_adjoint(act, K, out, cs_out=cs, rs_out=rs, **kw)
+        assert torch.equal(out, ref_out)
+        cs_ref = (rv.double()[:, None] * act.double() + s2.double()).sum(0)
+        torch.testing.assert_close(cs, cs_ref.float(), rtol=1e-5, atol=1e-4)
+        torch.testing.assert_close(rs, rv.double().sum().float().view(1), rtol=1e-5, atol=1e-5)
+
+
 def test_c_abi_rejects_bad_arguments():
     ops = _ops()
     A = torch.zeros(10, 30, device=DEV)
