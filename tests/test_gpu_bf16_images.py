@@ -95,6 +95,32 @@ def test_bf16_operand_images_bitwise(tile):
     assert torch.equal(ob, ref.bfloat16())
 
 
+@pytest.mark.parametrize("N", [256, 204, 228])
+@pytest.mark.parametrize("tile", [0, 2])
+def test_bf16_image_only_outputs_bitwise(N, tile):
+    """out0 NULL, the bf16 image alone, for every epilogue (the image-only epilogues zero-fill through
+    their v_perm selectors): equal to the image of the fp32 output, incl. the zero-filled columns
+    [N, nzero) and MUL's split columns (out_split written as with out0)."""
+    from copenerf import ops
+    M, K = 3001, 256
+    A = _rnd(M, K, seed=43, scale=0.3)
+    Bb = torch.zeros(256, K, device=DEV)
+    Bb[:N] = _rnd(N, K, seed=44, scale=0.06)
+    Bb = Bb.bfloat16().contiguous()
+    for name, epi, kw in _epi_cases(ops, M, N, 40):
+        ref, _, s_ref = _run(ops, A, Bb, N, K, epi, kw, tile)
+        kw = dict(kw)
+        split = None
+        if "nsplit" in kw:
+            split = torch.full((M, 64), float("nan"), device=DEV)
+            kw["out_split"] = split
+        ob = torch.full((M, 256), float("nan"), device=DEV).bfloat16()
+        ops.linear(A.bfloat16(), Bb, N, K, None, epi, nzero=256, tile=tile, out0_b=ob, **kw)
+        assert torch.equal(ob, ref.bfloat16()), name
+        if split is not None:
+            assert torch.equal(torch.nan_to_num(split, 7.0), torch.nan_to_num(s_ref, 7.0)), name
+
+
 @pytest.mark.parametrize("tile", [0, 2])
 def test_bf16_aux_images_bitwise(tile):
     """MUL / TANGENT / BWD_SOFTPLUS / BWD_RELU with every aux operand as a bf16 image equal the same
