@@ -889,10 +889,10 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 vbj[j] = n0 + c < cNzero ? ((lrow + (odd ? 1 : 0)) * ld + c) * 2 : (1 << 30);
             }
         };
-        auto bimg_pair = [&](const TileView& t, int rowi, int vb, float o_r, float o_r1) {
+        auto bimg_pair = [&](const TileView& t, int rowi, int vb, float o_r, float o_r1, unsigned sel) {
             const unsigned own = pack_b16x2(o_r, o_r1);
             const unsigned recv = __builtin_amdgcn_mov_dpp(own, 0xB1, 0xF, 0xF, true);  // lane ^ 1
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(recv, own, psel), view_at(t, rowi), vb, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(recv, own, sel), view_at(t, rowi), vb, 0, 0);
         };
         // The direct epilogues take the wave-uniform choices (fp32 out0 stored, bf16 image of it, MUL's
         // split output) as template flags: as branches inside the element loops they left the
@@ -992,7 +992,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                     if constexpr (B0) {
                         if (r & 1) {
 #pragma unroll
-                            for (int j = 0; j < TN; ++j) bimg_pair(tO0b, rowi - 1, vbj[j], prev[j], ov[j]);
+                            for (int j = 0; j < TN; ++j) bimg_pair(tO0b, rowi - 1, vbj[j], prev[j], ov[j], psel);
                         } else {
 #pragma unroll
                             for (int j = 0; j < TN; ++j) prev[j] = ov[j];
@@ -1010,6 +1010,18 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
             bool live[TN];
             direct_cols(vo, lcol, voj, live);
             if (B0) bimg_cols(p.ld_out0_b, lrow, lcol, vbj);
+            // image only (no fp32 out0) on the LDS-DMA tile: columns [N, nzero) zero-filled through the
+            // v_perm selector (0x0c: a zero byte) of each half of the lane's dword (columns c, c + 1:
+            // c = lcol for even lanes, lcol - 1 for odd ones) instead of a select per element.  (Not on
+            // the register-staged tiles: there the compiler answered it with vmcnt(0) waits that drain
+            // the next tile's prefetch.)
+            constexpr bool kSel = B0 && !O0 && kDma;
+            unsigned selj[TN];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int c = n0 + lcol - (odd ? 1 : 0) + 32 * j;
+                selj[j] = (c < cN ? (psel & 0xffffu) : 0x0c0cu) | (c + 1 < cN ? (psel & 0xffff0000u) : 0x0c0c0000u);
+            }
             float bj[TN];
 #pragma unroll
             for (int j = 0; j < TN; ++j) bj[j] = kDma ? tbias[j] : kBias ? sBias[min(n0 + lcol + 32 * j, kTblCols - 1)] : 0.0f;
@@ -1028,13 +1040,13 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         if constexpr (EPI == CN_EPI_SOFTPLUS) o = softplus_hw(z, c_exp, c_thr, c_log) * cInvOdiv;
                         else if constexpr (EPI == CN_EPI_RELU) o = z > 0.0f ? z : 0.0f;
                         else o = z;
-                        ov[j] = live[j] ? o : 0.0f;
+                        ov[j] = kSel ? o : live[j] ? o : 0.0f;
                         if constexpr (O0) bstore1(vw, voj[j], 0, ov[j]);
                     }
                     if constexpr (B0) {
                         if (r & 1) {
 #pragma unroll
-                            for (int j = 0; j < TN; ++j) bimg_pair(tO0b, rowi - 1, vbj[j], prev[j], ov[j]);
+                            for (int j = 0; j < TN; ++j) bimg_pair(tO0b, rowi - 1, vbj[j], prev[j], ov[j], kSel ? selj[j] : psel);
                         } else {
 #pragma unroll
                             for (int j = 0; j < TN; ++j) prev[j] = ov[j];
@@ -1085,8 +1097,8 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         if (r & 1) {
 #pragma unroll
                             for (int j = 0; j < TN; ++j) {
-                                if (has_b0) bimg_pair(tO0b, rowi - 1, vbj[j], prev0[j], ov0[j]);
-                                if (has_b1) bimg_pair(tO1b, rowi - 1, vb1[j], prev1[j], ov1[j]);
+                                if (has_b0) bimg_pair(tO0b, rowi - 1, vbj[j], prev0[j], ov0[j], psel);
+                                if (has_b1) bimg_pair(tO1b, rowi - 1, vb1[j], prev1[j], ov1[j], psel);
                             }
                         } else {
 #pragma unroll
