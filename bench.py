@@ -2,6 +2,10 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|...] [--graph]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+    python bench.py --gpus 2 --dry --backend gloo      (launcher check on the CPU, no HIP work)
+
+Without WORLD_SIZE in the environment, `--gpus N > 1` starts the N rank processes itself (one per
+GPU, before any GPU call); under a launcher WORLD_SIZE must equal --gpus.
 
 Metric (BASELINE.json): rays/sec of a full training step incl. backward at
 4096 rays x 128 samples per GPU (64 coarse + 4x16 importance, fp32, fixed
@@ -17,9 +21,12 @@ The JSON line also carries
                 (HIP events around each launch on the launching stream):
                 its algorithmic FLOPs and bytes per launch against the binding
                 ceiling, max(FLOPs / MFMA peak of the GEMM mode, bytes / HBM
-                peak); `traffic` is the rocprofv3 PMC (FETCH_SIZE + WRITE_SIZE)
-                per launch read from profiles/ when a counter pass for this
-                kernel is committed;
+                peak); the kernel's duration is the rocprofv3 average of a committed
+                kernel-stats CSV recorded for this very library build (its
+                _lib_stamp.txt equals the loaded .so's stamp), else this run's HIP
+                events (`frac_source` says which); `traffic` is the rocprofv3 PMC
+                (FETCH_SIZE + WRITE_SIZE) per launch read from profiles/ when a
+                counter pass for this kernel is committed;
   cpu_baseline  the CPU oracle (oracle/neus_oracle.py, a torch restatement of the
                 reference path pinned to the reference's outputs) timed on this
                 box's host cores: median of 5 steps at 1024 rays after a
@@ -55,15 +62,39 @@ SAMPLES = 128
 GFLOP_PER_RAY_REF = 1.4809  # reference GEMM FLOPs per ray per train step (64+4x16)
 
 
-def rocprof_launch_ns(symbol, config):
+def lib_stamp():
+    """Digest of the sources, headers and flags the loaded libcopenerf.so was built from (the
+    `.stamp` build() writes beside it), or None."""
+    from copenerf import _lib
+    try:
+        with open(_lib.LIB_PATH + ".stamp") as f:
+            return f.read().strip() or None
+    except OSError:
+        return None
+
+
+def stats_stamp(csv_path):
+    """The library stamp tools/profile_round.sh recorded beside a kernel-stats CSV, or None."""
+    try:
+        with open(csv_path.replace("_kernel_stats.csv", "_lib_stamp.txt")) as f:
+            return f.read().strip() or None
+    except OSError:
+        return None
+
+
+def rocprof_launch_ns(symbol, config, stamp):
     """Average duration (ns) of `symbol` in the newest committed rocprofv3 kernel-stats summary of
     this config's bench (profiles/<tag>_kernel_stats.csv for c2, <tag>_<config>_kernel_stats.csv
-    otherwise), and the file; (None, None) when no committed profile has the kernel."""
+    otherwise) that was recorded for this very library build (its `_lib_stamp.txt` equals `stamp`),
+    and the file; (None, None) otherwise."""
     import csv
+    if not stamp:
+        return None, None
     pat = "*_kernel_stats.csv" if config == "c2" else f"*_{config}_kernel_stats.csv"
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", pat)))
     if config == "c2":  # (another config's files carry its name before the suffix)
         files = [f for f in files if not any(f.endswith(f"_{c}_kernel_stats.csv") for c in CONFIGS if c != "c2")]
+    files = [f for f in files if stats_stamp(f) == stamp]
     for f in reversed(files):
         try:
             with open(f) as fh:
@@ -191,9 +222,60 @@ CONFIGS = {
 }
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without a launcher: start N rank processes of this script (one per GPU,
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment, rendezvous on 127.0.0.1) and
+    return the exit status.  Runs before anything touches the GPU: the parent only waits, so no
+    process that initialised HIP ever starts another program.  If one rank fails the others are
+    stopped (by their exact pids) and its status is returned."""
+    import subprocess
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return status
+
+
+def dry_step(rank, world, grad_numel=800_000):
+    """--dry: the launcher / process-group / timing plumbing with no HIP work (CPU tensors, gloo):
+    a small CPU computation and the flat gradient all-reduce of the real step's size (~3.2 MB)."""
+    g = torch.Generator().manual_seed(rank)
+    a = torch.rand(256, 256, generator=g)
+    flat = (a @ a).flatten().repeat(grad_numel // a.numel() + 1)[:grad_numel]
+    if world > 1:
+        dist.all_reduce(flat)
+        flat /= world
+    return flat.sum()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (= ranks) of this node; without WORLD_SIZE in the environment bench.py starts them "
+                         "itself (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c2")
@@ -201,7 +283,18 @@ def main():
     ap.add_argument("--graph", action="store_true", help="replay the step from a captured HIP graph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--timer-steps", type=int, default=3, help="instrumented steps after the timed ones (roofline)")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process-group backend (nccl = RCCL over xGMI; gloo only with --dry)")
+    ap.add_argument("--dry", action="store_true",
+                    help="launcher check on the CPU: ranks, process group, barriers and timing without HIP work")
     args = ap.parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if env_world is not None and args.gpus is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world} in the environment")
+    if args.backend == "gloo" and not args.dry:
+        sys.exit("bench.py: --backend gloo is for --dry runs only (the HIP path all-reduces over RCCL)")
     rays_cfg, kw, workload = CONFIGS[args.config]
     kw = dict(kw)
     graph = kw.pop("graph", False) or args.graph
@@ -212,11 +305,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # COPENERF_FORCE_DIST=1 runs the RCCL path (process group + flat all-reduce) even at one rank
     distributed = world > 1 or os.environ.get("COPENERF_FORCE_DIST") == "1"
+    if args.dry:
+        return dry_main(args, world, rank, distributed)
     torch.cuda.set_device(local)
     if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank, world_size=world)
+        joined = torch.ones(1, device=f"cuda:{local}")
+        dist.all_reduce(joined)
+        if int(joined.item()) != world:
+            raise RuntimeError(f"{int(joined.item())} of {world} ranks joined the process group")
 
     from copenerf import ops
     from copenerf.train_step import GraphedTrainer, SyntheticTrainer
@@ -276,6 +375,7 @@ def main():
         "value": round(rays_total / elapsed, 1),
         "unit": "rays/s",
         "n_gpus": world,
+        "ranks_joined": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -303,6 +403,39 @@ def main():
         dist.destroy_process_group()
 
 
+def dry_main(args, world, rank, distributed):
+    """The --dry line: same launch, barriers and max-over-ranks timing as the HIP bench, CPU work."""
+    if distributed:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group(args.backend, rank=rank, world_size=world)
+        joined = torch.ones(1)
+        dist.all_reduce(joined)
+        if int(joined.item()) != world:
+            raise RuntimeError(f"{int(joined.item())} of {world} ranks joined the process group")
+    for _ in range(args.warmup):
+        dry_step(rank, world)
+    if distributed:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dry_step(rank, world)
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if distributed:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    if rank == 0:
+        print(json.dumps({"metric": "dry launcher check (no HIP work)", "value": round(args.steps * world / elapsed, 1),
+                          "unit": "steps/s", "n_gpus": world, "ranks_joined": world, "steps": args.steps,
+                          "warmup": args.warmup, "backend": args.backend if distributed else None,
+                          "config": {"parallelism": f"dp{world}" if world > 1 else "single"}}), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
 def roofline_fields(timer, steps, rays_per_s, mode, config="c2"):
     agg = timer.summary()
     # the dominant launch class over every cn_linear and cn_wgrad class (a launch class is one
@@ -323,14 +456,17 @@ def roofline_fields(timer, steps, rays_per_s, mode, config="c2"):
     # bracket the library call: for a weight gradient also its slab reduction); the HIP-event
     # figure of this run beside it
     frac_ev = max(t_flop, t_byte) / avg_s
-    prof_ns, prof_src = rocprof_launch_ns(symbol, config)
+    stamp = lib_stamp()
+    prof_ns, prof_src = rocprof_launch_ns(symbol, config, stamp)
     kern_s = prof_ns * 1e-9 if prof_ns else avg_s
     roof = {"bound": "hbm" if hbm else "mfma",
             "achieved": round(nbytes / kern_s / 1e9, 1) if hbm else round(flops / kern_s / 1e12, 2),
             "peak": HBM_PEAK_GBS if hbm else round(peak_tf, 1), "unit": "GB/s" if hbm else "TFLOP/s",
             "frac": round(max(t_flop, t_byte) / kern_s, 4),
             "frac_source": (f"{prof_src}: the kernel's rocprofv3 average duration" if prof_src else
-                            "HIP events of this run (no committed rocprofv3 stats name this kernel)"),
+                            "HIP events of this run (no committed rocprofv3 stats of this library build name "
+                            "this kernel)"),
+            "lib_stamp": stamp,
             "avg_launch_ms_rocprof": round(prof_ns * 1e-6, 4) if prof_ns else None,
             "frac_hip_events": round(frac_ev, 4),
             "traffic": traffic, "traffic_source": traffic_src,

@@ -66,3 +66,32 @@ def test_roofline_frac_follows_the_cited_kernel_stats():
         assert abs(frac - roof["frac"]) <= 0.01 * roof["frac"], (f, frac, roof["frac"])
         checked += 1
     assert checked >= 1, "no committed bench line cites rocprofv3 stats for its roofline"
+
+
+def test_cited_kernel_stats_were_recorded_for_the_reported_library():
+    """A bench line (round 5 on) that takes its frac from committed kernel stats cites a CSV whose
+    _lib_stamp.txt equals the library stamp the line reports."""
+    from bench import stats_stamp
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*bench*.json"))):
+        with open(f) as fh:
+            lines = [ln for ln in fh.read().strip().splitlines() if ln.startswith("{")]
+        if not lines:
+            continue
+        roof = json.loads(lines[-1]).get("roofline") or {}
+        if "lib_stamp" not in roof or not roof.get("frac_source", "").endswith("average duration"):
+            continue
+        csv_path = os.path.join(ROOT, roof["frac_source"].split(":")[0])
+        assert stats_stamp(csv_path) == roof["lib_stamp"], f
+
+
+def test_bench_cites_stats_only_for_the_same_library_build(tmp_path, monkeypatch):
+    import bench
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    (prof / "r9a_kernel_stats.csv").write_text("Name,Calls,TotalDurationNs,AverageNs\nk,2,200,100\n")
+    (prof / "r9a_lib_stamp.txt").write_text("aaaa\n")
+    (prof / "r9b_kernel_stats.csv").write_text("Name,Calls,TotalDurationNs,AverageNs\nk,2,400,200\n")
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench.rocprof_launch_ns("k", "c2", "aaaa") == (100.0, os.path.join("profiles", "r9a_kernel_stats.csv"))
+    assert bench.rocprof_launch_ns("k", "c2", "bbbb") == (None, None)  # r9b has no stamp, r9a another one
+    assert bench.rocprof_launch_ns("k", "c2", None) == (None, None)

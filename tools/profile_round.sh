@@ -16,8 +16,11 @@ for c in ${@:-c2}; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/ks_$c -o run --output-format csv -- \
     python3 $R/bench.py --config $c --steps 10 --warmup 3 --no-cpu-baseline > $O/${n}_bench_trace.json
   cp $O/ks_$c/run_kernel_stats.csv $O/${n}_kernel_stats.csv
+  # the library build the stats were taken on (bench.py cites stats only for the same build)
+  cp $R/cope-nerf_amd/copenerf/libcopenerf.so.stamp $O/${n}_lib_stamp.txt
   # the untraced line reads the stats for its roofline: copy them where bench.py looks first
   cp $O/${n}_kernel_stats.csv $R/profiles/${n}_kernel_stats.csv
+  cp $O/${n}_lib_stamp.txt $R/profiles/${n}_lib_stamp.txt
   if [ $c = c2 ]; then
     timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --timer-steps 1 > /dev/null
     timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --timer-steps 1 > /dev/null
