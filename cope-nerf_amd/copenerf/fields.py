@@ -196,12 +196,14 @@ def sig_beta(lay: SDFLayout, l: int) -> float:
     return lay.beta * (SQRT2 if (l + 1) == lay.skip else 1.0)
 
 
-def _img_mode(pk) -> bool:
+def _img_mode(pk, lay) -> bool:
     """bf16 MFMA mode (config C3): activations whose consumers are GEMM operands are stored as bf16
     operand images -- the bits the GEMM staging would round them to -- beside (or instead of) the fp32
-    values the epilogues read."""
+    values the epilogues read.  Only with 256-padded hidden buffers: image operands of a
+    weight gradient need the 256x256 stage ring (cn_wgrad's bf16 images); narrower networks keep fp32
+    operands, rounded on load."""
     B = pk.Bf[0]
-    return B.dtype == torch.bfloat16 and B.dim() == 2
+    return B.dtype == torch.bfloat16 and B.dim() == 2 and lay.HL % 256 == 0
 
 
 def _empty_b(M, n, dev):
@@ -235,7 +237,7 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
     M, dev = x.shape[0], x.device
     nl, sk, HL, KE = lay.n_lin, lay.skip, lay.HL, lay.KE
     keep_u = keep or want_grad
-    img = _img_mode(pk)
+    img = _img_mode(pk, lay)
     L8 = nl - 1
     U, Ub = [None] * nl, [None] * nl
     U[0] = _empty(M, KE, dev)
@@ -293,7 +295,7 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
     if want_grad:
         S, Sb = [None] * (nl - 1), [None] * (nl - 1)
         S[L8 - 1], Sb[L8 - 1] = S7, S7b
-        if S7 is None:
+        if S7 is None and S7b is None:
             S[L8 - 1] = _empty(M, HL, dev)
             ops.scale_cols(U[L8], HL, pk.w80p, S[L8 - 1], act_beta=sig_beta(lay, L8 - 1))
         QE = _empty(M, KE, dev) if sk >= 0 else None
@@ -389,12 +391,23 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
     M, dev = U[0].shape[0], U[0].device
     nl, sk, HL, KE = lay.n_lin, lay.skip, lay.HL, lay.KE
     L8 = nl - 1
-    img = _img_mode(pk)
+    img = _img_mode(pk, lay)
     Ub = st.get("Ub") or [None] * nl
     Sb = st.get("Sb") or [None] * (nl - 1)
     second = dG is not None
     if second and S is None:
         raise RuntimeError("SDF double backward needs the ∇ pass buffers (want_grad=True in forward)")
+
+    def s_fp32(l):
+        """s_l in fp32.  The bf16-mode forward with the folded head keeps s_7 as an image only; the paths
+        that read it in fp32 (a second-order term without dh, a weight-gradient pair whose Y is fp32)
+        rebuild it from the stored activation: s_7 = w80 ⊙ σ_7."""
+        if S[l] is None:
+            if l != L8 - 1:
+                raise RuntimeError(f"sdf_backward: s_{l} was not kept in fp32")
+            S[l] = _empty(M, HL, dev)
+            ops.scale_cols(U[L8], HL, pk.w80p, S[l], act_beta=sig_beta(lay, L8 - 1))
+        return S[l]
     i8 = lay.in_dim[L8]
     # dW8[0] = Σ_m dsdf U8 (+ Ud8) / scale: fused into the adjoint kernel on the folded-head path
     # (also on the sdf-only first-order path, e.g. the consistency re-query: Z_7 = dsdf w80 σ_7)
@@ -466,7 +479,7 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
             return {}
         # (bf16 mode: the images; the top layer's only on the elementwise path, top_img)
         img2 = (l < L8 - 1 or top_img) and Sb[l] is not None and Udb[l + 1] is not None
-        return dict(aux1=Sb[l] if img2 else S[l], aux2=Udb[l + 1] if img2 else Ud[l + 1],
+        return dict(aux1=Sb[l] if img2 else s_fp32(l), aux2=Udb[l + 1] if img2 else Ud[l + 1],
                     aux2_scale=lay.beta * (SQRT2 if (l + 1) == sk else 1.0))
 
     Z = _empty_b(M, HL, dev) if (z_img(L8 - 1) and (dh is not None or (sdf_only and fused_cs))) else _empty(M, HL, dev)
@@ -520,7 +533,7 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
         yb = Zl.dtype == torch.bfloat16
         xb = Ub[l] is not None and (not second or Udb[l] is not None)
         wq.add(Zl, Ub[l] if xb else U[l], lay.out_dim[l], lay.in_dim[l], dW, db=db,
-               Y1=(Sb[l] if yb else S[l]) if second else None, X1=(Udb[l] if xb else Ud[l]) if second else None,
+               Y1=(Sb[l] if yb else s_fp32(l)) if second else None, X1=(Udb[l] if xb else Ud[l]) if second else None,
                mode=wmode)
         dWs[l], dbs[l] = dW, db
     wq.flush()
@@ -770,7 +783,7 @@ class _ColorFieldFn(torch.autograd.Function):
         ext = _empty(M, lay.KX, dev)
         ops.color_extras(G, pts, dirs, dir_div, lay.multires_view, ext)
         H = []
-        img = _img_mode(pk)
+        img = _img_mode(pk, lay)
         A, A2, K1, K = feat, ext, lay.F, lay.F + lay.KX
         for l in range(lay.n_lin - 1):
             # bf16 mode: the hidden activations but the last are read only as GEMM operands (the next
@@ -809,7 +822,7 @@ class _ColorFieldFn(torch.autograd.Function):
         dbs[n - 1] = torch.empty(3, device=dev)
         # bf16 mode: the last hidden layer's adjoint as an operand image (read by the next adjoint GEMM
         # and a weight gradient only)
-        dZ = _empty_b(M, lay.HL, dev) if (_img_mode(pk) and n - 2 >= 1) else _empty(M, lay.HL, dev)
+        dZ = _empty_b(M, lay.HL, dev) if (_img_mode(pk, lay) and n - 2 >= 1) else _empty(M, lay.HL, dev)
         ops.rgb_head_bwd(drgb, rgb, H[-1], lay.in_dim[n - 1], pk.W3, dZ, dWs[n - 1], dbs[n - 1])
         wq = ops.WgradQueue()  # the 256x256 weight gradients: one launch after the chain
         for l in range(n - 2, 0, -1):
@@ -817,7 +830,7 @@ class _ColorFieldFn(torch.autograd.Function):
             db = torch.empty(lay.out_dim[l], device=dev)
             wq.add(dZ, H[l - 1], lay.out_dim[l], lay.in_dim[l], dW, db=db, mode=wmode)
             dWs[l], dbs[l] = dW, db
-            if _img_mode(pk) and l - 1 >= 1:  # dZ_{l-1}: read by the next adjoint GEMM and a weight gradient only
+            if _img_mode(pk, lay) and l - 1 >= 1:  # dZ_{l-1}: read by the next adjoint GEMM and a weight gradient only
                 dZp = _empty_b(M, lay.HL, dev)
                 ops.linear(dZ, pk.Bt[l], lay.out_dim[l - 1], rup(lay.out_dim[l], 32), None, EPI_BWD_RELU,
                            aux0=H[l - 1], nzero=lay.HL, out0_b=dZp)

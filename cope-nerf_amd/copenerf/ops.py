@@ -430,6 +430,11 @@ class WgradQueue(object):
     def flush(self):
         if not self.jobs:
             return
+        # the batch layout (each job's share of the CUs) and the stream are the jobs' device's
+        with torch.cuda.device(self.jobs[0][2][0].device):
+            self._flush()
+
+    def _flush(self):
         lib = _lib.load()
         n = len(self.jobs)
         arr = (_lib.WgradDesc * n)(*[d for d, _, _ in self.jobs])

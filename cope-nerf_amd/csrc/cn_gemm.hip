@@ -391,6 +391,14 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     }
     if (kDma && kHead) thb = sHeadW[TBLC];
     const bool epi_big = !kHead || p.out0 || p.out1 || p.out0_b || p.out1_b;  // (kDma) see the main loop
+    // (kDma) the ring's waits: chunk kc's pieces are done once at most the ops issued after them are
+    // outstanding -- DNS - 2 later chunks (4 pieces each), and for a tile's first DNS - 1 chunks after
+    // the first tile also the previous epilogue's >= kEpiMinVmem (a wait of at most 63: the counter)
+    constexpr int kRingWait = 4 * (DNS - 2);
+    constexpr int kEpiMinVmem = TM * 8 * TN;
+    constexpr int kEpiWait = kRingWait + kEpiMinVmem < 63 ? kRingWait + kEpiMinVmem : 63;
+    static_assert(!kDma || (kEpiWait > kRingWait && kRingWait + kEpiMinVmem >= kEpiWait),
+                  "the epilogue's memory operations must cover the wait past the ring's chunks");
     int gs = 0;             // (kDma) ring slot of the current tile's chunk 0
     bool gs_first = true;   // (kDma) the workgroup's first tile: no epilogue issued before its chunks
 
@@ -530,13 +538,13 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 // this wave's pieces of chunk kc landed.  vmcnt retires in issue order, so the wait
                 // counts what was issued after them: DNS - 2 later chunks (4 pieces each), and for
                 // the first DNS - 1 chunks of a tile after the first, the previous tile's epilogue
-                // too (>= 64 loads / stores per thread -- epi_big: the aux epilogues read 128 values,
-                // the others store 128 fp32 values or 64 image dwords, SOFTPLUS_HEAD may store
-                // neither): vmcnt(63) then, so the epilogue's stores are not drained first
+                // too (>= kEpiMinVmem loads / stores per wave -- epi_big: the aux epilogues read 128
+                // values, the others store 128 fp32 values or 64 image dwords, SOFTPLUS_HEAD may store
+                // neither): kEpiWait (63) then, so the epilogue's stores are not drained first
                 if (gs_first || !epi_big || kc >= DNS - 1)
-                    wait_vmcnt<4 * (DNS - 2)>();
+                    wait_vmcnt<kRingWait>();
                 else
-                    wait_vmcnt<63>();
+                    wait_vmcnt<kEpiWait>();
                 asm volatile("" ::: "memory");
                 __builtin_amdgcn_s_barrier();  // every wave's pieces landed; chunk kc - 1 consumed
                 asm volatile("" ::: "memory");
@@ -1125,11 +1133,15 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         };
         using T1 = std::true_type;
         using F0 = std::false_type;
+        // out0 or its image out0_b is present (host-checked): no instance without stores, so every
+        // epilogue issues at least TM * 8 * TN vector-memory operations per wave (one image dword per
+        // row pair and column block), which the LDS-DMA ring's vmcnt(63) relies on (kEpiMinVmem;
+        // tools/isa_check.py verifies it on the built ISA)
         auto run_direct_plain = [&]() {
             if (has_o0) {
                 if (has_b0) direct_plain(T1{}, T1{}); else direct_plain(T1{}, F0{});
             } else {
-                if (has_b0) direct_plain(F0{}, T1{}); else direct_plain(F0{}, F0{});  // (out0_b required then)
+                direct_plain(F0{}, T1{});
             }
         };
         auto run_direct_aux = [&]() {
@@ -1137,7 +1149,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 if (has_o0) {
                     if (has_b0) direct_aux(T1{}, T1{}, spl); else direct_aux(T1{}, F0{}, spl);
                 } else {
-                    if (has_b0) direct_aux(F0{}, T1{}, spl); else direct_aux(F0{}, F0{}, spl);
+                    direct_aux(F0{}, T1{}, spl);
                 }
             };
             if constexpr (EPI == CN_EPI_MUL) {

@@ -910,23 +910,25 @@ __global__ void __launch_bounds__(512, 2) wgrad_b16d_kernel(WgradBatch batch) {
     const int64_t src1 = p.npairs > 1 ? ufirst(reinterpret_cast<int64_t>(reinterpret_cast<const bf16_t*>(sx ? p.X1 : p.Y1) +
                                                                          (int64_t)mbeg * ld1 + col0))
                                       : src0;
-    const int bytes0 = mend > mbeg ? ((mend - mbeg) * ld0 - col0) * 2 : 0;
-    const int bytes1 = mend > mbeg && p.npairs > 1 ? ((mend - mbeg) * ld1 - col0) * 2 : 0;
+    const int slice_rows = mend - mbeg;
     const int drow = (lane >> 5), dch = lane & 31;
     auto issue = [&](int c) {  // stage c (or zeros past the last: an empty view) into buffer c % NS
         const bool valid = c < total;
         const int pair = valid && c >= nch;
         const int r0 = valid ? (c - pair * nch) * MC : 0;
         const int ld = pair ? ld1 : ld0;
-        const int bytes = __builtin_amdgcn_readfirstlane(valid ? (pair ? bytes1 : bytes0) : 0);
-        const rsrc_t v = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(pair ? src1 : src0), 0, bytes,
-                                                           0x00020000);
+        // a view per chunk, based at its first row: rows past the slice's end read as zero, and no
+        // byte count or offset spans the slice (int32-safe at any rows_per_slice)
+        const int nrow = valid ? min(MC, slice_rows - r0) : 0;
+        const int bytes = __builtin_amdgcn_readfirstlane(nrow > 0 ? (nrow * ld - col0) * 2 : 0);
+        const int64_t base = (pair ? src1 : src0) + (int64_t)r0 * ld * 2;
+        const rsrc_t v = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), 0, bytes, 0x00020000);
         char* dst = smem + (c % NS) * STAGE + (sx ? SIDE : 0) + wq * 8 * ROWB;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int row = wq * 8 + 2 * j + drow;
             const int ch = dch ^ ((row & 3) << 2);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(v, (lds_void*)(dst + j * 1024), 16, (r0 + row) * ld * 2 + ch * 16,
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(v, (lds_void*)(dst + j * 1024), 16, row * ld * 2 + ch * 16,
                                                      0, 0, 0);
         }
     };

@@ -123,3 +123,31 @@ def test_render_bf16_mode_against_fp32_oracle():
     loss.backward()
     for p in list(sdf.parameters()) + list(col.parameters()):
         assert p.grad is not None and torch.isfinite(p.grad).all()
+
+
+def test_sdf_field_bf16_mode_narrow_width():
+    """bf16 mode at a hidden width that is not 256-padded (d_hidden = 64: 128-wide buffers): the
+    operand images stay off (their weight gradients need the 256x256 ring), fp32 operands are
+    rounded on load; the field and a double-backward loss's parameter gradients against the fp32
+    mode within bf16 rounding."""
+    from copenerf import SDFNetwork, fields
+    from helpers import SDF_CFG
+    torch.manual_seed(5)
+    net = SDFNetwork(**dict(SDF_CFG, d_hidden=64)).to(DEV)
+    lay = net.layout()
+    x = torch.rand(3001, 4, device=DEV) * 2 - 1
+    res = []
+    for mode in ("bf16", "fp32"):
+        net.mfma_dtype = mode
+        if mode == "bf16":
+            assert not fields._img_mode(net.params_and_pack()[2], lay)
+        sdf, feat, g = net.field(x)
+        loss = ((g.norm(dim=-1) - 1) ** 2).mean() + sdf.abs().mean() + 1e-2 * feat.square().mean()
+        grads = torch.autograd.grad(loss, list(net.parameters()))
+        res.append([sdf.detach(), g.detach()] + list(grads))
+    names = ["sdf", "grad"] + [n for n, _ in net.named_parameters()]
+    for n, a, b in zip(names, res[0], res[1]):
+        assert torch.isfinite(a).all(), n
+        rel = ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+        print(f"{n}: relative L2 {rel:.2e}")
+        assert rel <= 5e-2, (n, rel)

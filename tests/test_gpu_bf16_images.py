@@ -185,6 +185,59 @@ def test_bf16_concat_image_and_head():
     assert torch.equal(sb2, sb) and torch.equal(sdf3, sdf)
 
 
+def test_bf16_dma_tile_across_tiles_bitwise():
+    """The LDS-DMA ring of the 256x256 bf16 tile (image A) with more 256-row tiles than CUs, so every
+    workgroup runs several tiles and the ring's stages cross tile boundaries (the next tile's first
+    chunks under the previous tile's epilogue, its vmcnt(63) wait): the image-only epilogues with the
+    fewest memory operations per wave -- STORE / SOFTPLUS (64 image dwords), MUL with its split
+    output, SOFTPLUS_HEAD storing only the ∇-pass seed's image, and with no output at all (the
+    sampler's sdf-only launch) -- bitwise equal to the 128x128 register-staged tile."""
+    from copenerf import _lib, ops
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    M, N, K = 2 * 256 * cus + 37, 256, 256
+    A = _rnd(M, K, seed=51, scale=0.3).bfloat16()
+    Bb = _rnd(N, K, seed=52, scale=0.06).bfloat16().contiguous()
+    bias = _rnd(N, seed=53, scale=0.3)
+    d = _lib.LinearDesc()
+    d.M, d.N, d.K, d.K1, d.ldb, d.epilogue, d.tile, d.mfma_dtype, d.a_bf16 = M, N, K, K, K, ops.EPI_STORE, 0, 1, 1
+    assert ", 2, 4, 32, " in ops.kernel_name(_lib.load().cn_linear_kernel_name, d)
+    aux0 = torch.nn.functional.softplus(_rnd(M, 256, seed=54, scale=0.05), beta=100).bfloat16()
+    for name, epi, kw in (("store", ops.EPI_STORE, dict(bias=bias)), ("softplus", ops.EPI_SOFTPLUS, dict(bias=bias)),
+                          ("mul_split", ops.EPI_MUL, dict(aux0=aux0, aux_beta=100.0, nsplit=204, adiv=ops.SQRT2))):
+        outs = []
+        for tile in (0, 2):
+            k2 = dict(kw)
+            split = None
+            if "nsplit" in k2:
+                split = torch.full((M, 64), float("nan"), device=DEV)
+                k2["out_split"] = split
+            ob = torch.full((M, 256), float("nan"), device=DEV).bfloat16()
+            ops.linear(A, Bb, N, K, None, epi, nzero=256, tile=tile, out0_b=ob, **k2)
+            outs.append((ob, split))
+        assert torch.equal(outs[0][0], outs[1][0]), name
+        if outs[0][1] is not None:
+            assert torch.equal(torch.nan_to_num(outs[0][1], 7.0), torch.nan_to_num(outs[1][1], 7.0)), name
+    # SOFTPLUS_HEAD spans whole rows only on the 256-wide tile: the reference is the same kernel over
+    # row blocks of at most one tile per workgroup (rows are independent)
+    hw, hb, colv = _rnd(N, seed=55), _rnd(1, seed=56), _rnd(N, seed=57)
+    step = 256 * (cus // 2)
+    for seed_only in (True, False):
+        res = []
+        for blocks in (False, True):
+            sdf = torch.full((M,), float("nan"), device=DEV)
+            sb = torch.full((M, 256), float("nan"), device=DEV).bfloat16() if seed_only else None
+            for r0 in (range(0, M, step) if blocks else [0]):
+                r1 = min(M, r0 + step) if blocks else M
+                ops.linear(A[r0:r1], Bb, N, K, None, ops.EPI_SOFTPLUS_HEAD, bias=bias,
+                           colv=colv if seed_only else None, aux_beta=100.0, head_w=hw, head_b=hb,
+                           head_out=sdf[r0:r1], out1_b=sb[r0:r1] if seed_only else None)
+            res.append((sdf, sb))
+        assert not torch.isnan(res[0][0]).any()
+        assert torch.equal(res[0][0], res[1][0]), seed_only
+        if seed_only:
+            assert torch.equal(res[0][1], res[1][1])
+
+
 @pytest.mark.parametrize("M,pairs", [(70001, 2), (4097, 1), (33, 2)])
 def test_wgrad_bf16_ring_images(M, pairs):
     """The bf16 stage-ring weight gradient from fp32 operands and from their bf16 images: dW bitwise
@@ -242,7 +295,7 @@ def test_sdf_field_bf16_images_match_fp32_operand_path():
     saved = fields._img_mode
     try:
         for img in (True, False):
-            fields._img_mode = (lambda pk: saved(pk)) if img else (lambda pk: False)
+            fields._img_mode = (lambda pk, lay: saved(pk, lay)) if img else (lambda pk, lay: False)
             sdf, feat, g = net.field(x)
             loss = ((g.norm(dim=-1) - 1) ** 2).mean() + sdf.abs().mean() + 1e-2 * feat.square().mean()
             grads = torch.autograd.grad(loss, list(net.parameters()))
@@ -281,7 +334,7 @@ def test_color_bf16_images_match_fp32_operand_path():
     saved = fields._img_mode
     try:
         for img in (True, False):
-            fields._img_mode = (lambda pk: saved(pk)) if img else (lambda pk: False)
+            fields._img_mode = (lambda pk, lay: saved(pk, lay)) if img else (lambda pk, lay: False)
             rgb = net(pts, nrm, dirs, feat)
             loss = (rgb * torch.linspace(0.5, 1.5, 3, device=DEV)).square().sum()
             grads = torch.autograd.grad(loss, [pts, nrm, dirs, feat] + list(net.parameters()))
