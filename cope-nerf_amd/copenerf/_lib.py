@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libcopenerf.so"
 LIB_PATH = os.environ.get("COPENERF_LIB", os.path.join(_HERE, LIB_NAME))
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 c_f32p = ctypes.c_void_p  # device pointers are passed as integers
 c_i32 = ctypes.c_int32
@@ -74,6 +74,17 @@ class PackJob(ctypes.Structure):
         ("src", c_ptr), ("dst", c_ptr), ("src_ld", c_i64), ("dst_ld", c_i64),
         ("rows", c_i32), ("cols", c_i32), ("r0", c_i32), ("r1", c_i32), ("c0", c_i32), ("c1", c_i32),
         ("transpose", c_i32), ("format", c_i32),
+    ]
+
+
+class SdfMlpDesc(ctypes.Structure):
+    _fields_ = [
+        ("u0", c_ptr), ("tail", c_ptr), ("ld_u0", c_i64), ("ld_t", c_i64),
+        ("M", c_i32), ("n_layers", c_i32), ("hidden", c_i32), ("kpad0", c_i32), ("multires", c_i32),
+        ("skip_layer", c_i32),
+        ("W", c_ptr * 8), ("ldw", c_i64 * 8), ("bias", c_ptr * 8),
+        ("head_w", c_ptr), ("head_b", c_ptr), ("sdf", c_ptr), ("idx", c_ptr),
+        ("skip_div", c_f32), ("beta", c_f32), ("threshold", c_f32),
     ]
 
 
@@ -136,6 +147,7 @@ SIGNATURES = {
                               c_ptr]),
     "cn_mat4_chain_fwd": (c_i32, [c_i32, c_ptr, c_ptr, c_ptr]),
     "cn_mat4_chain_bwd": (c_i32, [c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr]),
+    "cn_sdf_mlp": (c_i32, [ctypes.POINTER(SdfMlpDesc), c_ptr]),
 }
 
 _lock = threading.Lock()

@@ -216,6 +216,37 @@ def _act(U, Ub, l):
     return U[l] if U[l] is not None else Ub[l]
 
 
+# The no-grad SDF query (the sampler's, neus_renderer.py:492-525) in one launch in the bf16 mode
+# (cn_sdf_mlp: activations on chip, bitwise equal to the layer-by-layer path); False: layer by layer
+FUSED_SDF_QUERY = True
+
+
+def _fused_query_ok(lay: SDFLayout, pk: SDFPack) -> bool:
+    """cn_sdf_mlp's shape: 8 hidden layers of 256 (the skip layer 256 - E), K0 = 64, bf16 images."""
+    if not (FUSED_SDF_QUERY and _img_mode(pk, lay) and lay.n_lin == 9 and lay.HL == 256 and lay.KE == 64):
+        return False
+    sk = lay.skip
+    if not (2 <= sk <= 7 and lay.E + lay.out_dim[sk - 1] == 256):
+        return False
+    return all(lay.out_dim[l] == 256 for l in range(8) if l != sk - 1) and lay.out_dim[8] >= 1 and \
+        all(pk.Bf[l].shape[0] == 256 for l in range(8)) and lay.in_dim[8] == 256
+
+
+def sdf_query_fused(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, sdf_out: Optional[torch.Tensor] = None,
+                    dst: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """SDFNetwork.sdf(x) with no gradient (neus_fields.py:268-283) in two launches: cn_sdf_embed writes the
+    embedding's bf16 images (lin0's input, the skip concat's tail / sqrt 2), cn_sdf_mlp runs lin0 .. lin7 and
+    the sdf head with the activations on chip."""
+    M, dev = x.shape[0], x.device
+    u0b = _empty_b(M, lay.KE, dev)
+    tail = _empty_b(M, 64, dev)
+    ops.sdf_embed(x, lay.multires, lay.scale, u0b, tail[:, :lay.E], SQRT2)
+    sdf = sdf_out if sdf_out is not None else _empty(M, 1, dev)
+    ops.sdf_mlp(u0b, tail[:, :lay.E], pk.Bf[:8], pk.b[:8], pk.w80[0], pk.b80, sdf, multires=lay.multires,
+                skip_layer=lay.skip - 1, skip_div=SQRT2, beta=lay.beta, threshold=lay.threshold, idx=dst)
+    return sdf
+
+
 def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool, want_grad: bool, keep: bool,
                 sdf_out: Optional[torch.Tensor] = None, dst: Optional[torch.Tensor] = None):
     """Forward of SDFNetwork (neus_fields.py:268-283) and, with want_grad, the
@@ -235,6 +266,9 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
     read them as A, the weight gradients as X, and MUL / TANGENT / BWD_SOFTPLUS recover σ from them.
     """
     M, dev = x.shape[0], x.device
+    if want_feat is False and not want_grad and not keep and _fused_query_ok(lay, pk):
+        return {"U": None, "Ub": None, "S": None, "Sb": None, "sdf": sdf_query_fused(lay, pk, x, sdf_out, dst),
+                "feat": None, "G": None}
     nl, sk, HL, KE = lay.n_lin, lay.skip, lay.HL, lay.KE
     keep_u = keep or want_grad
     img = _img_mode(pk, lay)

@@ -525,13 +525,55 @@ def colsum(X, K, out, *, w=None, wdiv=1.0, accumulate=False):
 
 
 def sdf_embed(x, multires, scale, U0, U4e=None, u4div=1.0):
-    """U0 = the encoding of x; U4e (fp32, or a bfloat16 operand image) = its first columns / u4div."""
+    """U0 = the encoding of x; U4e = its first columns / u4div; each fp32 or a bfloat16 operand image."""
     _need(x, "x")
     _need(U0, "U0")
     _need(U4e, "U4e")
+    flags = int(U4e is not None and U4e.dtype == torch.bfloat16) | (2 if U0.dtype == torch.bfloat16 else 0)
     _lib.call("cn_sdf_embed", x.shape[0], _ptr(x), _ld(x), multires, scale, U0.shape[1], _ptr(U0), _ld(U0),
-              _ptr(U4e), _ld(U4e), u4div, int(U4e is not None and U4e.dtype == torch.bfloat16), _stream())
+              _ptr(U4e), _ld(U4e), u4div, flags, _stream())
     return U0
+
+
+def sdf_mlp(u0b, tail, Ws, biases, head_w, head_b, sdf, *, multires, skip_layer, skip_div, beta, threshold,
+            idx=None):
+    """The sampler's SDF query in one launch (cn_sdf_mlp, bf16 mode): sdf[idx[m] or m] from the embedding's
+    bf16 images u0b [M, 64] and tail [M, >= E] through lin0 .. lin7 (bf16 weight images [256][K]) and the
+    head row.  Raises if the library does not support the network's shape."""
+    for t, n in ((u0b, "u0b"), (tail, "tail")):
+        _need(t, n)
+        if t.dtype != torch.bfloat16:
+            raise RuntimeError(f"sdf_mlp: {n} must be a bfloat16 image")
+    if len(Ws) != 8 or len(biases) != 8:
+        raise RuntimeError("sdf_mlp: 8 hidden layers")
+    d = _lib.SdfMlpDesc()
+    d.u0, d.tail, d.ld_u0, d.ld_t = _ptr(u0b), _ptr(tail), _ld(u0b), _ld(tail)
+    d.M, d.n_layers, d.hidden, d.kpad0 = u0b.shape[0], 8, Ws[1].shape[0], Ws[0].shape[1]
+    d.multires, d.skip_layer = multires, skip_layer
+    for i, (W, b) in enumerate(zip(Ws, biases)):
+        _need(W, f"W{i}")
+        if W.dtype != torch.bfloat16 or W.shape[0] != 256 or not b.is_contiguous() or b.dtype != torch.float32:
+            raise RuntimeError(f"sdf_mlp: layer {i} needs a bf16 [256][K] weight image and an fp32 bias")
+        d.W[i], d.ldw[i], d.bias[i] = W.data_ptr(), W.stride(0), b.data_ptr()
+    if not (head_w.is_contiguous() and head_w.numel() >= 256 and head_b.numel() >= 1):
+        raise RuntimeError("sdf_mlp: head_w [256], head_b [1]")
+    if not sdf.is_contiguous() or (idx is None and sdf.numel() < u0b.shape[0]):
+        raise RuntimeError("sdf_mlp: sdf must be contiguous with M entries (or idx)")
+    if idx is not None and (idx.dtype != torch.int32 or idx.numel() < u0b.shape[0]):
+        raise RuntimeError("sdf_mlp: idx must be int32 with M entries")
+    d.head_w, d.head_b, d.sdf, d.idx = head_w.data_ptr(), head_b.data_ptr(), sdf.data_ptr(), _ptr(idx)
+    d.skip_div, d.beta, d.threshold = skip_div, beta, threshold
+    if _timer is not None:
+        e0 = _timer.start()
+        _lib.check(_lib.load().cn_sdf_mlp(d, _stream()), "cn_sdf_mlp")
+        M = u0b.shape[0]
+        ka = [W.shape[1] for W in Ws]
+        fl = sum(2.0 * M * 256 * k for k in ka)
+        _timer.symbols[("sdf_mlp",)] = "cn::sdf_mlp_kernel(cn::SdfMlpArgs)"
+        _timer.stop(("sdf_mlp",), e0, fl, 2.0 * M * (64 + tail.shape[1]) + 4.0 * M)
+    else:
+        _lib.check(_lib.load().cn_sdf_mlp(d, _stream()), "cn_sdf_mlp")
+    return sdf
 
 
 def sdf_grad_assemble(multires, scale, U0, Q0, QE, G):

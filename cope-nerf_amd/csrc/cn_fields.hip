@@ -24,14 +24,14 @@ __device__ __forceinline__ void st4_tail(void* base, bool bf16, int64_t m, int64
 }
 
 __global__ void sdf_embed_kernel(int M, const float* __restrict__ x, int64_t ldx, int L, float scale, int G,
-                                 float* U0, int64_t ld_u0, void* U4e, int64_t ld_u4, float u4div, bool u4b) {
+                                 void* U0, int64_t ld_u0, bool u0b, void* U4e, int64_t ld_u4, float u4div, bool u4b) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t m = idx / G;
     const int g = idx % G;
     if (m >= M) return;
     const floatx4 o = sdf_embed_group(ld4(x + m * ldx), g, L, scale);
     const int ng = 1 + 2 * L;
-    st4(U0 + m * ld_u0 + 4 * g, o);
+    st4_tail(U0, u0b, m, ld_u0, g, o);
     if (U4e && g < ng) {
         floatx4 q;
         for (int c = 0; c < 4; ++c) q[c] = o[c] / u4div;
@@ -197,18 +197,20 @@ static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 using namespace cn;
 
 extern "C" int cn_sdf_embed(int32_t M, const float* x, int64_t ldx, int32_t multires, float scale, int32_t kpad,
-                            float* U0, int64_t ld_u0, void* U4e, int64_t ld_u4, float u4_scale, int32_t u4_bf16,
+                            void* U0, int64_t ld_u0, void* U4e, int64_t ld_u4, float u4_scale, int32_t flags,
                             cn_stream_t stream) {
     CN_REQUIRE(x && U0, CN_ERR_ARG, "cn_sdf_embed: null pointer");
     CN_REQUIRE(multires >= 0 && 4 * (1 + 2 * multires) <= kpad && kpad % 4 == 0 && ld_u0 >= kpad && multires < 16,
                CN_ERR_SHAPE, "cn_sdf_embed: multires=%d kpad=%d ld_u0=%lld", multires, kpad, (long long)ld_u0);
-    CN_REQUIRE(al16(x) && al16(U0) && ldx % 4 == 0 && ld_u0 % 4 == 0 && (!U4e || (((uintptr_t)U4e & 7) == 0 && ld_u4 % 4 == 0)),
+    const bool u0b = (flags & 2) != 0;
+    CN_REQUIRE(al16(x) && ((uintptr_t)U0 & (u0b ? 7 : 15)) == 0 && ldx % 4 == 0 && ld_u0 % 4 == 0 &&
+                   (!U4e || (((uintptr_t)U4e & 7) == 0 && ld_u4 % 4 == 0)),
                CN_ERR_ALIGN, "cn_sdf_embed: alignment");
     if (M == 0) return CN_OK;
     const int G = kpad / 4;
     const int64_t tot = (int64_t)M * G;
     sdf_embed_kernel<<<(int)((tot + 255) / 256), 256, 0, (hipStream_t)stream>>>(
-        M, x, ldx, multires, scale, G, U0, ld_u0, U4e, ld_u4, u4_scale == 0.f ? 1.f : u4_scale, u4_bf16 != 0);
+        M, x, ldx, multires, scale, G, U0, ld_u0, u0b, U4e, ld_u4, u4_scale == 0.f ? 1.f : u4_scale, (flags & 1) != 0);
     return check_launch("cn_sdf_embed");
 }
 

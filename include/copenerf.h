@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define CN_ABI_VERSION 10
+#define CN_ABI_VERSION 11
 
 typedef void* cn_stream_t; /* hipStream_t */
 
@@ -304,11 +304,12 @@ int cn_softplus_adjoint(int32_t M, int32_t N, const void* D, int64_t ldd, const 
  * neus_fields.py:269-271 to x*scale):
  *   U0[m][0..4+8*multires) = embed(scale * x[m][0..4)),  zeros up to kpad.
  *   If U4e != NULL also U4e[m][j] = U0[m][j] / u4_scale (the skip-connection
- *   copy of neus_fields.py:276-277); u4_bf16 (ABI v10): U4e is a bf16 operand
- *   image (RNE; ld_u4 in bf16 elements, 8-byte aligned).
+ *   copy of neus_fields.py:276-277).  flags bit 0 (ABI v10): U4e is a bf16
+ *   operand image (RNE; ld_u4 in bf16 elements, 8-byte aligned); bit 1 (ABI
+ *   v11): U0 is one too (the operand of cn_sdf_mlp; 8-byte aligned).
  * ------------------------------------------------------------------------ */
 int cn_sdf_embed(int32_t M, const float* x, int64_t ldx, int32_t multires, float scale, int32_t kpad,
-                 float* U0, int64_t ld_u0, void* U4e, int64_t ld_u4, float u4_scale, int32_t u4_bf16,
+                 void* U0, int64_t ld_u0, void* U4e, int64_t ld_u4, float u4_scale, int32_t flags,
                  cn_stream_t stream);
 
 /* ∇ₓSDF from the embedding adjoint: G[m][i] = scale * J_embed(x)ᵀ (Q0[m] + QE[m])
@@ -491,6 +492,45 @@ int cn_stage1_bwd(int32_t R, int32_t S, const float* pts, int64_t ld_p, const fl
  * adjoint: dA from dC (every C_j may carry a gradient).  One lane walks the chain. */
 int cn_mat4_chain_fwd(int32_t n, const float* A, float* C, cn_stream_t stream);
 int cn_mat4_chain_bwd(int32_t n, const float* A, const float* C, const float* dC, float* dA, cn_stream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * The sampler's SDF query in one launch (ABI v11): SDFNetwork.sdf(x) with no
+ * gradient, as NeuSRenderer.up_sample calls it (model/neus_renderer.py:492-525,
+ * the coarse samples and each round's new ones; neus_fields.py:268-283) -- eight
+ * softplus layers with the skip concat and the sdf row of the last Linear -- for
+ * the bf16 MLP MFMA mode (config C3), from the embedding's bf16 images that
+ * cn_sdf_embed writes (flags 3).  Activations stay on chip: per sample 128 + 2E
+ * bytes are read and the sdf (4 B) written.  Bitwise equal to the
+ * layer-by-layer bf16 path (cn_linear on bf16 weight images, SOFTPLUS /
+ * SOFTPLUS_HEAD epilogues).
+ *   u0      [M][ld_u0] bf16: the embedding, 64 columns (lin0's input; zero past E),
+ *           ld_u0 % 8 == 0, 16-byte aligned;
+ *   tail    [M][ld_t] bf16: the embedding / skip_div, E = 4 (1 + 2 multires)
+ *           columns (the skip concat's tail), ld_t % 4 == 0, 8-byte aligned;
+ *   W[l]    bf16 weight images [256][ldw[l]] of lin0 .. lin7, K = 64 (lin0) or 256,
+ *           rows past a layer's width zero (as cn_pack_weights builds them);
+ *   bias[l] fp32 [width]; the skip layer (feeding the skip concat) has width
+ *           256 - E, its output divided by skip_div;
+ *   head_w  [256] = lin8.weight[0] / scale, head_b [1] = lin8.bias[0] / scale;
+ *   sdf     written at idx[m] (idx NULL: m).
+ * Supported: n_layers 8, hidden 256, kpad0 64, multires <= 7; else
+ * CN_ERR_UNSUPPORTED (the caller composes cn_linear launches instead).
+ * ------------------------------------------------------------------------ */
+typedef struct cn_sdf_mlp_desc {
+    const void* u0;   /* bf16 */
+    const void* tail; /* bf16 */
+    int64_t ld_u0, ld_t;
+    int32_t M, n_layers, hidden, kpad0, multires, skip_layer;
+    const void* W[8]; /* bf16 */
+    int64_t ldw[8];
+    const float* bias[8];
+    const float* head_w;
+    const float* head_b;
+    float* sdf;
+    const int32_t* idx;
+    float skip_div, beta, threshold;
+} cn_sdf_mlp_desc;
+int cn_sdf_mlp(const cn_sdf_mlp_desc* d, cn_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -34,7 +34,8 @@ def test_library_exports_every_declared_symbol():
 def test_struct_layouts_match_header_order():
     from copenerf import _lib
     src = open(HEADER).read()
-    for cname, py in (("cn_linear_desc", _lib.LinearDesc), ("cn_wgrad_desc", _lib.WgradDesc)):
+    for cname, py in (("cn_linear_desc", _lib.LinearDesc), ("cn_wgrad_desc", _lib.WgradDesc),
+                      ("cn_sdf_mlp_desc", _lib.SdfMlpDesc)):
         body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (cname, cname), src, re.S).group(1)
         body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
         names = []
@@ -43,7 +44,7 @@ def test_struct_layouts_match_header_order():
             if not decl:
                 continue
             decl = re.sub(r"^(const\s+)?\w+\s*\**", "", decl)
-            names += [n.strip(" *") for n in decl.split(",")]
+            names += [re.sub(r"\[\d+\]", "", n.strip(" *")) for n in decl.split(",")]
         assert names == [f[0] for f in py._fields_], (cname, names)
     assert ctypes.sizeof(_lib.LinearDesc) % 8 == 0
 
@@ -97,6 +98,13 @@ def test_argument_validation_without_gpu():
                                    1, 9, None, None, 1.0, None, 0, None) == -1
     assert b"3-bit mask" in lib.cn_last_error()
     assert lib.cn_rgb_head_bwd(8, 256, 16, 16, 16, 256, 16, 18, 256, 1, 16, 16, 16, 1 << 20, None) == -3
+    # ABI v11: the fused sampler query takes the 8 x 256 SDF network only
+    assert lib.cn_sdf_mlp(None, None) == -1
+    m = _lib.SdfMlpDesc()
+    m.u0 = m.tail = m.sdf = m.head_w = m.head_b = 16
+    m.n_layers, m.hidden, m.kpad0 = 8, 128, 64
+    assert lib.cn_sdf_mlp(ctypes.byref(m), None) == -5
+    assert b"8 x 256" in lib.cn_last_error()
 
 
 def test_product_path_refuses_cpu_tensors():

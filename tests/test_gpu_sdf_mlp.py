@@ -1,0 +1,96 @@
+"""cn_sdf_mlp, the sampler's no-grad SDF query in one launch (bf16 mode, config C3), against the
+layer-by-layer bf16 path it replaces (cn_sdf_embed + nine cn_linear launches on the same weight
+images): bitwise equal sdf values -- ragged row counts, more row blocks than CUs (the weight ring and
+the persistent loop across blocks), the scattered head (the sampler's merged slots), a perturbed
+network (no geometric-init symmetry) -- and the sampler's z-values through NeuSRenderer.sample_z."""
+import pytest
+import torch
+
+from helpers import REN_CFG, SDF_CFG, build_modules
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _net(seed):
+    from copenerf import SDFNetwork
+    torch.manual_seed(seed)
+    net = SDFNetwork(**SDF_CFG).to(DEV)
+    with torch.no_grad():  # off the geometric init: every layer's weights matter
+        for p in net.parameters():
+            p.add_(0.02 * torch.randn_like(p))
+    net.mfma_dtype = "bf16"
+    return net
+
+
+def _query(net, x, fused, sdf_out=None, dst=None):
+    from copenerf import fields
+    saved = fields.FUSED_SDF_QUERY
+    fields.FUSED_SDF_QUERY = fused
+    try:
+        with torch.no_grad():
+            Ws, bs, pk = net.params_and_pack()
+            st = fields.sdf_forward(net.layout(), pk, x, want_feat=False, want_grad=False, keep=False,
+                                    sdf_out=sdf_out, dst=dst)
+        return st["sdf"]
+    finally:
+        fields.FUSED_SDF_QUERY = saved
+
+
+@pytest.mark.parametrize("M", [1, 255, 4099, 2 * 256 * 256 + 77])
+def test_fused_query_bitwise_equals_layer_by_layer(M):
+    from copenerf import fields
+    net = _net(3)
+    assert fields._fused_query_ok(net.layout(), net.params_and_pack()[2])
+    g = torch.Generator(device=DEV).manual_seed(M)
+    x = torch.rand(M, 4, device=DEV, generator=g) * 2.4 - 1.2
+    a = _query(net, x, True)
+    b = _query(net, x, False)
+    assert torch.isfinite(a).all()
+    assert torch.equal(a, b), (a - b).abs().max().item()
+
+
+def test_fused_query_scatter_and_fallbacks():
+    """The head's scatter into the merged slots (head_idx), and the shapes the kernel does not take
+    (the 64-wide network, the fp32-class modes) going layer by layer."""
+    from copenerf import SDFNetwork, fields
+    net = _net(5)
+    M = 70001
+    x = torch.rand(M, 4, device=DEV) * 2 - 1
+    dst = torch.randperm(2 * M, device=DEV)[:M].to(torch.int32)
+    a = _query(net, x, True, sdf_out=torch.full((2 * M,), float("nan"), device=DEV), dst=dst)
+    b = _query(net, x, False, sdf_out=torch.full((2 * M,), float("nan"), device=DEV), dst=dst)
+    assert torch.equal(torch.nan_to_num(a, 9.0), torch.nan_to_num(b, 9.0))
+    assert not torch.isnan(a[dst.long()]).any()
+    narrow = SDFNetwork(**dict(SDF_CFG, d_hidden=64)).to(DEV)
+    narrow.mfma_dtype = "bf16"
+    assert not fields._fused_query_ok(narrow.layout(), narrow.params_and_pack()[2])
+    net.mfma_dtype = "bf16x6"
+    assert not fields._fused_query_ok(net.layout(), net.params_and_pack()[2])
+
+
+def test_sampler_z_values_fused_equal_layer_by_layer():
+    """NeuSRenderer.sample_z (coarse 64 + 4 rounds of 16, the C3 sample counts) with the fused query
+    and layer by layer: the same z-values bit for bit (the importance samples follow the sdf)."""
+    from copenerf import NeuSRenderer, fields
+    sdf, col, dev = build_modules(21, device=DEV)
+    with torch.no_grad():
+        for p in sdf.parameters():
+            p.add_(0.01 * torch.randn_like(p))
+    r = NeuSRenderer(None, sdf, dev, col, None, **dict(REN_CFG, n_importance=64)).to(DEV).set_mfma_dtype("bf16")
+    R = 4096
+    g = torch.Generator(device=DEV).manual_seed(7)
+    o = torch.zeros(R, 3, device=DEV)
+    d = torch.cat([(torch.rand(R, 2, device=DEV, generator=g) - 0.5), -torch.ones(R, 1, device=DEV)], -1)
+    d = d / d.norm(dim=-1, keepdim=True)
+    near, far = torch.full((R, 1), 0.01, device=DEV), torch.full((R, 1), 3.0, device=DEV)
+    t = torch.zeros(1, device=DEV)
+    t_rand = torch.rand(R, 64, device=DEV, generator=g)
+    zs = []
+    for fused in (True, False):
+        fields.FUSED_SDF_QUERY = fused
+        try:
+            zs.append(r.sample_z(o, d, t, near, far, 64, 64, t_rand, sdf.params_and_pack()))
+        finally:
+            fields.FUSED_SDF_QUERY = True
+    assert torch.equal(zs[0], zs[1])
