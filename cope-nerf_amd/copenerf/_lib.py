@@ -84,7 +84,7 @@ class SdfMlpDesc(ctypes.Structure):
         ("skip_layer", c_i32),
         ("W", c_ptr * 8), ("ldw", c_i64 * 8), ("bias", c_ptr * 8),
         ("head_w", c_ptr), ("head_b", c_ptr), ("sdf", c_ptr), ("idx", c_ptr),
-        ("skip_div", c_f32), ("beta", c_f32), ("threshold", c_f32),
+        ("skip_div", c_f32), ("beta", c_f32), ("threshold", c_f32), ("debug", c_ptr),
     ]
 
 

@@ -536,7 +536,7 @@ def sdf_embed(x, multires, scale, U0, U4e=None, u4div=1.0):
 
 
 def sdf_mlp(u0b, tail, Ws, biases, head_w, head_b, sdf, *, multires, skip_layer, skip_div, beta, threshold,
-            idx=None):
+            idx=None, debug=None):
     """The sampler's SDF query in one launch (cn_sdf_mlp, bf16 mode): sdf[idx[m] or m] from the embedding's
     bf16 images u0b [M, 64] and tail [M, >= E] through lin0 .. lin7 (bf16 weight images [256][K]) and the
     head row.  Raises if the library does not support the network's shape."""
@@ -563,6 +563,7 @@ def sdf_mlp(u0b, tail, Ws, biases, head_w, head_b, sdf, *, multires, skip_layer,
         raise RuntimeError("sdf_mlp: idx must be int32 with M entries")
     d.head_w, d.head_b, d.sdf, d.idx = head_w.data_ptr(), head_b.data_ptr(), sdf.data_ptr(), _ptr(idx)
     d.skip_div, d.beta, d.threshold = skip_div, beta, threshold
+    d.debug = _ptr(debug)  # tests: bf16 [8][M][256], every layer's input
     if _timer is not None:
         e0 = _timer.start()
         _lib.check(_lib.load().cn_sdf_mlp(d, _stream()), "cn_sdf_mlp")

@@ -63,8 +63,10 @@ struct SdfMlpArgs {
     const int* idx;                   // scatter: sdf[idx[m]] (or NULL: sdf[m])
     int skip_layer;                   // the layer whose columns >= nout carry the tail
     float beta, threshold;
+    bf16_t* dbg;                      // (DBG) every layer's input, [8][M][256] natural feature order
 };
 
+template <bool DBG>
 __global__ void __launch_bounds__(256, 1) sdf_mlp_kernel(SdfMlpArgs p) {
     __shared__ __attribute__((aligned(16))) char smem[kMlpNS * kMlpChunk + kMlpLayers * 256 * 4 + 256 * 4];
     float* sBias = reinterpret_cast<float*>(smem + kMlpNS * kMlpChunk);
@@ -134,6 +136,19 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_kernel(SdfMlpArgs p) {
 
     bf16x8 bq[2][16];  // the current layer's input: [sample block][k-step], B-operand order
     floatx16 acc[8][2];
+    // (DBG) layer l's input as the B operand holds it: lane half h of k-step ks = features 16 ks + 8 h ..
+    auto dump = [&](int l, int nks) __attribute__((always_inline)) {
+        if constexpr (DBG) {
+            for (int jb = 0; jb < 2; ++jb) {
+                const int m = blk * 256 + wave * 64 + 32 * jb + l31;
+                if (m < p.M)
+#pragma unroll
+                    for (int ks = 0; ks < 16; ++ks)
+                        if (ks < nks)
+                            *reinterpret_cast<bf16x8*>(p.dbg + ((int64_t)l * p.M + m) * 256 + 16 * ks + 8 * h) = bq[jb][ks];
+            }
+        }
+    };
 
     // one 32-deep weight chunk (stream position g, k-steps 2q, 2q + 1 of the layer)
     auto chunk = [&](auto q_c) __attribute__((always_inline)) {
@@ -241,8 +256,13 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_kernel(SdfMlpArgs p) {
         for (int jb = 0; jb < 2; ++jb) {
             const int m = blk * 256 + wave * 64 + 32 * jb + l31;
 #pragma unroll
-            for (int k = 0; k < 4; ++k)  // (a negative column offset is out of the view for row 0: zeros)
-                t[jb][k] = __builtin_amdgcn_raw_buffer_load_b128(vt, (m * p.ld_t + 16 * (12 + k) + 8 * h - nout) * 2, 0, 0);
+            for (int k = 0; k < 4; ++k) {
+                // the group straddling nout starts at column -4 (nout % 4 == 0): load from column 0 and move
+                // the first two dwords up to the features >= nout
+                const int c0 = 16 * (12 + k) + 8 * h - nout;
+                const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(vt, (m * p.ld_t + max(c0, 0)) * 2, 0, 0);
+                t[jb][k] = c0 < 0 ? u32x4{w[0], w[1], w[0], w[1]} : w;
+            }
         }
         wait_vmcnt<0>();  // (a drain: the ring's chunks in flight land too; once per block)
 #pragma unroll
@@ -312,14 +332,17 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_kernel(SdfMlpArgs p) {
             is[jb] = __builtin_amdgcn_raw_buffer_load_b32(vi, m * 4, 0, 0);
         }
         wait_vmcnt<0>();
+        dump(0, 4);
         zero_acc();
         static_for<2>(chunk);
         epi_pack(0);
+        dump(1, 16);
         for (int l = 1; l < kMlpLayers - 1; ++l) {
             zero_acc();
             static_for<8>(chunk);
             epi_pack(l);
             if (l == p.skip_layer) fix_tail(l);
+            dump(l + 1, 16);
         }
         // lin7 and the head (peeled: the chain's input registers are dead in the head's epilogue)
         zero_acc();
@@ -376,6 +399,10 @@ extern "C" int cn_sdf_mlp(const cn_sdf_mlp_desc* d, cn_stream_t stream) {
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         cus = 256;
     const int grid = a.nblocks < cus ? a.nblocks : cus;
-    sdf_mlp_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(a);
+    a.dbg = static_cast<bf16_t*>(d->debug);
+    if (a.dbg)
+        sdf_mlp_kernel<true><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+    else
+        sdf_mlp_kernel<false><<<grid, 256, 0, (hipStream_t)stream>>>(a);
     return check_launch("cn_sdf_mlp");
 }

@@ -529,6 +529,7 @@ typedef struct cn_sdf_mlp_desc {
     float* sdf;
     const int32_t* idx;
     float skip_div, beta, threshold;
+    void* debug; /* NULL, or bf16 [8][M][256]: every layer's input as the kernel holds it (tests) */
 } cn_sdf_mlp_desc;
 int cn_sdf_mlp(const cn_sdf_mlp_desc* d, cn_stream_t stream);
 

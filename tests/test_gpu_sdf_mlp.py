@@ -94,3 +94,36 @@ def test_sampler_z_values_fused_equal_layer_by_layer():
         finally:
             fields.FUSED_SDF_QUERY = True
     assert torch.equal(zs[0], zs[1])
+
+
+def test_fused_query_layer_inputs_match():
+    """cn_sdf_mlp's debug dump (every layer's input as its B operand holds it) against the layer-by-layer
+    path's operand images: layer 0 = the embedding's image, layer l = U_l's image."""
+    from copenerf import fields, ops
+    net = _net(9)
+    lay = net.layout()
+    M = 300
+    x = torch.rand(M, 4, device=DEV) * 2 - 1
+    with torch.no_grad():
+        Ws, bs, pk = net.params_and_pack()
+        st = fields.sdf_forward(lay, pk, x, want_feat=False, want_grad=False, keep=True)
+        u0b = torch.empty(M, 64, device=DEV, dtype=torch.bfloat16)
+        tail = torch.empty(M, 64, device=DEV, dtype=torch.bfloat16)
+        ops.sdf_embed(x, lay.multires, lay.scale, u0b, tail[:, :lay.E], ops.SQRT2)
+        dbg = torch.zeros(8, M, 256, device=DEV, dtype=torch.bfloat16)
+        sdf = torch.empty(M, device=DEV)
+        ops.sdf_mlp(u0b, tail[:, :lay.E], pk.Bf[:8], pk.b[:8], pk.w80[0], pk.b80, sdf, multires=lay.multires,
+                    skip_layer=lay.skip - 1, skip_div=ops.SQRT2, beta=lay.beta, threshold=lay.threshold, debug=dbg)
+    refs = [st["U"][0].bfloat16()] + [st["Ub"][l] for l in range(1, 8)]
+    report = []
+    for l in range(8):
+        w = 64 if l == 0 else 256
+        a, b = dbg[l, :, :w], refs[l][:, :w]
+        bad = (a != b)
+        if bad.any():
+            cols = bad.any(0).nonzero().flatten()[:24].tolist()
+            rows = bad.any(1).nonzero().flatten()[:12].tolist()
+            report.append(f"layer {l}: {bad.float().mean().item():.4f} of values differ, cols {cols}, rows {rows}, "
+                          f"max |d| {(a.float() - b.float()).abs().max().item():.3g}")
+    assert not report, "\n".join(report)
+    torch.testing.assert_close(sdf.view(-1, 1), st["sdf"], rtol=0, atol=0)
