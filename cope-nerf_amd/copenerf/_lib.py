@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libcopenerf.so"
 LIB_PATH = os.environ.get("COPENERF_LIB", os.path.join(_HERE, LIB_NAME))
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 c_f32p = ctypes.c_void_p  # device pointers are passed as integers
 c_i32 = ctypes.c_int32
@@ -88,6 +88,27 @@ class SdfMlpDesc(ctypes.Structure):
     ]
 
 
+SDF_MAX_LIN = 16
+
+
+class SdfNet(ctypes.Structure):
+    _fields_ = [
+        ("n_lin", c_i32), ("in_dim", c_i32 * SDF_MAX_LIN), ("out_dim", c_i32 * SDF_MAX_LIN), ("skip", c_i32),
+        ("multires", c_i32), ("scale", c_f32), ("beta", c_f32), ("threshold", c_f32), ("mfma_dtype", c_i32),
+        ("flags", c_i32),
+        ("W", c_ptr * (SDF_MAX_LIN - 1)), ("w_rows", c_i32 * (SDF_MAX_LIN - 1)), ("w_cols", c_i32 * (SDF_MAX_LIN - 1)),
+        ("bias", c_ptr * (SDF_MAX_LIN - 1)), ("head_w", c_ptr), ("head_b", c_ptr),
+    ]
+
+
+class SampleDesc(ctypes.Structure):
+    _fields_ = [
+        ("R", c_i32), ("n_samples", c_i32), ("n_importance", c_i32), ("up_sample_steps", c_i32),
+        ("rays_o", c_ptr), ("rays_d", c_ptr), ("near", c_ptr), ("far", c_ptr), ("t_rand", c_ptr),
+        ("time_step", c_ptr), ("net", ctypes.POINTER(SdfNet)), ("z", c_ptr),
+    ]
+
+
 # name -> (restype, argtypes); mirrors include/copenerf.h one to one.
 SIGNATURES = {
     "cn_abi_version": (c_i32, []),
@@ -148,6 +169,10 @@ SIGNATURES = {
     "cn_mat4_chain_fwd": (c_i32, [c_i32, c_ptr, c_ptr, c_ptr]),
     "cn_mat4_chain_bwd": (c_i32, [c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr]),
     "cn_sdf_mlp": (c_i32, [ctypes.POINTER(SdfMlpDesc), c_ptr]),
+    "cn_sdf_query_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(SdfNet), c_i32]),
+    "cn_sdf_query": (c_i32, [ctypes.POINTER(SdfNet), c_i32, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_i64, c_ptr]),
+    "cn_sample_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(SampleDesc)]),
+    "cn_sample": (c_i32, [ctypes.POINTER(SampleDesc), c_ptr, c_i64, c_ptr]),
 }
 
 _lock = threading.Lock()

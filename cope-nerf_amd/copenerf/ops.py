@@ -577,6 +577,79 @@ def sdf_mlp(u0b, tail, Ws, biases, head_w, head_b, sdf, *, multires, skip_layer,
     return sdf
 
 
+def sdf_net(lay, pk, layered=False):
+    """cn_sdf_net of a packed SDF network (fields.SDFLayout + fields.pack_sdf's images), and the tensors
+    it points into (hold them while the descriptor is used).  layered: never the fused cn_sdf_mlp query."""
+    if lay.n_lin > _lib.SDF_MAX_LIN:
+        raise RuntimeError(f"sdf_net: {lay.n_lin} Linear layers (at most {_lib.SDF_MAX_LIN})")
+    n, keep = _lib.SdfNet(), []
+    n.n_lin, n.skip, n.multires = lay.n_lin, lay.skip, lay.multires
+    n.scale, n.beta, n.threshold = lay.scale, lay.beta, lay.threshold
+    for l in range(lay.n_lin):
+        n.in_dim[l], n.out_dim[l] = lay.in_dim[l], lay.out_dim[l]
+    B0 = pk.Bf[0]
+    x6 = B0.dim() == 3
+    n.mfma_dtype = 2 if x6 else (1 if B0.dtype == torch.bfloat16 else 0)
+    n.flags = 1 if layered else 0
+
+    def aligned(t):
+        t = t.contiguous()
+        if t.data_ptr() % 16:
+            t = t.clone()
+        keep.append(t)
+        return t.data_ptr()
+
+    for l in range(lay.n_lin - 1):
+        B = pk.Bf[l]
+        if not B.is_contiguous():
+            raise RuntimeError(f"sdf_net: layer {l} image must be contiguous")
+        keep.append(B)
+        n.W[l] = B.data_ptr()
+        n.w_rows[l], n.w_cols[l] = (B.shape[1], 16 * B.shape[0]) if x6 else (B.shape[0], B.shape[1])
+        n.bias[l] = aligned(pk.b[l])
+    n.head_w = aligned(pk.w80.reshape(-1))
+    n.head_b = aligned(pk.b80.reshape(-1))
+    return n, keep
+
+
+def sdf_query(net, x, sdf, idx=None):
+    """sdf[idx[m] or m] = SDFNetwork.sdf(x[m]) -- cn_sdf_query (net: sdf_net's descriptor)."""
+    _need(x, "x")
+    M = x.shape[0]
+    if idx is not None and (idx.dtype != torch.int32 or idx.numel() < M or not idx.is_contiguous()):
+        raise RuntimeError("sdf_query: idx must be contiguous int32 with M entries")
+    if not sdf.is_contiguous() or (idx is None and sdf.numel() < M):
+        raise RuntimeError("sdf_query: sdf must be contiguous with M entries (or idx)")
+    lib = _lib.load()
+    ws = torch.empty(max(int(lib.cn_sdf_query_workspace_bytes(ctypes.byref(net), M)), 1), dtype=torch.uint8,
+                     device=x.device)
+    _lib.check(lib.cn_sdf_query(ctypes.byref(net), M, _ptr(x), _ld(x), _ptr(sdf), _ptr(idx), _ptr(ws), ws.numel(),
+                                _stream()), "cn_sdf_query")
+    return sdf
+
+
+def sample(net, rays_o, rays_d, near, far, t_rand, time_step, n_samples, n_importance, up_sample_steps, z):
+    """z [R, n_samples + up_sample_steps * (n_importance // up_sample_steps)] -- cn_sample: coarse z and the
+    up-sampling rounds with their SDF queries in one call (net: sdf_net's descriptor)."""
+    for t, nm in ((rays_o, "rays_o"), (rays_d, "rays_d"), (near, "near"), (far, "far"), (t_rand, "t_rand"),
+                  (time_step, "time_step"), (z, "z")):
+        if t is not None and (t.dtype != torch.float32 or not t.is_contiguous()):
+            raise RuntimeError(f"sample: {nm} must be a contiguous fp32 tensor")
+    R = z.shape[0]
+    k = n_importance // up_sample_steps if n_importance > 0 else 0
+    if z.shape[1] != n_samples + up_sample_steps * k or (t_rand is not None and t_rand.shape != (R, n_samples)):
+        raise RuntimeError("sample: z [R, n_samples + up_sample_steps * k] and t_rand [R, n_samples]")
+    d = _lib.SampleDesc()
+    d.R, d.n_samples, d.n_importance, d.up_sample_steps = R, n_samples, n_importance, up_sample_steps
+    d.rays_o, d.rays_d, d.near, d.far = _ptr(rays_o), _ptr(rays_d), _ptr(near), _ptr(far)
+    d.t_rand, d.time_step, d.z = _ptr(t_rand), _ptr(time_step), _ptr(z)
+    d.net = ctypes.pointer(net)
+    lib = _lib.load()
+    ws = torch.empty(max(int(lib.cn_sample_workspace_bytes(ctypes.byref(d))), 1), dtype=torch.uint8, device=z.device)
+    _lib.check(lib.cn_sample(ctypes.byref(d), _ptr(ws), ws.numel(), _stream()), "cn_sample")
+    return z
+
+
 def sdf_grad_assemble(multires, scale, U0, Q0, QE, G):
     _lib.call("cn_sdf_grad_assemble", U0.shape[0], multires, scale, _ptr(U0), _ld(U0), _ptr(Q0), _ld(Q0),
               _ptr(QE), _ld(QE), _ptr(G), _ld(G), _stream())

@@ -18,6 +18,10 @@ import torch.nn as nn
 from . import ops
 from .fields import _empty
 
+# the sampler as one C call (cn_sample: coarse z, the up-sampling rounds and their SDF queries composed in
+# C++); False: launch by launch from Python (sample_z_composed)
+SAMPLE_NATIVE = True
+
 
 class _PointsFn(torch.autograd.Function):
     """Section midpoints along the rays (neus_renderer.py:337-350):
@@ -140,7 +144,24 @@ class NeuSRenderer(nn.Module):
     # -- sampling ------------------------------------------------------------
     @torch.no_grad()
     def sample_z(self, rays_o, rays_d, time_step, near, far, n_samples, n_importance, t_rand, sdf_packed):
-        """Coarse + hierarchical z-values [R, n_samples + n_importance] (neus_renderer.py:466-525)."""
+        """Coarse + hierarchical z-values [R, n_samples + n_importance] (neus_renderer.py:466-525): one
+        cn_sample call (SAMPLE_NATIVE), or launch by launch (sample_z_composed: the same kernels, the same
+        bits) when the kernel timer attributes every launch."""
+        if not SAMPLE_NATIVE or ops._timer is not None or n_importance <= 0:
+            return self.sample_z_composed(rays_o, rays_d, time_step, near, far, n_samples, n_importance, t_rand,
+                                          sdf_packed)
+        from . import fields  # local: avoid a cycle at import
+        R = rays_o.shape[0]
+        k = n_importance // self.up_sample_steps
+        z = _empty(R, n_samples + self.up_sample_steps * k, rays_o.device)
+        net, keep = ops.sdf_net(self.sdf_network.layout(), sdf_packed[2], layered=not fields.FUSED_SDF_QUERY)
+        ops.sample(net, rays_o.detach(), rays_d.detach(), near, far, t_rand, time_step.detach(), n_samples,
+                   n_importance, self.up_sample_steps, z)
+        del keep
+        return z
+
+    def sample_z_composed(self, rays_o, rays_d, time_step, near, far, n_samples, n_importance, t_rand, sdf_packed):
+        """sample_z launch by launch from Python (the composition cn_sample makes in C++)."""
         R, dev = rays_o.shape[0], rays_o.device
         z = _empty(R, n_samples, dev)
         ops.coarse_z(near, far, n_samples, t_rand, z)

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define CN_ABI_VERSION 11
+#define CN_ABI_VERSION 12
 
 typedef void* cn_stream_t; /* hipStream_t */
 
@@ -532,6 +532,78 @@ typedef struct cn_sdf_mlp_desc {
     void* debug; /* NULL, or bf16 [8][M][256]: every layer's input as the kernel holds it (tests) */
 } cn_sdf_mlp_desc;
 int cn_sdf_mlp(const cn_sdf_mlp_desc* d, cn_stream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * Composed entry points (ABI v12): the sampler of NeuSRenderer.render
+ * (neus_renderer.py:466-525) and the SDF query it makes (SDFNetwork.sdf,
+ * neus_fields.py:268-283, 286-287), each one C call over the kernels above --
+ * no host code between the launches, all on the caller's stream, scratch from
+ * a caller-owned workspace (size from the *_workspace_bytes function; 256-byte
+ * aligned; it may be reused as soon as the stream has passed the call).
+ * Results are bitwise those of the same kernels composed one by one
+ * (copenerf.fields.sdf_forward / copenerf.renderer.sample_z).
+ *
+ * cn_sdf_net describes SDFNetwork's weights as cn_pack_weights images
+ * (copenerf.fields.pack_sdf): for lin0 .. lin(n_lin-2) the forward image
+ * W[l] (rows w_rows[l] >= the output width rounded up to 128, columns w_cols[l]:
+ * KE = 64-rounded encoding width for lin0, the 32- (bf16: 64-) rounded input
+ * width after; CN_MFMA_F32_BF16X6 images are chunk-major [w_cols/16][w_rows][48]),
+ * bias[l] fp32 [out_dim[l]] (16-byte aligned); the sdf row of the last Linear
+ * as head_w [in_dim[n_lin-1]] = weight[0] / scale (16-byte aligned) and head_b
+ * [1] = bias[0] / scale.  skip: the layer whose input is cat([h, embed(x)]) / sqrt 2
+ * (SDFNetwork skip_in, one entry) or -1; the layer before it has width
+ * out_dim = d_hidden - E.  Inputs are (x, y, z, t) points (d_in = 4), E = 4 (1 + 2 multires).
+ * flags bit 0 (CN_SDF_LAYERED): never the fused cn_sdf_mlp query (tests compare the two).
+ * ------------------------------------------------------------------------ */
+#define CN_SDF_MAX_LIN 16
+#define CN_SDF_LAYERED 1
+typedef struct cn_sdf_net {
+    int32_t n_lin;                      /* Linear layers (SDFNetwork n_layers + 1), 2 .. 16 */
+    int32_t in_dim[CN_SDF_MAX_LIN];     /* lin_l.weight.shape[1] */
+    int32_t out_dim[CN_SDF_MAX_LIN];    /* lin_l.weight.shape[0] */
+    int32_t skip;
+    int32_t multires;
+    float scale, beta, threshold;       /* SDFNetwork scale, Softplus(beta, threshold) */
+    int32_t mfma_dtype;                 /* cn_mfma_dtype of the images */
+    int32_t flags;
+    const void* W[CN_SDF_MAX_LIN - 1];
+    int32_t w_rows[CN_SDF_MAX_LIN - 1];
+    int32_t w_cols[CN_SDF_MAX_LIN - 1];
+    const float* bias[CN_SDF_MAX_LIN - 1];
+    const float* head_w;
+    const float* head_b;
+} cn_sdf_net;
+
+/* sdf[idx ? idx[m] : m] = SDFNetwork.sdf(x[m]) for M points x [M][ldx >= 4] (no gradient):
+ * cn_sdf_embed + cn_sdf_mlp (bf16 images, the fused shape) or cn_sdf_embed + one cn_linear per
+ * layer (SOFTPLUS, the last with the SOFTPLUS_HEAD epilogue where one tile spans the row) +
+ * cn_row_head otherwise. */
+size_t cn_sdf_query_workspace_bytes(const cn_sdf_net* net, int32_t M);
+int cn_sdf_query(const cn_sdf_net* net, int32_t M, const float* x, int64_t ldx, float* sdf,
+                 const int32_t* idx, void* workspace, int64_t workspace_bytes, cn_stream_t stream);
+
+/* The sampler: z [R][n_samples + up_sample_steps k] (k = n_importance / up_sample_steps >= 1, or
+ * [R][n_samples] when n_importance == 0) = the coarse samples (stratified with
+ * t_rand [R][n_samples], or none when t_rand is NULL -- eval) and, when n_importance > 0,
+ * up_sample_steps rounds of k new samples each, round i with
+ * inv_s = 64 * 2^i from the SDF of the current samples (the coarse SDF query, then one query per
+ * round's new samples scattered into the merged order; no query after the last round).
+ * rays_o / rays_d [R][3], near / far [R], time_step [1] (the frame's time value; points are
+ * (o + d z, t)).  The caller picks n_samples / n_importance by the iteration (the
+ * importance_sampling_start switch of neus_renderer.py:455-459). */
+typedef struct cn_sample_desc {
+    int32_t R, n_samples, n_importance, up_sample_steps;
+    const float* rays_o;
+    const float* rays_d;
+    const float* near;
+    const float* far;
+    const float* t_rand;
+    const float* time_step;
+    const cn_sdf_net* net;
+    float* z;
+} cn_sample_desc;
+size_t cn_sample_workspace_bytes(const cn_sample_desc* d);
+int cn_sample(const cn_sample_desc* d, void* workspace, int64_t workspace_bytes, cn_stream_t stream);
 
 #ifdef __cplusplus
 }

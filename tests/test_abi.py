@@ -35,7 +35,8 @@ def test_struct_layouts_match_header_order():
     from copenerf import _lib
     src = open(HEADER).read()
     for cname, py in (("cn_linear_desc", _lib.LinearDesc), ("cn_wgrad_desc", _lib.WgradDesc),
-                      ("cn_sdf_mlp_desc", _lib.SdfMlpDesc)):
+                      ("cn_sdf_mlp_desc", _lib.SdfMlpDesc), ("cn_sdf_net", _lib.SdfNet),
+                      ("cn_sample_desc", _lib.SampleDesc)):
         body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (cname, cname), src, re.S).group(1)
         body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
         names = []
@@ -44,7 +45,7 @@ def test_struct_layouts_match_header_order():
             if not decl:
                 continue
             decl = re.sub(r"^(const\s+)?\w+\s*\**", "", decl)
-            names += [re.sub(r"\[\d+\]", "", n.strip(" *")) for n in decl.split(",")]
+            names += [re.sub(r"\[[\w\s+-]+\]", "", n.strip(" *")) for n in decl.split(",")]
         assert names == [f[0] for f in py._fields_], (cname, names)
     assert ctypes.sizeof(_lib.LinearDesc) % 8 == 0
 
@@ -105,6 +106,61 @@ def test_argument_validation_without_gpu():
     m.n_layers, m.hidden, m.kpad0 = 8, 128, 64
     assert lib.cn_sdf_mlp(ctypes.byref(m), None) == -5
     assert b"8 x 256" in lib.cn_last_error()
+
+
+
+def _fake_net(mode=1, dh=256, multires=6, skip=4):
+    """A cn_sdf_net of SDFNetwork(d_hidden=dh, n_layers=8, skip_in=[skip]) with placeholder (aligned,
+    never dereferenced) pointers: host planning only."""
+    from copenerf import _lib
+    n = _lib.SdfNet()
+    E = 4 * (1 + 2 * multires)
+    n.n_lin, n.skip, n.multires, n.scale, n.beta, n.threshold, n.mfma_dtype = 9, skip, multires, 1.0, 100.0, 20.0, mode
+    kq = 64 if mode == 1 else 32
+    for l in range(9):
+        n.out_dim[l] = 257 if l == 8 else (dh - E if l + 1 == skip else dh)
+        n.in_dim[l] = E if l == 0 else n.out_dim[l - 1] + (E if l == skip else 0)
+    for l in range(8):
+        n.W[l], n.bias[l] = 4096, 4096
+        n.w_rows[l] = -(-n.out_dim[l] // 128) * 128
+        n.w_cols[l] = 64 if l == 0 else -(-n.in_dim[l] // kq) * kq
+    n.head_w = n.head_b = 4096
+    return n
+
+
+def test_composed_entry_points_plan_without_gpu():
+    """ABI v12: cn_sdf_query / cn_sample validate and size their workspace on the host."""
+    from copenerf import _lib
+    lib = _lib.load()
+    assert lib.cn_sdf_query(None, 1, 16, 4, 16, None, 16, 1 << 20, None) == -1
+    assert lib.cn_sdf_query_workspace_bytes(None, 10) == 0
+    assert lib.cn_sample(None, None, 0, None) == -1
+    n = _fake_net()
+    M = 262144
+    assert lib.cn_sdf_query_workspace_bytes(ctypes.byref(n), M) == 2 * M * 64 * 2  # fused: the two bf16 images
+    n.flags = 1  # layered: U0 fp32 [M][64], the skip input's bf16 image, two bf16 ping-pong buffers
+    assert lib.cn_sdf_query_workspace_bytes(ctypes.byref(n), M) == M * 64 * 4 + 3 * M * 256 * 2
+    n.flags = 0
+    x = _fake_net(mode=0)  # fp32 buffers
+    assert lib.cn_sdf_query_workspace_bytes(ctypes.byref(x), M) == M * 64 * 4 + 3 * M * 256 * 4
+    x.in_dim[3] = 200  # inconsistent widths
+    assert lib.cn_sdf_query(ctypes.byref(x), 4, 4096, 4, 4096, None, 4096, 1 << 30, None) == -2
+    assert b"lin3 takes 200" in lib.cn_last_error()
+    d = _lib.SampleDesc()
+    d.R, d.n_samples, d.n_importance, d.up_sample_steps = 4096, 64, 64, 4
+    d.rays_o = d.rays_d = d.near = d.far = d.time_step = d.z = 4096
+    d.net = ctypes.pointer(n)
+    R, k = 4096, 16
+    want = 4 * (R * 128 * 4) + R * 64 * 16 + 2 * R * k * 4 + 2 * (R * 64) * 64 * 2
+    assert lib.cn_sample_workspace_bytes(ctypes.byref(d)) == want
+    assert lib.cn_sample(ctypes.byref(d), 4096 * 256, want - 1, None) == -2
+    assert b"workspace" in lib.cn_last_error()
+    d.n_importance = 3  # fewer than one sample per round
+    assert lib.cn_sample(ctypes.byref(d), 4096 * 256, want, None) == -2
+    d.n_importance = 64
+    n.w_rows[2] = 128  # an image too small for its layer
+    assert lib.cn_sample(ctypes.byref(d), 4096 * 256, want, None) == -2
+    assert b"layer 2 image" in lib.cn_last_error()
 
 
 def test_product_path_refuses_cpu_tensors():

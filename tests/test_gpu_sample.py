@@ -1,0 +1,137 @@
+"""The composed entry points cn_sample / cn_sdf_query (ABI v12) called through the C ABI.
+
+cn_sample runs the whole sampler of NeuSRenderer.render (neus_renderer.py:466-525: coarse z, four
+up-sampling rounds, the SDF query of each round's samples) from one C call -- no Python between the
+launches -- so it must give the bits of the Python composition (renderer.sample_z_composed) in every
+GEMM mode, and match the reference's own z_vals in the golden fixtures (computed in fp64 on the CPU:
+importance positions come from a searchsorted on the SDF-derived cdf, so 99 % of entries within 2e-6
+and all within 2e-3 -- the bar test_gpu_render holds the renderer's per-sample outputs to)."""
+import ctypes
+
+import pytest
+import torch
+
+from helpers import REN_CFG, build_modules, fixture
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+MODES = ["fp32", "bf16x6", "bf16"]
+
+
+def _renderer(mods, mode):
+    from copenerf import NeuSRenderer
+    sdf, col, dev = mods
+    return NeuSRenderer(None, sdf, dev, col, None, **REN_CFG).to(DEV).set_mfma_dtype(mode)
+
+
+def _c_sample(r, pk, rays_o, rays_d, t, near, far, t_rand, layered=False):
+    """cn_sample through ctypes: descriptor, workspace size, one call."""
+    from copenerf import _lib, ops
+    lib = _lib.load()
+    net, keep = ops.sdf_net(r.sdf_network.layout(), pk, layered=layered)
+    R = rays_o.shape[0]
+    k = r.n_importance // r.up_sample_steps
+    z = torch.empty(R, r.n_samples + r.up_sample_steps * k, device=DEV)
+    d = _lib.SampleDesc()
+    d.R, d.n_samples, d.n_importance, d.up_sample_steps = R, r.n_samples, r.n_importance, r.up_sample_steps
+    d.rays_o, d.rays_d, d.near, d.far = rays_o.data_ptr(), rays_d.data_ptr(), near.data_ptr(), far.data_ptr()
+    d.t_rand = t_rand.data_ptr() if t_rand is not None else None
+    d.time_step, d.z, d.net = t.data_ptr(), z.data_ptr(), ctypes.pointer(net)
+    nbytes = lib.cn_sample_workspace_bytes(ctypes.byref(d))
+    assert nbytes > 0
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=DEV)
+    rc = lib.cn_sample(ctypes.byref(d), ctypes.c_void_p(ws.data_ptr()), nbytes,
+                       ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert rc == 0, lib.cn_last_error()
+    # a workspace one byte short is refused
+    assert lib.cn_sample(ctypes.byref(d), ctypes.c_void_p(ws.data_ptr()), nbytes - 1, None) == -2
+    torch.cuda.synchronize()
+    del keep
+    return z
+
+
+def _inputs(fx):
+    g = lambda k: fx[k].to(DEV).float().contiguous()  # noqa: E731
+    t_rand = g("t_rand") if not bool(fx["eval"]) else None
+    return g("rays_o"), g("rays_d"), g("t").reshape(-1)[:1].contiguous(), g("near"), g("far"), t_rand
+
+
+def _composed(r, pk, rays_o, rays_d, t, near, far, t_rand):
+    with torch.no_grad():
+        return r.sample_z_composed(rays_o, rays_d, t, near, far, r.n_samples, r.n_importance, t_rand,
+                                   (None, None, pk))
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("name", ["render_small_train", "render_small_eval", "render_full_train"])
+def test_c_sample_matches_composition_and_reference(name, mode):
+    fx = fixture(name)
+    mods = build_modules(int(fx["seed"]), int(fx["dh_sdf"]), int(fx["dh_col"]), device=DEV)
+    r = _renderer(mods, mode)
+    with torch.no_grad():
+        pk = r.sdf_network.params_and_pack()[2]
+    args = _inputs(fx)
+    z = _c_sample(r, pk, *args)
+    zc = _composed(r, pk, *args)
+    assert torch.equal(z, zc), (z - zc).abs().max().item()
+    if mode == "bf16":
+        return  # bf16 MFMA operands: judged by training quality (test_gpu_quality), not by 2e-6
+    ref = fx["z_vals"].to(DEV)
+    assert z.shape == ref.shape
+    diff = (z - ref).abs()
+    assert (diff <= 2e-6 + 1e-6 * ref.abs()).float().mean().item() >= 0.99, diff.max().item()
+    assert diff.max().item() <= 2e-3, diff.max().item()
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_c_sample_equals_renderer_and_layered_query(mode):
+    """Larger batch (2048 rays, d_hidden 256): cn_sample = the composition; the layered query (no fused
+    cn_sdf_mlp) gives the same bits as the fused one; the renderer's sample_z is cn_sample."""
+    from copenerf import renderer as rmod
+    mods = build_modules(5, device=DEV)
+    r = _renderer(mods, mode)
+    gen = torch.Generator(device=DEV).manual_seed(3)
+    R = 2048
+    rays_o = (torch.rand(R, 3, device=DEV, generator=gen) - 0.5) * 0.4
+    rays_d = torch.nn.functional.normalize(torch.randn(R, 3, device=DEV, generator=gen), dim=-1)
+    near = torch.full((R, 1), 0.2, device=DEV)
+    far = torch.full((R, 1), 1.8, device=DEV)
+    t = torch.full((1,), -0.3, device=DEV)
+    t_rand = torch.rand(R, r.n_samples, device=DEV, generator=gen)
+    with torch.no_grad():
+        pk = r.sdf_network.params_and_pack()[2]
+        z = _c_sample(r, pk, rays_o, rays_d, t, near, far, t_rand)
+        assert torch.equal(z, _composed(r, pk, rays_o, rays_d, t, near, far, t_rand))
+        assert torch.equal(z, _c_sample(r, pk, rays_o, rays_d, t, near, far, t_rand, layered=True))
+        assert rmod.SAMPLE_NATIVE
+        zr = r.sample_z(rays_o, rays_d, t, near, far, r.n_samples, r.n_importance, t_rand, (None, None, pk))
+    assert torch.equal(z, zr)
+    assert bool((z[:, 1:] >= z[:, :-1]).all())  # merged in order
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("dh", [256, 64])
+def test_c_sdf_query_matches_sdf_forward(mode, dh):
+    """cn_sdf_query = fields.sdf_forward's no-grad sdf, plain and scattered through idx; d_hidden 64 takes the
+    layer-by-layer path (fp32 buffers in the bf16 mode, the row head when the last layer cannot fuse it)."""
+    from copenerf import ops
+    from copenerf.fields import sdf_forward
+    sdfn = build_modules(7, dh_sdf=dh, device=DEV)[0]
+    sdfn.mfma_dtype = mode
+    lay = sdfn.layout()
+    M = 3000
+    gen = torch.Generator(device=DEV).manual_seed(11)
+    x = torch.cat([torch.rand(M, 3, device=DEV, generator=gen) * 2 - 1, torch.full((M, 1), 0.25, device=DEV)], 1)
+    with torch.no_grad():
+        pk = sdfn.params_and_pack()[2]
+        ref = sdf_forward(lay, pk, x, want_feat=False, want_grad=False, keep=False)["sdf"].reshape(-1)
+        for layered in (False, True):
+            net, keep = ops.sdf_net(lay, pk, layered=layered)
+            out = torch.full((M,), float("nan"), device=DEV)
+            ops.sdf_query(net, x, out)
+            assert torch.equal(out, ref), (layered, (out - ref).abs().max().item())
+            perm = torch.randperm(M, device=DEV, generator=gen).to(torch.int32)
+            out2 = torch.full((M,), float("nan"), device=DEV)
+            ops.sdf_query(net, x, out2, idx=perm)
+            assert torch.equal(out2[perm.long()], ref)
+            del keep
