@@ -1626,6 +1626,11 @@ enum LinearTile { LT_BF_SQ, LT_BF_T0, LT_BF_T1, LT_X6_SQ, LT_X6_TALL, LT_X6_WIDE
     X(LT_F_T1_D2, 4, 1, 1, 2, 32, 2, 2, 0) \
     X(LT_F_T1_D1, 4, 1, 1, 2, 32, 2, 1, 0)
 
+// measurement build only (-DCN_AB_X6_BWD_SQ=1, profiles/r5_ab.txt): bf16x6 BWD_SOFTPLUS on the 256x256 tile
+#ifndef CN_AB_X6_BWD_SQ
+#define CN_AB_X6_BWD_SQ 0
+#endif
+
 static LinearTile choose_linear_tile(const cn_linear_desc* d) {
     const int e = d->epilogue;
     const bool head = e == CN_EPI_SOFTPLUS_HEAD;
@@ -1642,7 +1647,8 @@ static LinearTile choose_linear_tile(const cn_linear_desc* d) {
         if (d->tile == 2) return LT_X6_T128;
         // (BWD_SOFTPLUS on the 256x256 tile: re-measured in round 4 with the branch-free epilogue, equal or
         // slower -- 4.25 vs 4.17 ms per C2 step, profiles/r4_ab.txt r4m)
-        if (wide_n && d->K % 32 == 0 && d->ldb >= 256 && e != CN_EPI_BWD_SOFTPLUS && (longk || head)) return LT_X6_SQ;
+        if (wide_n && d->K % 32 == 0 && d->ldb >= 256 && (e != CN_EPI_BWD_SOFTPLUS || CN_AB_X6_BWD_SQ) && (longk || head))
+            return LT_X6_SQ;
         const bool tall = e == CN_EPI_MUL || e == CN_EPI_TANGENT || head;
         if (d->K % 64 == 0 && tall && d->N > 128 && d->ldb >= 256 && (longk || head)) return LT_X6_TALL;
         // (an aux-reading epilogue with one workgroup per CU no longer overlaps a partner's main loop)
