@@ -106,10 +106,18 @@ def rocprof_launch_ns(symbol, config, stamp):
     return None, None
 
 
-def pmc_traffic(symbol):
-    """Per-launch HBM bytes of `symbol` from the newest committed counter pass."""
+def pmc_traffic(symbol, stamp=None):
+    """Per-launch HBM bytes of `symbol` from the newest committed counter pass of this library build
+    (tools/pmc_round.sh writes the build's stamp beside the pass: profiles/<tag>_pmc.json with
+    <tag>_lib_stamp.txt)."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
     for f in reversed(files):
+        st = f[:-len("pmc.json")] + "lib_stamp.txt"
+        try:
+            if stamp is None or open(st).read().strip() != stamp:
+                continue
+        except OSError:
+            continue
         try:
             with open(f) as fh:
                 d = json.load(fh)
@@ -450,7 +458,7 @@ def roofline_fields(timer, steps, rays_per_s, mode, config="c2"):
     t_flop, t_byte = flops / (peak_tf * 1e12), nbytes / (HBM_PEAK_GBS * 1e9)
     hbm = t_byte > t_flop  # the binding ceiling: the larger of the two times
     symbol = timer.symbols[dom_key]
-    traffic, traffic_src = pmc_traffic(symbol)
+    traffic, traffic_src = pmc_traffic(symbol, lib_stamp())
     kernels_ms = sum(a["ms"] for a in agg.values()) / steps
     # the kernel's own duration from the committed rocprofv3 stats of this config (the HIP events
     # bracket the library call: for a weight gradient also its slab reduction); the HIP-event
@@ -488,7 +496,10 @@ def roofline_fields(timer, steps, rays_per_s, mode, config="c2"):
         "gemm_ms_per_step": round(kernels_ms, 3),
         "gemm_tflops_avg": round(sum(a["flops"] for a in agg.values()) / sum(a["ms"] for a in agg.values()) / 1e9, 2),
         "roofline_by_class": {"/".join(map(str, k)): {"tflops": round(v["flops"] / v["ms"] / 1e9, 1),
-                                                       "gbs": round(v["bytes"] / v["ms"] / 1e6, 1)}
+                                                       "gbs": round(v["bytes"] / v["ms"] / 1e6, 1),
+                                                       "launches_per_step": round(v["launches"] / steps, 2),
+                                                       "algorithmic_mb_per_launch":
+                                                           round(v["bytes"] / v["launches"] / 1e6, 1)}
                               for k, v in sorted(agg.items(), key=lambda kv: -kv[1]["ms"])},
         "kernel_breakdown_ms_per_step": {"/".join(map(str, k)): round(v["ms"] / steps, 3) for k, v in
                                          sorted(agg.items(), key=lambda kv: -kv[1]["ms"])},

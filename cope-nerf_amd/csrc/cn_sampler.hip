@@ -357,318 +357,9 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_kernel(SdfMlpArgs p) {
 }
 
 
-// ---------------------------------------------------------------------------------------------
-// The pipelined form (the library's choice; sdf_mlp_kernel above is the serial reference of the
-// same arithmetic, kept for the A/B in profiles/r5_ab.txt).  At one wave per SIMD the serial
-// form's epilogue VALU (softplus: two transcendentals per value, ~12 issue slots) outweighs the
-// layer's MFMAs, and the two do not overlap.  Here a wave's 64 samples are two halves of 32
-// (jb), each layer's chunks are applied to one half at a time (the ring streams every chunk
-// twice: 116 chunks per block), and the epilogue of the other half runs in the MFMA gaps:
-//
-//   P(0,0)  P(0,1)  E(0,0)  [P(1,0) | E(0,1)]  [P(1,1) | E(1,0)]  ...  [P(7,1) | H(0)]  H(1)
-//
-// P(l, j): layer l's MFMAs on half j; E(l, j): its epilogue (bias, softplus, RNE bf16, next
-// B-operand order); H(j): lin7's epilogue with the sdf head.  E(l, j) of feature block ib rides
-// in chunk ib of the pass beside it, one value per MFMA.  Registers: E(l, j) reads acc[.][j] and
-// writes bq[j] while P(., 1 - j) reads bq[1 - j] and accumulates acc[.][1 - j] -- the serial
-// form's register sets, no more.  Same roundings, same k order, same instructions per value as
-// the serial form: bitwise equal (tests/test_gpu_sdf_mlp.py compares both with the layer path).
-constexpr int kPipeChunksPerBlock = 2 * kMlpChunksPerBlock;
-
-template <bool DBG>
-__global__ void __launch_bounds__(256, 1) sdf_mlp_pipe_kernel(SdfMlpArgs p) {
-    __shared__ __attribute__((aligned(16))) char smem[kMlpNS * kMlpChunk + kMlpLayers * 256 * 4 + 256 * 4];
-    float* sBias = reinterpret_cast<float*>(smem + kMlpNS * kMlpChunk);
-    float* sHead = sBias + kMlpLayers * 256;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int h = lane >> 5;
-    const int l31 = lane & 31;
-
-    for (int i = tid; i < kMlpLayers * 256; i += 256) {
-        const int l = i >> 8, n = i & 255;
-        sBias[i] = n < p.nout[l] ? p.bias[l][n] : 0.0f;
-    }
-    sHead[tid] = p.head_w[tid];
-    __syncthreads();
-
-    const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem);
-    const uint32_t ldsBias = lds0 + kMlpNS * kMlpChunk;
-    const uint32_t ldsHead = ldsBias + kMlpLayers * 256 * 4;
-
-    // ---- weight chunk stream: per sample block lin0's 2 chunks twice, then each of lin1 .. lin7's 8
-    // chunks twice (one pass per half)
-    auto chunk_of = [](int cb, int& l, int& k0) __attribute__((always_inline)) {
-        if (cb < 4) {
-            l = 0;
-            k0 = 32 * (cb & 1);
-        } else {
-            const int c = cb - 4;
-            l = 1 + (c >> 4);
-            k0 = 32 * (c & 7);
-        }
-    };
-    auto issue = [&](int g) __attribute__((always_inline)) {
-        int l, k0;
-        chunk_of(g % kPipeChunksPerBlock, l, k0);
-        const int ldw = p.ldw[l];
-        const rsrc_t v = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.W[l]), 0, 256 * ldw * 2, 0x00020000);
-        char* dst = smem + (g % kMlpNS) * kMlpChunk + wave * 64 * 64;
-        const int vo = ((lane >> 2) * ldw + 8 * ((lane & 3) ^ ((lane >> 4) & 3))) * 2;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(v, (__attribute__((address_space(3))) void*)(dst + j * 1024), 16, vo,
-                                                     ((wave * 64 + 16 * j) * ldw + k0) * 2, 0, 0);
-    };
-    uint32_t aoff[2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) aoff[s] = l31 * 64 + (((2 * s + h) ^ ((l31 >> 2) & 3)) << 4);
-
-    const float c_exp = p.beta * 1.44269504088896341f;
-    const float c_thr = p.threshold * 1.44269504088896341f;
-    const float c_log = 0.693147180559945309f / p.beta;
-
-    const rsrc_t vu = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.u0), 0, p.M * p.ld_u0 * 2, 0x00020000);
-    const rsrc_t vt = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.tail), 0, p.M * p.ld_t * 2, 0x00020000);
-    const rsrc_t vi = __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(p.idx), 0, p.idx ? p.M * 4 : 0, 0x00020000);
-    int is[2];
-
-    int blk = blockIdx.x;
-    if (blk >= p.nblocks) return;
-    int g = 0;
-#pragma unroll
-    for (int d = 0; d < kMlpNS - 1; ++d) issue(d);
-
-    bf16x8 bq[2][16];  // each half's current layer input, B-operand order
-    floatx16 acc[8][2];
-    auto dump = [&](int l, auto jb_c, int nks) __attribute__((always_inline)) {
-        if constexpr (DBG) {
-            constexpr int jb = decltype(jb_c)::value;
-            const int m = blk * 256 + wave * 64 + 32 * jb + l31;
-            if (m < p.M)
-#pragma unroll
-                for (int ks = 0; ks < 16; ++ks)
-                    if (ks < nks)
-                        *reinterpret_cast<bf16x8*>(p.dbg + ((int64_t)l * p.M + m) * 256 + 16 * ks + 8 * h) = bq[jb][ks];
-        }
-    };
-    auto read4 = [&](uint32_t base, auto ib_c, floatx4* v) __attribute__((always_inline)) {
-        constexpr int ib = decltype(ib_c)::value;
-        const uint32_t a = base + 16 * h;
-        v[0] = __builtin_bit_cast(floatx4, lds_read_b128<(32 * ib + 0) * 4>(a));
-        v[1] = __builtin_bit_cast(floatx4, lds_read_b128<(32 * ib + 8) * 4>(a));
-        v[2] = __builtin_bit_cast(floatx4, lds_read_b128<(32 * ib + 16) * 4>(a));
-        v[3] = __builtin_bit_cast(floatx4, lds_read_b128<(32 * ib + 24) * 4>(a));
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
-    };
-
-    // one 32-deep weight chunk (stream position g, k-steps 2q, 2q + 1) on half JB: pre() before the
-    // A-fragment reads (the epilogue slice's LDS table reads), fill(i) after MFMA i = 0 .. 15
-    auto chunk = [&](auto q_c, auto jb_c, auto&& pre, auto&& fill) __attribute__((always_inline)) {
-        constexpr int q = decltype(q_c)::value;
-        constexpr int JB = decltype(jb_c)::value;
-        wait_vmcnt<4 * (kMlpNS - 2)>();
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        issue(g + kMlpNS - 1);
-        pre();
-        const uint32_t sb = lds0 + (g % kMlpNS) * kMlpChunk;
-        static_for<2>([&](auto s_c) {
-            constexpr int s = decltype(s_c)::value;
-            const uint32_t a = sb + aoff[s];
-            bf16x8 af[8];
-            af[0] = __builtin_bit_cast(bf16x8, lds_read_b128<0 * 2048>(a));
-            af[1] = __builtin_bit_cast(bf16x8, lds_read_b128<1 * 2048>(a));
-            af[2] = __builtin_bit_cast(bf16x8, lds_read_b128<2 * 2048>(a));
-            af[3] = __builtin_bit_cast(bf16x8, lds_read_b128<3 * 2048>(a));
-            af[4] = __builtin_bit_cast(bf16x8, lds_read_b128<4 * 2048>(a));
-            af[5] = __builtin_bit_cast(bf16x8, lds_read_b128<5 * 2048>(a));
-            af[6] = __builtin_bit_cast(bf16x8, lds_read_b128<6 * 2048>(a));
-            af[7] = __builtin_bit_cast(bf16x8, lds_read_b128<7 * 2048>(a));
-            asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(af[0]), "+v"(af[1]), "+v"(af[2]), "+v"(af[3]));
-            static_for<8>([&](auto i_c) {
-                constexpr int ib = decltype(i_c)::value;
-                if constexpr (ib == 4)
-                    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[4]), "+v"(af[5]), "+v"(af[6]), "+v"(af[7]));
-                if constexpr (q == 0 && s == 0)  // the layer's first k-step: from zero
-                    acc[ib][JB] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ib], bq[JB][2 * q + s], floatx16{}, 0, 0, 0);
-                else
-                    acc[ib][JB] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ib], bq[JB][2 * q + s], acc[ib][JB], 0, 0, 0);
-                fill(std::integral_constant<int, 8 * s + ib>{});
-            });
-            __builtin_amdgcn_sched_barrier(0);
-        });
-        ++g;
-    };
-    auto no_pre = []() __attribute__((always_inline)) {};
-    auto no_fill = [](auto) __attribute__((always_inline)) {};
-
-    // ---- epilogue pieces: feature n = 32 ib + 8 (r >> 2) + 4 h + (r & 3) of sample (lane, jb)
-    auto value = [&](auto ib_c, auto jb_c, auto r_c, const floatx4* bb) __attribute__((always_inline)) {
-        constexpr int ib = decltype(ib_c)::value, jb = decltype(jb_c)::value, r = decltype(r_c)::value;
-        return softplus_hw(acc[ib][jb][r] + bb[r >> 2][r & 3], c_exp, c_thr, c_log);
-    };
-    // values o[16] of block ib, half jb, layer l -> bq[jb][2 ib], bq[jb][2 ib + 1] (the divisor where
-    // it is not 1; RNE bf16; two permlane32 swaps per 8 values into the next layer's B order)
-    auto finish = [&](auto ib_c, auto jb_c, int l, float* o) __attribute__((always_inline)) {
-        constexpr int ib = decltype(ib_c)::value, jb = decltype(jb_c)::value;
-        if (l == p.skip_layer) {
-            const float inv_odiv = p.inv_odiv[l];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) o[r] *= inv_odiv;
-        }
-#pragma unroll
-        for (int hs = 0; hs < 2; ++hs) {
-            unsigned P0 = pack_b16x2(o[8 * hs + 0], o[8 * hs + 1]);
-            unsigned P1 = pack_b16x2(o[8 * hs + 2], o[8 * hs + 3]);
-            unsigned P2 = pack_b16x2(o[8 * hs + 4], o[8 * hs + 5]);
-            unsigned P3 = pack_b16x2(o[8 * hs + 6], o[8 * hs + 7]);
-            const auto s02 = __builtin_amdgcn_permlane32_swap(P0, P2, false, false);
-            const auto s13 = __builtin_amdgcn_permlane32_swap(P1, P3, false, false);
-            const u32x4 w = {(unsigned)s02[0], (unsigned)s13[0], (unsigned)s02[1], (unsigned)s13[1]};
-            bq[jb][2 * ib + hs] = __builtin_bit_cast(bf16x8, w);
-        }
-    };
-    // the skip layer's tail features (n >= nout) of half JB: RNE(emb / skip_div) as cn_sdf_embed wrote them
-    auto fix_tail = [&](int l, auto jb_c) __attribute__((always_inline)) {
-        constexpr int jb = decltype(jb_c)::value;
-        const int nout = p.nout[l];
-        const int m = blk * 256 + wave * 64 + 32 * jb + l31;
-        u32x4 t[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int c0 = 16 * (12 + k) + 8 * h - nout;
-            const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(vt, (m * p.ld_t + max(c0, 0)) * 2, 0, 0);
-            t[k] = c0 < 0 ? u32x4{w[0], w[1], w[0], w[1]} : w;
-        }
-        wait_vmcnt<0>();  // (a drain: the ring's chunks in flight land too; twice per block)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            u32x4 w = __builtin_bit_cast(u32x4, bq[jb][12 + k]);
-#pragma unroll
-            for (int d = 0; d < 4; ++d) w[d] = 16 * (12 + k) + 8 * h + 2 * d >= nout ? t[k][d] : w[d];
-            bq[jb][12 + k] = __builtin_bit_cast(bf16x8, w);
-        }
-    };
-    // pass P(l, JB) with E(lE, 1 - JB) in its gaps
-    auto pass_hidden = [&](auto jb_c, int lE) __attribute__((always_inline)) {
-        constexpr int JB = decltype(jb_c)::value;
-        constexpr std::integral_constant<int, 1 - JB> je{};
-        static_for<8>([&](auto q_c) {
-            floatx4 bb[4];
-            float o[16];
-            chunk(q_c, jb_c, [&]() __attribute__((always_inline)) { read4(ldsBias + lE * 1024, q_c, bb); },
-                  [&](auto r_c) __attribute__((always_inline)) { o[decltype(r_c)::value] = value(q_c, je, r_c, bb); });
-            finish(q_c, je, lE, o);
-        });
-    };
-    // an exposed epilogue E(l, JB)
-    auto epi_alone = [&](auto jb_c, int l) __attribute__((always_inline)) {
-        static_for<8>([&](auto ib_c) {
-            floatx4 bb[4];
-            float o[16];
-            read4(ldsBias + l * 1024, ib_c, bb);
-            static_for<16>([&](auto r_c) { o[decltype(r_c)::value] = value(ib_c, jb_c, r_c, bb); });
-            finish(ib_c, jb_c, l, o);
-        });
-    };
-    // the head of half jb: the DMA tile's row-dot order (per column half wn = ib >> 2: Σ over the column
-    // blocks ib & 3 in order; the 32-lane butterfly; the halves in order; the bias)
-    auto head_store = [&](auto jb_c, float (*part)[16]) __attribute__((always_inline)) {
-        constexpr int jb = decltype(jb_c)::value;
-        float sw2[2];
-#pragma unroll
-        for (int wn = 0; wn < 2; ++wn) {
-            float t1[8], t2[4], t3[4];
-#pragma unroll
-            for (int r = 0; r < 8; ++r) t1[r] = part[wn][r] + part[wn][r ^ 8];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) t2[r] = t1[r] + t1[r ^ 4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const unsigned u = __builtin_bit_cast(unsigned, t2[r]);
-                const auto sw = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-                t3[r] = __builtin_bit_cast(float, (unsigned)sw[0]) + __builtin_bit_cast(float, (unsigned)sw[1]);
-            }
-            const float t4a = t3[0] + t3[2], t4b = t3[1] + t3[3];
-            sw2[wn] = t4a + t4b;
-        }
-        const int row = blk * 256 + wave * 64 + 32 * jb + l31;
-        if (h == 0 && row < p.M) p.sdf[p.idx ? is[jb] : row] = (sw2[0] + sw2[1]) + p.head_b[0];
-    };
-    auto head_term = [&](auto ib_c, auto jb_c, auto r_c, const floatx4* bb, const floatx4* hw, float (*part)[16])
-        __attribute__((always_inline)) {
-        constexpr int ib = decltype(ib_c)::value, r = decltype(r_c)::value;
-        const float x = value(ib_c, jb_c, r_c, bb) * hw[r >> 2][r & 3];
-        part[ib >> 2][r] = (ib & 3) == 0 ? 0.0f + x : part[ib >> 2][r] + x;
-    };
-    constexpr std::integral_constant<int, 0> J0{};
-    constexpr std::integral_constant<int, 1> J1{};
-    constexpr int L7 = kMlpLayers - 1;
-
-    for (; blk < p.nblocks; blk += gridDim.x) {
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb) {
-            const int m = blk * 256 + wave * 64 + 32 * jb + l31;
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks)
-                bq[jb][ks] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(vu, (m * p.ld_u0 + 16 * ks + 8 * h) * 2, 0, 0));
-            is[jb] = __builtin_amdgcn_raw_buffer_load_b32(vi, m * 4, 0, 0);
-        }
-        wait_vmcnt<0>();
-        dump(0, J0, 4);
-        dump(0, J1, 4);
-        static_for<2>([&](auto q_c) { chunk(q_c, J0, no_pre, no_fill); });
-        static_for<2>([&](auto q_c) { chunk(q_c, J1, no_pre, no_fill); });
-        epi_alone(J0, 0);
-        dump(1, J0, 16);
-        for (int l = 1; l < L7; ++l) {
-            pass_hidden(J0, l - 1);  // P(l, 0) | E(l - 1, 1)
-            if (l - 1 == p.skip_layer) fix_tail(l - 1, J1);
-            dump(l, J1, 16);
-            pass_hidden(J1, l);      // P(l, 1) | E(l, 0)
-            if (l == p.skip_layer) fix_tail(l, J0);
-            dump(l + 1, J0, 16);
-        }
-        pass_hidden(J0, L7 - 1);     // P(7, 0) | E(6, 1)
-        if (L7 - 1 == p.skip_layer) fix_tail(L7 - 1, J1);
-        dump(L7, J1, 16);
-        {
-            float part[2][16];        // P(7, 1) | H(0)
-            static_for<8>([&](auto q_c) {
-                floatx4 bb[4], hw[4];
-                chunk(q_c, J1,
-                      [&]() __attribute__((always_inline)) {
-                          read4(ldsBias + L7 * 1024, q_c, bb);
-                          read4(ldsHead, q_c, hw);
-                      },
-                      [&](auto r_c) __attribute__((always_inline)) { head_term(q_c, J0, r_c, bb, hw, part); });
-            });
-            head_store(J0, part);
-        }
-        {
-            float part[2][16];        // H(1)
-            static_for<8>([&](auto ib_c) {
-                floatx4 bb[4], hw[4];
-                read4(ldsBias + L7 * 1024, ib_c, bb);
-                read4(ldsHead, ib_c, hw);
-                static_for<16>([&](auto r_c) { head_term(ib_c, J1, r_c, bb, hw, part); });
-            });
-            head_store(J1, part);
-        }
-    }
-    wait_vmcnt<0>();
-}
-
 }  // namespace cn
 
 using namespace cn;
-
-// measurement build only (-DCN_AB_SDF_MLP_SERIAL=1, profiles/r5_ab.txt): the serial kernel
-#ifndef CN_AB_SDF_MLP_SERIAL
-#define CN_AB_SDF_MLP_SERIAL 0
-#endif
 
 extern "C" int cn_sdf_mlp(const cn_sdf_mlp_desc* d, cn_stream_t stream) {
     CN_REQUIRE(d && d->u0 && d->tail && d->sdf && d->head_w && d->head_b, CN_ERR_ARG, "cn_sdf_mlp: null pointer");
@@ -714,16 +405,9 @@ extern "C" int cn_sdf_mlp(const cn_sdf_mlp_desc* d, cn_stream_t stream) {
         cus = 256;
     const int grid = a.nblocks < cus ? a.nblocks : cus;
     a.dbg = static_cast<bf16_t*>(d->debug);
-#if CN_AB_SDF_MLP_SERIAL
     if (a.dbg)
         sdf_mlp_kernel<true><<<grid, 256, 0, (hipStream_t)stream>>>(a);
     else
         sdf_mlp_kernel<false><<<grid, 256, 0, (hipStream_t)stream>>>(a);
-#else
-    if (a.dbg)
-        sdf_mlp_pipe_kernel<true><<<grid, 256, 0, (hipStream_t)stream>>>(a);
-    else
-        sdf_mlp_pipe_kernel<false><<<grid, 256, 0, (hipStream_t)stream>>>(a);
-#endif
     return check_launch("cn_sdf_mlp");
 }

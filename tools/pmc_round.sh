@@ -13,6 +13,8 @@ mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 B="python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --timer-steps 1 $*"
 timeout -k 10 120 rocprofv3 -L > $O/counters.txt 2>&1 || true
+# the library build these counters belong to (bench.py reads PMC traffic only for its own build)
+cp $R/cope-nerf_amd/copenerf/libcopenerf.so.stamp $O/lib_stamp.txt
 have() { for c in "$@"; do grep -qw "$c" $O/counters.txt && printf '%s ' "$c"; done; }
 echo "pass1: $(have SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT)"
 echo "pass2: $(have SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM)"

@@ -29,6 +29,12 @@ def main(d, steps=None):
     pmc = json.load(open(os.path.join(d, "pmc.json")))["kernels"]
     bench = json.loads(open(os.path.join(d, "bench_trace.json")).read().strip().splitlines()[-1])
     steps = steps or (bench["steps"] + bench["warmup"] + 1)
+    # algorithmic bytes per launch of each kernel symbol (bench.py's launch classes)
+    alg = {}
+    for cls, sym in bench.get("kernel_symbols", {}).items():
+        c = bench.get("roofline_by_class", {}).get(cls, {})
+        if "algorithmic_mb_per_launch" in c:
+            alg[sym] = c["algorithmic_mb_per_launch"]
     rows = []
     for r in stats:
         k = short(r["Name"])
@@ -45,15 +51,21 @@ def main(d, steps=None):
         p = pmc.get(r["Name"])
         if p:
             row["hbm_mb_per_launch"] = p["hbm_bytes_per_launch"] / 1e6
+            if alg.get(r["Name"]):
+                row["algorithmic_mb_per_launch"] = alg[r["Name"]]
+                row["pmc_over_algorithmic"] = row["hbm_mb_per_launch"] / alg[r["Name"]]
+                row["hbm_tbs"] = row["hbm_mb_per_launch"] / row["avg_us"]
         rows.append(row)
     rows.sort(key=lambda x: -x["ms_per_step"])
-    out = ["| kernel | ms/step | avg µs | GHz | MFMA busy | wait | issue stall | PMC MB/launch |",
-           "|---|---|---|---|---|---|---|---|"]
+    out = ["| kernel | ms/step | avg µs | GHz | MFMA busy | wait | issue stall | PMC MB/launch | algorithmic MB | "
+           "PMC / alg. | PMC TB/s |",
+           "|---|---|---|---|---|---|---|---|---|---|---|"]
     for x in rows[:16]:
         f = lambda k, fmt: (fmt % x[k]) if k in x else "—"  # noqa: E731
         out.append(f"| `{short(x['kernel'])}` | {x['ms_per_step']:.2f} | {x['avg_us']:.1f} | {f('clock_ghz', '%.2f')} | "
                    f"{f('mfma_busy', '%.3f')} | {f('wait', '%.2f')} | {f('issue_stall', '%.2f')} | "
-                   f"{f('hbm_mb_per_launch', '%.0f')} |")
+                   f"{f('hbm_mb_per_launch', '%.0f')} | {f('algorithmic_mb_per_launch', '%.0f')} | "
+                   f"{f('pmc_over_algorithmic', '%.2f')} | {f('hbm_tbs', '%.2f')} |")
     print("\n".join(out))
     json.dump(rows, open(os.path.join(d, "kernel_table.json"), "w"), indent=1)
 
