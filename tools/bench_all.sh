@@ -13,6 +13,7 @@ for c in $CONFIGS; do
     c2) args="";;
     c2graph) args="--graph --no-cpu-baseline";;
     distgraph) args="--graph --no-cpu-baseline"; export COPENERF_FORCE_DIST=1;;
+    *graph) args="--config ${c%graph} --graph --no-cpu-baseline";;
     *) args="--config $c";;
   esac
   echo "== $c $args" >&2
