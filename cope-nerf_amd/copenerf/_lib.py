@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libcopenerf.so"
 LIB_PATH = os.environ.get("COPENERF_LIB", os.path.join(_HERE, LIB_NAME))
 
-ABI_VERSION = 13
+ABI_VERSION = 12
 
 c_f32p = ctypes.c_void_p  # device pointers are passed as integers
 c_i32 = ctypes.c_int32
@@ -109,19 +109,6 @@ class SampleDesc(ctypes.Structure):
     ]
 
 
-CHAIN_MAX = 8
-
-
-class MulChainDesc(ctypes.Structure):
-    _fields_ = [
-        ("M", c_i32), ("n", c_i32), ("src", c_ptr), ("ld_src", c_i64),
-        ("W", c_ptr * CHAIN_MAX), ("ldw", c_i64 * CHAIN_MAX), ("aux", c_ptr * CHAIN_MAX), ("ld_aux", c_i64 * CHAIN_MAX),
-        ("aux_beta", c_f32 * CHAIN_MAX), ("adiv", c_f32 * CHAIN_MAX), ("nsplit", c_i32 * CHAIN_MAX),
-        ("split", c_ptr * CHAIN_MAX), ("ld_split", c_i64 * CHAIN_MAX), ("out_b", c_ptr * CHAIN_MAX),
-        ("ld_out_b", c_i64 * CHAIN_MAX), ("out_f", c_ptr * CHAIN_MAX), ("ld_out_f", c_i64 * CHAIN_MAX),
-    ]
-
-
 # name -> (restype, argtypes); mirrors include/copenerf.h one to one.
 SIGNATURES = {
     "cn_abi_version": (c_i32, []),
@@ -186,7 +173,6 @@ SIGNATURES = {
     "cn_sdf_query": (c_i32, [ctypes.POINTER(SdfNet), c_i32, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_i64, c_ptr]),
     "cn_sample_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(SampleDesc)]),
     "cn_sample": (c_i32, [ctypes.POINTER(SampleDesc), c_ptr, c_i64, c_ptr]),
-    "cn_mul_chain": (c_i32, [ctypes.POINTER(MulChainDesc), c_ptr]),
 }
 
 _lock = threading.Lock()

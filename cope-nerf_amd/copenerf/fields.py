@@ -232,31 +232,6 @@ def _fused_query_ok(lay: SDFLayout, pk: SDFPack) -> bool:
         all(pk.Bf[l].shape[0] == 256 for l in range(8)) and lay.in_dim[8] == 256
 
 
-# The MUL chains of the bf16 mode (the ∇ pass of the forward, the first-order adjoint of the backward) in one
-# launch each (cn_mul_chain: the chained operand on chip, bitwise equal to the layer-by-layer MULs); False:
-# one cn_linear per layer
-MUL_CHAIN = True
-
-
-def _mul_chain_ok(lay: SDFLayout, pk: SDFPack) -> bool:
-    """cn_mul_chain's shape: bf16 images, hidden buffers 256 wide, every transposed image [256][256]."""
-    if not (MUL_CHAIN and _img_mode(pk, lay) and lay.HL == 256 and 2 <= lay.n_lin - 1 <= 9):
-        return False
-    L8 = lay.n_lin - 1
-    return all(pk.Bt[l].dim() == 2 and pk.Bt[l].shape[0] >= 256 and pk.Bt[l].shape[1] >= 256 and
-               lay.out_dim[l - 1] % 4 == 0 for l in range(1, L8)) and \
-        (lay.skip < 0 or lay.skip >= L8 or lay.in_dim[lay.skip] == 256)
-
-
-def _mul_chain_steps(lay: SDFLayout, pk: SDFPack, U, Ub, outs_b, outs_f, split):
-    """cn_mul_chain steps for l = L8-1 .. 1: Z_{l-1} = (W_lᵀ Z_l) ⊙ σ_{l-1}, the skip layer's split
-    (columns >= out_dim[sk-1] raw to `split`, or zero without it) and its 1/sqrt 2."""
-    L8, sk = lay.n_lin - 1, lay.skip
-    return [dict(W=pk.Bt[l], aux=_act(U, Ub, l), aux_beta=sig_beta(lay, l - 1), adiv=SQRT2 if l == sk else 1.0,
-                 nsplit=lay.out_dim[l - 1], split=split if l == sk else None, out_b=outs_b[l - 1], out_f=outs_f[l - 1])
-            for l in range(L8 - 1, 0, -1)]
-
-
 def sdf_query_fused(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, sdf_out: Optional[torch.Tensor] = None,
                     dst: Optional[torch.Tensor] = None) -> torch.Tensor:
     """SDFNetwork.sdf(x) with no gradient (neus_fields.py:268-283) in two launches: cn_sdf_embed writes the
@@ -358,15 +333,7 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
             S[L8 - 1] = _empty(M, HL, dev)
             ops.scale_cols(U[L8], HL, pk.w80p, S[L8 - 1], act_beta=sig_beta(lay, L8 - 1))
         QE = _empty(M, KE, dev) if sk >= 0 else None
-        chain = img and Sb[L8 - 1] is not None and _mul_chain_ok(lay, pk)
-        if chain:  # s_6 .. s_0 in one launch (the images, s_0 also in fp32, QE the skip's embedding columns)
-            for l in range(L8 - 1, 0, -1):
-                Sb[l - 1] = _empty_b(M, HL, dev)
-                S[l - 1] = _empty(M, HL, dev) if l - 1 == 0 else None
-            ops.mul_chain(Sb[L8 - 1], _mul_chain_steps(lay, pk, U, Ub, Sb, S, QE))
         for l in range(L8 - 1, 0, -1):
-            if chain:
-                break
             Kl = rup(lay.out_dim[l], 32)
             # bf16 mode: s_l is read by the next ∇ GEMM, a weight gradient and the second-order term
             # of the adjoint (all from its image); s_0 also by the first layer's fp32 weight gradient
@@ -576,19 +543,9 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
     share = want_dx and not second  # Z_l == P_l: dx from the parameter adjoint chain
     PE = _empty(M, KE, dev) if (share and sk >= 0) else None
     wq = ops.WgradQueue()  # the hidden layers' weight gradients: one launch after the chain
-    # first order with Z_7 and Z_1 .. Z_6 as images: Z_6 .. Z_0 in one launch (cn_mul_chain)
-    Zs = None
-    if not second and Z.dtype == torch.bfloat16 and _mul_chain_ok(lay, pk) and all(z_img(l) for l in range(1, L8 - 1)):
-        Zs = [None] * L8
-        Zs[L8 - 1] = Z
-        for l in range(L8 - 1, 0, -1):
-            Zs[l - 1] = _empty_b(M, HL, dev) if z_img(l - 1) else _empty(M, HL, dev)
-        zb = [z if z is not None and z.dtype == torch.bfloat16 else None for z in Zs]
-        zf = [z if z is not None and z.dtype == torch.float32 else None for z in Zs]
-        ops.mul_chain(Z, _mul_chain_steps(lay, pk, U, Ub, zb, zf, PE if share else None))
     for l in range(L8 - 1, -1, -1):
-        Zl = Z if Zs is None else Zs[l]
-        if l > 0 and Zs is None:
+        Zl = Z
+        if l > 0:
             zb = z_img(l - 1)  # Z_{l-1} as an operand image only
             Z = _empty_b(M, HL, dev) if zb else _empty(M, HL, dev)
             zo = dict(out0_b=Z) if zb else {}

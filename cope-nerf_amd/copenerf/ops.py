@@ -650,48 +650,6 @@ def sample(net, rays_o, rays_d, near, far, t_rand, time_step, n_samples, n_impor
     return z
 
 
-def mul_chain(src, steps):
-    """A chain of MUL layers in one launch (cn_mul_chain, bf16 mode): step t reads the previous step's
-    output (step 0: the bf16 image src [M, >= 256]) as the A operand.  steps: dicts with W (bf16 Bt image
-    [256][>= 256]), aux (bf16 activation image), aux_beta, adiv (1.0), nsplit (256), split (fp32 or None),
-    out_b (bf16 image or None for the last) and out_f (fp32 or None) -- each the cn_linear MUL arguments of
-    that layer with K = N = nzero = 256."""
-    if not 1 <= len(steps) <= _lib.CHAIN_MAX:
-        raise RuntimeError(f"mul_chain: 1 .. {_lib.CHAIN_MAX} steps")
-    _need(src, "src")
-    if src.dtype != torch.bfloat16:
-        raise RuntimeError("mul_chain: src must be a bfloat16 image")
-    M = src.shape[0]
-    d = _lib.MulChainDesc()
-    d.M, d.n, d.src, d.ld_src = M, len(steps), _ptr(src), _ld(src)
-    for t, st in enumerate(steps):
-        for k in ("W", "aux", "out_b"):
-            if st.get(k) is not None and st[k].dtype != torch.bfloat16:
-                raise RuntimeError(f"mul_chain: step {t} {k} must be bfloat16")
-        for k in ("W", "aux", "out_b", "out_f", "split"):
-            _need(st.get(k), f"step {t} {k}")
-            if k != "W" and st.get(k) is not None and st[k].shape[0] < M:
-                raise RuntimeError(f"mul_chain: step {t} {k} has fewer than M rows")
-        d.W[t], d.ldw[t] = _ptr(st["W"]), _ld(st["W"])
-        d.aux[t], d.ld_aux[t] = _ptr(st["aux"]), _ld(st["aux"])
-        d.aux_beta[t], d.adiv[t] = st["aux_beta"], st.get("adiv", 1.0)
-        d.nsplit[t] = st.get("nsplit", 256)
-        d.split[t], d.ld_split[t] = _ptr(st.get("split")), _ld(st.get("split"))
-        d.out_b[t], d.ld_out_b[t] = _ptr(st.get("out_b")), _ld(st.get("out_b"))
-        d.out_f[t], d.ld_out_f[t] = _ptr(st.get("out_f")), _ld(st.get("out_f"))
-    lib = _lib.load()
-    if _timer is not None:
-        e0 = _timer.start()
-        _lib.check(lib.cn_mul_chain(ctypes.byref(d), _stream()), "cn_mul_chain")
-        n = len(steps)
-        fl = 2.0 * M * 256 * 256 * n
-        nb = 2.0 * M * 256 * (1 + 2 * n) + sum(4.0 * M * 256 for st in steps if st.get("out_f") is not None)
-        _timer.symbols[("mul_chain",)] = "cn::mul_chain_kernel(cn::MulChainArgs)"
-        _timer.stop(("mul_chain",), e0, fl, nb)
-    else:
-        _lib.check(lib.cn_mul_chain(ctypes.byref(d), _stream()), "cn_mul_chain")
-
-
 def sdf_grad_assemble(multires, scale, U0, Q0, QE, G):
     _lib.call("cn_sdf_grad_assemble", U0.shape[0], multires, scale, _ptr(U0), _ld(U0), _ptr(Q0), _ld(Q0),
               _ptr(QE), _ld(QE), _ptr(G), _ld(G), _stream())

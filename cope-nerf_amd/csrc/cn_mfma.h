@@ -3,8 +3,6 @@
 // XCD-aware tile order.
 #pragma once
 
-#include <utility>
-
 #include "cn_common.h"
 
 namespace cn {
@@ -137,17 +135,6 @@ __device__ __forceinline__ void split3(floatx4 v, bf16x4& t0, bf16x4& t1, bf16x4
     t0 = __builtin_bit_cast(bf16x4, (u32x2){p0[0], p0[1]});
     t1 = __builtin_bit_cast(bf16x4, (u32x2){p1[0], p1[1]});
     t2 = __builtin_bit_cast(bf16x4, (u32x2){p2[0], p2[1]});
-}
-
-// f(integral_constant<int, I>) for I = 0 .. N-1, unrolled by construction (register arrays indexed by
-// I stay in registers; a loop the compiler declines to unroll would send them to scratch)
-template <typename F, int... I>
-__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
-    (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-    static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
 // s_waitcnt that waits for this wave's vector-memory count to drop to N (expcnt, lgkmcnt untouched).

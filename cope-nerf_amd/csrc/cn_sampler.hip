@@ -28,7 +28,20 @@
 // butterfly, then the two column halves).
 #include "cn_mfma.h"
 
+#include <utility>
+
 namespace cn {
+
+// f(integral_constant<int, I>) for I = 0 .. N-1, unrolled by construction (register arrays indexed by
+// I stay in registers; a loop the compiler declines to unroll would send them to scratch)
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 
 constexpr int kMlpLayers = 8;       // lin0 .. lin7 (lin8's sdf row is the head)
 constexpr int kMlpNS = 8;           // weight ring slots

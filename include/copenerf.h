@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define CN_ABI_VERSION 13
+#define CN_ABI_VERSION 12
 
 typedef void* cn_stream_t; /* hipStream_t */
 
@@ -532,52 +532,6 @@ typedef struct cn_sdf_mlp_desc {
     void* debug; /* NULL, or bf16 [8][M][256]: every layer's input as the kernel holds it (tests) */
 } cn_sdf_mlp_desc;
 int cn_sdf_mlp(const cn_sdf_mlp_desc* d, cn_stream_t stream);
-
-/* ------------------------------------------------------------------------ *
- * A chain of MUL layers in one launch (ABI v13; bf16 MFMA mode, 256-wide SDF
- * network): the ∇ₓSDF pass of the forward (neus_fields.py:291-303, s_{l-1} =
- * (W_lᵀ s_l) ⊙ σ_{l-1}) and the first-order adjoint chain of the backward
- * (Z_{l-1} = (W_lᵀ Z_l) ⊙ σ_{l-1}), each layer the cn_linear MUL epilogue with
- * bf16 operand images.  The chained operand stays on chip between the steps;
- * per step only σ's activation image is read and the step's outputs written.
- * Bitwise equal to the same steps as cn_linear launches (A = the previous
- * step's image, B = W[t], aux0 = aux[t], out0_b = out_b[t], out0 = out_f[t],
- * nsplit / out_split / adiv as given, K = N = nzero = 256; the first A = src).
- *   src      [M][ld_src] bf16: the chain's input (s_7 / Z_7 image);
- *   W[t]     bf16 images [256][ldw[t]] (K = 256 columns used) of the
- *            transposed weights (cn_pack_weights' Bt), t = 0 .. n - 1;
- *   aux[t]   [M][ld_aux[t]] bf16: the stored activation σ is recovered from,
- *            with aux_beta[t] as cn_linear's aux_beta (> 0);
- *   adiv[t]  divides W·in as cn_linear's adiv (0 or 1: none; sqrt 2 at the skip layer);
- *   nsplit[t] 256, or the split column: columns >= nsplit are 0 in the step's
- *            outputs and, when split[t] is given, go raw to it (fp32
- *            [M][ld_split], column c at c - nsplit: cn_linear's MUL split);
- *            without split[t] the step is cn_linear's MUL with N = nsplit;
- *   out_b[t] bf16 image [M][ld_out_b] of the step's output (required for
- *            t < n - 1: the next step's operand, as the layer path stores it;
- *            may be NULL for the last);  out_f[t] fp32 [M][ld_out_f] or NULL.
- * Leading dimensions: bf16 ones multiples of 8 (16-byte rows), fp32 ones of 4.
- * ------------------------------------------------------------------------ */
-#define CN_CHAIN_MAX 8
-typedef struct cn_mul_chain_desc {
-    int32_t M, n;
-    const void* src;
-    int64_t ld_src;
-    const void* W[CN_CHAIN_MAX];
-    int64_t ldw[CN_CHAIN_MAX];
-    const void* aux[CN_CHAIN_MAX];
-    int64_t ld_aux[CN_CHAIN_MAX];
-    float aux_beta[CN_CHAIN_MAX];
-    float adiv[CN_CHAIN_MAX];
-    int32_t nsplit[CN_CHAIN_MAX];
-    float* split[CN_CHAIN_MAX];
-    int64_t ld_split[CN_CHAIN_MAX];
-    void* out_b[CN_CHAIN_MAX];
-    int64_t ld_out_b[CN_CHAIN_MAX];
-    float* out_f[CN_CHAIN_MAX];
-    int64_t ld_out_f[CN_CHAIN_MAX];
-} cn_mul_chain_desc;
-int cn_mul_chain(const cn_mul_chain_desc* d, cn_stream_t stream);
 
 /* ------------------------------------------------------------------------ *
  * Composed entry points (ABI v12): the sampler of NeuSRenderer.render

@@ -36,7 +36,7 @@ def test_struct_layouts_match_header_order():
     src = open(HEADER).read()
     for cname, py in (("cn_linear_desc", _lib.LinearDesc), ("cn_wgrad_desc", _lib.WgradDesc),
                       ("cn_sdf_mlp_desc", _lib.SdfMlpDesc), ("cn_sdf_net", _lib.SdfNet),
-                      ("cn_sample_desc", _lib.SampleDesc), ("cn_mul_chain_desc", _lib.MulChainDesc)):
+                      ("cn_sample_desc", _lib.SampleDesc)):
         body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (cname, cname), src, re.S).group(1)
         body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
         names = []
@@ -161,36 +161,6 @@ def test_composed_entry_points_plan_without_gpu():
     n.w_rows[2] = 128  # an image too small for its layer
     assert lib.cn_sample(ctypes.byref(d), 4096 * 256, want, None) == -2
     assert b"layer 2 image" in lib.cn_last_error()
-
-
-def test_mul_chain_validation_without_gpu():
-    """ABI v13: cn_mul_chain checks its steps on the host."""
-    from copenerf import _lib
-    lib = _lib.load()
-    assert lib.cn_mul_chain(None, None) == -1
-    d = _lib.MulChainDesc()
-    d.M, d.n, d.src, d.ld_src = 1000, 2, 4096, 256
-    for t in range(2):
-        d.W[t], d.ldw[t], d.aux[t], d.ld_aux[t] = 4096, 256, 4096, 256
-        d.aux_beta[t], d.nsplit[t], d.out_b[t], d.ld_out_b[t] = 100.0, 256, 4096, 256
-    d.n = 9
-    assert lib.cn_mul_chain(ctypes.byref(d), None) == -2
-    d.n = 2
-    d.out_b[0] = None  # the next step's operand
-    assert lib.cn_mul_chain(ctypes.byref(d), None) == -1
-    assert b"step 0 needs its image" in lib.cn_last_error()
-    d.out_b[0] = 4096
-    d.aux_beta[1] = 0.0
-    assert lib.cn_mul_chain(ctypes.byref(d), None) == -1
-    assert b"aux_beta" in lib.cn_last_error()
-    d.aux_beta[1] = 100.0
-    d.nsplit[1] = 202  # not a multiple of 4
-    assert lib.cn_mul_chain(ctypes.byref(d), None) == -2
-    d.nsplit[1], d.split[1], d.ld_split[1] = 204, 4096, 16  # a split view narrower than its 52 columns
-    assert lib.cn_mul_chain(ctypes.byref(d), None) == -1
-    d.ld_split[1] = 64
-    d.ldw[0] = 100  # weights narrower than K = 256
-    assert lib.cn_mul_chain(ctypes.byref(d), None) == -3
 
 
 def test_product_path_refuses_cpu_tensors():
