@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libcopenerf.so"
 LIB_PATH = os.environ.get("COPENERF_LIB", os.path.join(_HERE, LIB_NAME))
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 c_f32p = ctypes.c_void_p  # device pointers are passed as integers
 c_i32 = ctypes.c_int32
@@ -98,6 +98,17 @@ class SdfNet(ctypes.Structure):
         ("flags", c_i32),
         ("W", c_ptr * (SDF_MAX_LIN - 1)), ("w_rows", c_i32 * (SDF_MAX_LIN - 1)), ("w_cols", c_i32 * (SDF_MAX_LIN - 1)),
         ("bias", c_ptr * (SDF_MAX_LIN - 1)), ("head_w", c_ptr), ("head_b", c_ptr),
+        ("Wt", c_ptr * (SDF_MAX_LIN - 1)), ("wt_rows", c_i32 * (SDF_MAX_LIN - 1)), ("wt_cols", c_i32 * (SDF_MAX_LIN - 1)),
+        ("head_wp", c_ptr),
+    ]
+
+
+class ColorNet(ctypes.Structure):
+    _fields_ = [
+        ("n_lin", c_i32), ("in_dim", c_i32 * SDF_MAX_LIN), ("out_dim", c_i32 * SDF_MAX_LIN), ("d_feature", c_i32),
+        ("multires_view", c_i32), ("mfma_dtype", c_i32),
+        ("W", c_ptr * (SDF_MAX_LIN - 1)), ("w_rows", c_i32 * (SDF_MAX_LIN - 1)), ("w_cols", c_i32 * (SDF_MAX_LIN - 1)),
+        ("bias", c_ptr * (SDF_MAX_LIN - 1)), ("head_w", c_ptr), ("head_b", c_ptr),
     ]
 
 
@@ -106,6 +117,16 @@ class SampleDesc(ctypes.Structure):
         ("R", c_i32), ("n_samples", c_i32), ("n_importance", c_i32), ("up_sample_steps", c_i32),
         ("rays_o", c_ptr), ("rays_d", c_ptr), ("near", c_ptr), ("far", c_ptr), ("t_rand", c_ptr),
         ("time_step", c_ptr), ("net", ctypes.POINTER(SdfNet)), ("z", c_ptr),
+    ]
+
+
+class RenderDesc(ctypes.Structure):
+    _fields_ = [
+        ("R", c_i32), ("n_samples", c_i32), ("n_importance", c_i32), ("up_sample_steps", c_i32), ("S_in", c_i32),
+        ("rays_o", c_ptr), ("rays_d", c_ptr), ("near", c_ptr), ("far", c_ptr), ("t_rand", c_ptr), ("time_step", c_ptr),
+        ("z_in", c_ptr), ("inv_s", c_ptr), ("cos_anneal_ratio", c_ptr), ("sdf_net", ctypes.POINTER(SdfNet)),
+        ("color_net", ctypes.POINTER(ColorNet)), ("z", c_ptr), ("pts", c_ptr), ("sdf", c_ptr), ("grad", c_ptr),
+        ("rgb", c_ptr), ("color", c_ptr), ("depth", c_ptr), ("weights", c_ptr), ("cdf", c_ptr),
     ]
 
 
@@ -173,6 +194,8 @@ SIGNATURES = {
     "cn_sdf_query": (c_i32, [ctypes.POINTER(SdfNet), c_i32, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_i64, c_ptr]),
     "cn_sample_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(SampleDesc)]),
     "cn_sample": (c_i32, [ctypes.POINTER(SampleDesc), c_ptr, c_i64, c_ptr]),
+    "cn_render_fwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(RenderDesc)]),
+    "cn_render_fwd": (c_i32, [ctypes.POINTER(RenderDesc), c_ptr, c_i64, c_ptr]),
 }
 
 _lock = threading.Lock()

@@ -609,7 +609,73 @@ def sdf_net(lay, pk, layered=False):
         n.bias[l] = aligned(pk.b[l])
     n.head_w = aligned(pk.w80.reshape(-1))
     n.head_b = aligned(pk.b80.reshape(-1))
+    for l in range(lay.n_lin - 1):  # the transposed images (cn_render_fwd's ∇ pass)
+        B = pk.Bt[l]
+        if not B.is_contiguous():
+            raise RuntimeError(f"sdf_net: layer {l} transposed image must be contiguous")
+        keep.append(B)
+        n.Wt[l] = B.data_ptr()
+        n.wt_rows[l], n.wt_cols[l] = (B.shape[1], 16 * B.shape[0]) if x6 else (B.shape[0], B.shape[1])
+    n.head_wp = aligned(pk.w80p)
     return n, keep
+
+
+def color_net(lay, pk):
+    """cn_color_net of a packed RenderingNetwork (fields.ColorLayout + fields.pack_color's images, lin0 folded
+    or not), and the tensors it points into."""
+    n, keep = _lib.ColorNet(), []
+    n.n_lin, n.d_feature, n.multires_view = lay.n_lin, lay.F, lay.multires_view
+    for l in range(lay.n_lin):
+        n.in_dim[l], n.out_dim[l] = lay.in_dim[l], lay.out_dim[l]
+    B0 = pk.Bf[0]
+    x6 = B0.dim() == 3
+    n.mfma_dtype = 2 if x6 else (1 if B0.dtype == torch.bfloat16 else 0)
+
+    def aligned(t):
+        t = t.contiguous()
+        if t.data_ptr() % 16:
+            t = t.clone()
+        keep.append(t)
+        return t.data_ptr()
+
+    for l in range(lay.n_lin - 1):
+        B = pk.Bf[l]
+        keep.append(B)
+        n.W[l] = B.data_ptr()
+        n.w_rows[l], n.w_cols[l] = (B.shape[1], 16 * B.shape[0]) if x6 else (B.shape[0], B.shape[1])
+        n.bias[l] = aligned(pk.b[l])
+    n.head_w = aligned(pk.W3)
+    n.head_b = aligned(pk.b3)
+    return n, keep
+
+
+def render_fwd(sdf_net_, color_net_, rays_o, rays_d, near, far, time_step, inv_s, car, n_samples, n_importance,
+               up_sample_steps, t_rand=None, z_in=None):
+    """NeuSRenderer.forward without gradient in one call (cn_render_fwd): returns z, pts, sdf, grad, rgb, color,
+    depth, weights, cdf."""
+    R, dev = rays_o.shape[0], rays_o.device
+    if z_in is not None:
+        z_in = z_in.contiguous().float()
+        S = z_in.shape[1]
+    else:
+        k = n_importance // up_sample_steps if n_importance > 0 else 0
+        S = n_samples + up_sample_steps * k
+    f = lambda *s: torch.empty(*s, device=dev)  # noqa: E731
+    out = dict(z=f(R, S), pts=f(R * S, 4), sdf=f(R * S), grad=f(R * S, 4), rgb=f(R * S, 3), color=f(R, 3),
+               depth=f(R), weights=f(R, S), cdf=f(R, S))
+    d = _lib.RenderDesc()
+    d.R, d.n_samples, d.n_importance, d.up_sample_steps = R, n_samples, n_importance, up_sample_steps
+    d.S_in = S if z_in is not None else 0
+    d.rays_o, d.rays_d, d.near, d.far = _ptr(rays_o), _ptr(rays_d), _ptr(near), _ptr(far)
+    d.t_rand, d.time_step, d.z_in = _ptr(t_rand), _ptr(time_step), _ptr(z_in)
+    d.inv_s, d.cos_anneal_ratio = _ptr(inv_s), _ptr(car)
+    d.sdf_net, d.color_net = ctypes.pointer(sdf_net_), ctypes.pointer(color_net_)
+    for k, v in out.items():
+        setattr(d, k, v.data_ptr())
+    lib = _lib.load()
+    ws = torch.empty(max(int(lib.cn_render_fwd_workspace_bytes(ctypes.byref(d))), 1), dtype=torch.uint8, device=dev)
+    _lib.check(lib.cn_render_fwd(ctypes.byref(d), _ptr(ws), ws.numel(), _stream()), "cn_render_fwd")
+    return out
 
 
 def sdf_query(net, x, sdf, idx=None):

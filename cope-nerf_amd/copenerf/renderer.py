@@ -21,6 +21,9 @@ from .fields import _empty
 # the sampler as one C call (cn_sample: coarse z, the up-sampling rounds and their SDF queries composed in
 # C++); False: launch by launch from Python (sample_z_composed)
 SAMPLE_NATIVE = True
+# the forward without gradient (evaluation, inference) as one C call (cn_render_fwd) where the feature head folds;
+# False: launch by launch from Python
+RENDER_NATIVE = True
 
 
 class _PointsFn(torch.autograd.Function):
@@ -221,6 +224,9 @@ class NeuSRenderer(nn.Module):
         col_packed = self.color_network.params_and_pack(
             fold_feature=(sdf_packed[0][-1], sdf_packed[1][-1]) if fold else None)
         self.last_sdf_pack = sdf_packed if self.expose_sdf_pack else None
+        if RENDER_NATIVE and fold and not torch.is_grad_enabled() and background_rgb is None and ops._timer is None:
+            return self._forward_native(rays_o, rays_d, ray_d_norm, time_step, near, far, n_samples, n_importance,
+                                        t_rand, z_vals, sdf_packed, col_packed, cos_anneal_ratio, eval)
         if z_vals is None:
             z = self.sample_z(rays_o, rays_d, time_step, near, far, n_samples, n_importance, t_rand, sdf_packed)
         else:
@@ -265,6 +271,40 @@ class NeuSRenderer(nn.Module):
             "inside_sphere": torch.ones_like(weights),
             "weight_inside": weight_inside,
             "weight_outside": weight_outside,
+        }
+
+    def _forward_native(self, rays_o, rays_d, ray_d_norm, time_step, near, far, n_samples, n_importance, t_rand,
+                        z_vals, sdf_packed, col_packed, cos_anneal_ratio, eval):
+        """forward without gradient as one cn_render_fwd call (the sampler, the fields with the folded feature
+        head and the compositing composed in C++: the same launches as the path below, the same bits)."""
+        R, dev = rays_o.shape[0], rays_o.device
+        sn, k1 = ops.sdf_net(self.sdf_network.layout(), sdf_packed[2])
+        cn, k2 = ops.color_net(self.color_network.layout(), col_packed[2])
+        inv_s = self.deviation_network(torch.zeros([1, 3], device=dev))[:, :1].clip(1 / 1e3, 1 / 1e-3).contiguous()
+        car = ops.device_scalar(cos_anneal_ratio, dev)
+        o = ops.render_fwd(sn, cn, rays_o, rays_d, near, far, time_step, inv_s, car, n_samples, n_importance,
+                           self.up_sample_steps, t_rand=t_rand, z_in=z_vals)
+        del k1, k2
+        S = o["z"].shape[1]
+        depth = o["depth"].view(R, 1)
+        weights = o["weights"]
+        G = o["grad"]
+        return {
+            "sdf": o["sdf"].view(R * S, 1),
+            "color_fine": o["color"],
+            "depth_pred": depth / ray_d_norm if eval else depth,
+            "weighted_z_vals": depth.clone(),
+            "s_val": (1.0 / inv_s).expand(R * S, 1).reshape(R, S).mean(dim=-1, keepdim=True),
+            "cdf_fine": o["cdf"],
+            "weight_sum": weights.sum(dim=-1, keepdim=True),
+            "weight_max": torch.max(weights, dim=-1, keepdim=True)[0],
+            "normals": G[:, :3].reshape(R, S, 3),
+            "sdf_flows": G[:, 3:].reshape(R, S, 1),
+            "sampled_points": o["pts"][:, :3].reshape(R, S, 3),
+            "weights": weights,
+            "inside_sphere": torch.ones_like(weights),
+            "weight_inside": weights.sum(dim=-1),
+            "weight_outside": weights.new_zeros(R),
         }
 
     def extract_geometry(self, bound_min, bound_max, resolution, threshold=0.0):

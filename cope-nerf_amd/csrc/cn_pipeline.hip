@@ -344,3 +344,455 @@ extern "C" int cn_sample(const cn_sample_desc* d, void* workspace, int64_t works
     (void)st;
     return CN_OK;
 }
+
+// ---------------------------------------------------------------------------------------------
+// cn_render_fwd: NeuSRenderer.forward without gradient (neus_renderer.py:453-584, render_core
+// 307-450) composed from the launches copenerf's renderer makes in eval mode with the folded
+// feature head: cn_sample, cn_points (midpoints), the SDF field (fields.sdf_forward with
+// want_feat "hidden", want_grad, keep False), the colour field (_ColorFieldFn.forward) and
+// cn_composite_fwd -- descriptor for descriptor, so the same bits.
+namespace {
+
+struct ColorShape {
+    int KX, HL;
+    bool bf, x6, img;
+};
+
+int color_shape(const cn_color_net* c, ColorShape* s) {
+    CN_REQUIRE(c, CN_ERR_ARG, "cn_color_net: null");
+    CN_REQUIRE(c->n_lin >= 2 && c->n_lin <= CN_SDF_MAX_LIN, CN_ERR_SHAPE, "cn_color_net: n_lin %d", c->n_lin);
+    CN_REQUIRE(c->mfma_dtype >= CN_MFMA_F32 && c->mfma_dtype <= CN_MFMA_F32_BF16X6, CN_ERR_ARG, "cn_color_net: mfma_dtype");
+    CN_REQUIRE(c->multires_view >= 0 && c->multires_view <= 12 && c->d_feature % 32 == 0 && c->d_feature > 0,
+               CN_ERR_SHAPE, "cn_color_net: multires_view %d / d_feature %d", c->multires_view, c->d_feature);
+    const int n = c->n_lin;
+    s->KX = rup_i(4 + 4 + 3 * (1 + 2 * c->multires_view), 64);
+    CN_REQUIRE(c->out_dim[n - 1] == 3 && c->in_dim[0] == 4 + 3 * (1 + 2 * c->multires_view) + 4 + c->d_feature,
+               CN_ERR_SHAPE, "cn_color_net: lin0 takes %d inputs, the head gives %d", c->in_dim[0], c->out_dim[n - 1]);
+    int hl = 0;
+    for (int l = 0; l < n - 1; ++l) hl = c->out_dim[l] > hl ? c->out_dim[l] : hl;
+    for (int l = 1; l < n; ++l)
+        CN_REQUIRE(c->in_dim[l] == c->out_dim[l - 1], CN_ERR_SHAPE, "cn_color_net: lin%d widths", l);
+    s->HL = rup_i(hl, 128);
+    s->x6 = c->mfma_dtype == CN_MFMA_F32_BF16X6;
+    s->bf = c->mfma_dtype == CN_MFMA_BF16;
+    s->img = s->bf && s->HL % 256 == 0;
+    const int kq = s->bf ? 64 : 32;
+    for (int l = 0; l < n - 1; ++l) {
+        const int kp = l == 0 ? c->d_feature + s->KX : rup_i(c->in_dim[l], kq);
+        CN_REQUIRE(c->W[l] && c->bias[l] && ((uintptr_t)c->W[l] & 15) == 0 && ((uintptr_t)c->bias[l] & 15) == 0,
+                   CN_ERR_ALIGN, "cn_color_net: layer %d weights / bias null or not 16-byte aligned", l);
+        CN_REQUIRE(c->w_rows[l] >= rup_i(c->out_dim[l], 128) && c->w_cols[l] >= kp, CN_ERR_SHAPE,
+                   "cn_color_net: layer %d image [%d][%d] too small", l, c->w_rows[l], c->w_cols[l]);
+    }
+    CN_REQUIRE(c->head_w && c->head_b, CN_ERR_ARG, "cn_color_net: head null");
+    return CN_OK;
+}
+
+// copenerf.ops.linear's descriptor for these arguments (K rounded to 64 in the bf16 mode, the tile by
+// the widths, ldb by the image format)
+struct LinCall {
+    const void* A = nullptr;
+    bool a_b = false;
+    int64_t lda = 0;
+    const void* A2 = nullptr;
+    int64_t lda2 = 0;
+    int K1 = -1;
+    const void* B = nullptr;
+    int b_rows = 0, b_cols = 0;
+    int N = 0, K = 0, nzero = -1, nsplit = -1, epi = CN_EPI_STORE;
+    const float* bias = nullptr;
+    const float* colv = nullptr;
+    const void* aux0 = nullptr;
+    bool aux0_b = false;
+    int64_t ld_aux0 = 0;
+    float aux_beta = 0.0f, adiv = 1.0f, odiv = 1.0f, beta = 100.0f, threshold = 20.0f;
+    float* out0 = nullptr;
+    int64_t ld_out0 = 0;
+    void* out0_b = nullptr;
+    int64_t ld_out0_b = 0;
+    float* out1 = nullptr;
+    int64_t ld_out1 = 0;
+    void* out1_b = nullptr;
+    int64_t ld_out1_b = 0;
+    float* out_split = nullptr;
+    int64_t ld_split = 0;
+    const float* head_w = nullptr;
+    const float* head_b = nullptr;
+    float* head_out = nullptr;
+    int M = 0;
+};
+
+int run_linear(int mode, const LinCall& c, int flip, hipStream_t st) {
+    const bool x6 = mode == CN_MFMA_F32_BF16X6, bf = mode == CN_MFMA_BF16;
+    cn_linear_desc d{};
+    int K = c.K, K1 = c.K1 < 0 ? -1 : c.K1;
+    if (bf) {
+        K = rup_i(K, 64);
+        if (K1 >= 0) K1 = rup_i(K1, 64);
+    }
+    d.A = c.A;
+    d.A2 = c.A2;
+    d.B = static_cast<const float*>(c.B);
+    d.bias = c.bias;
+    d.colv = c.colv;
+    d.aux0 = c.aux0;
+    d.out0 = c.out0;
+    d.out1 = c.out1;
+    d.out_split = c.out_split;
+    d.head_w = c.head_w;
+    d.head_b = c.head_b;
+    d.head_out = c.head_out;
+    d.aux_beta = c.aux_beta;
+    d.lda = c.lda;
+    d.lda2 = c.lda2;
+    d.ldb = x6 ? c.b_rows : c.b_cols;
+    d.ld_aux0 = c.ld_aux0;
+    d.ld_out0 = c.ld_out0;
+    d.ld_out1 = c.ld_out1;
+    d.ld_split = c.ld_split;
+    d.M = c.M;
+    d.N = c.N;
+    d.K = K;
+    d.K1 = K1 >= 0 ? K1 : K;
+    d.nzero = c.nzero >= 0 ? c.nzero : c.N;
+    d.nsplit = c.nsplit >= 0 ? c.nsplit : c.N;
+    d.epilogue = c.epi;
+    const int nz = c.nzero >= 0 ? c.nzero : 0;
+    d.tile = (c.N > nz ? c.N : nz) <= 64 ? 1 : 0;
+    d.adiv = c.adiv;
+    d.odiv = c.odiv;
+    d.beta = c.beta;
+    d.threshold = c.threshold;
+    d.mfma_dtype = mode;
+    d.a_bf16 = c.a_b ? 1 : 0;
+    d.aux0_bf16 = c.aux0_b ? 1 : 0;
+    d.out0_b = c.out0_b;
+    d.ld_out0_b = c.ld_out0_b;
+    d.out1_b = c.out1_b;
+    d.ld_out1_b = c.ld_out1_b;
+    d.flags = flip & 1;
+    return cn_linear(&d, st);
+}
+
+// softplus' σ_l's aux_beta as fields.sig_beta computes it (in double, then to float)
+float sig_beta(const cn_sdf_net* n, int l) {
+    return (float)((double)n->beta * ((l + 1) == n->skip ? std::sqrt(2.0) : 1.0));
+}
+
+// The SDF field with its ∇ₓSDF pass (fields.sdf_forward, want_feat "hidden", want_grad, keep False):
+// sdf [M], U8 (the last hidden activation, fp32 [M][HL]: the colour network's operand) and G [M][4].
+int sdf_field_plan(const cn_sdf_net* n, const NetShape& s, int M, const float* x, float* sdf, float** U8_out,
+                   float* G, Plan& ws, hipStream_t st, bool run) {
+    const float kSqrt2 = (float)std::sqrt(2.0);
+    const int L8 = s.L8, HL = s.HL, sk = s.sk, KE = s.KE;
+    const size_t eh = s.img ? 2 : 4;  // the hidden activations' element size (bf16 images in the image mode)
+    const bool usk_b = s.img && sk >= 1 && sk < L8;
+    float* U0 = static_cast<float*>(ws.take((size_t)M * KE * 4));
+    // U[1 .. L8]: every activation is kept (σ's source in the ∇ pass); U[sk] is the skip input
+    char* U[CN_SDF_MAX_LIN] = {};
+    bool ub[CN_SDF_MAX_LIN] = {};
+    for (int l = 1; l <= L8; ++l) {
+        ub[l] = (l == sk) ? usk_b : (s.img && l < L8);
+        U[l] = static_cast<char*>(ws.take((size_t)M * HL * (ub[l] ? 2 : 4)));
+    }
+    const bool fp32_s7 = !s.img;  // the image mode with the folded head keeps s_7 as its image only
+    float* S7 = static_cast<float*>(ws.take((size_t)M * HL * 4));
+    void* S7b = s.img ? ws.take((size_t)M * HL * 2) : nullptr;
+    // the ∇ pass: two ping-pong adjoints (images in the image mode), s_0 also fp32, QE, Q0
+    char* Sp[2] = {static_cast<char*>(ws.take((size_t)M * HL * eh)), static_cast<char*>(ws.take((size_t)M * HL * eh))};
+    float* S0 = static_cast<float*>(ws.take((size_t)M * HL * 4));
+    float* QE = sk >= 0 ? static_cast<float*>(ws.take((size_t)M * KE * 4)) : nullptr;
+    float* Q0 = static_cast<float*>(ws.take((size_t)M * KE * 4));
+    if (!run) return CN_OK;
+    void* e_view = nullptr;
+    if (sk >= 0) e_view = U[sk] + (size_t)n->out_dim[sk - 1] * (usk_b ? 2 : 4);
+    int rc = cn_sdf_embed(M, x, 4, n->multires, n->scale, KE, U0, KE, e_view, e_view ? HL : 0, kSqrt2, usk_b ? 1 : 0, st);
+    if (rc) return rc;
+    int flip = 0;
+    bool have_s7 = false, have_s7b = false;
+    for (int l = 0; l < L8; ++l) {
+        const bool into = (l + 1) == sk;
+        LinCall c;
+        c.A = l == 0 ? static_cast<const void*>(U0) : U[l];
+        c.a_b = l > 0 && ub[l];
+        c.lda = l == 0 ? KE : HL;
+        c.B = n->W[l];
+        c.b_rows = n->w_rows[l];
+        c.b_cols = n->w_cols[l];
+        c.N = n->out_dim[l];
+        c.K = l == 0 ? KE : rup_i(n->in_dim[l], 32);
+        c.bias = n->bias[l];
+        c.beta = n->beta;
+        c.threshold = n->threshold;
+        c.M = M;
+        if (l == L8 - 1 && s.fuse_head) {
+            c.epi = CN_EPI_SOFTPLUS_HEAD;
+            c.out0 = reinterpret_cast<float*>(U[L8]);
+            c.ld_out0 = HL;
+            c.nzero = HL;
+            if (fp32_s7) {
+                c.out1 = S7;
+                c.ld_out1 = HL;
+                have_s7 = true;
+            }
+            if (S7b) {
+                c.out1_b = S7b;
+                c.ld_out1_b = HL;
+                have_s7b = true;
+            }
+            c.colv = n->head_wp;
+            c.aux_beta = sig_beta(n, l);
+            c.head_w = n->head_w;
+            c.head_b = n->head_b;
+            c.head_out = sdf;
+        } else {
+            c.epi = CN_EPI_SOFTPLUS;
+            c.nzero = into ? n->out_dim[l] : HL;
+            if (into) c.odiv = kSqrt2;
+            if (ub[l + 1]) {
+                c.out0_b = U[l + 1];
+                c.ld_out0_b = HL;
+            } else {
+                c.out0 = reinterpret_cast<float*>(U[l + 1]);
+                c.ld_out0 = HL;
+            }
+        }
+        if ((rc = run_linear(n->mfma_dtype, c, flip++, st))) return rc;
+    }
+    float* U8 = reinterpret_cast<float*>(U[L8]);
+    *U8_out = U8;
+    if (!s.fuse_head &&
+        (rc = cn_row_head(M, n->in_dim[L8], U8, HL, n->head_w, n->in_dim[L8], n->head_b, 1, 0, sdf, 1, nullptr, st)))
+        return rc;
+    if (!have_s7 && !have_s7b) {
+        if ((rc = cn_scale_cols(M, HL, U8, HL, n->head_wp, nullptr, S7, HL, sig_beta(n, L8 - 1), st))) return rc;
+        have_s7 = true;
+    }
+    // ∇ pass: s_{l-1} = (W_lᵀ s_l) ⊙ σ_{l-1}, l = L8-1 .. 1 (the skip layer's embedding columns to QE)
+    const void* A = have_s7b ? S7b : static_cast<const void*>(S7);
+    bool a_b = have_s7b;
+    for (int l = L8 - 1; l >= 1; --l) {
+        LinCall c;
+        c.A = A;
+        c.a_b = a_b;
+        c.lda = HL;
+        c.B = n->Wt[l];
+        c.b_rows = n->wt_rows[l];
+        c.b_cols = n->wt_cols[l];
+        c.K = rup_i(n->out_dim[l], 32);
+        c.epi = CN_EPI_MUL;
+        c.aux0 = U[l];
+        c.aux0_b = ub[l];
+        c.ld_aux0 = HL;
+        c.aux_beta = sig_beta(n, l - 1);
+        c.nzero = HL;
+        c.M = M;
+        c.beta = n->beta;
+        c.threshold = n->threshold;
+        if (l == sk) {
+            c.N = n->in_dim[l];
+            c.nsplit = n->out_dim[l - 1];
+            c.out_split = QE;
+            c.ld_split = KE;
+            c.adiv = kSqrt2;
+        } else {
+            c.N = n->out_dim[l - 1];
+        }
+        char* dst = Sp[l & 1];
+        if (s.img) {
+            c.out0_b = dst;
+            c.ld_out0_b = HL;
+            if (l - 1 == 0) {
+                c.out0 = S0;
+                c.ld_out0 = HL;
+            }
+        } else {
+            c.out0 = l - 1 == 0 ? S0 : reinterpret_cast<float*>(dst);
+            c.ld_out0 = HL;
+        }
+        if ((rc = run_linear(n->mfma_dtype, c, flip++, st))) return rc;
+        A = s.img ? static_cast<const void*>(dst) : static_cast<const void*>(c.out0);
+        a_b = s.img;
+    }
+    {  // Q0 = W_0ᵀ s_0 (the embedding's adjoint), then ∇ₓSDF
+        LinCall c;
+        c.A = A;
+        c.a_b = a_b;
+        c.lda = HL;
+        c.B = n->Wt[0];
+        c.b_rows = n->wt_rows[0];
+        c.b_cols = n->wt_cols[0];
+        c.N = s.E;
+        c.K = rup_i(n->out_dim[0], 32);
+        c.epi = CN_EPI_STORE;
+        c.out0 = Q0;
+        c.ld_out0 = KE;
+        c.nzero = KE;
+        c.M = M;
+        c.beta = n->beta;
+        c.threshold = n->threshold;
+        if ((rc = run_linear(n->mfma_dtype, c, flip++, st))) return rc;
+    }
+    return cn_sdf_grad_assemble(M, n->multires, n->scale, U0, KE, Q0, KE, QE, QE ? KE : 0, G, 4, st);
+}
+
+// the colour network (_ColorFieldFn.forward): rgb [M][3]
+int color_field_plan(const cn_color_net* c, const ColorShape& s, int M, const float* G, const float* pts,
+                     const float* dirs, int dir_div, const float* feat, int64_t ld_feat, float* rgb, Plan& ws,
+                     hipStream_t st, bool run) {
+    const int n = c->n_lin, HL = s.HL;
+    float* ext = static_cast<float*>(ws.take((size_t)M * s.KX * 4));
+    char* H[2] = {static_cast<char*>(ws.take((size_t)M * HL * 4)), static_cast<char*>(ws.take((size_t)M * HL * 4))};
+    if (!run) return CN_OK;
+    int rc = cn_color_extras(M, G, 4, pts, 4, dirs, 3, dir_div, c->multires_view, s.KX, ext, s.KX, st);
+    if (rc) return rc;
+    const void* A = feat;
+    bool a_b = false;
+    int64_t lda = ld_feat;
+    const float* last = nullptr;
+    for (int l = 0; l < n - 1; ++l) {
+        LinCall k;
+        k.A = A;
+        k.a_b = a_b;
+        k.lda = lda;
+        if (l == 0) {
+            k.A2 = ext;
+            k.lda2 = s.KX;
+            k.K1 = c->d_feature;
+            k.K = c->d_feature + s.KX;
+        } else {
+            k.K = rup_i(c->out_dim[l - 1], 32);
+        }
+        k.B = c->W[l];
+        k.b_rows = c->w_rows[l];
+        k.b_cols = c->w_cols[l];
+        k.N = c->out_dim[l];
+        k.epi = CN_EPI_RELU;
+        k.bias = c->bias[l];
+        k.nzero = HL;
+        k.M = M;
+        char* dst = H[l & 1];
+        const bool img = s.img && l < n - 2;  // the next layer's operand image, the activation's only copy
+        if (img) {
+            k.out0_b = dst;
+            k.ld_out0_b = HL;
+        } else {
+            k.out0 = reinterpret_cast<float*>(dst);
+            k.ld_out0 = HL;
+        }
+        if ((rc = run_linear(c->mfma_dtype, k, l, st))) return rc;
+        A = dst;
+        a_b = img;
+        lda = HL;
+        last = reinterpret_cast<const float*>(dst);
+    }
+    return cn_row_head(M, c->in_dim[n - 1], last, HL, c->head_w, c->in_dim[n - 1], c->head_b, 3, 1, rgb, 3, nullptr, st);
+}
+
+int render_check(const cn_render_desc* d, NetShape* s, ColorShape* cs) {
+    CN_REQUIRE(d, CN_ERR_ARG, "cn_render_fwd: null descriptor");
+    int rc = net_shape(d->sdf_net, s);
+    if (rc) return rc;
+    if ((rc = color_shape(d->color_net, cs))) return rc;
+    const cn_sdf_net* n = d->sdf_net;
+    const cn_color_net* c = d->color_net;
+    CN_REQUIRE(n->mfma_dtype == c->mfma_dtype, CN_ERR_ARG, "cn_render_fwd: the networks' GEMM modes differ");
+    // the folded feature head (copenerf.renderer's fold): the colour network reads the SDF's last hidden layer
+    CN_REQUIRE(n->in_dim[s->L8] == s->HL && s->HL == c->d_feature && n->out_dim[s->L8] == 1 + c->d_feature,
+               CN_ERR_UNSUPPORTED, "cn_render_fwd: needs the folded feature head (SDF hidden width == d_feature)");
+    for (int l = 0; l < s->L8; ++l) {
+        const int kq = s->bf ? 64 : 32;
+        CN_REQUIRE(n->Wt[l] && ((uintptr_t)n->Wt[l] & 15) == 0 && n->wt_rows[l] >= rup_i(n->in_dim[l], 128) &&
+                       n->wt_cols[l] >= rup_i(n->out_dim[l], kq),
+                   CN_ERR_SHAPE, "cn_render_fwd: transposed image %d missing or too small", l);
+    }
+    CN_REQUIRE(n->head_wp && ((uintptr_t)n->head_wp & 15) == 0, CN_ERR_ALIGN, "cn_render_fwd: head_wp [HL] (16-byte aligned)");
+    CN_REQUIRE(d->R >= 0 && d->rays_o && d->rays_d && d->near && d->far && d->time_step && d->inv_s &&
+                   d->cos_anneal_ratio,
+               CN_ERR_ARG, "cn_render_fwd: null input");
+    CN_REQUIRE(d->z && d->pts && d->sdf && d->grad && d->rgb && d->color && d->depth && d->weights && d->cdf,
+               CN_ERR_ARG, "cn_render_fwd: null output");
+    CN_REQUIRE(((uintptr_t)d->pts & 15) == 0 && ((uintptr_t)d->grad & 15) == 0, CN_ERR_ALIGN,
+               "cn_render_fwd: pts / grad 16-byte aligned");
+    if (d->z_in)
+        CN_REQUIRE(d->S_in >= 1 && d->n_samples >= 1, CN_ERR_SHAPE, "cn_render_fwd: z_in needs S_in and n_samples");
+    return CN_OK;
+}
+
+int render_S(const cn_render_desc* d) {
+    if (d->z_in) return d->S_in;
+    const int k = d->n_importance > 0 ? d->n_importance / d->up_sample_steps : 0;
+    return d->n_samples + d->up_sample_steps * k;
+}
+
+cn_sample_desc render_sample_desc(const cn_render_desc* d) {
+    cn_sample_desc sd{};
+    sd.R = d->R;
+    sd.n_samples = d->n_samples;
+    sd.n_importance = d->n_importance;
+    sd.up_sample_steps = d->up_sample_steps;
+    sd.rays_o = d->rays_o;
+    sd.rays_d = d->rays_d;
+    sd.near = d->near;
+    sd.far = d->far;
+    sd.t_rand = d->t_rand;
+    sd.time_step = d->time_step;
+    sd.net = d->sdf_net;
+    sd.z = d->z;
+    return sd;
+}
+
+}  // namespace
+
+extern "C" size_t cn_render_fwd_workspace_bytes(const cn_render_desc* d) {
+    NetShape s;
+    ColorShape cs;
+    if (render_check(d, &s, &cs) != CN_OK) return 0;
+    const int M = d->R * render_S(d);
+    Plan ws(nullptr);
+    float* U8 = nullptr;
+    sdf_field_plan(d->sdf_net, s, M, nullptr, nullptr, &U8, nullptr, ws, nullptr, false);
+    color_field_plan(d->color_net, cs, M, nullptr, nullptr, nullptr, 1, nullptr, 0, nullptr, ws, nullptr, false);
+    size_t bytes = ws.used;
+    if (!d->z_in) {
+        const cn_sample_desc sd = render_sample_desc(d);
+        const size_t sb = cn_sample_workspace_bytes(&sd);
+        bytes = bytes > sb ? bytes : sb;  // the sampler's workspace is free again once z is written
+    }
+    return bytes;
+}
+
+extern "C" int cn_render_fwd(const cn_render_desc* d, void* workspace, int64_t workspace_bytes, cn_stream_t stream) {
+    NetShape s;
+    ColorShape cs;
+    int rc = render_check(d, &s, &cs);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    const int R = d->R, S = render_S(d);
+    CN_REQUIRE((int64_t)R * S < ((int64_t)1 << 31) / 256, CN_ERR_SHAPE, "cn_render_fwd: R x S = %lld too large",
+               (long long)R * S);
+    if (R == 0) return CN_OK;
+    const size_t need = cn_render_fwd_workspace_bytes(d);
+    CN_REQUIRE(workspace && workspace_bytes >= 0 && (size_t)workspace_bytes >= need, CN_ERR_SHAPE,
+               "cn_render_fwd: workspace %lld bytes, %zu needed", (long long)workspace_bytes, need);
+    CN_REQUIRE(((uintptr_t)workspace & (kAlign - 1)) == 0, CN_ERR_ALIGN, "cn_render_fwd: workspace not 256-byte aligned");
+    // the samples (neus_renderer.py:466-525), or the caller's
+    if (d->z_in) {
+        CN_REQUIRE(hipMemcpyAsync(d->z, d->z_in, (size_t)R * S * 4, hipMemcpyDeviceToDevice, st) == hipSuccess,
+                   CN_ERR_LAUNCH, "cn_render_fwd: z copy failed");
+    } else {
+        const cn_sample_desc sd = render_sample_desc(d);
+        if ((rc = cn_sample(&sd, workspace, workspace_bytes, stream))) return rc;
+    }
+    const int M = R * S;
+    // render_core (neus_renderer.py:337-420): the midpoints, the fields, the compositing
+    if ((rc = cn_points(R, S, d->rays_o, d->rays_d, d->z, d->time_step, 1, d->near, d->far, d->n_samples, d->pts, stream)))
+        return rc;
+    Plan ws(workspace);
+    float* U8 = nullptr;
+    if ((rc = sdf_field_plan(d->sdf_net, s, M, d->pts, d->sdf, &U8, d->grad, ws, st, true))) return rc;
+    if ((rc = color_field_plan(d->color_net, cs, M, d->grad, d->pts, d->rays_d, S, U8, s.HL, d->rgb, ws, st, true)))
+        return rc;
+    return cn_composite_fwd(R, S, d->z, d->sdf, d->grad, 4, d->rgb, d->rays_d, d->inv_s, d->near, d->far, d->n_samples,
+                            d->cos_anneal_ratio, d->color, d->depth, d->weights, d->cdf, stream);
+}

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define CN_ABI_VERSION 12
+#define CN_ABI_VERSION 13
 
 typedef void* cn_stream_t; /* hipStream_t */
 
@@ -572,6 +572,13 @@ typedef struct cn_sdf_net {
     const float* bias[CN_SDF_MAX_LIN - 1];
     const float* head_w;
     const float* head_b;
+    /* ABI v13 (cn_render_fwd's ∇ₓSDF pass only): the transposed images Wt[l] (fields.pack_sdf's Bt:
+       rows >= the input width rounded up to 128, columns the output width rounded up to 32 / 64) and
+       head_wp [HL] = head_w zero-padded to the hidden buffers' width (16-byte aligned) */
+    const void* Wt[CN_SDF_MAX_LIN - 1];
+    int32_t wt_rows[CN_SDF_MAX_LIN - 1];
+    int32_t wt_cols[CN_SDF_MAX_LIN - 1];
+    const float* head_wp;
 } cn_sdf_net;
 
 /* sdf[idx ? idx[m] : m] = SDFNetwork.sdf(x[m]) for M points x [M][ldx >= 4] (no gradient):
@@ -604,6 +611,66 @@ typedef struct cn_sample_desc {
 } cn_sample_desc;
 size_t cn_sample_workspace_bytes(const cn_sample_desc* d);
 int cn_sample(const cn_sample_desc* d, void* workspace, int64_t workspace_bytes, cn_stream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * The rendering forward in one call (ABI v13): NeuSRenderer.forward of the
+ * eval path (neus_renderer.py:453-584 with render_core 307-450, no gradient):
+ * the sampler (cn_sample, or the caller's z), the section midpoints, the SDF
+ * field with its ∇ₓSDF pass and the feature head folded into the colour
+ * network (copenerf.renderer's fold: the colour network's first layer reads
+ * the SDF's last hidden activation), the colour network, the compositing.
+ * Bitwise equal to copenerf's renderer with the same packs.
+ *
+ * cn_color_net: RenderingNetwork (mode idr, squeeze_out) as its images
+ * (copenerf.fields.pack_color with the folded first layer): W[0] is lin0's
+ * image over [feature (F) | gradient | pts | emb(dirs) | 0] (K = F + KX,
+ * KX = 64-rounded 4 + 4 + 3 (1 + 2 multires_view)), W[l] the hidden layers';
+ * head_w [3][in_dim[n_lin-1]] fp32 and head_b [3] the sigmoid head.
+ * ------------------------------------------------------------------------ */
+typedef struct cn_color_net {
+    int32_t n_lin;                      /* Linear layers, 2 .. 16 */
+    int32_t in_dim[CN_SDF_MAX_LIN];
+    int32_t out_dim[CN_SDF_MAX_LIN];
+    int32_t d_feature, multires_view;
+    int32_t mfma_dtype;
+    const void* W[CN_SDF_MAX_LIN - 1];
+    int32_t w_rows[CN_SDF_MAX_LIN - 1];
+    int32_t w_cols[CN_SDF_MAX_LIN - 1];
+    const float* bias[CN_SDF_MAX_LIN - 1];
+    const float* head_w;
+    const float* head_b;
+} cn_color_net;
+
+/* z_in: [R][S] sample positions (the renderer's z_vals hook), or NULL: cn_sample's
+ * (t_rand as there; NULL: eval).  inv_s, cos_anneal_ratio: device scalars [1].
+ * Outputs (all required): z [R][S] (S = n_samples + up_sample_steps k, or z_in's S),
+ * pts [R S][4] (the midpoints, (x, t)), sdf [R S], grad [R S][4] (∇ₓSDF: normals and the
+ * sdf flow), rgb [R S][3], color [R][3], depth [R] (weighted z), weights [R][S], cdf [R][S]. */
+typedef struct cn_render_desc {
+    int32_t R, n_samples, n_importance, up_sample_steps, S_in;
+    const float* rays_o;
+    const float* rays_d;
+    const float* near;
+    const float* far;
+    const float* t_rand;
+    const float* time_step;
+    const float* z_in;
+    const float* inv_s;
+    const float* cos_anneal_ratio;
+    const cn_sdf_net* sdf_net;
+    const cn_color_net* color_net;
+    float* z;
+    float* pts;
+    float* sdf;
+    float* grad;
+    float* rgb;
+    float* color;
+    float* depth;
+    float* weights;
+    float* cdf;
+} cn_render_desc;
+size_t cn_render_fwd_workspace_bytes(const cn_render_desc* d);
+int cn_render_fwd(const cn_render_desc* d, void* workspace, int64_t workspace_bytes, cn_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -36,7 +36,8 @@ def test_struct_layouts_match_header_order():
     src = open(HEADER).read()
     for cname, py in (("cn_linear_desc", _lib.LinearDesc), ("cn_wgrad_desc", _lib.WgradDesc),
                       ("cn_sdf_mlp_desc", _lib.SdfMlpDesc), ("cn_sdf_net", _lib.SdfNet),
-                      ("cn_sample_desc", _lib.SampleDesc)):
+                      ("cn_sample_desc", _lib.SampleDesc), ("cn_color_net", _lib.ColorNet),
+                      ("cn_render_desc", _lib.RenderDesc)):
         body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (cname, cname), src, re.S).group(1)
         body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
         names = []
@@ -161,6 +162,43 @@ def test_composed_entry_points_plan_without_gpu():
     n.w_rows[2] = 128  # an image too small for its layer
     assert lib.cn_sample(ctypes.byref(d), 4096 * 256, want, None) == -2
     assert b"layer 2 image" in lib.cn_last_error()
+
+
+def test_render_fwd_checks_without_gpu():
+    """ABI v13: cn_render_fwd validates both networks and the fold on the host."""
+    from copenerf import _lib
+    lib = _lib.load()
+    assert lib.cn_render_fwd(None, None, 0, None) == -1
+    assert lib.cn_render_fwd_workspace_bytes(None) == 0
+    n = _fake_net()
+    for l in range(8):
+        n.Wt[l], n.wt_rows[l], n.wt_cols[l] = 4096, 256, 256
+    n.head_wp = 4096
+    c = _lib.ColorNet()
+    c.n_lin, c.d_feature, c.multires_view, c.mfma_dtype = 5, 256, 4, 1
+    dims = [4 + 27 + 4 + 256, 256, 256, 256, 256]
+    for l in range(5):
+        c.in_dim[l], c.out_dim[l] = dims[l], (3 if l == 4 else 256)
+    for l in range(4):
+        c.W[l], c.w_rows[l], c.w_cols[l], c.bias[l] = 4096, 256, (256 + 64 if l == 0 else 256), 4096
+    c.head_w = c.head_b = 4096
+    d = _lib.RenderDesc()
+    d.R, d.n_samples, d.n_importance, d.up_sample_steps = 4096, 64, 64, 4
+    for k in ("rays_o", "rays_d", "near", "far", "time_step", "inv_s", "cos_anneal_ratio", "z", "pts", "sdf", "grad",
+              "rgb", "color", "depth", "weights", "cdf"):
+        setattr(d, k, 4096)
+    d.sdf_net, d.color_net = ctypes.pointer(n), ctypes.pointer(c)
+    M = 4096 * 128
+    ws = lib.cn_render_fwd_workspace_bytes(ctypes.byref(d))
+    assert ws >= M * 256 * 2 * 7  # at least the kept activations
+    assert lib.cn_render_fwd(ctypes.byref(d), 4096 * 256, ws - 1, None) == -2
+    c.mfma_dtype = 2
+    assert lib.cn_render_fwd(ctypes.byref(d), 4096 * 256, ws, None) == -1
+    assert b"modes differ" in lib.cn_last_error()
+    c.mfma_dtype, c.d_feature = 1, 128  # no fold: the colour network's feature is not the SDF's hidden layer
+    c.in_dim[0] = 4 + 27 + 4 + 128
+    c.w_cols[0] = 128 + 64
+    assert lib.cn_render_fwd(ctypes.byref(d), 4096 * 256, ws, None) == -5
 
 
 def test_product_path_refuses_cpu_tensors():
