@@ -496,7 +496,8 @@ int sdf_field_plan(const cn_sdf_net* n, const NetShape& s, int M, const float* x
         U[l] = static_cast<char*>(ws.take((size_t)M * HL * (ub[l] ? 2 : 4)));
     }
     const bool fp32_s7 = !s.img;  // the image mode with the folded head keeps s_7 as its image only
-    float* S7 = static_cast<float*>(ws.take((size_t)M * HL * 4));
+    // (fp32 s_7 also from cn_scale_cols where the head is not fused)
+    float* S7 = (fp32_s7 || !s.fuse_head) ? static_cast<float*>(ws.take((size_t)M * HL * 4)) : nullptr;
     void* S7b = s.img ? ws.take((size_t)M * HL * 2) : nullptr;
     // the ∇ pass: two ping-pong adjoints (images in the image mode), s_0 also fp32, QE, Q0
     char* Sp[2] = {static_cast<char*>(ws.take((size_t)M * HL * eh)), static_cast<char*>(ws.take((size_t)M * HL * eh))};
