@@ -770,7 +770,7 @@ extern "C" int cn_render_fwd(const cn_render_desc* d, void* workspace, int64_t w
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
     const int R = d->R, S = render_S(d);
-    CN_REQUIRE((int64_t)R * S < ((int64_t)1 << 31) / 256, CN_ERR_SHAPE, "cn_render_fwd: R x S = %lld too large",
+    CN_REQUIRE((int64_t)R * S < ((int64_t)1 << 31), CN_ERR_SHAPE, "cn_render_fwd: R x S = %lld too large",
                (long long)R * S);
     if (R == 0) return CN_OK;
     const size_t need = cn_render_fwd_workspace_bytes(d);
