@@ -717,6 +717,17 @@ int render_check(const cn_render_desc* d, NetShape* s, ColorShape* cs) {
                "cn_render_fwd: pts / grad 16-byte aligned");
     if (d->z_in)
         CN_REQUIRE(d->S_in >= 1 && d->n_samples >= 1, CN_ERR_SHAPE, "cn_render_fwd: z_in needs S_in and n_samples");
+    else
+        CN_REQUIRE(d->n_samples >= 1 && d->n_importance >= 0 &&
+                       (d->n_importance == 0 || (d->up_sample_steps >= 1 && d->n_importance >= d->up_sample_steps)),
+                   CN_ERR_SHAPE, "cn_render_fwd: n_samples %d, n_importance %d over %d up-sample steps", d->n_samples,
+                   d->n_importance, d->up_sample_steps);
+    const int64_t S = d->z_in ? d->S_in
+                              : d->n_samples + (d->n_importance > 0 ? (int64_t)d->up_sample_steps *
+                                                                          (d->n_importance / d->up_sample_steps)
+                                                                    : 0);
+    CN_REQUIRE((int64_t)d->R * S < ((int64_t)1 << 31), CN_ERR_SHAPE, "cn_render_fwd: R x S = %lld too large",
+               (long long)d->R * S);
     return CN_OK;
 }
 
@@ -769,9 +780,7 @@ extern "C" int cn_render_fwd(const cn_render_desc* d, void* workspace, int64_t w
     int rc = render_check(d, &s, &cs);
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
-    const int R = d->R, S = render_S(d);
-    CN_REQUIRE((int64_t)R * S < ((int64_t)1 << 31), CN_ERR_SHAPE, "cn_render_fwd: R x S = %lld too large",
-               (long long)R * S);
+    const int R = d->R, S = render_S(d);  // (R x S < 2^31: render_check)
     if (R == 0) return CN_OK;
     const size_t need = cn_render_fwd_workspace_bytes(d);
     CN_REQUIRE(workspace && workspace_bytes >= 0 && (size_t)workspace_bytes >= need, CN_ERR_SHAPE,

@@ -192,6 +192,10 @@ def test_render_fwd_checks_without_gpu():
     ws = lib.cn_render_fwd_workspace_bytes(ctypes.byref(d))
     assert ws >= M * 256 * 2 * 7  # at least the kept activations
     assert lib.cn_render_fwd(ctypes.byref(d), 4096 * 256, ws - 1, None) == -2
+    d.up_sample_steps = 0  # importance samples without rounds
+    assert lib.cn_render_fwd_workspace_bytes(ctypes.byref(d)) == 0
+    assert lib.cn_render_fwd(ctypes.byref(d), 4096 * 256, ws, None) == -2
+    d.up_sample_steps = 4
     c.mfma_dtype = 2
     assert lib.cn_render_fwd(ctypes.byref(d), 4096 * 256, ws, None) == -1
     assert b"modes differ" in lib.cn_last_error()
