@@ -255,6 +255,8 @@ int sample_check(const cn_sample_desc* d) {
     CN_REQUIRE(d->near && d->far && d->z, CN_ERR_ARG, "cn_sample: null near / far / z");
     CN_REQUIRE(d->n_importance == 0 || (d->rays_o && d->rays_d && d->time_step && d->net), CN_ERR_ARG,
                "cn_sample: null rays / time_step / net");
+    CN_REQUIRE((int64_t)d->R * ((int64_t)d->n_samples + d->n_importance) < ((int64_t)1 << 31), CN_ERR_SHAPE,
+               "cn_sample: R = %d too large", d->R);
     return CN_OK;
 }
 
@@ -307,9 +309,6 @@ extern "C" int cn_sample(const cn_sample_desc* d, void* workspace, int64_t works
     CN_REQUIRE(workspace && workspace_bytes >= 0 && (size_t)workspace_bytes >= need, CN_ERR_SHAPE,
                "cn_sample: workspace %lld bytes, %zu needed", (long long)workspace_bytes, need);
     CN_REQUIRE(((uintptr_t)workspace & (kAlign - 1)) == 0, CN_ERR_ALIGN, "cn_sample: workspace not 256-byte aligned");
-    CN_REQUIRE((int64_t)R * (ns > d->n_importance ? ns : d->n_importance) < ((int64_t)1 << 31) &&
-                   (int64_t)R * (ns + d->n_importance) < ((int64_t)1 << 31),
-               CN_ERR_SHAPE, "cn_sample: R = %d too large", R);
     Plan ws(workspace);
     SamplePlan p;
     sample_plan(d, s, ws, &p);
