@@ -68,6 +68,15 @@ PAIR_WEIGHTS = ("sdf_weight", "flow_rgb_weight", "sdf_consistency_weight", "edge
                 "smoothness_weight")
 
 
+def prefer_small_gemm_blas():
+    """torch's fp32 GEMMs of the step (the MotionNetwork's layers and their gradients, ray and pose
+    matrices: tens to a few hundred rows) through rocBLAS instead of hipBLASLt: hipBLASLt's tiles for these
+    shapes run ~30 us each, rocBLAS's in a few.  C3 +1.9 % (profiles/r5_ab.txt r5q); both fp32.  A process-wide
+    torch setting: the training entry points (SyntheticTrainer, Trainer) make it."""
+    if torch.cuda.is_available():
+        torch.backends.cuda.preferred_blas_library("cublas")  # (rocBLAS on ROCm)
+
+
 def normalise_train_cfg(cfg):
     """Accept the reference's cfg['training'] as it is (default.yaml:40-46 stores every loss
     weight as a [start, end] pair): rgb / eikonal weights use their first entry
@@ -177,6 +186,7 @@ class SyntheticTrainer:
                  capturable=False, mfma_dtype="fp32", train_cfg=None, stage1_fused=True):
         if schedule not in ("fixed", "reference"):
             raise ValueError(f"schedule must be 'fixed' or 'reference' (got {schedule!r})")
+        prefer_small_gemm_blas()
         self.device = torch.device(device)
         self.R, self.H, self.W, self.patch = rays, H, W, patch
         self.depth_range = depth_range

@@ -40,6 +40,8 @@ class Trainer(object):
     def __init__(self, renderer, optimizer, motion_optimizer, cfg, device=None, patch_rng="cpu", nan_check="sync",
                  **kwargs):
         """Reference: model/training.py:16-50."""
+        from .train_step import prefer_small_gemm_blas
+        prefer_small_gemm_blas()
         self.total_nb_images = kwargs["total_nb_images"]
         self.renderer = renderer
         self.optimizer = optimizer
