@@ -17,7 +17,8 @@ vmcnt(63) wait.  The direct epilogues are fully unrolled and branch-free per ele
 variant is one basic block holding all of its memory operations: every region block that issues
 vector-memory operations must issue at least 63 - W of them, unless every path from it to the wait
 passes an `s_waitcnt vmcnt(0)` (everything older retired: SOFTPLUS_HEAD's epilogue, whose row sums
-cross a barrier).  The dispatch between the variants cannot skip all of them (the host requires out0
+cross a barrier), or every path from the chunk loop to it does (the ring's pieces retired before the
+block issues anything: the head epilogues' row stores after that barrier).  The dispatch between the variants cannot skip all of them (the host requires out0
 or out0_b), which the graph alone does not show.  `flat_*` instructions in the region (which vmcnt
 does not order) fail the check too."""
 from __future__ import annotations
@@ -188,14 +189,23 @@ def dma_ring_report(text: str) -> list:
                 st.extend(blocks[j]["succ"])
             return False
 
-        # every block issuing vector-memory operations issues enough of them itself, or is followed
+        # blocks reachable from the loop's exits without passing a drain
+        undrained, stack = set(), [s for s in starts if s not in drains]
+        while stack:
+            k = stack.pop()
+            if k in undrained or k in loop or k in w63 or k in drains:
+                continue
+            undrained.add(k)
+            stack.extend(blocks[k]["succ"])
+
+        # every block issuing vector-memory operations issues enough of them itself, or is preceded or followed
         # by a drain on every path to the wait (the direct epilogues are fully unrolled: one block
         # per output variant; the host requires out0 or out0_b, so no variant stores nothing)
         best, flat = None, False
         for k in region:
             nv = sum(1 for i in blocks[k]["ins"] if _vmem(i))
             flat = flat or any(i.startswith("flat_") for i in blocks[k]["ins"])
-            if nv == 0 or k in drains or not undrained_to_wait(k):
+            if nv == 0 or k in drains or k not in undrained or not undrained_to_wait(k):
                 continue
             best = nv if best is None else min(best, nv)
         need = 63 - (ring if ring is not None else 0)
