@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libcopenerf.so"
 LIB_PATH = os.environ.get("COPENERF_LIB", os.path.join(_HERE, LIB_NAME))
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 c_f32p = ctypes.c_void_p  # device pointers are passed as integers
 c_i32 = ctypes.c_int32
@@ -130,6 +130,13 @@ class RenderDesc(ctypes.Structure):
     ]
 
 
+class MlpDesc(ctypes.Structure):
+    _fields_ = [
+        ("M", c_i32), ("x", c_ptr), ("net", ctypes.POINTER(SdfNet)), ("sdf", c_ptr), ("dsdf", c_ptr),
+        ("dW", c_ptr * SDF_MAX_LIN), ("db", c_ptr * SDF_MAX_LIN), ("dx", c_ptr),
+    ]
+
+
 # name -> (restype, argtypes); mirrors include/copenerf.h one to one.
 SIGNATURES = {
     "cn_abi_version": (c_i32, []),
@@ -196,6 +203,10 @@ SIGNATURES = {
     "cn_sample": (c_i32, [ctypes.POINTER(SampleDesc), c_ptr, c_i64, c_ptr]),
     "cn_render_fwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(RenderDesc)]),
     "cn_render_fwd": (c_i32, [ctypes.POINTER(RenderDesc), c_ptr, c_i64, c_ptr]),
+    "cn_mlp_state_bytes": (ctypes.c_size_t, [ctypes.POINTER(MlpDesc)]),
+    "cn_mlp_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(MlpDesc)]),
+    "cn_mlp_fwd": (c_i32, [ctypes.POINTER(MlpDesc), c_ptr, c_i64, c_ptr]),
+    "cn_mlp_bwd": (c_i32, [ctypes.POINTER(MlpDesc), c_ptr, c_i64, c_ptr, c_i64, c_ptr]),
 }
 
 _lock = threading.Lock()

@@ -583,6 +583,12 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
     return dWs, dbs, dx
 
 
+# SDFNetwork.sdf under autograd (the stage-1 consistency re-query, train.py:502-505) through the composed
+# entry points cn_mlp_fwd / cn_mlp_bwd (bitwise the layer-by-layer composition below); the per-kernel
+# timer (ops.set_timer) sees the launches only when they are made one by one, so it keeps the composition
+MLP_NATIVE = True
+
+
 class _SDFFieldFn(torch.autograd.Function):
     """(x [M,4], weights...) -> (sdf [M,1], feature [M,H], ∇ₓSDF [M,4])."""
 
@@ -590,9 +596,19 @@ class _SDFFieldFn(torch.autograd.Function):
     def forward(ctx, x, lay, pk, want_feat, want_grad, *params):
         ctx.set_materialize_grads(False)
         keep = any(ctx.needs_input_grad[5:]) or ctx.needs_input_grad[0]
+        ctx.nparams = len(params)
+        if keep and want_feat is False and not want_grad and MLP_NATIVE and ops._timer is None:
+            net, refs = ops.sdf_net(lay, pk)
+            sdf = _empty(x.shape[0], 1, x.device)
+            state = ops.mlp_fwd(net, x, sdf.view(-1))
+            ctx.lay, ctx.hidden, ctx.st = lay, False, None
+            ctx.native = (net, refs, state)
+            feat, G = x.new_empty(0), x.new_empty(0)
+            ctx.mark_non_differentiable(feat, G)
+            return sdf, feat, G
+        ctx.native = None
         st = sdf_forward(lay, pk, x, want_feat=want_feat, want_grad=want_grad, keep=keep)
         ctx.lay, ctx.pk, ctx.st = lay, pk, (st if keep else None)
-        ctx.nparams = len(params)
         ctx.hidden = want_feat == "hidden"
         empty = x.new_empty(0)
         if ctx.hidden:  # the last hidden activation in place of the feature (folded feature head)
@@ -609,6 +625,8 @@ class _SDFFieldFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dsdf, dfeat, dG):
         none4 = (None,) * 4
+        if ctx.native is not None:
+            return _SDFFieldFn._native_backward(ctx, dsdf)
         if ctx.st is None:
             return (None,) + none4 + (None,) * ctx.nparams
         if dfeat is not None and dfeat.stride(1) != 1:
@@ -632,6 +650,30 @@ class _SDFFieldFn(torch.autograd.Function):
         elif want_dx:
             dx = sdf_input_grad(ctx.lay, ctx.pk, ctx.st, dsdf, dfeat, dh=dh)
         ctx.st = None
+        return (dx,) + none4 + tuple(grads)
+
+    @staticmethod
+    def _native_backward(ctx, dsdf):
+        """cn_mlp_bwd: sdf_backward (sdf only, first order, want_dx) or sdf_input_grad in one call."""
+        net, refs, state = ctx.native
+        ctx.native = None
+        lay = ctx.lay
+        none4 = (None,) * 4
+        want_dx, params = ctx.needs_input_grad[0], any(ctx.needs_input_grad[5:])
+        if dsdf is None or not (want_dx or params):
+            return (None,) + none4 + (None,) * ctx.nparams
+        dev = dsdf.device
+        M = dsdf.shape[0]
+        dWs = [torch.empty(lay.out_dim[l], lay.in_dim[l], device=dev) for l in range(lay.n_lin)] if params else None
+        dbs = [torch.empty(lay.out_dim[l], device=dev) for l in range(lay.n_lin)] if params else None
+        dx = _empty(M, 4, dev) if want_dx else None
+        ops.mlp_bwd(net, M, state, dsdf.reshape(M).contiguous(), dWs, dbs, dx)
+        del refs, state
+        grads = [None] * ctx.nparams
+        if params:
+            grads = []
+            for w, b in zip(dWs, dbs):
+                grads += [w, b]
         return (dx,) + none4 + tuple(grads)
 
 

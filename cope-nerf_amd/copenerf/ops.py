@@ -694,6 +694,47 @@ def sdf_query(net, x, sdf, idx=None):
     return sdf
 
 
+def _mlp_desc(net, M, x=None, sdf=None, dsdf=None, dWs=None, dbs=None, dx=None):
+    d = _lib.MlpDesc()
+    d.M, d.x, d.net, d.sdf, d.dsdf, d.dx = M, _ptr(x), ctypes.pointer(net), _ptr(sdf), _ptr(dsdf), _ptr(dx)
+    for l, (w, b) in enumerate(zip(dWs or [], dbs or [])):
+        d.dW[l], d.db[l] = _ptr(w), _ptr(b)
+    return d
+
+
+def mlp_fwd(net, x, sdf):
+    """sdf[m] = SDFNetwork.sdf(x[m]) keeping the activations the backward reads -- cn_mlp_fwd; returns the
+    state buffer mlp_bwd takes (net: sdf_net's descriptor, with its transposed images)."""
+    _need(x, "x")
+    M = x.shape[0]
+    if x.dim() != 2 or x.shape[1] != 4 or x.stride(0) != 4 or x.dtype != torch.float32:
+        raise RuntimeError("mlp_fwd: x must be a contiguous float32 [M, 4]")
+    if not sdf.is_contiguous() or sdf.numel() < M:
+        raise RuntimeError("mlp_fwd: sdf must be contiguous with M entries")
+    lib = _lib.load()
+    d = _mlp_desc(net, M, x=x, sdf=sdf)
+    state = torch.empty(max(int(lib.cn_mlp_state_bytes(ctypes.byref(d))), 1), dtype=torch.uint8, device=x.device)
+    _lib.check(lib.cn_mlp_fwd(ctypes.byref(d), _ptr(state), state.numel(), _stream()), "cn_mlp_fwd")
+    return state
+
+
+def mlp_bwd(net, M, state, dsdf, dWs=None, dbs=None, dx=None):
+    """The gradients of SDFNetwork.sdf from dsdf [M] -- cn_mlp_bwd: dWs[l] [out_dim, in_dim] / dbs[l]
+    (every Linear, or None: dx only) and dx [M, 4] (or None)."""
+    _need(dsdf, "dsdf", ndim=1)
+    if not dsdf.is_contiguous() or dsdf.numel() < M:
+        raise RuntimeError("mlp_bwd: dsdf must be contiguous with M entries")
+    for t in list(dWs or []) + list(dbs or []) + [dx]:
+        if t is not None and (not t.is_contiguous() or t.dtype != torch.float32):
+            raise RuntimeError("mlp_bwd: gradients must be contiguous float32")
+    lib = _lib.load()
+    d = _mlp_desc(net, M, dsdf=dsdf, dWs=dWs, dbs=dbs, dx=dx)
+    ws = torch.empty(max(int(lib.cn_mlp_bwd_workspace_bytes(ctypes.byref(d))), 1), dtype=torch.uint8,
+                     device=dsdf.device)
+    _lib.check(lib.cn_mlp_bwd(ctypes.byref(d), _ptr(state), state.numel(), _ptr(ws), ws.numel(), _stream()),
+               "cn_mlp_bwd")
+
+
 def sample(net, rays_o, rays_d, near, far, t_rand, time_step, n_samples, n_importance, up_sample_steps, z):
     """z [R, n_samples + up_sample_steps * (n_importance // up_sample_steps)] -- cn_sample: coarse z and the
     up-sampling rounds with their SDF queries in one call (net: sdf_net's descriptor)."""

@@ -7,6 +7,7 @@
 // copenerf.renderer.sample_z launch for launch, so the results are the same bits; host code
 // only plans buffers in the caller's workspace and fills descriptors -- nothing synchronises,
 // allocates or touches the default stream, so a caller may capture cn_sample in a hipGraph.
+#include <algorithm>
 #include <cmath>
 
 #include "cn_common.h"
@@ -804,4 +805,349 @@ extern "C" int cn_render_fwd(const cn_render_desc* d, void* workspace, int64_t w
         return rc;
     return cn_composite_fwd(R, S, d->z, d->sdf, d->grad, 4, d->rgb, d->rays_d, d->inv_s, d->near, d->far, d->n_samples,
                             d->cos_anneal_ratio, d->color, d->depth, d->weights, d->cdf, stream);
+}
+
+// ---------------------------------------------------------------------------------------------
+// cn_mlp_fwd / cn_mlp_bwd (ABI v14): SDFNetwork.sdf(x) under autograd -- the stage-1 consistency
+// re-query of train.py:502-505 (neus_fields.py:268-283 and its backward) -- composed from the
+// launches copenerf.fields.sdf_forward (keep, want_feat / want_grad False) and sdf_backward (dsdf
+// only, first order, want_dx) or sdf_input_grad (no parameter gradients) make, descriptor for
+// descriptor: the same bits.
+namespace {
+
+// Zero fill of n floats (the feature rows of lin8's gradient).  A kernel, not hipMemsetAsync: with
+// the memsets, replays of a captured training step left those rows differing from the eager step
+// from the second replay on (tests/test_gpu_configs.py::test_c5_graph_stage1_joint_pose_replays).
+__global__ void __launch_bounds__(256) zero_kernel(float* __restrict__ p, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = 0.0f;
+}
+
+int zero_fill(float* p, int64_t n, hipStream_t stream) {
+    if (n <= 0) return CN_OK;
+    const int blocks = (int)std::min<int64_t>((n + 255) / 256, 1024);
+    zero_kernel<<<blocks, 256, 0, stream>>>(p, n);
+    CN_REQUIRE(hipGetLastError() == hipSuccess, CN_ERR_LAUNCH, "cn_mlp_bwd: zero fill launch failed");
+    return CN_OK;
+}
+
+// The forward's kept activations in the caller's state buffer: U_0 (fp32 [M][KE]) and U_1 .. U_L8
+// ([M][HL]; bf16 operand images where fields.sdf_forward keeps images only: the image mode's hidden
+// layers and the skip input below L8).
+struct MlpState {
+    float* U0;
+    char* U[CN_SDF_MAX_LIN];
+    bool ub[CN_SDF_MAX_LIN];
+};
+
+void mlp_state_plan(const NetShape& s, int M, Plan& p, MlpState* st) {
+    const int L8 = s.L8, sk = s.sk;
+    const bool usk_b = s.img && sk >= 1 && sk < L8;
+    st->U0 = static_cast<float*>(p.take((size_t)M * s.KE * 4));
+    st->U[0] = nullptr;
+    st->ub[0] = false;
+    for (int l = 1; l <= L8; ++l) {
+        st->ub[l] = (l == sk) ? usk_b : (s.img && l < L8);
+        st->U[l] = static_cast<char*>(p.take((size_t)M * s.HL * (st->ub[l] ? 2 : 4)));
+    }
+}
+
+int mlp_check(const cn_mlp_desc* d, NetShape* s, bool bwd) {
+    CN_REQUIRE(d, CN_ERR_ARG, "cn_mlp: null descriptor");
+    int rc = net_shape(d->net, s);
+    if (rc) return rc;
+    CN_REQUIRE(d->M >= 0 && d->M < (1 << 30), CN_ERR_SHAPE, "cn_mlp: M = %d", d->M);
+    if (!bwd) {
+        CN_REQUIRE(d->M == 0 || (d->x && d->sdf), CN_ERR_ARG, "cn_mlp_fwd: null x / sdf");
+        return CN_OK;
+    }
+    const cn_sdf_net* n = d->net;
+    CN_REQUIRE(d->M == 0 || d->dsdf, CN_ERR_ARG, "cn_mlp_bwd: null dsdf");
+    CN_REQUIRE(d->dW[0] || d->dx, CN_ERR_ARG, "cn_mlp_bwd: neither parameter gradients (dW) nor dx asked for");
+    if (d->dW[0])
+        for (int l = 0; l <= s->L8; ++l)
+            CN_REQUIRE(d->dW[l] && d->db[l], CN_ERR_ARG, "cn_mlp_bwd: dW[%d] / db[%d] null", l, l);
+    CN_REQUIRE(!d->dx || ((uintptr_t)d->dx & 15) == 0, CN_ERR_ALIGN, "cn_mlp_bwd: dx [M][4] 16-byte aligned");
+    const int kq = s->bf ? 64 : 32;
+    for (int l = 0; l < s->L8; ++l)
+        CN_REQUIRE(n->Wt[l] && ((uintptr_t)n->Wt[l] & 15) == 0 && n->wt_rows[l] >= rup_i(n->in_dim[l], 128) &&
+                       n->wt_cols[l] >= rup_i(n->out_dim[l], kq),
+                   CN_ERR_SHAPE, "cn_mlp_bwd: transposed image %d missing or too small", l);
+    CN_REQUIRE(n->head_wp && ((uintptr_t)n->head_wp & 15) == 0, CN_ERR_ALIGN, "cn_mlp_bwd: head_wp [HL] (16-byte aligned)");
+    return CN_OK;
+}
+
+int mlp_fwd_run(const cn_mlp_desc* d, const NetShape& s, const MlpState& st, hipStream_t stream) {
+    const cn_sdf_net* n = d->net;
+    const float kSqrt2 = (float)std::sqrt(2.0);
+    const int L8 = s.L8, HL = s.HL, sk = s.sk, M = d->M;
+    const bool usk_b = s.img && sk >= 1 && sk < L8;
+    void* e_view = nullptr;
+    if (sk >= 0) e_view = st.U[sk] + (size_t)n->out_dim[sk - 1] * (usk_b ? 2 : 4);
+    int rc = cn_sdf_embed(M, d->x, 4, n->multires, n->scale, s.KE, st.U0, s.KE, e_view, e_view ? HL : 0, kSqrt2,
+                          usk_b ? 1 : 0, stream);
+    if (rc) return rc;
+    for (int l = 0; l < L8; ++l) {
+        const bool into = (l + 1) == sk;
+        LinCall c;
+        c.A = l == 0 ? static_cast<const void*>(st.U0) : st.U[l];
+        c.a_b = st.ub[l];
+        c.lda = l == 0 ? s.KE : HL;
+        c.B = n->W[l];
+        c.b_rows = n->w_rows[l];
+        c.b_cols = n->w_cols[l];
+        c.N = n->out_dim[l];
+        c.K = l == 0 ? s.KE : rup_i(n->in_dim[l], 32);
+        c.bias = n->bias[l];
+        c.beta = n->beta;
+        c.threshold = n->threshold;
+        c.M = M;
+        if (l == L8 - 1 && s.fuse_head) {  // the sdf head in the epilogue, the activation stored (kept)
+            c.epi = CN_EPI_SOFTPLUS_HEAD;
+            c.out0 = reinterpret_cast<float*>(st.U[L8]);
+            c.ld_out0 = HL;
+            c.nzero = HL;
+            c.head_w = n->head_w;
+            c.head_b = n->head_b;
+            c.head_out = d->sdf;
+        } else {
+            c.epi = CN_EPI_SOFTPLUS;
+            c.nzero = into ? n->out_dim[l] : HL;
+            if (into) c.odiv = kSqrt2;
+            if (st.ub[l + 1]) {
+                c.out0_b = st.U[l + 1];
+                c.ld_out0_b = HL;
+            } else {
+                c.out0 = reinterpret_cast<float*>(st.U[l + 1]);
+                c.ld_out0 = HL;
+            }
+        }
+        if ((rc = run_linear(n->mfma_dtype, c, l, stream))) return rc;
+    }
+    if (!s.fuse_head)
+        return cn_row_head(M, n->in_dim[L8], reinterpret_cast<const float*>(st.U[L8]), HL, n->head_w, n->in_dim[L8],
+                           n->head_b, 1, 0, d->sdf, 1, nullptr, stream);
+    return CN_OK;
+}
+
+// The adjoint chain's MUL launch (fields.sdf_backward / sdf_input_grad): Z_{l-1} = (W_lᵀ Z_l) ⊙ σ_{l-1}
+// (+ the skip layer's embedding columns to PE when split)
+int mlp_mul(const cn_sdf_net* n, const NetShape& s, const MlpState& st, int M, int l, const void* A, bool a_b,
+            void* out, bool out_b, float* PE, bool split, bool skip_div, hipStream_t stream) {
+    const float kSqrt2 = (float)std::sqrt(2.0);
+    LinCall c;
+    c.A = A;
+    c.a_b = a_b;
+    c.lda = s.HL;
+    c.B = n->Wt[l];
+    c.b_rows = n->wt_rows[l];
+    c.b_cols = n->wt_cols[l];
+    c.K = rup_i(n->out_dim[l], 32);
+    c.epi = CN_EPI_MUL;
+    c.aux0 = st.U[l];
+    c.aux0_b = st.ub[l];
+    c.ld_aux0 = s.HL;
+    c.aux_beta = sig_beta(n, l - 1);
+    c.nzero = s.HL;
+    c.M = M;
+    c.beta = n->beta;
+    c.threshold = n->threshold;
+    if (split) {
+        c.N = n->in_dim[l];
+        c.nsplit = n->out_dim[l - 1];
+        c.out_split = PE;
+        c.ld_split = s.KE;
+        c.adiv = kSqrt2;
+    } else {
+        c.N = n->out_dim[l - 1];
+        if (skip_div) c.adiv = kSqrt2;
+    }
+    if (out_b) {
+        c.out0_b = out;
+        c.ld_out0_b = s.HL;
+    } else {
+        c.out0 = static_cast<float*>(out);
+        c.ld_out0 = s.HL;
+    }
+    return run_linear(n->mfma_dtype, c, l, stream);
+}
+
+// dx from the embedding adjoint: P0 = W_0ᵀ Z_0, then the assembly with the skip columns PE
+int mlp_dx(const cn_sdf_net* n, const NetShape& s, const MlpState& st, int M, const float* Z0, float* P0,
+           const float* PE, float* dx, hipStream_t stream) {
+    LinCall c;
+    c.A = Z0;
+    c.lda = s.HL;
+    c.B = n->Wt[0];
+    c.b_rows = n->wt_rows[0];
+    c.b_cols = n->wt_cols[0];
+    c.N = s.E;
+    c.K = rup_i(n->out_dim[0], 32);
+    c.epi = CN_EPI_STORE;
+    c.out0 = P0;
+    c.ld_out0 = s.KE;
+    c.nzero = s.KE;
+    c.M = M;
+    c.beta = n->beta;
+    c.threshold = n->threshold;
+    int rc = run_linear(n->mfma_dtype, c, 0, stream);
+    if (rc) return rc;
+    return cn_sdf_grad_assemble(M, n->multires, n->scale, st.U0, s.KE, P0, s.KE, PE, PE ? s.KE : 0, dx, 4, stream);
+}
+
+// The backward's plan over the workspace (run false: sizing only).  With parameter gradients
+// (fields.sdf_backward, sdf only, first order, want_dx = dx != NULL): Z_7 .. Z_0 each kept until the
+// weight gradients' batch (Z_l a bf16 image where sdf_backward's z_img keeps one), PE, P0, the
+// colsum / adjoint column-sum slabs and the cn_wgrad_batch workspace.  Without (sdf_input_grad): two
+// fp32 ping-pong adjoints, PE, P0.
+int mlp_bwd_plan(const cn_mlp_desc* d, const NetShape& s, const MlpState& st, Plan& ws, hipStream_t stream,
+                 bool run) {
+    const cn_sdf_net* n = d->net;
+    const int L8 = s.L8, HL = s.HL, sk = s.sk, M = d->M;
+    const bool params = d->dW[0] != nullptr;
+    int rc = CN_OK;
+    if (!params) {  // dx only: sdf_input_grad with dsdf alone
+        float* P[2] = {static_cast<float*>(ws.take((size_t)M * HL * 4)), static_cast<float*>(ws.take((size_t)M * HL * 4))};
+        float* PE = sk >= 0 ? static_cast<float*>(ws.take((size_t)M * s.KE * 4)) : nullptr;
+        float* P0 = static_cast<float*>(ws.take((size_t)M * s.KE * 4));
+        if (!run) return CN_OK;
+        const float* U8 = reinterpret_cast<const float*>(st.U[L8]);
+        if ((rc = cn_scale_cols(M, HL, U8, HL, n->head_wp, d->dsdf, P[0], HL, sig_beta(n, L8 - 1), stream))) return rc;
+        int cur = 0;
+        for (int l = L8 - 1; l >= 1; --l) {
+            if ((rc = mlp_mul(n, s, st, M, l, P[cur], false, P[cur ^ 1], false, PE, l == sk, false, stream))) return rc;
+            cur ^= 1;
+        }
+        return mlp_dx(n, s, st, M, P[cur], P0, PE, d->dx, stream);
+    }
+    const int i8 = n->in_dim[L8], o8 = n->out_dim[L8];
+    const bool fused_cs = i8 == HL;
+    const bool share = d->dx != nullptr;
+    auto z_img = [&](int l) { return s.img && l >= 1 && l < L8 && st.ub[l]; };
+    // Z[l]: the parameter adjoint of layer l's output (Z[L8 - 1] the elementwise seed)
+    void* Z[CN_SDF_MAX_LIN] = {};
+    bool zb[CN_SDF_MAX_LIN] = {};
+    zb[L8 - 1] = z_img(L8 - 1) && fused_cs;
+    Z[L8 - 1] = ws.take((size_t)M * HL * (zb[L8 - 1] ? 2 : 4));
+    for (int l = L8 - 1; l >= 1; --l) {
+        zb[l - 1] = z_img(l - 1);
+        Z[l - 1] = ws.take((size_t)M * HL * (zb[l - 1] ? 2 : 4));
+    }
+    float* PE = (share && sk >= 0) ? static_cast<float*>(ws.take((size_t)M * s.KE * 4)) : nullptr;
+    float* P0 = share ? static_cast<float*>(ws.take((size_t)M * s.KE * 4)) : nullptr;
+    const size_t cs_bytes = fused_cs ? cn_softplus_adjoint_workspace_bytes(M, HL)
+                                     : std::max(cn_colsum_workspace_bytes(M, i8), cn_colsum_workspace_bytes(M, 1));
+    float* cs_ws = static_cast<float*>(ws.take(cs_bytes));
+    // the hidden layers' weight gradients, in sdf_backward's queue order (l = L8-1 .. 0)
+    cn_wgrad_desc wd[CN_SDF_MAX_LIN] = {};
+    for (int l = L8 - 1; l >= 0; --l) {
+        cn_wgrad_desc& w = wd[L8 - 1 - l];
+        const bool xb = st.ub[l];
+        w.Y0 = Z[l];
+        w.X0 = l == 0 ? static_cast<const void*>(st.U0) : st.U[l];
+        w.dW = d->dW[l];
+        w.db = d->db[l];
+        w.ldy0 = HL;
+        w.ldx0 = l == 0 ? s.KE : HL;
+        w.ld_dw = n->in_dim[l];
+        w.M = M;
+        w.N = n->out_dim[l];
+        w.K = rup_i(n->in_dim[l], 64);
+        w.npairs = 1;
+        w.n_out = n->out_dim[l];
+        w.k_out = n->in_dim[l];
+        w.mfma_dtype = n->mfma_dtype;
+        w.y_bf16 = zb[l] ? 1 : 0;
+        w.x_bf16 = xb ? 1 : 0;
+    }
+    int64_t offs[CN_SDF_MAX_LIN];
+    const size_t wg_bytes = cn_wgrad_batch_workspace_bytes(wd, L8, offs);
+    char* wg_ws = static_cast<char*>(ws.take(wg_bytes));
+    if (!run) return CN_OK;
+    const float* U8 = reinterpret_cast<const float*>(st.U[L8]);
+    float* dW8 = d->dW[L8];
+    float* db8 = d->db[L8];
+    // lin8's rows past the sdf row (the feature head sdf() does not read): zero
+    if ((rc = zero_fill(dW8 + i8, (int64_t)(o8 - 1) * i8, stream)) || (rc = zero_fill(db8 + 1, o8 - 1, stream)))
+        return rc;
+    const float beta7 = sig_beta(n, L8 - 1);
+    if (fused_cs) {  // Z_7 = dsdf[m] w80[n] σ_7 with lin8's sdf row / bias gradients from the same pass
+        if ((rc = cn_softplus_adjoint(M, HL, nullptr, 0, U8, HL, beta7, d->dsdf, n->head_wp, nullptr, 0, nullptr, 0, 0.0f,
+                                      Z[L8 - 1], HL, zb[L8 - 1] ? 1 : 0, 0, dW8, db8, n->scale, cs_ws,
+                                      (int64_t)cs_bytes, stream)))
+            return rc;
+    } else {
+        if ((rc = cn_colsum(M, i8, d->dsdf, U8, HL, n->scale, dW8, 0, cs_ws, (int64_t)cs_bytes, stream))) return rc;
+        if ((rc = cn_colsum(M, 1, nullptr, d->dsdf, 1, n->scale, db8, 0, cs_ws, (int64_t)cs_bytes, stream))) return rc;
+        if ((rc = cn_scale_cols(M, HL, U8, HL, n->head_wp, d->dsdf, static_cast<float*>(Z[L8 - 1]), HL, beta7, stream)))
+            return rc;
+    }
+    for (int l = L8 - 1; l >= 1; --l) {
+        if ((rc = mlp_mul(n, s, st, M, l, Z[l], zb[l], Z[l - 1], zb[l - 1], PE, share && l == sk, l == sk, stream)))
+            return rc;
+    }
+    for (int i = 0; i < L8; ++i) {
+        wd[i].workspace = reinterpret_cast<float*>(wg_ws + offs[i]);
+        wd[i].workspace_bytes = (int64_t)wg_bytes - offs[i];
+    }
+    if ((rc = cn_wgrad_batch(wd, L8, stream))) return rc;
+    if (!share) return CN_OK;
+    return mlp_dx(n, s, st, M, static_cast<const float*>(Z[0]), P0, PE, d->dx, stream);
+}
+
+}  // namespace
+
+extern "C" size_t cn_mlp_state_bytes(const cn_mlp_desc* d) {
+    NetShape s;
+    if (mlp_check(d, &s, false) != CN_OK) return 0;
+    Plan p(nullptr);
+    MlpState st;
+    mlp_state_plan(s, d->M, p, &st);
+    return p.used;
+}
+
+extern "C" size_t cn_mlp_bwd_workspace_bytes(const cn_mlp_desc* d) {
+    NetShape s;
+    if (mlp_check(d, &s, true) != CN_OK) return 0;
+    Plan p(nullptr);
+    MlpState st;
+    mlp_state_plan(s, d->M, p, &st);
+    Plan ws(nullptr);
+    mlp_bwd_plan(d, s, st, ws, nullptr, false);
+    return ws.used;
+}
+
+extern "C" int cn_mlp_fwd(const cn_mlp_desc* d, void* state, int64_t state_bytes, cn_stream_t stream) {
+    NetShape s;
+    int rc = mlp_check(d, &s, false);
+    if (rc) return rc;
+    if (d->M == 0) return CN_OK;
+    const size_t need = cn_mlp_state_bytes(d);
+    CN_REQUIRE(state && state_bytes >= 0 && (size_t)state_bytes >= need, CN_ERR_SHAPE,
+               "cn_mlp_fwd: state %lld bytes, %zu needed", (long long)state_bytes, need);
+    CN_REQUIRE(((uintptr_t)state & (kAlign - 1)) == 0, CN_ERR_ALIGN, "cn_mlp_fwd: state not 256-byte aligned");
+    Plan p(state);
+    MlpState st;
+    mlp_state_plan(s, d->M, p, &st);
+    return mlp_fwd_run(d, s, st, (hipStream_t)stream);
+}
+
+extern "C" int cn_mlp_bwd(const cn_mlp_desc* d, const void* state, int64_t state_bytes, void* workspace,
+                          int64_t workspace_bytes, cn_stream_t stream) {
+    NetShape s;
+    int rc = mlp_check(d, &s, true);
+    if (rc) return rc;
+    if (d->M == 0) return CN_OK;  // (M = 0: nothing to sum; the caller's gradients are left as they are)
+    const size_t need_st = cn_mlp_state_bytes(d);
+    CN_REQUIRE(state && state_bytes >= 0 && (size_t)state_bytes >= need_st, CN_ERR_SHAPE,
+               "cn_mlp_bwd: state %lld bytes, %zu needed", (long long)state_bytes, need_st);
+    const size_t need = cn_mlp_bwd_workspace_bytes(d);
+    CN_REQUIRE(workspace && workspace_bytes >= 0 && (size_t)workspace_bytes >= need, CN_ERR_SHAPE,
+               "cn_mlp_bwd: workspace %lld bytes, %zu needed", (long long)workspace_bytes, need);
+    CN_REQUIRE(((uintptr_t)state & (kAlign - 1)) == 0 && ((uintptr_t)workspace & (kAlign - 1)) == 0, CN_ERR_ALIGN,
+               "cn_mlp_bwd: state / workspace not 256-byte aligned");
+    Plan p(const_cast<void*>(state));
+    MlpState st;
+    mlp_state_plan(s, d->M, p, &st);
+    Plan ws(workspace);
+    return mlp_bwd_plan(d, s, st, ws, (hipStream_t)stream, true);
 }

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define CN_ABI_VERSION 13
+#define CN_ABI_VERSION 14
 
 typedef void* cn_stream_t; /* hipStream_t */
 
@@ -671,6 +671,39 @@ typedef struct cn_render_desc {
 } cn_render_desc;
 size_t cn_render_fwd_workspace_bytes(const cn_render_desc* d);
 int cn_render_fwd(const cn_render_desc* d, void* workspace, int64_t workspace_bytes, cn_stream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * The SDF query under autograd (ABI v14): SDFNetwork.sdf(x) with gradients to the
+ * network's parameters and to x -- the stage-1 consistency re-query of
+ * train.py:502-505 (neus_fields.py:268-283 and its autograd backward; the §8(b)
+ * cn_mlp_fwd / cn_mlp_bwd) -- as two calls.  cn_mlp_fwd writes sdf [M] and keeps the
+ * layer activations in the caller's `state` buffer (cn_mlp_state_bytes; unchanged until
+ * cn_mlp_bwd has run).  cn_mlp_bwd takes dsdf [M] = dL/dsdf and that state and writes
+ *   dW[l] [out_dim[l]][in_dim[l]] (row-major) and db[l] [out_dim[l]], l = 0 .. n_lin-1:
+ *     the gradients of the effective weights (weight-norm's backward stays the caller's);
+ *     the last Linear's rows past the sdf row (the feature head, unused by sdf()) are zero;
+ *   dx [M][4] (16-byte aligned) = dL/dx when dx != NULL;
+ *   dW[0] == NULL: dx only, no parameter gradients.
+ * The network needs the transposed images (Wt, head_wp; cn_sdf_net ABI v13).  Scratch
+ * from workspace (cn_mlp_bwd_workspace_bytes); state and workspace 256-byte aligned.
+ * Bitwise equal to copenerf.fields.sdf_forward (keep) and sdf_backward (sdf only, first
+ * order) / sdf_input_grad with the same packs.  M = 0: nothing is written.
+ * ------------------------------------------------------------------------ */
+typedef struct cn_mlp_desc {
+    int32_t M;
+    const float* x;                     /* [M][4] (x, y, z, t) -- cn_mlp_fwd */
+    const cn_sdf_net* net;
+    float* sdf;                         /* [M] -- cn_mlp_fwd */
+    const float* dsdf;                  /* [M] -- cn_mlp_bwd */
+    float* dW[CN_SDF_MAX_LIN];
+    float* db[CN_SDF_MAX_LIN];
+    float* dx;
+} cn_mlp_desc;
+size_t cn_mlp_state_bytes(const cn_mlp_desc* d);
+size_t cn_mlp_bwd_workspace_bytes(const cn_mlp_desc* d);
+int cn_mlp_fwd(const cn_mlp_desc* d, void* state, int64_t state_bytes, cn_stream_t stream);
+int cn_mlp_bwd(const cn_mlp_desc* d, const void* state, int64_t state_bytes, void* workspace,
+               int64_t workspace_bytes, cn_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -37,7 +37,7 @@ def test_struct_layouts_match_header_order():
     for cname, py in (("cn_linear_desc", _lib.LinearDesc), ("cn_wgrad_desc", _lib.WgradDesc),
                       ("cn_sdf_mlp_desc", _lib.SdfMlpDesc), ("cn_sdf_net", _lib.SdfNet),
                       ("cn_sample_desc", _lib.SampleDesc), ("cn_color_net", _lib.ColorNet),
-                      ("cn_render_desc", _lib.RenderDesc)):
+                      ("cn_render_desc", _lib.RenderDesc), ("cn_mlp_desc", _lib.MlpDesc)):
         body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (cname, cname), src, re.S).group(1)
         body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
         names = []
@@ -203,6 +203,48 @@ def test_render_fwd_checks_without_gpu():
     c.in_dim[0] = 4 + 27 + 4 + 128
     c.w_cols[0] = 128 + 64
     assert lib.cn_render_fwd(ctypes.byref(d), 4096 * 256, ws, None) == -5
+
+
+def test_mlp_entry_points_check_and_plan_without_gpu():
+    """ABI v14: cn_mlp_fwd / cn_mlp_bwd size the kept state and the backward's workspace on the host and
+    refuse incomplete descriptors before anything launches."""
+    from copenerf import _lib
+    lib = _lib.load()
+    assert lib.cn_mlp_fwd(None, None, 0, None) == -1
+    assert lib.cn_mlp_state_bytes(None) == 0 and lib.cn_mlp_bwd_workspace_bytes(None) == 0
+    n = _fake_net()  # bf16 images, d_hidden 256, skip 4
+    M = 65536
+    d = _lib.MlpDesc()
+    d.M, d.x, d.sdf, d.net = M, 4096, 4096, ctypes.pointer(n)
+    # U_0 fp32 [M][64], U_1 .. U_7 bf16 images (the skip input's too), U_8 fp32
+    want = M * 64 * 4 + 7 * M * 256 * 2 + M * 256 * 4
+    assert lib.cn_mlp_state_bytes(ctypes.byref(d)) == want
+    assert lib.cn_mlp_fwd(ctypes.byref(d), 4096 * 256, want - 1, None) == -2
+    f = _fake_net(mode=0)
+    d.net = ctypes.pointer(f)
+    assert lib.cn_mlp_state_bytes(ctypes.byref(d)) == M * 64 * 4 + 8 * M * 256 * 4
+    d.net = ctypes.pointer(n)
+    d.dsdf = 4096
+    assert lib.cn_mlp_bwd(ctypes.byref(d), 4096 * 256, want, 4096 * 256, 1 << 40, None) == -1
+    assert b"neither" in lib.cn_last_error()
+    d.dx = 4096
+    assert lib.cn_mlp_bwd(ctypes.byref(d), 4096 * 256, want, 4096 * 256, 1 << 40, None) == -2
+    assert b"transposed image 0" in lib.cn_last_error()
+    for l in range(8):
+        n.Wt[l], n.wt_rows[l], n.wt_cols[l] = 4096, 256, 256
+    n.head_wp = 4096
+    dx_only = lib.cn_mlp_bwd_workspace_bytes(ctypes.byref(d))
+    assert dx_only == 2 * M * 256 * 4 + 2 * M * 64 * 4  # two fp32 adjoints, PE, P0
+    for l in range(9):
+        d.dW[l], d.db[l] = 4096, 4096
+    d.db[3] = None
+    assert lib.cn_mlp_bwd(ctypes.byref(d), 4096 * 256, want, 4096 * 256, 1 << 40, None) == -1
+    assert b"db[3]" in lib.cn_last_error()
+    d.db[3] = 4096
+    full = lib.cn_mlp_bwd_workspace_bytes(ctypes.byref(d))
+    assert full >= 7 * M * 256 * 2 + M * 256 * 4 + 2 * M * 64 * 4  # Z_7 .. Z_1 images, Z_0, PE, P0
+    assert lib.cn_mlp_bwd(ctypes.byref(d), 4096 * 256, want, 4096 * 256, full - 1, None) == -2
+    assert b"workspace" in lib.cn_last_error()
 
 
 def test_product_path_refuses_cpu_tensors():
