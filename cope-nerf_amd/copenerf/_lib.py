@@ -109,6 +109,9 @@ class ColorNet(ctypes.Structure):
         ("multires_view", c_i32), ("mfma_dtype", c_i32),
         ("W", c_ptr * (SDF_MAX_LIN - 1)), ("w_rows", c_i32 * (SDF_MAX_LIN - 1)), ("w_cols", c_i32 * (SDF_MAX_LIN - 1)),
         ("bias", c_ptr * (SDF_MAX_LIN - 1)), ("head_w", c_ptr), ("head_b", c_ptr),
+        ("Wt", c_ptr * (SDF_MAX_LIN - 1)), ("wt_rows", c_i32 * (SDF_MAX_LIN - 1)), ("wt_cols", c_i32 * (SDF_MAX_LIN - 1)),
+        ("Wtf", c_ptr), ("wtf_rows", c_i32), ("wtf_cols", c_i32), ("Wg", c_ptr), ("wg_ld", c_i32), ("Wxt", c_ptr),
+        ("wxt_rows", c_i32), ("wxt_cols", c_i32),
     ]
 
 
@@ -127,6 +130,15 @@ class RenderDesc(ctypes.Structure):
         ("z_in", c_ptr), ("inv_s", c_ptr), ("cos_anneal_ratio", c_ptr), ("sdf_net", ctypes.POINTER(SdfNet)),
         ("color_net", ctypes.POINTER(ColorNet)), ("z", c_ptr), ("pts", c_ptr), ("sdf", c_ptr), ("grad", c_ptr),
         ("rgb", c_ptr), ("color", c_ptr), ("depth", c_ptr), ("weights", c_ptr), ("cdf", c_ptr),
+    ]
+
+
+class RenderGrads(ctypes.Structure):
+    _fields_ = [
+        ("dcolor", c_ptr), ("ddepth", c_ptr), ("dweights", c_ptr), ("dcdf", c_ptr), ("dsdf", c_ptr), ("dgrad", c_ptr),
+        ("dpts", c_ptr), ("sdf_dW", c_ptr * SDF_MAX_LIN), ("sdf_db", c_ptr * SDF_MAX_LIN),
+        ("col_dW", c_ptr * SDF_MAX_LIN), ("col_db", c_ptr * SDF_MAX_LIN), ("dinv_s", c_ptr), ("drays_o", c_ptr),
+        ("drays_d", c_ptr),
     ]
 
 
@@ -203,6 +215,10 @@ SIGNATURES = {
     "cn_sample": (c_i32, [ctypes.POINTER(SampleDesc), c_ptr, c_i64, c_ptr]),
     "cn_render_fwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(RenderDesc)]),
     "cn_render_fwd": (c_i32, [ctypes.POINTER(RenderDesc), c_ptr, c_i64, c_ptr]),
+    "cn_render_state_bytes": (ctypes.c_size_t, [ctypes.POINTER(RenderDesc)]),
+    "cn_render_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(RenderDesc), c_i32]),
+    "cn_render_train_fwd": (c_i32, [ctypes.POINTER(RenderDesc), c_ptr, c_i64, c_ptr]),
+    "cn_render_bwd": (c_i32, [ctypes.POINTER(RenderDesc), ctypes.POINTER(RenderGrads), c_ptr, c_i64, c_ptr, c_i64, c_ptr]),
     "cn_mlp_state_bytes": (ctypes.c_size_t, [ctypes.POINTER(MlpDesc)]),
     "cn_mlp_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(MlpDesc)]),
     "cn_mlp_fwd": (c_i32, [ctypes.POINTER(MlpDesc), c_ptr, c_i64, c_ptr]),

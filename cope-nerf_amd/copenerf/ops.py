@@ -646,6 +646,17 @@ def color_net(lay, pk):
         n.bias[l] = aligned(pk.b[l])
     n.head_w = aligned(pk.W3)
     n.head_b = aligned(pk.b3)
+
+    def image(B):  # (pointer, rows, columns) of a GEMM image as cn_linear reads it
+        keep.append(B)
+        return (B.data_ptr(),) + ((B.shape[1], 16 * B.shape[0]) if x6 else (B.shape[0], B.shape[1]))
+
+    for l in range(1, lay.n_lin - 1):  # the backward's transposed images (cn_render_bwd)
+        n.Wt[l], n.wt_rows[l], n.wt_cols[l] = image(pk.Bt[l])
+    n.Wtf, n.wtf_rows, n.wtf_cols = image(pk.Btf)
+    n.Wxt, n.wxt_rows, n.wxt_cols = image(pk.Bxt)
+    n.Wg = aligned(pk.Wg)
+    n.wg_ld = pk.Wg.stride(0)
     return n, keep
 
 
@@ -676,6 +687,48 @@ def render_fwd(sdf_net_, color_net_, rays_o, rays_d, near, far, time_step, inv_s
     ws = torch.empty(max(int(lib.cn_render_fwd_workspace_bytes(ctypes.byref(d))), 1), dtype=torch.uint8, device=dev)
     _lib.check(lib.cn_render_fwd(ctypes.byref(d), _ptr(ws), ws.numel(), _stream()), "cn_render_fwd")
     return out
+
+
+def render_train_fwd(sdf_net_, color_net_, rays_o, rays_d, near, far, time_step, inv_s, car, n_coarse, z):
+    """render_core at the samples z [R, S] keeping its backward's state -- cn_render_train_fwd: returns the outputs
+    (pts [M, 4], sdf [M, 1], grad [M, 4], color [R, 3], depth [R, 1], weights, cdf [R, S]), the state buffer and the
+    descriptor render_bwd takes (the inputs must stay alive and unchanged until then)."""
+    R, S = z.shape
+    M, dev = R * S, z.device
+    f = lambda *s: torch.empty(*s, device=dev)  # noqa: E731
+    out = dict(pts=f(M, 4), sdf=f(M, 1), grad=f(M, 4), color=f(R, 3), depth=f(R, 1), weights=f(R, S), cdf=f(R, S))
+    d = _lib.RenderDesc()
+    d.R, d.n_samples, d.S_in = R, n_coarse, S
+    d.rays_o, d.rays_d, d.near, d.far = _ptr(rays_o), _ptr(rays_d), _ptr(near), _ptr(far)
+    d.time_step, d.z_in, d.inv_s, d.cos_anneal_ratio = _ptr(time_step), _ptr(z), _ptr(inv_s), _ptr(car)
+    d.sdf_net, d.color_net = ctypes.pointer(sdf_net_), ctypes.pointer(color_net_)
+    for k, v in out.items():
+        setattr(d, k, v.data_ptr())
+    lib = _lib.load()
+    state = torch.empty(max(int(lib.cn_render_state_bytes(ctypes.byref(d))), 1), dtype=torch.uint8, device=dev)
+    _lib.check(lib.cn_render_train_fwd(ctypes.byref(d), _ptr(state), state.numel(), _stream()), "cn_render_train_fwd")
+    return out, state, d
+
+
+def render_bwd(d, state, *, dcolor=None, ddepth=None, dweights=None, dcdf=None, dsdf=None, dgrad=None, dpts=None,
+               sdf_dWs, sdf_dbs, col_dWs, col_dbs, dinv_s, drays_o=None, drays_d=None):
+    """The backward of render_train_fwd -- cn_render_bwd (upstream gradients contiguous float32 or None)."""
+    for t in (dcolor, ddepth, dweights, dcdf, dsdf, dgrad, dpts):
+        if t is not None and (not t.is_contiguous() or t.dtype != torch.float32):
+            raise RuntimeError("render_bwd: upstream gradients must be contiguous float32")
+    g = _lib.RenderGrads()
+    g.dcolor, g.ddepth, g.dweights, g.dcdf = _ptr(dcolor), _ptr(ddepth), _ptr(dweights), _ptr(dcdf)
+    g.dsdf, g.dgrad, g.dpts = _ptr(dsdf), _ptr(dgrad), _ptr(dpts)
+    for l, (w, b) in enumerate(zip(sdf_dWs, sdf_dbs)):
+        g.sdf_dW[l], g.sdf_db[l] = _ptr(w), _ptr(b)
+    for l, (w, b) in enumerate(zip(col_dWs, col_dbs)):
+        g.col_dW[l], g.col_db[l] = _ptr(w), _ptr(b)
+    g.dinv_s, g.drays_o, g.drays_d = _ptr(dinv_s), _ptr(drays_o), _ptr(drays_d)
+    lib = _lib.load()
+    nb = int(lib.cn_render_bwd_workspace_bytes(ctypes.byref(d), 1 if drays_o is not None else 0))
+    ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=state.device)
+    _lib.check(lib.cn_render_bwd(ctypes.byref(d), ctypes.byref(g), _ptr(state), state.numel(), _ptr(ws), ws.numel(),
+                                 _stream()), "cn_render_bwd")
 
 
 def sdf_query(net, x, sdf, idx=None):

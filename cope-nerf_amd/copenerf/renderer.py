@@ -91,6 +91,61 @@ class _CompositeFn(torch.autograd.Function):
                 drgb if ctx.needs_input_grad[3] else None, drays_d, dinv_s, None, None, None, None)
 
 
+class _RenderTrainFn(torch.autograd.Function):
+    """render_core under autograd (neus_renderer.py:307-450) as two C calls, cn_render_train_fwd / cn_render_bwd:
+    the points, the SDF field with ∇ₓSDF, the colour network with the folded feature head and the compositing,
+    and their backward with the gradient sums autograd makes between _PointsFn, _SDFFieldFn, _ColorFieldFn and
+    _CompositeFn -- bitwise that composition (RENDER_NATIVE off).
+    (rays_o, rays_d, inv_s, z, time_step, near, far, car, n_coarse, layouts and packs, *sdf params, *colour params)
+    -> (sdf [M,1], ∇ₓSDF [M,4], points [M,4], colour [R,3], weighted z [R,1], weights [R,S], cdf [R,S])."""
+
+    @staticmethod
+    def forward(ctx, rays_o, rays_d, inv_s, z, time_step, near, far, car, n_coarse, sdf_lay, sdf_pk, col_lay, col_pk,
+                n_sdf, *params):
+        ctx.set_materialize_grads(False)
+        sn, k1 = ops.sdf_net(sdf_lay, sdf_pk)
+        cn, k2 = ops.color_net(col_lay, col_pk)
+        inv_s = inv_s.contiguous()
+        out, state, d = ops.render_train_fwd(sn, cn, rays_o, rays_d, near, far, time_step, inv_s, car, n_coarse, z)
+        # the descriptor points into the inputs, the networks' images and the sdf / ∇ₓSDF outputs: hold them
+        ctx.native = (sn, cn, k1, k2, state, d, (rays_o, rays_d, inv_s, z, time_step, near, far, car))
+        ctx.save_for_backward(out["sdf"], out["grad"])
+        ctx.lays, ctx.n_sdf, ctx.inv_shape = (sdf_lay, col_lay), n_sdf, inv_s.shape
+        ctx.pose = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+        if not ctx.pose:
+            ctx.mark_non_differentiable(out["pts"])
+        return out["sdf"], out["grad"], out["pts"], out["color"], out["depth"], out["weights"], out["cdf"]
+
+    @staticmethod
+    def backward(ctx, dsdf, dgrad, dpts, dcolor, ddepth, dweights, dcdf):
+        sn, cn, k1, k2, state, d, inputs = ctx.native
+        ctx.native = None
+        saved = ctx.saved_tensors  # (sdf, ∇ₓSDF: read by the compositing's backward)
+        sdf_lay, col_lay = ctx.lays
+        dev = state.device
+        R = inputs[3].shape[0]
+        c = lambda t: None if t is None else t.contiguous()  # noqa: E731
+        sdf_dWs = [torch.empty(sdf_lay.out_dim[l], sdf_lay.in_dim[l], device=dev) for l in range(sdf_lay.n_lin)]
+        sdf_dbs = [torch.empty(sdf_lay.out_dim[l], device=dev) for l in range(sdf_lay.n_lin)]
+        col_dWs = [torch.empty(col_lay.out_dim[l], col_lay.in_dim[l], device=dev) for l in range(col_lay.n_lin)]
+        col_dbs = [torch.empty(col_lay.out_dim[l], device=dev) for l in range(col_lay.n_lin)]
+        dinv = torch.empty(R, device=dev)
+        do = torch.empty(R, 3, device=dev) if ctx.pose else None
+        dd = torch.empty(R, 3, device=dev) if ctx.pose else None
+        ops.render_bwd(d, state, dcolor=c(dcolor), ddepth=c(ddepth), dweights=c(dweights), dcdf=c(dcdf), dsdf=c(dsdf),
+                       dgrad=c(dgrad), dpts=c(dpts) if ctx.pose else None, sdf_dWs=sdf_dWs, sdf_dbs=sdf_dbs,
+                       col_dWs=col_dWs, col_dbs=col_dbs, dinv_s=dinv, drays_o=do, drays_d=dd)
+        del k1, k2, state, inputs, saved
+        dinv_s = dinv.sum().reshape(ctx.inv_shape) if ctx.needs_input_grad[2] else None
+        grads = []
+        for w, b in zip(sdf_dWs, sdf_dbs):
+            grads += [w, b]
+        for w, b in zip(col_dWs, col_dbs):
+            grads += [w, b]
+        return (do if ctx.needs_input_grad[0] else None, dd if ctx.needs_input_grad[1] else None, dinv_s) + \
+            (None,) * 11 + tuple(grads)
+
+
 class NeuSRenderer(nn.Module):
     """Reference: model/neus_renderer.py:107-135 (constructor) and 453-584 (forward)."""
 
@@ -234,6 +289,9 @@ class NeuSRenderer(nn.Module):
         S = z.shape[1]
 
         # render_core (neus_renderer.py:307-450)
+        if RENDER_NATIVE and fold and torch.is_grad_enabled() and background_rgb is None and ops._timer is None:
+            return self._forward_train_native(rays_o, rays_d, ray_d_norm, time_step, near, far, n_samples, z,
+                                              sdf_packed, col_packed, cos_anneal_ratio, eval)
         if rays_o.requires_grad or rays_d.requires_grad:  # pose optimisation (eval.py:51-82, joint pose training)
             pts_time = _PointsFn.apply(rays_o, rays_d, z, time_step, near, far, n_samples)
         else:
@@ -249,6 +307,47 @@ class NeuSRenderer(nn.Module):
         depth_pred = depth / ray_d_norm if eval else depth
         if background_rgb is not None:
             color = color + background_rgb * (1.0 - weights.sum(dim=-1, keepdim=True))
+        normals = G[:, :3].reshape(R, S, 3)
+        sdf_flows = G[:, 3:].reshape(R, S, 1)
+        s_val = (1.0 / inv_s).expand(R * S, 1).reshape(R, S).mean(dim=-1, keepdim=True)
+        with torch.no_grad():
+            weight_inside = weights.sum(dim=-1).detach()
+            weight_outside = weights.new_zeros(R)
+        return {
+            "sdf": sdf,
+            "color_fine": color,
+            "depth_pred": depth_pred,
+            "weighted_z_vals": weighted_z_vals,
+            "s_val": s_val,
+            "cdf_fine": cdf,
+            "weight_sum": weights.sum(dim=-1, keepdim=True),
+            "weight_max": torch.max(weights, dim=-1, keepdim=True)[0],
+            "normals": normals,
+            "sdf_flows": sdf_flows,
+            "sampled_points": pts_time[:, :3].reshape(R, S, 3),
+            "weights": weights,
+            "inside_sphere": torch.ones_like(weights),
+            "weight_inside": weight_inside,
+            "weight_outside": weight_outside,
+        }
+
+    def _forward_train_native(self, rays_o, rays_d, ray_d_norm, time_step, near, far, n_samples, z, sdf_packed,
+                              col_packed, cos_anneal_ratio, eval):
+        """render_core under autograd as _RenderTrainFn (cn_render_train_fwd / cn_render_bwd): the outputs of the
+        path below, the same bits forward and backward."""
+        R, S, dev = rays_o.shape[0], z.shape[1], rays_o.device
+        inv_s = self.deviation_network(torch.zeros([1, 3], device=dev))[:, :1].clip(1 / 1e3, 1 / 1e-3)
+        car = ops.device_scalar(cos_anneal_ratio, dev)
+        params = []
+        for w, b in zip(sdf_packed[0], sdf_packed[1]):
+            params += [w, b]
+        for w, b in zip(col_packed[0], col_packed[1]):
+            params += [w, b]
+        sdf, G, pts_time, color, depth, weights, cdf = _RenderTrainFn.apply(
+            rays_o, rays_d, inv_s, z, time_step, near, far, car, n_samples, self.sdf_network.layout(), sdf_packed[2],
+            self.color_network.layout(), col_packed[2], len(sdf_packed[0]), *params)
+        weighted_z_vals = depth.detach().clone()
+        depth_pred = depth / ray_d_norm if eval else depth
         normals = G[:, :3].reshape(R, S, 3)
         sdf_flows = G[:, 3:].reshape(R, S, 1)
         s_val = (1.0 / inv_s).expand(R * S, 1).reshape(R, S).mean(dim=-1, keepdim=True)

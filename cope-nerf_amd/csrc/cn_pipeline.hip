@@ -405,6 +405,11 @@ struct LinCall {
     const void* aux0 = nullptr;
     bool aux0_b = false;
     int64_t ld_aux0 = 0;
+    const void* aux1 = nullptr;  // BWD_SOFTPLUS's second-order operands (fp32, or images with aux12_b)
+    const void* aux2 = nullptr;
+    int64_t ld_aux1 = 0, ld_aux2 = 0;
+    float aux2_scale = 0.0f;
+    bool aux12_b = false;
     float aux_beta = 0.0f, adiv = 1.0f, odiv = 1.0f, beta = 100.0f, threshold = 20.0f;
     float* out0 = nullptr;
     int64_t ld_out0 = 0;
@@ -436,6 +441,12 @@ int run_linear(int mode, const LinCall& c, int flip, hipStream_t st) {
     d.bias = c.bias;
     d.colv = c.colv;
     d.aux0 = c.aux0;
+    d.aux1 = static_cast<const float*>(c.aux1);
+    d.aux2 = static_cast<const float*>(c.aux2);
+    d.ld_aux1 = c.ld_aux1;
+    d.ld_aux2 = c.ld_aux2;
+    d.aux2_scale = c.aux2_scale;
+    d.aux12_bf16 = c.aux12_b ? 1 : 0;
     d.out0 = c.out0;
     d.out1 = c.out1;
     d.out_split = c.out_split;
@@ -479,10 +490,23 @@ float sig_beta(const cn_sdf_net* n, int l) {
     return (float)((double)n->beta * ((l + 1) == n->skip ? std::sqrt(2.0) : 1.0));
 }
 
-// The SDF field with its ∇ₓSDF pass (fields.sdf_forward, want_feat "hidden", want_grad, keep False):
-// sdf [M], U8 (the last hidden activation, fp32 [M][HL]: the colour network's operand) and G [M][4].
+// What the training forward keeps for the backward (fields.sdf_forward keep=True): the activations U_l (bf16
+// images where ub[l]) and the ∇ pass's adjoints s_l (fp32 S[l] and / or the image Sb[l]).
+struct SdfKeep {
+    float* U0;
+    char* U[CN_SDF_MAX_LIN];
+    bool ub[CN_SDF_MAX_LIN];
+    float* S[CN_SDF_MAX_LIN];
+    void* Sb[CN_SDF_MAX_LIN];
+    bool sf[CN_SDF_MAX_LIN];   // S[l] kept (the pointers are null in a sizing pass: these say what exists)
+    bool sbf[CN_SDF_MAX_LIN];  // Sb[l] kept
+};
+
+// The SDF field with its ∇ₓSDF pass (fields.sdf_forward, want_feat "hidden", want_grad; keep False, or True
+// with `keep` != nullptr: every s_l in its own buffer, recorded there): sdf [M], U8 (the last hidden
+// activation, fp32 [M][HL]: the colour network's operand) and G [M][4].
 int sdf_field_plan(const cn_sdf_net* n, const NetShape& s, int M, const float* x, float* sdf, float** U8_out,
-                   float* G, Plan& ws, hipStream_t st, bool run) {
+                   float* G, Plan& ws, hipStream_t st, bool run, SdfKeep* keep = nullptr) {
     const float kSqrt2 = (float)std::sqrt(2.0);
     const int L8 = s.L8, HL = s.HL, sk = s.sk, KE = s.KE;
     const size_t eh = s.img ? 2 : 4;  // the hidden activations' element size (bf16 images in the image mode)
@@ -499,11 +523,46 @@ int sdf_field_plan(const cn_sdf_net* n, const NetShape& s, int M, const float* x
     // (fp32 s_7 also from cn_scale_cols where the head is not fused)
     float* S7 = (fp32_s7 || !s.fuse_head) ? static_cast<float*>(ws.take((size_t)M * HL * 4)) : nullptr;
     void* S7b = s.img ? ws.take((size_t)M * HL * 2) : nullptr;
-    // the ∇ pass: two ping-pong adjoints (images in the image mode), s_0 also fp32, QE, Q0
-    char* Sp[2] = {static_cast<char*>(ws.take((size_t)M * HL * eh)), static_cast<char*>(ws.take((size_t)M * HL * eh))};
-    float* S0 = static_cast<float*>(ws.take((size_t)M * HL * 4));
+    // the ∇ pass: two ping-pong adjoints (images in the image mode), s_0 also fp32, QE, Q0; kept: s_0 .. s_{L8-2}
+    // each in its own buffer (fp32 where not the image mode or l = 0, the image in the image mode)
+    char* Sp[2] = {nullptr, nullptr};
+    float* S0 = nullptr;
+    float* Sk[CN_SDF_MAX_LIN] = {};
+    void* Sbk[CN_SDF_MAX_LIN] = {};
+    if (keep) {
+        for (int l = 0; l + 1 < L8; ++l) {
+            Sbk[l] = s.img ? ws.take((size_t)M * HL * 2) : nullptr;
+            Sk[l] = (!s.img || l == 0) ? static_cast<float*>(ws.take((size_t)M * HL * 4)) : nullptr;
+        }
+        S0 = Sk[0];
+    } else {
+        Sp[0] = static_cast<char*>(ws.take((size_t)M * HL * eh));
+        Sp[1] = static_cast<char*>(ws.take((size_t)M * HL * eh));
+        S0 = static_cast<float*>(ws.take((size_t)M * HL * 4));
+    }
     float* QE = sk >= 0 ? static_cast<float*>(ws.take((size_t)M * KE * 4)) : nullptr;
     float* Q0 = static_cast<float*>(ws.take((size_t)M * KE * 4));
+    if (keep) {  // (fields.sdf_forward keep: st["U"], st["Ub"], st["S"], st["Sb"])
+        keep->U0 = U0;
+        keep->U[0] = nullptr;
+        keep->ub[0] = false;
+        for (int l = 1; l <= L8; ++l) {
+            keep->U[l] = U[l];
+            keep->ub[l] = ub[l];
+        }
+        for (int l = 0; l + 1 < L8; ++l) {
+            keep->S[l] = Sk[l];
+            keep->sf[l] = !s.img || l == 0;
+            keep->Sb[l] = Sbk[l];
+            keep->sbf[l] = s.img;
+        }
+        // s_7: fp32 from the head epilogue (not the image mode) or cn_scale_cols (no fused head); its image
+        // from the head epilogue in the image mode
+        keep->S[L8 - 1] = S7;
+        keep->sf[L8 - 1] = fp32_s7 || !s.fuse_head;
+        keep->Sb[L8 - 1] = (s.img && s.fuse_head) ? S7b : nullptr;
+        keep->sbf[L8 - 1] = s.img && s.fuse_head;
+    }
     if (!run) return CN_OK;
     void* e_view = nullptr;
     if (sk >= 0) e_view = U[sk] + (size_t)n->out_dim[sk - 1] * (usk_b ? 2 : 4);
@@ -599,7 +658,7 @@ int sdf_field_plan(const cn_sdf_net* n, const NetShape& s, int M, const float* x
         } else {
             c.N = n->out_dim[l - 1];
         }
-        char* dst = Sp[l & 1];
+        char* dst = keep ? static_cast<char*>(s.img ? Sbk[l - 1] : static_cast<void*>(Sk[l - 1])) : Sp[l & 1];
         if (s.img) {
             c.out0_b = dst;
             c.ld_out0_b = HL;
@@ -638,12 +697,31 @@ int sdf_field_plan(const cn_sdf_net* n, const NetShape& s, int M, const float* x
 }
 
 // the colour network (_ColorFieldFn.forward): rgb [M][3]
+// What the colour network's training forward keeps: the extras and every hidden activation (bf16 images
+// where the image mode stores images only).
+struct ColorKeep {
+    float* ext;
+    char* H[CN_SDF_MAX_LIN];
+    bool hb[CN_SDF_MAX_LIN];
+};
+
 int color_field_plan(const cn_color_net* c, const ColorShape& s, int M, const float* G, const float* pts,
                      const float* dirs, int dir_div, const float* feat, int64_t ld_feat, float* rgb, Plan& ws,
-                     hipStream_t st, bool run) {
+                     hipStream_t st, bool run, ColorKeep* keep = nullptr) {
     const int n = c->n_lin, HL = s.HL;
     float* ext = static_cast<float*>(ws.take((size_t)M * s.KX * 4));
-    char* H[2] = {static_cast<char*>(ws.take((size_t)M * HL * 4)), static_cast<char*>(ws.take((size_t)M * HL * 4))};
+    char* H[2] = {nullptr, nullptr};
+    char* Hk[CN_SDF_MAX_LIN] = {};
+    if (keep) {
+        keep->ext = ext;
+        for (int l = 0; l < n - 1; ++l) {
+            keep->hb[l] = s.img && l < n - 2;
+            Hk[l] = keep->H[l] = static_cast<char*>(ws.take((size_t)M * HL * (keep->hb[l] ? 2 : 4)));
+        }
+    } else {
+        H[0] = static_cast<char*>(ws.take((size_t)M * HL * 4));
+        H[1] = static_cast<char*>(ws.take((size_t)M * HL * 4));
+    }
     if (!run) return CN_OK;
     int rc = cn_color_extras(M, G, 4, pts, 4, dirs, 3, dir_div, c->multires_view, s.KX, ext, s.KX, st);
     if (rc) return rc;
@@ -672,7 +750,7 @@ int color_field_plan(const cn_color_net* c, const ColorShape& s, int M, const fl
         k.bias = c->bias[l];
         k.nzero = HL;
         k.M = M;
-        char* dst = H[l & 1];
+        char* dst = keep ? Hk[l] : H[l & 1];
         const bool img = s.img && l < n - 2;  // the next layer's operand image, the activation's only copy
         if (img) {
             k.out0_b = dst;
@@ -690,7 +768,7 @@ int color_field_plan(const cn_color_net* c, const ColorShape& s, int M, const fl
     return cn_row_head(M, c->in_dim[n - 1], last, HL, c->head_w, c->in_dim[n - 1], c->head_b, 3, 1, rgb, 3, nullptr, st);
 }
 
-int render_check(const cn_render_desc* d, NetShape* s, ColorShape* cs) {
+int render_check(const cn_render_desc* d, NetShape* s, ColorShape* cs, bool train = false) {
     CN_REQUIRE(d, CN_ERR_ARG, "cn_render_fwd: null descriptor");
     int rc = net_shape(d->sdf_net, s);
     if (rc) return rc;
@@ -711,7 +789,8 @@ int render_check(const cn_render_desc* d, NetShape* s, ColorShape* cs) {
     CN_REQUIRE(d->R >= 0 && d->rays_o && d->rays_d && d->near && d->far && d->time_step && d->inv_s &&
                    d->cos_anneal_ratio,
                CN_ERR_ARG, "cn_render_fwd: null input");
-    CN_REQUIRE(d->z && d->pts && d->sdf && d->grad && d->rgb && d->color && d->depth && d->weights && d->cdf,
+    CN_REQUIRE((train || (d->z && d->rgb)) && d->pts && d->sdf && d->grad && d->color && d->depth && d->weights &&
+                   d->cdf,
                CN_ERR_ARG, "cn_render_fwd: null output");
     CN_REQUIRE(((uintptr_t)d->pts & 15) == 0 && ((uintptr_t)d->grad & 15) == 0, CN_ERR_ALIGN,
                "cn_render_fwd: pts / grad 16-byte aligned");
@@ -1150,4 +1229,555 @@ extern "C" int cn_mlp_bwd(const cn_mlp_desc* d, const void* state, int64_t state
     mlp_state_plan(s, d->M, p, &st);
     Plan ws(workspace);
     return mlp_bwd_plan(d, s, st, ws, (hipStream_t)stream, true);
+}
+
+// ---------------------------------------------------------------------------------------------
+// cn_render_train_fwd / cn_render_bwd (ABI v14): render_core under autograd (neus_renderer.py:307-450) --
+// the training forward keeping its state, and the backward of copenerf's composition: _CompositeFn,
+// _ColorFieldFn, _SDFFieldFn (fields.sdf_backward with the folded feature head: second order, dh) and
+// _PointsFn, with the gradient sums autograd makes between them, in its order.
+namespace {
+
+// out[m][c] = a[m][c] + b[m][c], c < C <= 4 (strided rows; one thread per row): autograd's sum of two
+// gradients (one fp32 add each, the bits of torch's add)
+__global__ void __launch_bounds__(256) add2_kernel(int M, int C, const float* __restrict__ a, int64_t lda,
+                                                   const float* __restrict__ b, int64_t ldb, float* __restrict__ out,
+                                                   int64_t ldo) {
+    const int m = blockIdx.x * 256 + threadIdx.x;
+    if (m >= M) return;
+    float v[4];
+    for (int c = 0; c < C; ++c) v[c] = a[(int64_t)m * lda + c] + b[(int64_t)m * ldb + c];
+    for (int c = 0; c < C; ++c) out[(int64_t)m * ldo + c] = v[c];
+}
+
+int add2(int M, int C, const float* a, int64_t lda, const float* b, int64_t ldb, float* out, int64_t ldo,
+         hipStream_t stream) {
+    if (M <= 0) return CN_OK;
+    CN_REQUIRE(C >= 1 && C <= 4, CN_ERR_ARG, "cn_render_bwd: add of %d columns", C);
+    add2_kernel<<<(M + 255) / 256, 256, 0, stream>>>(M, C, a, lda, b, ldb, out, ldo);
+    CN_REQUIRE(hipGetLastError() == hipSuccess, CN_ERR_LAUNCH, "cn_render_bwd: add launch failed");
+    return CN_OK;
+}
+
+// dst[r][c] = src[r][c], c < C: the colour lin0 gradient's columns into the reference order
+__global__ void __launch_bounds__(256) copy_cols_kernel(int R, int C, const float* __restrict__ src, int64_t lds,
+                                                        float* __restrict__ dst, int64_t ldd) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < R * C) dst[(int64_t)(i / C) * ldd + i % C] = src[(int64_t)(i / C) * lds + i % C];
+}
+
+int copy_cols(int R, int C, const float* src, int64_t lds, float* dst, int64_t ldd, hipStream_t stream) {
+    if (R <= 0 || C <= 0) return CN_OK;
+    copy_cols_kernel<<<(R * C + 255) / 256, 256, 0, stream>>>(R, C, src, lds, dst, ldd);
+    CN_REQUIRE(hipGetLastError() == hipSuccess, CN_ERR_LAUNCH, "cn_render_bwd: copy launch failed");
+    return CN_OK;
+}
+
+struct TrainState {
+    SdfKeep sk;
+    ColorKeep ck;
+    float* rgb;
+};
+
+int train_check(const cn_render_desc* d, NetShape* s, ColorShape* cs) {
+    int rc = render_check(d, s, cs, true);
+    if (rc) return rc;
+    CN_REQUIRE(d->z_in && d->S_in >= 1, CN_ERR_ARG, "cn_render_train_fwd / bwd: the samples z_in [R][S_in] are required");
+    return CN_OK;
+}
+
+// The state's plan (and, run, the training forward): the points, the SDF field keeping its activations and
+// adjoints, the colour network keeping its hidden activations, the compositing.
+int train_fwd_plan(const cn_render_desc* d, const NetShape& s, const ColorShape& cs, Plan& p, TrainState* t,
+                   hipStream_t st, bool run) {
+    const int R = d->R, S = d->S_in, M = R * S;
+    t->rgb = static_cast<float*>(p.take((size_t)M * 12));
+    float* U8 = nullptr;
+    int rc = CN_OK;
+    if (run && (rc = cn_points(R, S, d->rays_o, d->rays_d, d->z_in, d->time_step, 1, d->near, d->far, d->n_samples,
+                               d->pts, st)))
+        return rc;
+    if ((rc = sdf_field_plan(d->sdf_net, s, M, d->pts, d->sdf, &U8, d->grad, p, st, run, &t->sk))) return rc;
+    if ((rc = color_field_plan(d->color_net, cs, M, d->grad, d->pts, d->rays_d, S, U8, s.HL, t->rgb, p, st, run,
+                               &t->ck)))
+        return rc;
+    if (!run) return CN_OK;
+    return cn_composite_fwd(R, S, d->z_in, d->sdf, d->grad, 4, t->rgb, d->rays_d, d->inv_s, d->near, d->far,
+                            d->n_samples, d->cos_anneal_ratio, d->color, d->depth, d->weights, d->cdf, st);
+}
+
+// a wgrad descriptor as ops._wgrad_desc builds it (K rounded to 64; ld_dw the destination's)
+// (npairs explicit: a sizing pass has null operand pointers)
+cn_wgrad_desc wgrad_job(int npairs, const void* Y0, bool yb, int64_t ldy, const void* X0, bool xb, int64_t ldx,
+                        const void* Y1, int64_t ldy1, const void* X1, int64_t ldx1, int M, int N, int K, float* dW,
+                        int64_t ld_dw, float* db, int mode) {
+    cn_wgrad_desc w{};
+    w.Y0 = Y0;
+    w.X0 = X0;
+    w.Y1 = Y1;
+    w.X1 = X1;
+    w.dW = dW;
+    w.db = db;
+    w.ldy0 = ldy;
+    w.ldx0 = ldx;
+    w.ldy1 = npairs == 2 ? ldy1 : 0;
+    w.ldx1 = npairs == 2 ? ldx1 : 0;
+    w.ld_dw = ld_dw;
+    w.M = M;
+    w.N = N;
+    w.K = rup_i(K, 64);
+    w.npairs = npairs;
+    w.n_out = N;
+    w.k_out = K;
+    w.mfma_dtype = mode;
+    w.y_bf16 = yb ? 1 : 0;
+    w.x_bf16 = xb ? 1 : 0;
+    return w;
+}
+
+// Runs a weight-gradient batch out of a workspace piece (sizing pass: only takes the piece).
+int wgrad_batch_run(cn_wgrad_desc* w, int n, Plan& ws, hipStream_t stream, bool run) {
+    int64_t offs[2 * CN_SDF_MAX_LIN];
+    const size_t bytes = cn_wgrad_batch_workspace_bytes(w, n, offs);
+    char* base = static_cast<char*>(ws.take(bytes));
+    if (!run) return CN_OK;
+    for (int i = 0; i < n; ++i) {
+        w[i].workspace = reinterpret_cast<float*>(base + offs[i]);
+        w[i].workspace_bytes = (int64_t)bytes - offs[i];
+    }
+    return cn_wgrad_batch(w, n, stream);
+}
+
+// The backward's plan (run false: sizing; the buffers are taken in the same order either way).
+int render_bwd_plan(const cn_render_desc* d, const cn_render_grads* g, const NetShape& s, const ColorShape& cs,
+                    const TrainState& t, bool pose, Plan& ws, hipStream_t st, bool run) {
+    const cn_sdf_net* n = d->sdf_net;
+    const cn_color_net* c = d->color_net;
+    const float kSqrt2 = (float)std::sqrt(2.0);
+    const int R = d->R, S = d->S_in, M = R * S;
+    const int L8 = s.L8, HL = s.HL, sk = s.sk, KE = s.KE;
+    const int nc = c->n_lin, CHL = cs.HL;
+    const int P = 4, Gd = 4, V = 3 * (1 + 2 * c->multires_view), F = c->d_feature, o0 = c->out_dim[0];
+    int rc = CN_OK;
+    // --- _CompositeFn.backward
+    float* dsdf_c = static_cast<float*>(ws.take((size_t)M * 4));
+    float* dG_c = static_cast<float*>(ws.take((size_t)M * 16));
+    float* drgb = static_cast<float*>(ws.take((size_t)M * 12));
+    float* drd_c = pose ? static_cast<float*>(ws.take((size_t)R * 12)) : nullptr;
+    if (run && (rc = cn_composite_bwd(R, S, d->z_in, d->sdf, d->grad, 4, t.rgb, d->rays_d, d->inv_s, d->near, d->far,
+                                      d->n_samples, d->cos_anneal_ratio, g->dcolor, g->ddepth, g->dweights, g->dcdf,
+                                      dsdf_c, dG_c, drgb, g->dinv_s, drd_c, st)))
+        return rc;
+    // --- _ColorFieldFn.backward (drgb): dZ[l] the adjoint of hidden layer l's output (an image where the
+    // image mode reads it only as an operand, l >= 1)
+    const ColorKeep& ck = t.ck;
+    char* dZ[CN_SDF_MAX_LIN] = {};
+    bool dzb[CN_SDF_MAX_LIN] = {};
+    for (int l = nc - 2; l >= 0; --l) {
+        dzb[l] = cs.img && l >= 1;
+        dZ[l] = static_cast<char*>(ws.take((size_t)M * CHL * (dzb[l] ? 2 : 4)));
+    }
+    const size_t rh_bytes = cn_rgb_head_bwd_workspace_bytes(M, c->in_dim[nc - 1]);
+    float* rh_ws = static_cast<float*>(ws.take(rh_bytes));
+    if (run && (rc = cn_rgb_head_bwd(M, c->in_dim[nc - 1], drgb, t.rgb, reinterpret_cast<const float*>(ck.H[nc - 2]),
+                                     CHL, c->head_w, dZ[nc - 2], CHL, dzb[nc - 2] ? 1 : 0, g->col_dW[nc - 1],
+                                     g->col_db[nc - 1], rh_ws, (int64_t)rh_bytes, st)))
+        return rc;
+    cn_wgrad_desc cw[CN_SDF_MAX_LIN] = {};
+    int ncw = 0;
+    for (int l = nc - 2; l >= 1; --l) {
+        cw[ncw++] = wgrad_job(1, dZ[l], dzb[l], CHL, ck.H[l - 1], ck.hb[l - 1], CHL, nullptr, 0, nullptr, 0, M,
+                              c->out_dim[l], c->in_dim[l], g->col_dW[l], c->in_dim[l], g->col_db[l], c->mfma_dtype);
+        LinCall k;
+        k.A = dZ[l];
+        k.a_b = dzb[l];
+        k.lda = CHL;
+        k.B = c->Wt[l];
+        k.b_rows = c->wt_rows[l];
+        k.b_cols = c->wt_cols[l];
+        k.N = c->out_dim[l - 1];
+        k.K = rup_i(c->out_dim[l], 32);
+        k.epi = CN_EPI_BWD_RELU;
+        k.aux0 = ck.H[l - 1];
+        k.aux0_b = ck.hb[l - 1];
+        k.ld_aux0 = CHL;
+        k.nzero = CHL;
+        k.M = M;
+        if (dzb[l - 1]) {
+            k.out0_b = dZ[l - 1];
+            k.ld_out0_b = CHL;
+        } else {
+            k.out0 = reinterpret_cast<float*>(dZ[l - 1]);
+            k.ld_out0 = CHL;
+        }
+        if (run && (rc = run_linear(c->mfma_dtype, k, l, st))) return rc;
+    }
+    const float* U8 = reinterpret_cast<const float*>(t.sk.U[L8]);
+    const float* dZ0 = reinterpret_cast<const float*>(dZ[0]);
+    // lin0's feature columns to dWf, its extras columns to dWx: then both into the reference column order
+    float* dW0 = g->col_dW[0];
+    const int64_t ld0 = c->in_dim[0];
+    // (a buffer of its own, as fields' dWf: the weight gradient's tile choice reads the destination's alignment)
+    float* dWf = static_cast<float*>(ws.take((size_t)o0 * F * 4));
+    cw[ncw++] = wgrad_job(1, dZ0, false, CHL, U8, false, HL, nullptr, 0, nullptr, 0, M, o0, F, dWf, F, g->col_db[0],
+                          c->mfma_dtype);
+    float* dWx = static_cast<float*>(ws.take((size_t)o0 * cs.KX * 4));
+    {
+        cn_wgrad_desc w = wgrad_job(1, dZ0, false, CHL, ck.ext, false, cs.KX, nullptr, 0, nullptr, 0, M, o0, cs.KX, dWx,
+                                    cs.KX, nullptr, c->mfma_dtype);
+        const size_t b = cn_wgrad_workspace_bytes(M, o0, w.K);
+        w.workspace = static_cast<float*>(ws.take(b));
+        w.workspace_bytes = (int64_t)b;
+        if (run && (rc = cn_wgrad(&w, st))) return rc;
+    }
+    if ((rc = wgrad_batch_run(cw, ncw, ws, st, run))) return rc;
+    if (run) {  // [pts | emb(dirs) | gradient] from dWx's [gradient | pts | emb(dirs)]
+        if ((rc = copy_cols(o0, P, dWx + Gd, cs.KX, dW0, ld0, st)) ||
+            (rc = copy_cols(o0, V, dWx + Gd + P, cs.KX, dW0 + P, ld0, st)) ||
+            (rc = copy_cols(o0, Gd, dWx, cs.KX, dW0 + P + V, ld0, st)) ||
+            (rc = copy_cols(o0, F, dWf, F, dW0 + P + V + Gd, ld0, st)))
+            return rc;
+    }
+    float* dfeat = static_cast<float*>(ws.take((size_t)M * F * 4));
+    {
+        LinCall k;
+        k.A = dZ0;
+        k.lda = CHL;
+        k.B = c->Wtf;
+        k.b_rows = c->wtf_rows;
+        k.b_cols = c->wtf_cols;
+        k.N = F;
+        k.K = rup_i(o0, 32);
+        k.epi = CN_EPI_STORE;
+        k.out0 = dfeat;
+        k.ld_out0 = F;
+        k.nzero = F;
+        k.M = M;
+        if (run && (rc = run_linear(c->mfma_dtype, k, 0, st))) return rc;
+    }
+    const float* dG_col = nullptr;
+    int64_t ld_gcol = 4;
+    const float* dpts_col = nullptr;
+    float* ddirs = nullptr;
+    if (pose) {  // d ext = dZ0 W0[:, ext] in one GEMM, ext = [g | pts | emb(dirs)]
+        float* d_ext = static_cast<float*>(ws.take((size_t)M * 64 * 4));
+        ddirs = static_cast<float*>(ws.take((size_t)R * 12));
+        LinCall k;
+        k.A = dZ0;
+        k.lda = CHL;
+        k.B = c->Wxt;
+        k.b_rows = c->wxt_rows;
+        k.b_cols = c->wxt_cols;
+        k.N = rup_i(Gd + P + V, 4);
+        k.K = rup_i(o0, 32);
+        k.epi = CN_EPI_STORE;
+        k.out0 = d_ext;
+        k.ld_out0 = 64;
+        k.nzero = 64;
+        k.M = M;
+        if (run && (rc = run_linear(c->mfma_dtype, k, 0, st))) return rc;
+        dG_col = d_ext;
+        ld_gcol = 64;
+        dpts_col = d_ext + Gd;
+        if (run && (rc = cn_color_extras_bwd(R, S, d_ext, 64, d->rays_d, 3, c->multires_view, ddirs, 0, st))) return rc;
+    } else {
+        float* dg = static_cast<float*>(ws.take((size_t)M * 16));
+        if (run && (rc = cn_row_head(M, o0, dZ0, CHL, c->Wg, c->wg_ld, nullptr, Gd, 0, dg, Gd, nullptr, st))) return rc;
+        dG_col = dg;
+    }
+    // --- the sums into the SDF field's outputs: ∇ₓSDF = (its own consumers + the compositing's) + the colour
+    // network's; sdf = its own consumers + the compositing's
+    float* dG = static_cast<float*>(ws.take((size_t)M * 16));
+    float* dsdf = dsdf_c;
+    if (run) {
+        if (g->dgrad) {
+            if ((rc = add2(M, 4, g->dgrad, 4, dG_c, 4, dG, 4, st)) || (rc = add2(M, 4, dG, 4, dG_col, ld_gcol, dG, 4, st)))
+                return rc;
+        } else if ((rc = add2(M, 4, dG_c, 4, dG_col, ld_gcol, dG, 4, st))) {
+            return rc;
+        }
+    }
+    // (taken whether or not there is an upstream dsdf: the sizing pass does not see the gradients)
+    float* dsdf_sum = static_cast<float*>(ws.take((size_t)M * 4));
+    if (g->dsdf) {
+        if (run && (rc = add2(M, 1, g->dsdf, 1, dsdf_c, 1, dsdf_sum, 1, st))) return rc;
+        dsdf = dsdf_sum;
+    }
+    // --- _SDFFieldFn.backward: fields.sdf_backward(dsdf, dfeat None, dG, dh = the colour network's dfeat)
+    const SdfKeep& k8 = t.sk;
+    const bool img = s.img;
+    const bool top_img = img && k8.sbf[L8 - 1];  // (fused_cs: the fold makes in_dim[L8] == HL)
+    auto act = [&](int l) { return static_cast<const void*>(l == 0 ? static_cast<void*>(k8.U0) : k8.U[l]); };
+    // the tangent pass u̇
+    float* Ud[CN_SDF_MAX_LIN] = {};
+    void* Udb[CN_SDF_MAX_LIN] = {};
+    bool udb[CN_SDF_MAX_LIN] = {};  // u̇_l kept as its image
+    Ud[0] = static_cast<float*>(ws.take((size_t)M * KE * 4));
+    char* Usk_d = nullptr;
+    bool usk_db = false;
+    if (sk >= 0) {
+        usk_db = img && 1 <= sk && sk < L8;
+        Usk_d = static_cast<char*>(ws.take((size_t)M * HL * (usk_db ? 2 : 4)));
+    }
+    for (int l = 0; l < L8; ++l) {
+        const bool into = (l + 1) == sk;
+        const bool ob = img && (l + 1 < L8 || top_img);
+        char* dst = into ? Usk_d : static_cast<char*>(ws.take((size_t)M * HL * (ob ? 2 : 4)));
+        udb[l + 1] = ob;
+        if (ob)
+            Udb[l + 1] = dst;
+        else
+            Ud[l + 1] = reinterpret_cast<float*>(dst);
+    }
+    // s_{L8-1} in fp32 where a consumer reads it so and the forward kept only the image
+    float* S7f = k8.S[L8 - 1];
+    const bool need_s7f = !k8.sf[L8 - 1] && !top_img;
+    if (need_s7f) S7f = static_cast<float*>(ws.take((size_t)M * HL * 4));
+    auto s_fp32 = [&](int l) -> const float* { return l == L8 - 1 ? S7f : k8.S[l]; };
+    auto z_img = [&](int l) { return img && l >= 1 && l < L8 && k8.sbf[l] && k8.ub[l]; };
+    void* Z[CN_SDF_MAX_LIN] = {};
+    bool zb[CN_SDF_MAX_LIN] = {};
+    zb[L8 - 1] = z_img(L8 - 1);
+    Z[L8 - 1] = ws.take((size_t)M * HL * (zb[L8 - 1] ? 2 : 4));
+    for (int l = L8 - 1; l >= 1; --l) {
+        zb[l - 1] = z_img(l - 1);
+        Z[l - 1] = ws.take((size_t)M * HL * (zb[l - 1] ? 2 : 4));
+    }
+    const size_t sa_bytes = cn_softplus_adjoint_workspace_bytes(M, HL);
+    float* sa_ws = static_cast<float*>(ws.take(sa_bytes));
+    if (run) {
+        void* e_view = nullptr;
+        if (sk >= 0) e_view = Usk_d + (size_t)n->out_dim[sk - 1] * (usk_db ? 2 : 4);
+        if ((rc = cn_sdf_tangent_prep(M, n->multires, n->scale, KE, k8.U0, KE, dG, 4, Ud[0], KE, e_view,
+                                      e_view ? HL : 0, kSqrt2, usk_db ? 1 : 0, st)))
+            return rc;
+        for (int l = 0; l < L8; ++l) {
+            const bool into = (l + 1) == sk;
+            LinCall k;
+            k.A = udb[l] ? Udb[l] : static_cast<const void*>(Ud[l]);
+            k.a_b = udb[l];
+            k.lda = l == 0 ? KE : HL;
+            k.B = n->W[l];
+            k.b_rows = n->w_rows[l];
+            k.b_cols = n->w_cols[l];
+            k.N = n->out_dim[l];
+            k.K = l == 0 ? KE : rup_i(n->in_dim[l], 32);
+            k.epi = CN_EPI_TANGENT;
+            k.aux0 = act(l + 1);
+            k.aux0_b = k8.ub[l + 1];
+            k.ld_aux0 = HL;
+            k.aux_beta = sig_beta(n, l);
+            k.nzero = into ? n->out_dim[l] : HL;
+            if (into) k.odiv = kSqrt2;
+            k.beta = n->beta;
+            k.threshold = n->threshold;
+            k.M = M;
+            if (udb[l + 1]) {
+                k.out0_b = Udb[l + 1];
+                k.ld_out0_b = HL;
+            } else {
+                k.out0 = Ud[l + 1];
+                k.ld_out0 = HL;
+            }
+            if ((rc = run_linear(n->mfma_dtype, k, l, st))) return rc;
+        }
+        if (need_s7f && (rc = cn_scale_cols(M, HL, U8, HL, n->head_wp, nullptr, S7f, HL, sig_beta(n, L8 - 1), st)))
+            return rc;
+        // lin8's feature rows: the fold carries them (dW8[1:], db8[1:] zero)
+        const int i8 = n->in_dim[L8], o8 = n->out_dim[L8];
+        if ((rc = zero_fill(g->sdf_dW[L8] + i8, (int64_t)(o8 - 1) * i8, st)) ||
+            (rc = zero_fill(g->sdf_db[L8] + 1, o8 - 1, st)))
+            return rc;
+    }
+    // the second-order term's operands of layer l (fields.sdf_backward.second_order)
+    struct Second {
+        const void* a1;
+        const void* a2;
+        bool b;
+        float scale;
+    };
+    auto second = [&](int l) {
+        const bool img2 = (l < L8 - 1 || top_img) && k8.sbf[l] && udb[l + 1];
+        Second r;
+        r.a1 = img2 ? k8.Sb[l] : static_cast<const void*>(s_fp32(l));
+        r.a2 = img2 ? Udb[l + 1] : static_cast<const void*>(Ud[l + 1]);
+        r.b = img2;
+        r.scale = n->beta * ((l + 1) == sk ? kSqrt2 : 1.0f);
+        return r;
+    };
+    if (run) {  // Z_7 = (dh + dsdf w80) σ_7 + the second-order term, lin8's sdf row / bias gradients beside
+        const Second so = second(L8 - 1);
+        if ((rc = cn_softplus_adjoint(M, HL, dfeat, F, U8, HL, sig_beta(n, L8 - 1), dsdf, n->head_wp, so.a1, HL, so.a2,
+                                      HL, so.scale, Z[L8 - 1], HL, zb[L8 - 1] ? 1 : 0, so.b ? 4 : 0, g->sdf_dW[L8],
+                                      g->sdf_db[L8], n->scale, sa_ws, (int64_t)sa_bytes, st)))
+            return rc;
+    }
+    cn_wgrad_desc sw[CN_SDF_MAX_LIN] = {};
+    for (int l = L8 - 1; l >= 0; --l) {
+        if (l > 0 && run) {
+            const Second so = second(l - 1);
+            LinCall k;
+            k.A = Z[l];
+            k.a_b = zb[l];
+            k.lda = HL;
+            k.B = n->Wt[l];
+            k.b_rows = n->wt_rows[l];
+            k.b_cols = n->wt_cols[l];
+            k.N = n->out_dim[l - 1];
+            k.K = rup_i(n->out_dim[l], 32);
+            k.epi = CN_EPI_BWD_SOFTPLUS;
+            k.aux0 = act(l);
+            k.aux0_b = k8.ub[l];
+            k.ld_aux0 = HL;
+            k.aux_beta = sig_beta(n, l - 1);
+            k.nzero = HL;
+            if (l == sk) k.adiv = kSqrt2;
+            k.aux1 = so.a1;
+            k.aux2 = so.a2;
+            k.ld_aux1 = HL;
+            k.ld_aux2 = HL;
+            k.aux2_scale = so.scale;
+            k.aux12_b = so.b;
+            k.beta = n->beta;
+            k.threshold = n->threshold;
+            k.M = M;
+            if (zb[l - 1]) {
+                k.out0_b = Z[l - 1];
+                k.ld_out0_b = HL;
+            } else {
+                k.out0 = static_cast<float*>(Z[l - 1]);
+                k.ld_out0 = HL;
+            }
+            if ((rc = run_linear(n->mfma_dtype, k, l, st))) return rc;
+        }
+        const bool xb = k8.ub[l] && udb[l];
+        const int64_t ldx = l == 0 ? KE : HL;
+        sw[L8 - 1 - l] = wgrad_job(2, Z[l], zb[l], HL, xb ? act(l) : act(l), xb, ldx, zb[l] ? k8.Sb[l] : s_fp32(l), HL,
+                                   xb ? Udb[l] : static_cast<const void*>(Ud[l]), ldx, M, n->out_dim[l], n->in_dim[l],
+                                   g->sdf_dW[l], n->in_dim[l], g->sdf_db[l], n->mfma_dtype);
+    }
+    if ((rc = wgrad_batch_run(sw, L8, ws, st, run))) return rc;
+    if (!pose) return CN_OK;
+    // --- dx (fields.sdf_input_grad with dh): the first-order adjoint chain P in fp32
+    float* Pp[2] = {static_cast<float*>(ws.take((size_t)M * HL * 4)), static_cast<float*>(ws.take((size_t)M * HL * 4))};
+    float* PE = sk >= 0 ? static_cast<float*>(ws.take((size_t)M * KE * 4)) : nullptr;
+    float* P0 = static_cast<float*>(ws.take((size_t)M * KE * 4));
+    float* dx = static_cast<float*>(ws.take((size_t)M * 16));
+    float* dpts = static_cast<float*>(ws.take((size_t)M * 16));
+    float* drd_p = static_cast<float*>(ws.take((size_t)R * 12));
+    if (!run) return CN_OK;
+    if ((rc = cn_softplus_adjoint(M, HL, dfeat, F, U8, HL, sig_beta(n, L8 - 1), dsdf, n->head_wp, nullptr, 0, nullptr, 0,
+                                  0.0f, Pp[0], HL, 0, 0, nullptr, nullptr, 1.0f, nullptr, 0, st)))
+        return rc;
+    MlpState ms;
+    ms.U0 = k8.U0;
+    for (int l = 0; l <= L8; ++l) {
+        ms.U[l] = k8.U[l];
+        ms.ub[l] = k8.ub[l];
+    }
+    int cur = 0;
+    for (int l = L8 - 1; l >= 1; --l) {
+        if ((rc = mlp_mul(n, s, ms, M, l, Pp[cur], false, Pp[cur ^ 1], false, PE, l == sk, false, st))) return rc;
+        cur ^= 1;
+    }
+    if ((rc = mlp_dx(n, s, ms, M, Pp[cur], P0, PE, dx, st))) return rc;
+    // --- _PointsFn.backward: the points' gradient = (their own consumers + the colour network's) + the SDF's
+    if (g->dpts) {
+        if ((rc = add2(M, 4, g->dpts, 4, dpts_col, 64, dpts, 4, st)) || (rc = add2(M, 4, dpts, 4, dx, 4, dpts, 4, st)))
+            return rc;
+    } else if ((rc = add2(M, 4, dpts_col, 64, dx, 4, dpts, 4, st))) {
+        return rc;
+    }
+    if ((rc = cn_points_bwd(R, S, d->z_in, 1, d->near, d->far, d->n_samples, dpts, 4, g->drays_o, drd_p, st))) return rc;
+    // rays_d: (the compositing's + the view directions') + the points'
+    if ((rc = add2(R, 3, drd_c, 3, ddirs, 3, g->drays_d, 3, st))) return rc;
+    return add2(R, 3, g->drays_d, 3, drd_p, 3, g->drays_d, 3, st);
+}
+
+int train_bwd_check(const cn_render_desc* d, const cn_render_grads* g, const NetShape& s) {
+    CN_REQUIRE(g, CN_ERR_ARG, "cn_render_bwd: null gradients");
+    CN_REQUIRE((g->drays_o == nullptr) == (g->drays_d == nullptr), CN_ERR_ARG,
+               "cn_render_bwd: drays_o and drays_d both or neither");
+    CN_REQUIRE(g->dinv_s, CN_ERR_ARG, "cn_render_bwd: dinv_s [R] required");
+    for (int l = 0; l <= s.L8; ++l)
+        CN_REQUIRE(g->sdf_dW[l] && g->sdf_db[l], CN_ERR_ARG, "cn_render_bwd: sdf_dW[%d] / sdf_db[%d] null", l, l);
+    const cn_color_net* c = d->color_net;
+    for (int l = 0; l < c->n_lin; ++l)
+        CN_REQUIRE(g->col_dW[l] && g->col_db[l], CN_ERR_ARG, "cn_render_bwd: col_dW[%d] / col_db[%d] null", l, l);
+    const int kq = s.bf ? 64 : 32;
+    for (int l = 1; l + 1 < c->n_lin; ++l)
+        CN_REQUIRE(c->Wt[l] && ((uintptr_t)c->Wt[l] & 15) == 0 && c->wt_rows[l] >= rup_i(c->in_dim[l], 128) &&
+                       c->wt_cols[l] >= rup_i(c->out_dim[l], kq),
+                   CN_ERR_SHAPE, "cn_render_bwd: colour transposed image %d missing or too small", l);
+    CN_REQUIRE(c->Wtf && c->Wg && c->Wxt && c->wg_ld >= c->out_dim[0] && c->wtf_rows >= rup_i(c->d_feature, 128) &&
+                   c->wxt_rows >= 64,
+               CN_ERR_SHAPE, "cn_render_bwd: colour lin0's transposed images missing or too small");
+    return CN_OK;
+}
+
+}  // namespace
+
+extern "C" size_t cn_render_state_bytes(const cn_render_desc* d) {
+    NetShape s;
+    ColorShape cs;
+    if (train_check(d, &s, &cs) != CN_OK) return 0;
+    Plan p(nullptr);
+    TrainState t;
+    train_fwd_plan(d, s, cs, p, &t, nullptr, false);
+    return p.used;
+}
+
+extern "C" size_t cn_render_bwd_workspace_bytes(const cn_render_desc* d, int32_t pose) {
+    NetShape s;
+    ColorShape cs;
+    if (train_check(d, &s, &cs) != CN_OK) return 0;
+    Plan p(nullptr);
+    TrainState t;
+    train_fwd_plan(d, s, cs, p, &t, nullptr, false);
+    cn_render_grads g{};
+    Plan ws(nullptr);
+    render_bwd_plan(d, &g, s, cs, t, pose != 0, ws, nullptr, false);
+    return ws.used;
+}
+
+extern "C" int cn_render_train_fwd(const cn_render_desc* d, void* state, int64_t state_bytes, cn_stream_t stream) {
+    NetShape s;
+    ColorShape cs;
+    int rc = train_check(d, &s, &cs);
+    if (rc) return rc;
+    if (d->R == 0) return CN_OK;
+    const size_t need = cn_render_state_bytes(d);
+    CN_REQUIRE(state && state_bytes >= 0 && (size_t)state_bytes >= need, CN_ERR_SHAPE,
+               "cn_render_train_fwd: state %lld bytes, %zu needed", (long long)state_bytes, need);
+    CN_REQUIRE(((uintptr_t)state & (kAlign - 1)) == 0, CN_ERR_ALIGN, "cn_render_train_fwd: state not 256-byte aligned");
+    Plan p(state);
+    TrainState t;
+    return train_fwd_plan(d, s, cs, p, &t, (hipStream_t)stream, true);
+}
+
+extern "C" int cn_render_bwd(const cn_render_desc* d, const cn_render_grads* g, const void* state, int64_t state_bytes,
+                             void* workspace, int64_t workspace_bytes, cn_stream_t stream) {
+    NetShape s;
+    ColorShape cs;
+    int rc = train_check(d, &s, &cs);
+    if (rc) return rc;
+    if ((rc = train_bwd_check(d, g, s))) return rc;
+    if (d->R == 0) return CN_OK;
+    const bool pose = g->drays_o != nullptr;
+    const size_t need_st = cn_render_state_bytes(d);
+    const size_t need = cn_render_bwd_workspace_bytes(d, pose ? 1 : 0);
+    CN_REQUIRE(state && state_bytes >= 0 && (size_t)state_bytes >= need_st, CN_ERR_SHAPE,
+               "cn_render_bwd: state %lld bytes, %zu needed", (long long)state_bytes, need_st);
+    CN_REQUIRE(workspace && workspace_bytes >= 0 && (size_t)workspace_bytes >= need, CN_ERR_SHAPE,
+               "cn_render_bwd: workspace %lld bytes, %zu needed", (long long)workspace_bytes, need);
+    CN_REQUIRE(((uintptr_t)state & (kAlign - 1)) == 0 && ((uintptr_t)workspace & (kAlign - 1)) == 0, CN_ERR_ALIGN,
+               "cn_render_bwd: state / workspace not 256-byte aligned");
+    Plan p(const_cast<void*>(state));
+    TrainState t;
+    train_fwd_plan(d, s, cs, p, &t, nullptr, false);  // the state's layout (pointers only)
+    Plan dry(nullptr);  // the plan with these gradients must fit what was sized (nothing launched yet)
+    render_bwd_plan(d, g, s, cs, t, pose, dry, nullptr, false);
+    CN_REQUIRE(dry.used <= need, CN_ERR_SHAPE, "cn_render_bwd: internal plan %zu bytes > sized %zu", dry.used, need);
+    Plan ws(workspace);
+    return render_bwd_plan(d, g, s, cs, t, pose, ws, (hipStream_t)stream, true);
 }

@@ -639,6 +639,19 @@ typedef struct cn_color_net {
     const float* bias[CN_SDF_MAX_LIN - 1];
     const float* head_w;
     const float* head_b;
+    /* ABI v14 (cn_render_bwd only): the transposed images of the backward (copenerf.fields.pack_color):
+       Wt[l] for the hidden layers l >= 1 (rows >= the input width rounded up to 128, columns the output
+       width rounded up to 32 / 64); lin0's feature columns transposed Wtf; its gradient columns
+       transposed Wg [4][wg_ld] fp32; its extras columns [g | pts | emb(dirs)] transposed Wxt (rows 64). */
+    const void* Wt[CN_SDF_MAX_LIN - 1];
+    int32_t wt_rows[CN_SDF_MAX_LIN - 1];
+    int32_t wt_cols[CN_SDF_MAX_LIN - 1];
+    const void* Wtf;
+    int32_t wtf_rows, wtf_cols;
+    const float* Wg;
+    int32_t wg_ld;
+    const void* Wxt;
+    int32_t wxt_rows, wxt_cols;
 } cn_color_net;
 
 /* z_in: [R][S] sample positions (the renderer's z_vals hook), or NULL: cn_sample's
@@ -671,6 +684,52 @@ typedef struct cn_render_desc {
 } cn_render_desc;
 size_t cn_render_fwd_workspace_bytes(const cn_render_desc* d);
 int cn_render_fwd(const cn_render_desc* d, void* workspace, int64_t workspace_bytes, cn_stream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * The rendering step under autograd (ABI v14): render_core of NeuSRenderer.forward
+ * (neus_renderer.py:307-450) at given samples, with everything its backward needs kept
+ * in the caller's `state` buffer, and the backward in one call.
+ * cn_render_train_fwd takes the descriptor of cn_render_fwd with z_in required (the
+ * samples: cn_sample's, drawn without gradient as in the reference) and writes pts, sdf,
+ * grad, color, depth, weights, cdf (rgb, z unused: the colour values stay in the state);
+ * z_in, rays, near / far, time_step, inv_s, cos_anneal_ratio, the networks and those
+ * outputs must stay unchanged until cn_render_bwd has run.
+ * cn_render_bwd takes the gradients of the outputs (NULL: none) and writes
+ *   the SDF network's effective-weight gradients sdf_dW[l] [out][in] / sdf_db[l]
+ *     (the last Linear's feature rows zero: the colour network's folded lin0 carries them),
+ *   the colour network's col_dW[l] / col_db[l] (lin0 over the folded input in the
+ *     reference column order [pts | emb(dirs) | gradient | feature]),
+ *   dinv_s [R] (per-ray parts of dL/d inv_s; the caller sums them),
+ *   drays_o / drays_d [R][3] (both or neither: the pose gradient through the points,
+ *     the view directions and the compositing's cosine).
+ * Gradients that reach one buffer from several consumers are summed in the order
+ * autograd sums them for copenerf's composition (the sdf / ∇ₓSDF / point outputs' own
+ * consumers first, then the compositing's, then the colour network's, then the SDF
+ * network's), so the results are bitwise those of the composition
+ * (copenerf.renderer with RENDER_NATIVE off).  state: cn_render_state_bytes; workspace:
+ * cn_render_bwd_workspace_bytes (pose or not); both 256-byte aligned.
+ * ------------------------------------------------------------------------ */
+typedef struct cn_render_grads {
+    const float* dcolor;                /* [R][3] */
+    const float* ddepth;                /* [R] */
+    const float* dweights;              /* [R][S] */
+    const float* dcdf;                  /* [R][S] */
+    const float* dsdf;                  /* [R S] */
+    const float* dgrad;                 /* [R S][4] */
+    const float* dpts;                  /* [R S][4] */
+    float* sdf_dW[CN_SDF_MAX_LIN];
+    float* sdf_db[CN_SDF_MAX_LIN];
+    float* col_dW[CN_SDF_MAX_LIN];
+    float* col_db[CN_SDF_MAX_LIN];
+    float* dinv_s;
+    float* drays_o;
+    float* drays_d;
+} cn_render_grads;
+size_t cn_render_state_bytes(const cn_render_desc* d);
+size_t cn_render_bwd_workspace_bytes(const cn_render_desc* d, int32_t pose);
+int cn_render_train_fwd(const cn_render_desc* d, void* state, int64_t state_bytes, cn_stream_t stream);
+int cn_render_bwd(const cn_render_desc* d, const cn_render_grads* g, const void* state, int64_t state_bytes,
+                  void* workspace, int64_t workspace_bytes, cn_stream_t stream);
 
 /* ------------------------------------------------------------------------ *
  * The SDF query under autograd (ABI v14): SDFNetwork.sdf(x) with gradients to the

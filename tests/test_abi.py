@@ -37,7 +37,8 @@ def test_struct_layouts_match_header_order():
     for cname, py in (("cn_linear_desc", _lib.LinearDesc), ("cn_wgrad_desc", _lib.WgradDesc),
                       ("cn_sdf_mlp_desc", _lib.SdfMlpDesc), ("cn_sdf_net", _lib.SdfNet),
                       ("cn_sample_desc", _lib.SampleDesc), ("cn_color_net", _lib.ColorNet),
-                      ("cn_render_desc", _lib.RenderDesc), ("cn_mlp_desc", _lib.MlpDesc)):
+                      ("cn_render_desc", _lib.RenderDesc), ("cn_mlp_desc", _lib.MlpDesc),
+                      ("cn_render_grads", _lib.RenderGrads)):
         body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (cname, cname), src, re.S).group(1)
         body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
         names = []
