@@ -1,12 +1,14 @@
-// cn_pipeline.hip — composed entry points (ABI v12): the sampler's SDF query and the whole
-// sampler of NeuSRenderer.render as single C calls over the kernels of this library.
+// cn_pipeline.hip — composed entry points (ABI v12 - v14): the sampler's SDF query and the whole sampler
+// of NeuSRenderer.render (v12), the no-gradient rendering forward (v13), the SDF query under autograd and the
+// training render with its backward (v14), each as single C calls over the kernels of this library.
 //
-// Reference: neus_renderer.py:466-525 (coarse z, up_sample rounds, cat_z_vals with the new
-// samples' SDF) and neus_fields.py:268-283 / 286-287 (SDFNetwork.forward / .sdf).  The
-// composition follows copenerf.fields.sdf_forward (want_feat=False, no gradient) and
-// copenerf.renderer.sample_z launch for launch, so the results are the same bits; host code
-// only plans buffers in the caller's workspace and fills descriptors -- nothing synchronises,
-// allocates or touches the default stream, so a caller may capture cn_sample in a hipGraph.
+// Reference: neus_renderer.py:466-525 (coarse z, up_sample rounds, cat_z_vals with the new samples' SDF),
+// 307-450 (render_core) and neus_fields.py:268-303 (SDFNetwork.forward / .sdf / .gradient), 352-373
+// (RenderingNetwork), train.py:502-505 (the stage-1 re-query).  Each composition follows copenerf's Python
+// composition (fields.sdf_forward / sdf_backward / sdf_input_grad, renderer.sample_z, the autograd Functions
+// of renderer.py and fields.py) launch for launch, so the results are the same bits; host code only plans
+// buffers in the caller's workspace and fills descriptors -- nothing synchronises, allocates or touches the
+// default stream, so a caller may capture any of these calls in a hipGraph.
 #include <algorithm>
 #include <cmath>
 
