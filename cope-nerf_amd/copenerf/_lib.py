@@ -119,7 +119,7 @@ class SampleDesc(ctypes.Structure):
     _fields_ = [
         ("R", c_i32), ("n_samples", c_i32), ("n_importance", c_i32), ("up_sample_steps", c_i32),
         ("rays_o", c_ptr), ("rays_d", c_ptr), ("near", c_ptr), ("far", c_ptr), ("t_rand", c_ptr),
-        ("time_step", c_ptr), ("net", ctypes.POINTER(SdfNet)), ("z", c_ptr),
+        ("time_step", c_ptr), ("net", ctypes.POINTER(SdfNet)), ("z", c_ptr), ("philox", c_ptr),
     ]
 
 
@@ -129,7 +129,7 @@ class RenderDesc(ctypes.Structure):
         ("rays_o", c_ptr), ("rays_d", c_ptr), ("near", c_ptr), ("far", c_ptr), ("t_rand", c_ptr), ("time_step", c_ptr),
         ("z_in", c_ptr), ("inv_s", c_ptr), ("cos_anneal_ratio", c_ptr), ("sdf_net", ctypes.POINTER(SdfNet)),
         ("color_net", ctypes.POINTER(ColorNet)), ("z", c_ptr), ("pts", c_ptr), ("sdf", c_ptr), ("grad", c_ptr),
-        ("rgb", c_ptr), ("color", c_ptr), ("depth", c_ptr), ("weights", c_ptr), ("cdf", c_ptr),
+        ("rgb", c_ptr), ("color", c_ptr), ("depth", c_ptr), ("weights", c_ptr), ("cdf", c_ptr), ("philox", c_ptr),
     ]
 
 
@@ -186,6 +186,7 @@ SIGNATURES = {
     "cn_euler_chain": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr]),
     "cn_euler_chain_bwd": (c_i32, [c_i32, c_i32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr]),
     "cn_coarse_z": (c_i32, [c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr]),
+    "cn_uniform_philox": (c_i32, [c_i64, c_ptr, c_ptr, c_ptr]),
     "cn_points": (c_i32, [c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_i32, c_ptr, c_ptr, c_i32, c_ptr, c_ptr]),
     "cn_up_sample_merge": (c_i32, [c_i32, c_i32, c_i32, c_f32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
                                    c_ptr]),

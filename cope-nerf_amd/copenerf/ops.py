@@ -661,7 +661,7 @@ def color_net(lay, pk):
 
 
 def render_fwd(sdf_net_, color_net_, rays_o, rays_d, near, far, time_step, inv_s, car, n_samples, n_importance,
-               up_sample_steps, t_rand=None, z_in=None):
+               up_sample_steps, t_rand=None, z_in=None, philox=None):
     """NeuSRenderer.forward without gradient in one call (cn_render_fwd): returns z, pts, sdf, grad, rgb, color,
     depth, weights, cdf."""
     R, dev = rays_o.shape[0], rays_o.device
@@ -681,6 +681,8 @@ def render_fwd(sdf_net_, color_net_, rays_o, rays_d, near, far, time_step, inv_s
     d.t_rand, d.time_step, d.z_in = _ptr(t_rand), _ptr(time_step), _ptr(z_in)
     d.inv_s, d.cos_anneal_ratio = _ptr(inv_s), _ptr(car)
     d.sdf_net, d.color_net = ctypes.pointer(sdf_net_), ctypes.pointer(color_net_)
+    _check_philox(philox)
+    d.philox = _ptr(philox)
     for k, v in out.items():
         setattr(d, k, v.data_ptr())
     lib = _lib.load()
@@ -788,9 +790,12 @@ def mlp_bwd(net, M, state, dsdf, dWs=None, dbs=None, dx=None):
                "cn_mlp_bwd")
 
 
-def sample(net, rays_o, rays_d, near, far, t_rand, time_step, n_samples, n_importance, up_sample_steps, z):
+def sample(net, rays_o, rays_d, near, far, t_rand, time_step, n_samples, n_importance, up_sample_steps, z,
+           philox=None):
     """z [R, n_samples + up_sample_steps * (n_importance // up_sample_steps)] -- cn_sample: coarse z and the
-    up-sampling rounds with their SDF queries in one call (net: sdf_net's descriptor)."""
+    up-sampling rounds with their SDF queries in one call (net: sdf_net's descriptor).  philox (with t_rand
+    None): a device uint64 [2] (seed, offset) -- the jitter drawn on the device (cn_uniform_philox)."""
+    _check_philox(philox)
     for t, nm in ((rays_o, "rays_o"), (rays_d, "rays_d"), (near, "near"), (far, "far"), (t_rand, "t_rand"),
                   (time_step, "time_step"), (z, "z")):
         if t is not None and (t.dtype != torch.float32 or not t.is_contiguous()):
@@ -803,7 +808,7 @@ def sample(net, rays_o, rays_d, near, far, t_rand, time_step, n_samples, n_impor
     d.R, d.n_samples, d.n_importance, d.up_sample_steps = R, n_samples, n_importance, up_sample_steps
     d.rays_o, d.rays_d, d.near, d.far = _ptr(rays_o), _ptr(rays_d), _ptr(near), _ptr(far)
     d.t_rand, d.time_step, d.z = _ptr(t_rand), _ptr(time_step), _ptr(z)
-    d.net = ctypes.pointer(net)
+    d.net, d.philox = ctypes.pointer(net), _ptr(philox)
     lib = _lib.load()
     ws = torch.empty(max(int(lib.cn_sample_workspace_bytes(ctypes.byref(d))), 1), dtype=torch.uint8, device=z.device)
     _lib.check(lib.cn_sample(ctypes.byref(d), _ptr(ws), ws.numel(), _stream()), "cn_sample")
@@ -851,6 +856,20 @@ def patch_indices(h, w, ps, n_patches, key, out=None):
     if out is None:
         out = torch.empty(n_patches * ps * ps, dtype=torch.int64, device=key.device)
     _lib.call("cn_patch_indices", h, w, ps, n_patches, _ptr(key), _ptr(out), _stream())
+    return out
+
+
+def _check_philox(so):
+    if so is not None and (so.dtype != torch.uint64 or so.numel() < 2 or not so.is_contiguous() or not so.is_cuda):
+        raise RuntimeError("philox: a contiguous device uint64 tensor [2] = (seed, offset)")
+
+
+def uniform_philox(n, seed_offset, out=None):
+    """out[i] in [0, 1) from Philox4x32-10 (counter (i // 4, offset), key seed) -- cn_uniform_philox; seed_offset
+    is a device uint64 [2] read by the kernel (a replayed graph draws with its current value)."""
+    _check_philox(seed_offset)
+    out = torch.empty(n, device=seed_offset.device) if out is None else out
+    _lib.call("cn_uniform_philox", n, _ptr(seed_offset), _ptr(out), _stream())
     return out
 
 

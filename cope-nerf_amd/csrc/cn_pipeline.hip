@@ -227,13 +227,17 @@ int query_check(const cn_sdf_net* n, int32_t M, const float* x, int64_t ldx, flo
 // query, the new samples and their scatter targets, then the query's own workspace (reused by
 // every round: the stream orders them).
 struct SamplePlan {
+    float* jitter;  // the device-drawn t_rand (philox), or null
     float *z[2], *sdf[2], *pts, *z_new;
     int32_t* dst;
     int k, width, qmax;
 };
 
+bool sample_draws(const cn_sample_desc* d) { return !d->t_rand && d->philox; }
+
 int sample_plan(const cn_sample_desc* d, const NetShape& s, Plan& ws, SamplePlan* p) {
     const int R = d->R, ns = d->n_samples;
+    p->jitter = sample_draws(d) ? static_cast<float*>(ws.take((size_t)R * ns * 4)) : nullptr;
     p->k = d->n_importance > 0 ? d->n_importance / d->up_sample_steps : 0;
     p->width = ns + d->up_sample_steps * p->k;
     p->qmax = ns > p->k ? ns : p->k;
@@ -290,7 +294,7 @@ extern "C" int cn_sdf_query(const cn_sdf_net* net, int32_t M, const float* x, in
 
 extern "C" size_t cn_sample_workspace_bytes(const cn_sample_desc* d) {
     if (sample_check(d) != CN_OK) return 0;
-    if (d->n_importance == 0) return 0;
+    if (d->n_importance == 0) return sample_draws(d) ? rup_sz((size_t)d->R * d->n_samples * 4, kAlign) : 0;
     NetShape s;
     if (net_shape(d->net, &s) != CN_OK) return 0;
     Plan ws(nullptr);
@@ -304,7 +308,16 @@ extern "C" int cn_sample(const cn_sample_desc* d, void* workspace, int64_t works
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
     const int R = d->R, ns = d->n_samples;
-    if (d->n_importance == 0) return cn_coarse_z(R, ns, d->near, d->far, d->t_rand, d->z, stream);
+    if (d->n_importance == 0) {
+        const float* t_rand = d->t_rand;
+        if (sample_draws(d) && R > 0) {  // the jitter drawn on the device into the workspace
+            CN_REQUIRE(workspace && workspace_bytes >= (int64_t)R * ns * 4 && ((uintptr_t)workspace & (kAlign - 1)) == 0,
+                       CN_ERR_SHAPE, "cn_sample: workspace for the drawn jitter");
+            if ((rc = cn_uniform_philox((int64_t)R * ns, d->philox, static_cast<float*>(workspace), stream))) return rc;
+            t_rand = static_cast<const float*>(workspace);
+        }
+        return cn_coarse_z(R, ns, d->near, d->far, t_rand, d->z, stream);
+    }
     NetShape s;
     if ((rc = net_shape(d->net, &s))) return rc;
     if (R == 0) return CN_OK;
@@ -320,7 +333,12 @@ extern "C" int cn_sample(const cn_sample_desc* d, void* workspace, int64_t works
     // coarse samples and their SDF (neus_renderer.py:466-498)
     float* z = p.z[0];
     float* sdf = p.sdf[0];
-    if ((rc = cn_coarse_z(R, ns, d->near, d->far, d->t_rand, z, stream))) return rc;
+    const float* t_rand = d->t_rand;
+    if (p.jitter) {
+        if ((rc = cn_uniform_philox((int64_t)R * ns, d->philox, p.jitter, stream))) return rc;
+        t_rand = p.jitter;
+    }
+    if ((rc = cn_coarse_z(R, ns, d->near, d->far, t_rand, z, stream))) return rc;
     if ((rc = cn_points(R, ns, d->rays_o, d->rays_d, z, d->time_step, 0, nullptr, nullptr, 0, p.pts, stream)))
         return rc;
     if ((rc = cn_sdf_query(d->net, R * ns, p.pts, 4, sdf, nullptr, qws, qbytes, stream))) return rc;
@@ -829,6 +847,7 @@ cn_sample_desc render_sample_desc(const cn_render_desc* d) {
     sd.near = d->near;
     sd.far = d->far;
     sd.t_rand = d->t_rand;
+    sd.philox = d->philox;
     sd.time_step = d->time_step;
     sd.net = d->sdf_net;
     sd.z = d->z;

@@ -75,6 +75,37 @@ __global__ void coarse_z_kernel(int R, int n, const float* __restrict__ near, co
     z[idx] = lower + (upper - lower) * t_rand[idx];
 }
 
+// Philox4x32-10 (Salmon et al., "Parallel random numbers: as easy as 1, 2, 3", SC'11; the Random123
+// constants): ten rounds of two 32x32 -> 64-bit multiplies, the key bumped by the Weyl constants between rounds.
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+    for (int r = 0; r < 10; ++r) {
+        if (r) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+        c[0] = n0;
+        c[1] = (uint32_t)p1;
+        c[2] = n2;
+        c[3] = (uint32_t)p0;
+    }
+}
+
+// out[i] = the 24 high bits of word i % 4 of Philox4x32-10(counter (i / 4, offset), key seed) x 2^-24, in [0, 1);
+// seed and offset are read on the device (so = [seed, offset]: a captured launch replays with the current values)
+__global__ void __launch_bounds__(256) uniform_philox_kernel(int64_t n, const uint64_t* __restrict__ so,
+                                                             float* __restrict__ out) {
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g * 4 >= n) return;
+    const uint64_t seed = so[0], off = so[1];
+    uint32_t c[4] = {(uint32_t)g, (uint32_t)((uint64_t)g >> 32), (uint32_t)off, (uint32_t)(off >> 32)};
+    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    for (int k = 0; k < 4 && g * 4 + k < n; ++k) out[g * 4 + k] = (float)(c[k] >> 8) * (1.0f / 16777216.0f);
+}
+
 __global__ void points_kernel(int R, int n, const float* __restrict__ o, const float* __restrict__ d,
                               const float* __restrict__ z, const float* __restrict__ tptr, int mid,
                               const float* __restrict__ near, const float* __restrict__ far, int n_coarse,
@@ -690,6 +721,15 @@ extern "C" int cn_patch_indices(int32_t h, int32_t w, int32_t ps, int32_t n_patc
     while ((1LL << (2 * hb)) < n) ++hb;
     patch_indices_kernel<<<(n_patches + 255) / 256, 256, 0, (hipStream_t)stream>>>(h, w, ps, n_patches, hb, key, idx);
     return check_launch("cn_patch_indices");
+}
+
+extern "C" int cn_uniform_philox(int64_t n, const uint64_t* seed_offset, float* out, cn_stream_t stream) {
+    CN_REQUIRE(n >= 0 && (n == 0 || (seed_offset && out)), CN_ERR_ARG, "cn_uniform_philox: null pointer / n < 0");
+    if (n == 0) return CN_OK;
+    const int64_t groups = (n + 3) / 4;
+    CN_REQUIRE(groups < ((int64_t)1 << 40), CN_ERR_SHAPE, "cn_uniform_philox: n too large");
+    uniform_philox_kernel<<<(unsigned)((groups + 255) / 256), 256, 0, (hipStream_t)stream>>>(n, seed_offset, out);
+    return check_launch("cn_uniform_philox");
 }
 
 extern "C" int cn_coarse_z(int32_t R, int32_t n, const float* near, const float* far, const float* t_rand, float* z,

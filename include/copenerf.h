@@ -379,6 +379,12 @@ int cn_euler_chain_bwd(int32_t K, int32_t n, const float* omega, int64_t ld_o, c
 /* ------------------------------------------------------------------------ *
  * Sampling along rays (neus_renderer.py:453-525).
  * ------------------------------------------------------------------------ */
+/* Uniform jitter from a counter-based generator (ABI v14; the §8(b) device Philox seed): out[i] =
+ * (word i % 4 of Philox4x32-10(counter = (i / 4 as 64 bits, offset), key = seed)) >> 8, x 2^-24, in [0, 1).
+ * seed_offset: DEVICE uint64 [2] = (seed, offset), read by the kernel, so a captured launch replays with
+ * the current values (the caller advances offset by ceil(n / 4) per draw to keep streams disjoint). */
+int cn_uniform_philox(int64_t n, const uint64_t* seed_offset, float* out, cn_stream_t stream);
+
 /* z[r][i] = near*(1-lin_i) + far*lin_i, lin = linspace(0,1,n); stratified
  * jitter with t_rand [R][n] when t_rand != NULL (neus_renderer.py:466-483). */
 int cn_coarse_z(int32_t R, int32_t n, const float* near, const float* far, const float* t_rand,
@@ -608,6 +614,9 @@ typedef struct cn_sample_desc {
     const float* time_step;
     const cn_sdf_net* net;
     float* z;
+    /* ABI v14: with t_rand NULL and philox != NULL (DEVICE uint64 [2] = (seed, offset)), the jitter is
+       drawn on the device: t_rand = cn_uniform_philox(R n_samples, philox) in the workspace */
+    const uint64_t* philox;
 } cn_sample_desc;
 size_t cn_sample_workspace_bytes(const cn_sample_desc* d);
 int cn_sample(const cn_sample_desc* d, void* workspace, int64_t workspace_bytes, cn_stream_t stream);
@@ -681,6 +690,7 @@ typedef struct cn_render_desc {
     float* depth;
     float* weights;
     float* cdf;
+    const uint64_t* philox;             /* ABI v14: as cn_sample_desc.philox (the sampler's jitter) */
 } cn_render_desc;
 size_t cn_render_fwd_workspace_bytes(const cn_render_desc* d);
 int cn_render_fwd(const cn_render_desc* d, void* workspace, int64_t workspace_bytes, cn_stream_t stream);

@@ -206,6 +206,20 @@ def test_render_fwd_checks_without_gpu():
     assert lib.cn_render_fwd(ctypes.byref(d), 4096 * 256, ws, None) == -5
 
 
+def test_uniform_philox_checks_without_gpu():
+    """ABI v14: cn_uniform_philox refuses null pointers; n = 0 draws nothing."""
+    from copenerf import _lib
+    lib = _lib.load()
+    assert lib.cn_uniform_philox(10, None, 4096, None) == -1
+    assert lib.cn_uniform_philox(0, None, None, None) == 0
+    d = _lib.SampleDesc()
+    d.R, d.n_samples, d.n_importance, d.up_sample_steps = 4096, 64, 0, 4
+    d.near = d.far = d.z = 4096
+    assert lib.cn_sample_workspace_bytes(ctypes.byref(d)) == 0  # no draws: no workspace
+    d.philox = 4096
+    assert lib.cn_sample_workspace_bytes(ctypes.byref(d)) == 4096 * 64 * 4  # the drawn jitter
+
+
 def test_mlp_entry_points_check_and_plan_without_gpu():
     """ABI v14: cn_mlp_fwd / cn_mlp_bwd size the kept state and the backward's workspace on the host and
     refuse incomplete descriptors before anything launches."""
