@@ -101,7 +101,7 @@ class _RenderTrainFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, rays_o, rays_d, inv_s, z, time_step, near, far, car, n_coarse, sdf_lay, sdf_pk, col_lay, col_pk,
-                n_sdf, *params):
+                *params):
         ctx.set_materialize_grads(False)
         sn, k1 = ops.sdf_net(sdf_lay, sdf_pk)
         cn, k2 = ops.color_net(col_lay, col_pk)
@@ -110,7 +110,7 @@ class _RenderTrainFn(torch.autograd.Function):
         # the descriptor points into the inputs, the networks' images and the sdf / ∇ₓSDF outputs: hold them
         ctx.native = (sn, cn, k1, k2, state, d, (rays_o, rays_d, inv_s, z, time_step, near, far, car))
         ctx.save_for_backward(out["sdf"], out["grad"])
-        ctx.lays, ctx.n_sdf, ctx.inv_shape = (sdf_lay, col_lay), n_sdf, inv_s.shape
+        ctx.lays, ctx.inv_shape = (sdf_lay, col_lay), inv_s.shape
         ctx.pose = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         if not ctx.pose:
             ctx.mark_non_differentiable(out["pts"])
@@ -143,7 +143,7 @@ class _RenderTrainFn(torch.autograd.Function):
         for w, b in zip(col_dWs, col_dbs):
             grads += [w, b]
         return (do if ctx.needs_input_grad[0] else None, dd if ctx.needs_input_grad[1] else None, dinv_s) + \
-            (None,) * 11 + tuple(grads)
+            (None,) * 10 + tuple(grads)
 
 
 class NeuSRenderer(nn.Module):
@@ -345,7 +345,7 @@ class NeuSRenderer(nn.Module):
             params += [w, b]
         sdf, G, pts_time, color, depth, weights, cdf = _RenderTrainFn.apply(
             rays_o, rays_d, inv_s, z, time_step, near, far, car, n_samples, self.sdf_network.layout(), sdf_packed[2],
-            self.color_network.layout(), col_packed[2], len(sdf_packed[0]), *params)
+            self.color_network.layout(), col_packed[2], *params)
         weighted_z_vals = depth.detach().clone()
         depth_pred = depth / ray_d_norm if eval else depth
         normals = G[:, :3].reshape(R, S, 3)
