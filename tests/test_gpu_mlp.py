@@ -56,7 +56,7 @@ def test_mlp_equals_composition(mode, dh, monkeypatch):
     monkeypatch.setattr(ops, "mlp_bwd", lambda *a, **k: calls.append("b") or bwd(*a, **k))
     sdfn = build_modules(21, dh_sdf=dh, device=DEV)[0]
     sdfn.mfma_dtype = mode
-    for M in (3000, 70001):
+    for M in (1, 7, 3000, 70001):
         x, g = _inputs(M, M)
         for want_x, want_params in ((True, True), (False, True), (True, False)):
             calls.clear()

@@ -70,6 +70,18 @@ def test_render_train_equals_composition(mode, pose):
         assert torch.equal(g_n[k], v), (k, (g_n[k] - v).abs().max().item())
 
 
+@pytest.mark.parametrize("R", [1, 3, 65])
+def test_render_train_ragged_batches(R):
+    """Ragged and tiny ray batches (one ray, a partial wave, a partial tile) with the pose gradient, bf16."""
+    out_c, g_c, _ = _run(False, "bf16", True, seed=8, R=R)
+    out_n, g_n, n_n = _run(True, "bf16", True, seed=8, R=R)
+    assert n_n == 1
+    for k in KEYS:
+        assert torch.equal(out_n[k], out_c[k]), k
+    for k, v in g_c.items():
+        assert torch.equal(g_n[k], v), (k, (g_n[k] - v).abs().max().item())
+
+
 @pytest.mark.parametrize("cfg", ["c2", "c3"])
 def test_training_steps_equal_composition(cfg):
     """Two training steps of SyntheticTrainer (C2: fixed poses, fp32-class; C3: stage 1 with the motion network,
