@@ -79,3 +79,33 @@ def test_sample_draws_its_jitter_on_the_device():
             torch.cuda.synchronize()
             assert torch.equal(z1, z2), n_imp
     del keep
+
+
+def test_render_fwd_draws_its_jitter_on_the_device():
+    """cn_render_fwd with the philox seed (no t_rand) = cn_render_fwd given that jitter, every output bitwise."""
+    from copenerf import NeuSRenderer, ops
+    sdf, col, dev = build_modules(6, device=DEV)
+    r = NeuSRenderer(None, sdf, dev, col, None, **REN_CFG).to(DEV).set_mfma_dtype("bf16")
+    R = 513
+    gen = torch.Generator(device=DEV).manual_seed(2)
+    rays_o = (torch.rand(R, 3, device=DEV, generator=gen) - 0.5) * 0.3
+    rays_d = torch.nn.functional.normalize(torch.randn(R, 3, device=DEV, generator=gen), dim=-1)
+    near, far = torch.full((R, 1), 0.1, device=DEV), torch.full((R, 1), 1.9, device=DEV)
+    t = torch.full((1,), 0.2, device=DEV)
+    so = _so(77, 1 << 20)
+    with torch.no_grad():
+        sp = r.sdf_network.params_and_pack()
+        cp = r.color_network.params_and_pack(fold_feature=(sp[0][-1], sp[1][-1]))
+        sn, k1 = ops.sdf_net(r.sdf_network.layout(), sp[2])
+        cn, k2 = ops.color_net(r.color_network.layout(), cp[2])
+        inv_s = torch.full((1, 1), 20.0, device=DEV)
+        car = ops.device_scalar(0.5, DEV)
+        a = ops.render_fwd(sn, cn, rays_o, rays_d, near, far, t, inv_s, car, r.n_samples, r.n_importance,
+                           r.up_sample_steps, philox=so)
+        t_rand = ops.uniform_philox(R * r.n_samples, so).view(R, r.n_samples)
+        b = ops.render_fwd(sn, cn, rays_o, rays_d, near, far, t, inv_s, car, r.n_samples, r.n_importance,
+                           r.up_sample_steps, t_rand=t_rand)
+        torch.cuda.synchronize()
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+    del k1, k2
