@@ -35,14 +35,20 @@ The JSON line also carries
 from __future__ import annotations
 
 import argparse
+import datetime
 import glob
 import json
 import os
 import sys
 import time
+import warnings
 
 import torch
 import torch.distributed as dist
+
+# no autograd graph may outlive a step (GraphedTrainer keeps none): an eager step after a captured one
+# that warns about the AccumulateGrad node's stream would run under extra stream synchronisation
+warnings.filterwarnings("error", message="The AccumulateGrad node's stream")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(ROOT, "cope-nerf_amd"), ROOT]
@@ -264,7 +270,26 @@ def launch_ranks(n, argv):
                 for q in live:
                     q.terminate()
         time.sleep(0.05)
+    if status != 0:  # every rank's exit status (a rank stopped by the parent shows its signal)
+        print(f"bench.py: rank exit statuses {[p.returncode for p in procs]}", file=sys.stderr, flush=True)
     return status
+
+
+def init_group(backend, rank, world, timeout_s, **kw):
+    """init_process_group with a timeout on the rendezvous and on every collective (RCCL's watchdog
+    tears the process down when one hangs), so a rank that never joins or a stuck all-reduce ends
+    the run with a message and a non-zero status instead of at the driver's limit."""
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+    if backend == "nccl":
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "3")  # a timed-out collective ends the process
+    try:
+        dist.init_process_group(backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    except Exception as e:  # (the store raises its own timeout / connection types)
+        print(f"bench.py rank {rank}: the {world}-rank process group did not form within {timeout_s:.0f} s: "
+              f"{type(e).__name__}: {e}", file=sys.stderr, flush=True)
+        sys.exit(3)
 
 
 def dry_step(rank, world, grad_numel=800_000):
@@ -295,6 +320,10 @@ def main():
                     help="process-group backend (nccl = RCCL over xGMI; gloo only with --dry)")
     ap.add_argument("--dry", action="store_true",
                     help="launcher check on the CPU: ranks, process group, barriers and timing without HIP work")
+    ap.add_argument("--pg-timeout", type=float, default=120.0,
+                    help="seconds a rank waits for the process group to form or for a collective before it exits "
+                         "non-zero (well inside the driver's limit)")
+    ap.add_argument("--dry-absent-rank", type=int, default=-1, help=argparse.SUPPRESS)  # test hook (--dry only)
     args = ap.parse_args()
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and (args.gpus or 1) > 1:
@@ -317,9 +346,7 @@ def main():
         return dry_main(args, world, rank, distributed)
     torch.cuda.set_device(local)
     if distributed:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29533")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank, world_size=world)
+        init_group("nccl", rank, world, args.pg_timeout, device_id=torch.device("cuda", local))
         joined = torch.ones(1, device=f"cuda:{local}")
         dist.all_reduce(joined)
         if int(joined.item()) != world:
@@ -414,9 +441,10 @@ def main():
 def dry_main(args, world, rank, distributed):
     """The --dry line: same launch, barriers and max-over-ranks timing as the HIP bench, CPU work."""
     if distributed:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29533")
-        dist.init_process_group(args.backend, rank=rank, world_size=world)
+        if rank == args.dry_absent_rank:  # (test hook) this rank never joins: the others must time out
+            time.sleep(10 * args.pg_timeout)
+            sys.exit(1)
+        init_group(args.backend, rank, world, args.pg_timeout)
         joined = torch.ones(1)
         dist.all_reduce(joined)
         if int(joined.item()) != world:

@@ -660,13 +660,34 @@ def color_net(lay, pk):
     return n, keep
 
 
+def _check_render_inputs(fn, R, rays_o, rays_d, near, far, time_step, inv_s, car, t_rand=None, n_samples=None,
+                         z=None):
+    """The shapes and types the C side assumes (it takes R from rays_o and S from z): anything else would be
+    read out of bounds on the device, so it is refused here with a RuntimeError, as ops.sample does."""
+    for t, nm in ((rays_o, "rays_o"), (rays_d, "rays_d"), (near, "near"), (far, "far"), (time_step, "time_step"),
+                  (inv_s, "inv_s"), (car, "cos_anneal_ratio"), (t_rand, "t_rand"), (z, "z")):
+        if t is not None and (t.dtype != torch.float32 or not t.is_contiguous() or not t.is_cuda):
+            raise RuntimeError(f"{fn}: {nm} must be a contiguous fp32 device tensor")
+    if rays_o.shape != (R, 3) or rays_d.shape != (R, 3):
+        raise RuntimeError(f"{fn}: rays_o and rays_d must be [R, 3] (got {tuple(rays_o.shape)}, {tuple(rays_d.shape)})")
+    if near.numel() != R or far.numel() != R:
+        raise RuntimeError(f"{fn}: near and far must hold R = {R} entries (got {near.numel()}, {far.numel()})")
+    if time_step.numel() < 1 or inv_s.numel() < 1 or car.numel() < 1:
+        raise RuntimeError(f"{fn}: time_step, inv_s and cos_anneal_ratio need one element each")
+    if t_rand is not None and t_rand.shape != (R, n_samples):
+        raise RuntimeError(f"{fn}: t_rand must be [R, n_samples] = [{R}, {n_samples}] (got {tuple(t_rand.shape)})")
+    if z is not None and (z.dim() != 2 or z.shape[0] != R):
+        raise RuntimeError(f"{fn}: z must be [R, S] with R = {R} rows (got {tuple(z.shape)})")
+
+
 def render_fwd(sdf_net_, color_net_, rays_o, rays_d, near, far, time_step, inv_s, car, n_samples, n_importance,
                up_sample_steps, t_rand=None, z_in=None, philox=None):
     """NeuSRenderer.forward without gradient in one call (cn_render_fwd): returns z, pts, sdf, grad, rgb, color,
     depth, weights, cdf."""
     R, dev = rays_o.shape[0], rays_o.device
+    _check_render_inputs("render_fwd", R, rays_o, rays_d, near, far, time_step, inv_s, car, t_rand=t_rand,
+                         n_samples=n_samples, z=z_in)
     if z_in is not None:
-        z_in = z_in.contiguous().float()
         S = z_in.shape[1]
     else:
         k = n_importance // up_sample_steps if n_importance > 0 else 0
@@ -697,6 +718,7 @@ def render_train_fwd(sdf_net_, color_net_, rays_o, rays_d, near, far, time_step,
     descriptor render_bwd takes (the inputs must stay alive and unchanged until then)."""
     R, S = z.shape
     M, dev = R * S, z.device
+    _check_render_inputs("render_train_fwd", rays_o.shape[0], rays_o, rays_d, near, far, time_step, inv_s, car, z=z)
     f = lambda *s: torch.empty(*s, device=dev)  # noqa: E731
     out = dict(pts=f(M, 4), sdf=f(M, 1), grad=f(M, 4), color=f(R, 3), depth=f(R, 1), weights=f(R, S), cdf=f(R, S))
     d = _lib.RenderDesc()

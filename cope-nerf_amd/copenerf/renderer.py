@@ -270,6 +270,10 @@ class NeuSRenderer(nn.Module):
             t_rand = torch.rand([R, n_samples], device=dev)
         if eval:
             t_rand = None
+        if t_rand is not None:
+            t_rand = t_rand.contiguous().float()
+        if z_vals is not None:
+            z_vals = z_vals.contiguous().float()
 
         sdf_packed = self.sdf_network.params_and_pack()
         fold = self._can_fold()
@@ -285,7 +289,7 @@ class NeuSRenderer(nn.Module):
         if z_vals is None:
             z = self.sample_z(rays_o, rays_d, time_step, near, far, n_samples, n_importance, t_rand, sdf_packed)
         else:
-            z = z_vals.contiguous().float()
+            z = z_vals
         S = z.shape[1]
 
         # render_core (neus_renderer.py:307-450)

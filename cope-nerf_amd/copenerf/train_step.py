@@ -68,13 +68,28 @@ PAIR_WEIGHTS = ("sdf_weight", "flow_rgb_weight", "sdf_consistency_weight", "edge
                 "smoothness_weight")
 
 
-def prefer_small_gemm_blas():
-    """torch's fp32 GEMMs of the step (the MotionNetwork's layers and their gradients, ray and pose
-    matrices: tens to a few hundred rows) through rocBLAS instead of hipBLASLt: hipBLASLt's tiles for these
-    shapes run ~30 us each, rocBLAS's in a few.  C3 +1.9 % (profiles/r5_ab.txt r5q); both fp32.  A process-wide
-    torch setting: the training entry points (SyntheticTrainer, Trainer) make it."""
-    if torch.cuda.is_available():
-        torch.backends.cuda.preferred_blas_library("cublas")  # (rocBLAS on ROCm)
+class small_gemm_blas:
+    """torch's fp32 GEMMs of a step (the MotionNetwork's layers and their gradients, ray and pose matrices: tens
+    to a few hundred rows) through rocBLAS instead of hipBLASLt for the duration of a `with` block, the caller's
+    preferred library restored on exit: hipBLASLt's tiles for these shapes run ~30 us each, rocBLAS's in a few
+    (C3 +1.9 %, profiles/r5_ab.txt r5q; both fp32).  torch's setting is process-wide, so the trainers scope it
+    to their own steps (SyntheticTrainer(small_gemm_blas=True), the default; the reference-API Trainer only on
+    request) instead of leaving it switched for the rest of the process.  Re-entrant."""
+
+    def __init__(self, enabled=True):
+        self.enabled = enabled and torch.cuda.is_available()
+        self.prev = None
+
+    def __enter__(self):
+        if self.enabled:
+            self.prev = torch.backends.cuda.preferred_blas_library()
+            torch.backends.cuda.preferred_blas_library("cublas")  # (rocBLAS on ROCm)
+        return self
+
+    def __exit__(self, *exc):
+        if self.enabled:
+            torch.backends.cuda.preferred_blas_library(self.prev)
+        return False
 
 
 def normalise_train_cfg(cfg):
@@ -183,10 +198,10 @@ class SyntheticTrainer:
     def __init__(self, device, rays=4096, H=540, W=960, patch=4, seed=678, depth_range=(0.01, 5.0),
                  cos_anneal_ratio=0.5, schedule="fixed", start_it=0, distributed=False, group=None,
                  sdf_cfg=None, col_cfg=None, ren_cfg=None, joint_pose=False, stage1=False, n_images=10,
-                 capturable=False, mfma_dtype="fp32", train_cfg=None, stage1_fused=True):
+                 capturable=False, mfma_dtype="fp32", train_cfg=None, stage1_fused=True, small_gemm_blas=True):
         if schedule not in ("fixed", "reference"):
             raise ValueError(f"schedule must be 'fixed' or 'reference' (got {schedule!r})")
-        prefer_small_gemm_blas()
+        self.small_gemm_blas = small_gemm_blas  # rocBLAS for torch's small GEMMs inside the steps only
         self.device = torch.device(device)
         self.R, self.H, self.W, self.patch = rays, H, W, patch
         self.depth_range = depth_range
@@ -380,6 +395,10 @@ class SyntheticTrainer:
     def iteration(self, batch, t_rand=None, z_vals=None, return_out=False):
         """Forward, losses, backward, gradient all-reduce and Adam for one batch
         (t_rand / z_vals: the renderer's test hooks, e.g. to pin sample positions)."""
+        with small_gemm_blas(self.small_gemm_blas):
+            return self._iteration(batch, t_rand, z_vals, return_out)
+
+    def _iteration(self, batch, t_rand, z_vals, return_out):
         near_far = (torch.full((batch["rays_o"].shape[0], 1), float(self.depth_range[0]), device=self.device),
                     torch.full((batch["rays_o"].shape[0], 1), float(self.depth_range[1]), device=self.device))
         if t_rand is None:
@@ -404,7 +423,8 @@ class SyntheticTrainer:
 
     def device_step(self):
         """The capturable part of an iteration (no host work)."""
-        return self.iteration(self.make_batch())
+        with small_gemm_blas(self.small_gemm_blas):
+            return self.iteration(self.make_batch())
 
     def step(self):
         self.begin_iteration()
@@ -457,7 +477,12 @@ class GraphedTrainer:
         trainer.opt.zero_grad(set_to_none=True)
         trainer.begin_iteration()  # the captured step is this iteration's
         with torch.cuda.graph(self.graph):
-            self.loss = trainer.device_step()
+            loss = trainer.device_step()
+        # the replays write the loss into this static storage; a detached view keeps it without the
+        # captured step's autograd graph, whose AccumulateGrad nodes would stay bound to the capture
+        # stream (an eager step afterwards -- bench.py's instrumented pass -- would then warn and sync)
+        self.loss = loss.detach()
+        del loss
         torch.cuda.synchronize(trainer.device)
         self.graph.replay()  # capture records without executing: run the captured iteration once
 

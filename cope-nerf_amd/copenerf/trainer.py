@@ -38,10 +38,12 @@ _WEIGHT_NAMES = ("rgb_weight", "eikonal_weight", "sdf_weight", "flow_rgb_weight"
 
 class Trainer(object):
     def __init__(self, renderer, optimizer, motion_optimizer, cfg, device=None, patch_rng="cpu", nan_check="sync",
-                 **kwargs):
-        """Reference: model/training.py:16-50."""
-        from .train_step import prefer_small_gemm_blas
-        prefer_small_gemm_blas()
+                 small_gemm_blas=False, **kwargs):
+        """Reference: model/training.py:16-50.  small_gemm_blas=True switches torch's preferred BLAS to rocBLAS
+        for the process (train.py's motion-network GEMMs run outside this class, so the switch cannot be scoped
+        to its methods); the default leaves the caller's setting alone."""
+        if small_gemm_blas and torch.cuda.is_available():
+            torch.backends.cuda.preferred_blas_library("cublas")  # (rocBLAS on ROCm; train_step.small_gemm_blas)
         self.total_nb_images = kwargs["total_nb_images"]
         self.renderer = renderer
         self.optimizer = optimizer

@@ -4,8 +4,10 @@ rank joins, rank 0 alone prints one line with n_gpus = N; a WORLD_SIZE that disa
 is refused."""
 import json
 import os
+import re
 import subprocess
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BENCH = os.path.join(ROOT, "bench.py")
@@ -55,3 +57,21 @@ def test_world_size_must_match_gpus():
 def test_gloo_needs_dry():
     p = _run(["--backend", "gloo"])
     assert p.returncode != 0 and "--dry" in p.stderr
+
+
+def test_rank_that_never_joins_ends_every_rank_nonzero():
+    """A rank that never reaches the rendezvous (test hook) must not hang the run until the driver's
+    limit: the others time out after --pg-timeout with a message, exit non-zero, the parent stops the
+    absent one and exits non-zero, listing every rank's status."""
+    t0 = time.time()
+    p = _run(["--gpus", "2", "--dry", "--backend", "gloo", "--steps", "2", "--warmup", "1", "--pg-timeout", "8",
+              "--dry-absent-rank", "1"], timeout=120)
+    elapsed = time.time() - t0
+    assert p.returncode != 0, p.stdout + p.stderr[-2000:]
+    assert not _lines(p.stdout)
+    assert "did not form within 8 s" in p.stderr, p.stderr[-2000:]
+    m = re.search(r"rank exit statuses \[([^\]]*)\]", p.stderr)
+    assert m, p.stderr[-2000:]
+    statuses = [int(x) for x in m.group(1).split(",")]
+    assert len(statuses) == 2 and all(s != 0 for s in statuses), statuses
+    assert elapsed < 60, elapsed

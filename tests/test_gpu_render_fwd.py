@@ -113,3 +113,27 @@ def test_render_fwd_given_samples_and_larger_batch(mode):
         out2 = _c_render(r, rays_o, rays_d, t, near, far, 0.7, z_in=z)
         _compare(out2, ref2, R, 96)
         assert torch.equal(out2["z"], z)
+
+
+def test_render_fwd_refuses_inputs_the_c_side_would_overrun():
+    """ops.render_fwd / render_train_fwd check what cn_render_fwd assumes (R from rays_o, S from z) before the
+    call: a short t_rand or z, near / far of another length, a non-fp32 or strided input raise RuntimeError."""
+    from copenerf import ops
+    R = 64
+    f = lambda *s: torch.zeros(*s, device=DEV)  # noqa: E731
+    good = dict(rays_o=f(R, 3), rays_d=f(R, 3), near=f(R, 1), far=f(R, 1), time_step=f(1), inv_s=f(1, 1), car=f(1))
+
+    def call(**kw):
+        a = dict(good, **kw)
+        t_rand, z = a.pop("t_rand", None), a.pop("z", None)
+        return ops.render_fwd(None, None, a["rays_o"], a["rays_d"], a["near"], a["far"], a["time_step"], a["inv_s"],
+                              a["car"], 64, 64, 4, t_rand=t_rand, z_in=z)
+
+    for bad in (dict(t_rand=f(R - 1, 64)), dict(t_rand=f(R, 32)), dict(z=f(R - 1, 128)), dict(near=f(R - 1, 1)),
+                dict(far=f(2 * R, 1)), dict(rays_d=f(R, 4)), dict(rays_o=f(R, 3).double()),
+                dict(t_rand=f(64, R).t()), dict(z=f(R, 128).half())):
+        with pytest.raises(RuntimeError):
+            call(**bad)
+    with pytest.raises(RuntimeError):
+        ops.render_train_fwd(None, None, good["rays_o"], good["rays_d"], good["near"], good["far"], good["time_step"],
+                             good["inv_s"], good["car"], 64, f(R + 1, 128))
