@@ -196,6 +196,16 @@ def sig_beta(lay: SDFLayout, l: int) -> float:
     return lay.beta * (SQRT2 if (l + 1) == lay.skip else 1.0)
 
 
+# Attribution switches of the bf16 mode's quality study (tools/quality_sweep.py), honoured by
+# the layer-by-layer composition only (renderer.RENDER_NATIVE / MLP_NATIVE off):
+#   BF16_IMAGES = False  no operand images: the bf16 GEMMs round fp32 operands while staging (the same
+#                        products), σ and the second-order term's s, u̇ from fp32 values;
+#   SIGMA_FP32 = True    the images stay the GEMMs' operands, but MUL / TANGENT / BWD_SOFTPLUS recover σ from
+#                        an fp32 copy of the activation (the second-order term's s, u̇ keep their image values).
+BF16_IMAGES = True
+SIGMA_FP32 = False
+
+
 def _img_mode(pk, lay) -> bool:
     """bf16 MFMA mode (config C3): activations whose consumers are GEMM operands are stored as bf16
     operand images -- the bits the GEMM staging would round them to -- beside (or instead of) the fp32
@@ -203,7 +213,7 @@ def _img_mode(pk, lay) -> bool:
     weight gradient need the 256x256 stage ring (cn_wgrad's bf16 images); narrower networks keep fp32
     operands, rounded on load."""
     B = pk.Bf[0]
-    return B.dtype == torch.bfloat16 and B.dim() == 2 and lay.HL % 256 == 0
+    return BF16_IMAGES and B.dtype == torch.bfloat16 and B.dim() == 2 and lay.HL % 256 == 0
 
 
 def _empty_b(M, n, dev):
@@ -281,6 +291,8 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
         if img and 1 <= sk < L8:
             Usk_b = _empty_b(M, HL, dev)  # the skip input's operand image, its tail written by the embedding
             e_view = Usk_b[:, o:o + lay.E]
+            if SIGMA_FP32 and keep_u:  # (attribution) σ's fp32 source; its embedding tail is never read
+                Usk = torch.zeros(M, HL, device=dev)
         else:
             Usk = _empty(M, HL, dev)
             e_view = Usk[:, o:o + lay.E]
@@ -310,6 +322,8 @@ def sdf_forward(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, *, want_feat: bool
             if img and l + 1 < L8:  # the next layer's operand image, the activation's only copy
                 ob = Usk_b if into else _empty_b(M, HL, dev)
                 out = None
+                if SIGMA_FP32 and keep_u:  # (attribution) + an fp32 copy that σ is recovered from
+                    out = Usk if into else _empty(M, HL, dev)
             else:
                 out = Usk if into else _empty(M, HL, dev)
             ops.linear(A, pk.Bf[l], lay.out_dim[l], K, out, EPI_SOFTPLUS, bias=pk.b[l],
@@ -513,8 +527,10 @@ def sdf_backward(lay: SDFLayout, pk: SDFPack, st, dsdf, dfeat, dG, dh=None, want
             return {}
         # (bf16 mode: the images; the top layer's only on the elementwise path, top_img)
         img2 = (l < L8 - 1 or top_img) and Sb[l] is not None and Udb[l + 1] is not None
-        return dict(aux1=Sb[l] if img2 else s_fp32(l), aux2=Udb[l + 1] if img2 else Ud[l + 1],
-                    aux2_scale=lay.beta * (SQRT2 if (l + 1) == sk else 1.0))
+        a1, a2 = (Sb[l], Udb[l + 1]) if img2 else (s_fp32(l), Ud[l + 1])
+        if img2 and SIGMA_FP32:  # (attribution) the image values in fp32, the dtype of σ's fp32 source
+            a1, a2 = a1.float(), a2.float()
+        return dict(aux1=a1, aux2=a2, aux2_scale=lay.beta * (SQRT2 if (l + 1) == sk else 1.0))
 
     Z = _empty_b(M, HL, dev) if (z_img(L8 - 1) and (dh is not None or (sdf_only and fused_cs))) else _empty(M, HL, dev)
     if dh is not None:  # Z_7 = (dh + dsdf w80) σ_7 + the second-order term: elementwise

@@ -553,8 +553,9 @@ __global__ void __launch_bounds__(512, 2) wgrad_x6r_kernel(WgradBatch batch) {
     auto split_col = [&](const floatx4 (&r4)[4], int e, int buf, bool bias) {
         float* img = smem + buf * IMG + (sx ? BNo * LSB : 0) + mq * 2;
         const floatx4 col = {r4[0][e], r4[1][e], r4[2][e], r4[3][e]};
-        const float s = (col[0] + col[1]) + (col[2] + col[3]);
-        bsum[e] += bias ? s : 0.0f;
+        // (scalar adds: a packed pair beside the MFMAs costs more issue cycles than two scalar ones)
+        const float s = add_f32(add_f32(col[0], col[1]), add_f32(col[2], col[3]));
+        bsum[e] = add_f32(bsum[e], bias ? s : 0.0f);
         bf16x4 t0, t1, t2;
         split3(col, t0, t1, t2);
         float* y = img + (cg * 4 + e) * LSB;
@@ -1091,8 +1092,8 @@ __global__ void __launch_bounds__(512, 4) wgrad_x6n_kernel(WgradArgs p) {  // 2 
         if (!stager) return;
         float* img = smem + buf * IMG + (sy ? 0 : BNo * LSB) + mq * 2;
         const floatx4 col = {r4[0][e], r4[1][e], r4[2][e], r4[3][e]};
-        const float sm = (col[0] + col[1]) + (col[2] + col[3]);
-        bsum[e] += bias ? sm : 0.0f;
+        const float sm = add_f32(add_f32(col[0], col[1]), add_f32(col[2], col[3]));
+        bsum[e] = add_f32(bsum[e], bias ? sm : 0.0f);
         bf16x4 t0, t1, t2;
         split3(col, t0, t1, t2);
         float* y = img + (cg * 4 + e) * LSB;

@@ -21,9 +21,12 @@ if [ $TESTS = 1 ]; then
 fi
 for c in ${@:-c2}; do
   # <config>graph: the config replayed from a captured HIP graph
-  case $c in *graph) args="--config ${c%graph} --graph";; *) args="--config $c";; esac
+  # distgraph: c2 through the data-parallel path (a 1-rank RCCL group, graph-captured all-reduce)
+  case $c in distgraph) args="--config c2 --graph"; export COPENERF_FORCE_DIST=1;;
+             *graph) args="--config ${c%graph} --graph";; *) args="--config $c";; esac
   timeout -k 10 400 python3 -u bench.py $args --no-cpu-baseline > $O/bench_$c.json 2> $O/bench_$c.err
   rc=$?
+  unset COPENERF_FORCE_DIST
   [ $rc = 0 ] || { echo "bench $c failed rc=$rc"; tail -5 $O/bench_$c.err; exit $rc; }
   python3 -c "import json,sys; d=json.load(open('$O/bench_$c.json')); print('$c', d['value'], d['ms_per_step'], d['roofline']['launch_class'], d['roofline']['frac'])"
 done
