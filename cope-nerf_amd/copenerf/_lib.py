@@ -270,3 +270,22 @@ def check(rc: int, name: str) -> None:
 def call(name: str, *args) -> None:
     lib = load()
     check(getattr(lib, name)(*args), name)
+
+
+def shape_key(st):
+    """What a composed entry point's sizing pass reads of a descriptor: every scalar field, every pointer
+    field only as present / absent (the planners see no pointer values -- a buffer's existence is a flag),
+    nested descriptors (networks) likewise.  Equal keys give equal workspace / state sizes, so the host
+    plans a shape once (ops._sized) instead of on every call."""
+    out = []
+    for name, typ in st._fields_:
+        v = getattr(st, name)
+        if typ is c_ptr:
+            out.append(v is not None and v != 0)
+        elif isinstance(v, ctypes.Array):
+            out.append(tuple((x is not None and x != 0) if typ._type_ is c_ptr else x for x in v))
+        elif hasattr(typ, "_type_") and issubclass(typ, ctypes._Pointer):
+            out.append(shape_key(v.contents) if v else None)
+        else:
+            out.append(v)
+    return (type(st).__name__, tuple(out))

@@ -660,6 +660,22 @@ def color_net(lay, pk):
     return n, keep
 
 
+_SIZES = {}
+
+
+def _sized(fn, desc, *extra):
+    """lib.<fn>(desc, *extra) memoised on the descriptor's shape key (_lib.shape_key): the composed entry
+    points' planners run once per shape, not once more per call (the entry point itself re-plans into the
+    caller's buffer and refuses a plan larger than it, so a stale size fails loudly, never silently)."""
+    key = (fn, _lib.shape_key(desc), extra)
+    n = _SIZES.get(key)
+    if n is None:
+        if len(_SIZES) > 4096:
+            _SIZES.clear()
+        n = _SIZES[key] = int(getattr(_lib.load(), fn)(ctypes.byref(desc), *extra))
+    return n
+
+
 def _check_render_inputs(fn, R, rays_o, rays_d, near, far, time_step, inv_s, car, t_rand=None, n_samples=None,
                          z=None):
     """The shapes and types the C side assumes (it takes R from rays_o and S from z): anything else would be
@@ -707,7 +723,7 @@ def render_fwd(sdf_net_, color_net_, rays_o, rays_d, near, far, time_step, inv_s
     for k, v in out.items():
         setattr(d, k, v.data_ptr())
     lib = _lib.load()
-    ws = torch.empty(max(int(lib.cn_render_fwd_workspace_bytes(ctypes.byref(d))), 1), dtype=torch.uint8, device=dev)
+    ws = torch.empty(max(_sized("cn_render_fwd_workspace_bytes", d), 1), dtype=torch.uint8, device=dev)
     _lib.check(lib.cn_render_fwd(ctypes.byref(d), _ptr(ws), ws.numel(), _stream()), "cn_render_fwd")
     return out
 
@@ -729,7 +745,7 @@ def render_train_fwd(sdf_net_, color_net_, rays_o, rays_d, near, far, time_step,
     for k, v in out.items():
         setattr(d, k, v.data_ptr())
     lib = _lib.load()
-    state = torch.empty(max(int(lib.cn_render_state_bytes(ctypes.byref(d))), 1), dtype=torch.uint8, device=dev)
+    state = torch.empty(max(_sized("cn_render_state_bytes", d), 1), dtype=torch.uint8, device=dev)
     _lib.check(lib.cn_render_train_fwd(ctypes.byref(d), _ptr(state), state.numel(), _stream()), "cn_render_train_fwd")
     return out, state, d
 
@@ -749,7 +765,7 @@ def render_bwd(d, state, *, dcolor=None, ddepth=None, dweights=None, dcdf=None, 
         g.col_dW[l], g.col_db[l] = _ptr(w), _ptr(b)
     g.dinv_s, g.drays_o, g.drays_d = _ptr(dinv_s), _ptr(drays_o), _ptr(drays_d)
     lib = _lib.load()
-    nb = int(lib.cn_render_bwd_workspace_bytes(ctypes.byref(d), 1 if drays_o is not None else 0))
+    nb = _sized("cn_render_bwd_workspace_bytes", d, 1 if drays_o is not None else 0)
     ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=state.device)
     _lib.check(lib.cn_render_bwd(ctypes.byref(d), ctypes.byref(g), _ptr(state), state.numel(), _ptr(ws), ws.numel(),
                                  _stream()), "cn_render_bwd")
@@ -790,7 +806,7 @@ def mlp_fwd(net, x, sdf):
         raise RuntimeError("mlp_fwd: sdf must be contiguous with M entries")
     lib = _lib.load()
     d = _mlp_desc(net, M, x=x, sdf=sdf)
-    state = torch.empty(max(int(lib.cn_mlp_state_bytes(ctypes.byref(d))), 1), dtype=torch.uint8, device=x.device)
+    state = torch.empty(max(_sized("cn_mlp_state_bytes", d), 1), dtype=torch.uint8, device=x.device)
     _lib.check(lib.cn_mlp_fwd(ctypes.byref(d), _ptr(state), state.numel(), _stream()), "cn_mlp_fwd")
     return state
 
@@ -806,7 +822,7 @@ def mlp_bwd(net, M, state, dsdf, dWs=None, dbs=None, dx=None):
             raise RuntimeError("mlp_bwd: gradients must be contiguous float32")
     lib = _lib.load()
     d = _mlp_desc(net, M, dsdf=dsdf, dWs=dWs, dbs=dbs, dx=dx)
-    ws = torch.empty(max(int(lib.cn_mlp_bwd_workspace_bytes(ctypes.byref(d))), 1), dtype=torch.uint8,
+    ws = torch.empty(max(_sized("cn_mlp_bwd_workspace_bytes", d), 1), dtype=torch.uint8,
                      device=dsdf.device)
     _lib.check(lib.cn_mlp_bwd(ctypes.byref(d), _ptr(state), state.numel(), _ptr(ws), ws.numel(), _stream()),
                "cn_mlp_bwd")
@@ -832,7 +848,7 @@ def sample(net, rays_o, rays_d, near, far, t_rand, time_step, n_samples, n_impor
     d.t_rand, d.time_step, d.z = _ptr(t_rand), _ptr(time_step), _ptr(z)
     d.net, d.philox = ctypes.pointer(net), _ptr(philox)
     lib = _lib.load()
-    ws = torch.empty(max(int(lib.cn_sample_workspace_bytes(ctypes.byref(d))), 1), dtype=torch.uint8, device=z.device)
+    ws = torch.empty(max(_sized("cn_sample_workspace_bytes", d), 1), dtype=torch.uint8, device=z.device)
     _lib.check(lib.cn_sample(ctypes.byref(d), _ptr(ws), ws.numel(), _stream()), "cn_sample")
     return z
 

@@ -1631,6 +1631,13 @@ enum LinearTile { LT_BF_SQ, LT_BF_T0, LT_BF_T1, LT_X6_SQ, LT_X6_TALL, LT_X6_WIDE
 #define CN_AB_X6_BWD_SQ 0
 #endif
 
+// bf16x6 launches of at most this many rows (the sampler's up-sampling queries: 65,536 rows = one 256x256
+// tile per CU, nothing to overlap an epilogue with) take the two-per-CU tiles: SOFTPLUS the 128x128 one,
+// SOFTPLUS_HEAD the 128x256 one.  0: off (measurement switch, profiles/r6_ab.txt)
+#ifndef CN_X6_SMALL_M
+#define CN_X6_SMALL_M 0
+#endif
+
 static LinearTile choose_linear_tile(const cn_linear_desc* d) {
     const int e = d->epilogue;
     const bool head = e == CN_EPI_SOFTPLUS_HEAD;
@@ -1645,6 +1652,10 @@ static LinearTile choose_linear_tile(const cn_linear_desc* d) {
     if (d->mfma_dtype == CN_MFMA_F32_BF16X6) {
         if (d->tile == 1) return LT_X6_T1;
         if (d->tile == 2) return LT_X6_T128;
+        if (d->M <= CN_X6_SMALL_M && wide_n && d->K % 64 == 0 && longk && d->ldb >= 256) {
+            if (e == CN_EPI_SOFTPLUS) return LT_X6_T128;
+            if (head) return LT_X6_TALL;
+        }
         // (BWD_SOFTPLUS on the 256x256 tile: re-measured in round 4 with the branch-free epilogue, equal or
         // slower -- 4.25 vs 4.17 ms per C2 step, profiles/r4_ab.txt r4m)
         if (wide_n && d->K % 32 == 0 && d->ldb >= 256 && (e != CN_EPI_BWD_SOFTPLUS || CN_AB_X6_BWD_SQ) && (longk || head))
