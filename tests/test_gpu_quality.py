@@ -7,7 +7,7 @@ MotionNetwork, scene-flow SDF loss, flow-RGB warp, SDF consistency with pose gra
 operand images, and the fp32-class bf16x6 GEMMs -- on a scene with a learnable surface: a camera at
 the centre of a textured spherical room (radius 1; the indoor-scene initialisation, inside_outside,
 starts the SDF as a room of radius 0.5), ten identical frames (a static camera: the motion network
-should stay still).  Each mode runs over three sample streams; every run must have learned the scene
+should stay still).  Each mode runs over six sample streams; every run must have learned the scene
 and the modes' mean final photometric loss and mean PSNR of a held-out eval render must agree within
 the stated tolerances (PSNR 12.1 dB at the start; see the tolerances below for the measured runs).
 COPENERF_QUALITY_LOG receives the loss curves (profiles/r5_bf16_quality.json)."""
@@ -23,14 +23,19 @@ DEV = "cuda"
 STEPS = 1000
 ROOM_RADIUS = 1.0
 EVAL_HW = (135, 240)
-# tolerances between the modes (bf16 vs bf16x6) from a sweep over four sample streams
-# (profiles/r5_bf16_quality_sweep.json; the first three are SEEDS): eval PSNR bf16 30.5 / 31.1 / 35.3 / 37.8,
-# bf16x6 42.3 / 36.4 / 35.9 / 38.1 dB -- one stream's pair differs by 0.4 .. 11.8 dB, the bf16x6 runs among
-# themselves by up to 6.4; means over SEEDS 32.3 vs 38.2 (5.9 dB) -- PSNR_TOL_DB on the means; photometric
-# loss (L1 rgb, mean of the last 100 steps) means 0.0123 vs 0.0116 (ratio 1.06) -- L1_RATIO_TOL; every run
-# gains >= 18.4 dB over the initial 12.1 -- MIN_PSNR_GAIN_DB
-L1_RATIO_TOL = 1.5
-PSNR_TOL_DB = 8.0
+# Tolerances between the modes (bf16 vs bf16x6) from the round-6 attribution sweep over these six sample streams
+# (profiles/r6_bf16_quality_sweep.json, tools/quality_sweep.py): eval PSNR bf16 30.5 / 31.1 / 35.3 / 37.8 /
+# 38.4 / 33.5, bf16x6 42.3 / 36.4 / 35.9 / 38.1 / 31.4 / 35.5 dB -- paired differences -11.8 .. +7.0 (training
+# is chaotic: bf16x6 runs among themselves span 31.4 .. 42.3) -- means 34.4 vs 36.6: a 2.15 dB gap, so
+# PSNR_TOL_DB = 2.15 + 1.35 dB of margin; photometric loss (L1 rgb, mean of the last 100 steps) means 0.0111 vs
+# 0.0101 (ratio 1.10): L1_RATIO_TOL = 1.10 + 0.15; every run gains >= 18.4 dB over the initial 12.1 --
+# MIN_PSNR_GAIN_DB.  The runs are bitwise reproducible for a build, so these bars hold exactly for this one; a
+# change to any GEMM's summation order re-draws every stream (the six-stream mean moves by ~2.7 dB std), and
+# a failure after such a change calls for a wider sweep (tools/quality_sweep.py --seeds ...), not a wider bar.
+# The sweep's attribution arms: sigma recovered from an fp32 copy of the activation 35.3 dB mean (images stay
+# the GEMM operands), no operand images at all 32.8 dB (L1 0.0180) -- the operand images do not cost quality.
+L1_RATIO_TOL = 1.25
+PSNR_TOL_DB = 3.5
 MIN_PSNR_GAIN_DB = 15.0
 
 
@@ -85,7 +90,7 @@ def _train(mode, sample_seed=None):
             "loss_curve": [round(v, 5) for v in losses.view(-1, 50).mean(1).tolist()]}
 
 
-SEEDS = [None, 12345, 777]  # the trainer's own sample stream, then two others (same weights and frames)
+SEEDS = [None, 12345, 777, 4242, 31337, 9001]  # the trainer's own sample stream, then others (same weights and frames)
 RUNS = {}
 
 
@@ -99,7 +104,7 @@ def test_quality_run(mode, seed):
 
 
 def test_bf16_training_tracks_fp32_class_training():
-    """bf16 and bf16x6 from the same weights over the same three sample streams (training is chaotic: one
+    """bf16 and bf16x6 from the same weights over the same six sample streams (training is chaotic: one
     stream's pair can differ by as much as two fp32-class streams, so the modes are compared on means)."""
     if len(RUNS) != 2 * len(SEEDS):
         pytest.skip("the runs did not all complete")
