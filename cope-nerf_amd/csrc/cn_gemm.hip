@@ -93,6 +93,10 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                                                 EPI == CN_EPI_BWD_SOFTPLUS);
     constexpr bool AUX12B = (MODE_ & 8) != 0 && EPI == CN_EPI_BWD_SOFTPLUS;
     static_assert(!ABF || MODE == 1, "bf16 A images only in the bf16 MFMA mode");
+    // MODE_ bit 4 (MODE 2, measurement build CN_AB_X6_AIMG): A arrives as a bf16x6 term image in B's chunk-major
+    // format ([K/16][lda rows][3 terms][16], lda = the image's rows), staged like B: no split
+    constexpr bool AX6 = (MODE_ & 16) != 0;
+    static_assert(!AX6 || (MODE == 2 && BK == 16), "bf16x6 A images: 16-deep stages of the bf16x6 mode");
     constexpr int NT = 64 * WM * WN;
     const float* const cA = p.A;
     const float* const cB = p.B;
@@ -115,7 +119,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     // modes 0/1: B rows tid/KCB + q*RSTEPB; mode 2 (6 pieces per row): piece tid + q*NT
     constexpr int RSTEPB = MODE == 2 ? 1 : NT / KCB;
     static_assert(BM % RSTEP == 0 && (MODE == 2 || (NT % KCB == 0 && BN % RSTEPB == 0)), "tile/thread mismatch");
-    constexpr int ALD = BM / RSTEP;
+    constexpr int ALD = AX6 ? (BM * 6 + NT - 1) / NT : BM / RSTEP;  // (AX6: 16-byte pieces like B's)
     constexpr int BLD = MODE == 2 ? (BN * KCB + NT - 1) / NT : BN / RSTEPB;
     constexpr int ESZB = BF ? 2 : 4;             // bytes per B element
     constexpr int PIECES_PL = BK / 8;            // MODE 2: 16-byte pieces per plane of a staged row
@@ -169,10 +173,18 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
     const int srowb = tid / KCB, scb = tid % KCB;
     int voA[ALD], voA2[ALD], voB[BLD];  // byte offsets of the staged rows (range-checked)
     int ldsB[BLD];                      // MODE 2: LDS dword offset of B piece q within a buffer
+    int ldsA[AX6 ? ALD : 1];            // (AX6) LDS dword offset of A piece q, as ldsB
 #pragma unroll
     for (int q = 0; q < ALD; ++q) {
-        voA[q] = ((srow + q * RSTEP) * p.lda + sc4 * EPA) * ESA;
-        voA2[q] = ((srow + q * RSTEP) * p.lda2 + sc4 * EPA) * ESA;
+        if constexpr (AX6) {  // piece idx: row w / 6, term (w % 6) / 2, k half w % 2 of the tile's contiguous chunk
+            const int w = tid + q * NT;
+            voA[q] = w < BM * 6 ? w * 16 : 0;
+            voA2[q] = 0;
+            ldsA[q] = (w / 6) * LS + ((w % 6) >> 1) * (BK / 2) + 4 * (w & 1);
+        } else {
+            voA[q] = ((srow + q * RSTEP) * p.lda + sc4 * EPA) * ESA;
+            voA2[q] = ((srow + q * RSTEP) * p.lda2 + sc4 * EPA) * ESA;
+        }
     }
 #pragma unroll
     for (int q = 0; q < BLD; ++q) {
@@ -206,9 +218,16 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                                    : reinterpret_cast<const char*>(cA) + (int64_t)m0 * p.lda * ESA;
         const int ald = second ? p.lda2 : p.lda;
         const int ak = second ? k0 - p.K1 : k0;
+        if constexpr (AX6) {  // chunk kc, rows m0 .. m0 + rows - 1: 96 * rows contiguous bytes
+            const rsrc_t rA = make_view(reinterpret_cast<const float*>(reinterpret_cast<const char*>(cA) +
+                                                                       ((int64_t)kc * p.lda + m0) * 96), rows * 96);
+#pragma unroll
+            for (int q = 0; q < ALD; ++q) ra[set][q] = bload4(rA, voA[q], 0);
+        } else {
         const rsrc_t rA = make_view(reinterpret_cast<const float*>(abase), rows * ald * ESA);
 #pragma unroll
         for (int q = 0; q < ALD; ++q) ra[set][q] = bload4(rA, second ? voA2[q] : voA[q], ak * ESA);
+        }
         // MODE 2: chunk kc of the image is [ldb rows][48 bf16]; the tile's BN rows are 96 * BN contiguous bytes
         const int64_t bofs = MODE == 2 ? ((int64_t)kc * (BK / 16) * p.ldb + n0) * 96 : (int64_t)n0 * p.ldb * ESZB;
         const rsrc_t rB = make_view(reinterpret_cast<const float*>(reinterpret_cast<const char*>(cB) + bofs),
@@ -223,7 +242,10 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
 #pragma unroll
         for (int q = 0; q < ALD; ++q) {
             if (piece >= 0 && piece != q) continue;
-            if constexpr (MODE == 2) {
+            if constexpr (AX6) {
+                if (BM * 6 % NT == 0 || tid + q * NT < BM * 6)  // wave-uniform
+                    *reinterpret_cast<floatx4*>(sA + buf * BM * LS + ldsA[q]) = ra[set][q];
+            } else if constexpr (MODE == 2) {
                 bf16x4 x0, x1, x2;
                 split3(ra[set][q], x0, x1, x2);
                 *reinterpret_cast<bf16x4*>(a + q * RSTEP * LS) = x0;
@@ -1580,11 +1602,21 @@ static int launch_linear_tile_m(const cn_linear_desc* d, LinearArgs& a, hipStrea
 // The template MODE_ of a descriptor on a tile of GEMM mode MODE: + 4 for bf16 A images, + 8 for a
 // bf16 aux0 (MODE 1 only).
 static int linear_mode_bits(const cn_linear_desc* d, int mode) {
+    if (mode == 2) return mode + (d->a_bf16 ? 16 : 0);  // (CN_AB_X6_AIMG) a bf16x6 term image of A
     return mode == 1 ? mode + (d->a_bf16 ? 4 : 0) + (d->aux0_bf16 || d->aux12_bf16 ? 8 : 0) : mode;
 }
 
+// measurement build only (-DCN_AB_X6_AIMG=1, profiles/r6_ab.txt): cn_linear reads A as a bf16x6 term image on the
+// 256x256 tile (a_bf16 set with CN_MFMA_F32_BF16X6; the layout of split_bf16x3's B images)
+#ifndef CN_AB_X6_AIMG
+#define CN_AB_X6_AIMG 0
+#endif
+
 template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int MODE = 0>
 static int launch_linear_tile(const cn_linear_desc* d, LinearArgs& a, hipStream_t s) {
+    if constexpr (MODE == 2 && CN_AB_X6_AIMG && BK == 16 && TM * TN >= 8) {
+        if (linear_mode_bits(d, MODE) == 18) return launch_linear_tile_m<WM, WN, TM, TN, BK, OCC, DEPTH, 18>(d, a, s);
+    }
     if constexpr (MODE == 1) {
         switch (linear_mode_bits(d, MODE)) {
             case 5: return launch_linear_tile_m<WM, WN, TM, TN, BK, OCC, DEPTH, 5>(d, a, s);
@@ -1685,7 +1717,11 @@ static int linear_plan(const cn_linear_desc* d, LinearArgs& a) {
     const bool x6 = d->mfma_dtype == CN_MFMA_F32_BF16X6;
     CN_REQUIRE(d->K % (bf ? 64 : 32) == 0, CN_ERR_SHAPE, "cn_linear: K=%d must be a multiple of %d", d->K, bf ? 64 : 32);
     CN_REQUIRE(d->tile >= 0 && d->tile <= 2, CN_ERR_ARG, "cn_linear: bad tile %d", d->tile);
-    if (d->a_bf16 || d->aux0_bf16 || d->aux12_bf16 || d->out0_b || d->out1_b) {  // bf16 operand images (ABI v10)
+    if (x6 && d->a_bf16 && CN_AB_X6_AIMG) {  // (measurement build) A as a bf16x6 term image, rows = lda
+        CN_REQUIRE(!d->A2 && !d->aux0_bf16 && !d->aux12_bf16 && !d->out0_b && !d->out1_b && d->lda >= d->M &&
+                       al16(d->A) && choose_linear_tile(d) == LT_X6_SQ,
+                   CN_ERR_UNSUPPORTED, "cn_linear: bf16x6 A images: 256x256 tile, no A2, lda = image rows >= M");
+    } else if (d->a_bf16 || d->aux0_bf16 || d->aux12_bf16 || d->out0_b || d->out1_b) {  // bf16 operand images (ABI v10)
         CN_REQUIRE(bf, CN_ERR_UNSUPPORTED, "cn_linear: bf16 operand images need mfma_dtype CN_MFMA_BF16");
         CN_REQUIRE(!d->a_bf16 || (d->lda % 8 == 0 && (!d->A2 || d->lda2 % 8 == 0)), CN_ERR_ALIGN,
                    "cn_linear: bf16 A / A2 need lda, lda2 multiples of 8");

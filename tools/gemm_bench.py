@@ -31,6 +31,24 @@ def bench(res, key, fn, div=1):
         res[key] = timeit(fn) / div
 
 
+def linear_x6_aimg(As, M, B, N, K, out0, epi, bias=None, aux0=None, aux1=None, aux2=None, aux_beta=0.0,
+                   aux2_scale=0.0):
+    """cn_linear with A given as a bf16x6 term image (a_bf16 in the bf16x6 mode: a measurement build's switch)."""
+    import ctypes  # noqa: F401
+    from copenerf import _lib
+    d = _lib.LinearDesc()
+    d.A, d.B, d.bias = As.data_ptr(), B.data_ptr(), ops._ptr(bias)
+    d.aux0, d.aux1, d.aux2 = ops._ptr(aux0), ops._ptr(aux1), ops._ptr(aux2)
+    d.ld_aux0, d.ld_aux1, d.ld_aux2 = ops._ld(aux0), ops._ld(aux1), ops._ld(aux2)
+    d.aux_beta, d.aux2_scale = aux_beta, aux2_scale
+    d.out0, d.ld_out0 = out0.data_ptr(), out0.stride(0)
+    d.lda, d.ldb = As.shape[1], B.shape[1]
+    d.M, d.N, d.K, d.K1, d.nzero, d.nsplit = M, N, K, K, N, N
+    d.epilogue, d.tile, d.adiv, d.odiv, d.beta, d.threshold = epi, 0, 1.0, 1.0, 100.0, 20.0
+    d.mfma_dtype, d.a_bf16 = 2, 1
+    _lib.check(_lib.load().cn_linear(d, ops._stream()), "cn_linear (x6 A image)")
+
+
 def main():
     M = int(os.environ.get("M", 524288))
     N = K = 256
@@ -80,6 +98,20 @@ def main():
                           ("tangent", ops.EPI_TANGENT, sg),
                           ("bwd_softplus", ops.EPI_BWD_SOFTPLUS, so)):
         bench(res, "cn_linear x6 " + name, lambda: ops.linear(A, Bs, N, K, o0, epi, **kw))
+    if os.environ.get("X6_AIMG"):  # (a -DCN_AB_X6_AIMG=1 library) A as a bf16x6 term image, no split while staging
+        As = ops.split_bf16x3(A)  # [K/16, M, 48]: the layout of B's images
+        for name, epi, kw in (("store", ops.EPI_STORE, dict(bias=bias)),
+                              ("softplus", ops.EPI_SOFTPLUS, dict(bias=bias)),
+                              ("relu", ops.EPI_RELU, dict(bias=bias)),
+                              ("mul", ops.EPI_MUL, sg),
+                              ("tangent", ops.EPI_TANGENT, sg)):  # (BWD_SOFTPLUS runs on the 128x128 tile)
+            bench(res, "cn_linear x6 imgA " + name, lambda: linear_x6_aimg(As, M, Bs, N, K, o0, epi, **kw))
+        # the image's products equal the split-while-staging ones bitwise
+        o1 = torch.empty_like(o0)
+        ops.linear(A, Bs, N, K, o1, ops.EPI_STORE, bias=bias)
+        linear_x6_aimg(As, M, Bs, N, K, o0, ops.EPI_STORE, bias=bias)
+        torch.cuda.synchronize()
+        print("x6 imgA STORE bitwise equal to the fp32-A split:", bool(torch.equal(o0, o1)))
     bench(res, "torch.matmul bf16 (hipBLASLt)", lambda: torch.matmul(A.bfloat16(), Bb.t()))
     dW = torch.empty(N, K, device=dev)
     db = torch.empty(N, device=dev)
