@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libcopenerf.so"
 LIB_PATH = os.environ.get("COPENERF_LIB", os.path.join(_HERE, LIB_NAME))
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 c_f32p = ctypes.c_void_p  # device pointers are passed as integers
 c_i32 = ctypes.c_int32
@@ -84,7 +84,7 @@ class SdfMlpDesc(ctypes.Structure):
         ("skip_layer", c_i32),
         ("W", c_ptr * 8), ("ldw", c_i64 * 8), ("bias", c_ptr * 8),
         ("head_w", c_ptr), ("head_b", c_ptr), ("sdf", c_ptr), ("idx", c_ptr),
-        ("skip_div", c_f32), ("beta", c_f32), ("threshold", c_f32), ("debug", c_ptr),
+        ("skip_div", c_f32), ("beta", c_f32), ("threshold", c_f32), ("debug", c_ptr), ("format", c_i32),
     ]
 
 

@@ -231,25 +231,34 @@ def _act(U, Ub, l):
 FUSED_SDF_QUERY = True
 
 
+def _x6_pack(pk) -> bool:
+    """The pack holds bf16x6 term images (chunk-major [K/16, rows, 48])."""
+    return pk.Bf[0].dim() == 3
+
+
 def _fused_query_ok(lay: SDFLayout, pk: SDFPack) -> bool:
-    """cn_sdf_mlp's shape: 8 hidden layers of 256 (the skip layer 256 - E), K0 = 64, bf16 images."""
-    if not (FUSED_SDF_QUERY and _img_mode(pk, lay) and lay.n_lin == 9 and lay.HL == 256 and lay.KE == 64):
+    """cn_sdf_mlp's shape: 8 hidden layers of 256 (the skip layer 256 - E), K0 = 64, bf16 images -- or, ABI v15,
+    the bf16x6 mode's term images of 256 rows."""
+    x6 = _x6_pack(pk)
+    if not (FUSED_SDF_QUERY and (_img_mode(pk, lay) or x6) and lay.n_lin == 9 and lay.HL == 256 and lay.KE == 64):
         return False
     sk = lay.skip
     if not (2 <= sk <= 7 and lay.E + lay.out_dim[sk - 1] == 256):
         return False
+    rows = (lambda B: B.shape[1]) if x6 else (lambda B: B.shape[0])
     return all(lay.out_dim[l] == 256 for l in range(8) if l != sk - 1) and lay.out_dim[8] >= 1 and \
-        all(pk.Bf[l].shape[0] == 256 for l in range(8)) and lay.in_dim[8] == 256
+        all(rows(pk.Bf[l]) == 256 for l in range(8)) and lay.in_dim[8] == 256
 
 
 def sdf_query_fused(lay: SDFLayout, pk: SDFPack, x: torch.Tensor, sdf_out: Optional[torch.Tensor] = None,
                     dst: Optional[torch.Tensor] = None) -> torch.Tensor:
     """SDFNetwork.sdf(x) with no gradient (neus_fields.py:268-283) in two launches: cn_sdf_embed writes the
-    embedding's bf16 images (lin0's input, the skip concat's tail / sqrt 2), cn_sdf_mlp runs lin0 .. lin7 and
-    the sdf head with the activations on chip."""
+    embedding's bf16 images (lin0's input, the skip concat's tail / sqrt 2) -- fp32 rows in the bf16x6 mode --,
+    cn_sdf_mlp runs lin0 .. lin7 and the sdf head with the activations on chip."""
     M, dev = x.shape[0], x.device
-    u0b = _empty_b(M, lay.KE, dev)
-    tail = _empty_b(M, 64, dev)
+    mk = _empty if _x6_pack(pk) else _empty_b
+    u0b = mk(M, lay.KE, dev)
+    tail = mk(M, 64, dev)
     ops.sdf_embed(x, lay.multires, lay.scale, u0b, tail[:, :lay.E], SQRT2)
     sdf = sdf_out if sdf_out is not None else _empty(M, 1, dev)
     ops.sdf_mlp(u0b, tail[:, :lay.E], pk.Bf[:8], pk.b[:8], pk.w80[0], pk.b80, sdf, multires=lay.multires,

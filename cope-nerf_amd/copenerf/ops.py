@@ -537,24 +537,31 @@ def sdf_embed(x, multires, scale, U0, U4e=None, u4div=1.0):
 
 def sdf_mlp(u0b, tail, Ws, biases, head_w, head_b, sdf, *, multires, skip_layer, skip_div, beta, threshold,
             idx=None, debug=None):
-    """The sampler's SDF query in one launch (cn_sdf_mlp, bf16 mode): sdf[idx[m] or m] from the embedding's
-    bf16 images u0b [M, 64] and tail [M, >= E] through lin0 .. lin7 (bf16 weight images [256][K]) and the
-    head row.  Raises if the library does not support the network's shape."""
+    """The sampler's SDF query in one launch (cn_sdf_mlp): sdf[idx[m] or m] from the embedding u0b [M, 64] and
+    the skip tail [M, >= E] through lin0 .. lin7 and the head row -- bf16 mode: bf16 images of both and bf16 weight
+    images [256][K]; bf16x6 mode (ABI v15, 3-D weight images [K/16, 256, 48]): fp32 inputs, bitwise the
+    layer-by-layer bf16x6 query.  Raises if the library does not support the network's shape."""
+    x6 = Ws[0].dim() == 3
     for t, n in ((u0b, "u0b"), (tail, "tail")):
         _need(t, n)
-        if t.dtype != torch.bfloat16:
-            raise RuntimeError(f"sdf_mlp: {n} must be a bfloat16 image")
+        if t.dtype != (torch.float32 if x6 else torch.bfloat16):
+            raise RuntimeError(f"sdf_mlp: {n} must be {'fp32' if x6 else 'a bfloat16 image'} in this mode")
     if len(Ws) != 8 or len(biases) != 8:
         raise RuntimeError("sdf_mlp: 8 hidden layers")
     d = _lib.SdfMlpDesc()
     d.u0, d.tail, d.ld_u0, d.ld_t = _ptr(u0b), _ptr(tail), _ld(u0b), _ld(tail)
-    d.M, d.n_layers, d.hidden, d.kpad0 = u0b.shape[0], 8, Ws[1].shape[0], Ws[0].shape[1]
+    d.M, d.n_layers = u0b.shape[0], 8
+    d.hidden, d.kpad0 = (Ws[1].shape[1], 16 * Ws[0].shape[0]) if x6 else (Ws[1].shape[0], Ws[0].shape[1])
     d.multires, d.skip_layer = multires, skip_layer
+    d.format = FORMATS["bf16x6"] if x6 else 0
     for i, (W, b) in enumerate(zip(Ws, biases)):
-        _need(W, f"W{i}")
-        if W.dtype != torch.bfloat16 or W.shape[0] != 256 or not b.is_contiguous() or b.dtype != torch.float32:
-            raise RuntimeError(f"sdf_mlp: layer {i} needs a bf16 [256][K] weight image and an fp32 bias")
-        d.W[i], d.ldw[i], d.bias[i] = W.data_ptr(), W.stride(0), b.data_ptr()
+        _need(W, f"W{i}", ndim=3 if x6 else 2)
+        rows = W.shape[1] if x6 else W.shape[0]
+        if W.dtype != torch.bfloat16 or rows != 256 or not b.is_contiguous() or b.dtype != torch.float32 or \
+                (x6 and (W.dim() != 3 or W.shape[2] != 48 or not W.is_contiguous())):
+            raise RuntimeError(f"sdf_mlp: layer {i} needs a bf16 [256][K] weight image (bf16x6: a [K/16, 256, 48] "
+                               f"term image) and an fp32 bias")
+        d.W[i], d.ldw[i], d.bias[i] = W.data_ptr(), (256 if x6 else W.stride(0)), b.data_ptr()
     if not (head_w.is_contiguous() and head_w.numel() >= 256 and head_b.numel() >= 1):
         raise RuntimeError("sdf_mlp: head_w [256], head_b [1]")
     if not sdf.is_contiguous() or (idx is None and sdf.numel() < u0b.shape[0]):
@@ -563,15 +570,17 @@ def sdf_mlp(u0b, tail, Ws, biases, head_w, head_b, sdf, *, multires, skip_layer,
         raise RuntimeError("sdf_mlp: idx must be int32 with M entries")
     d.head_w, d.head_b, d.sdf, d.idx = head_w.data_ptr(), head_b.data_ptr(), sdf.data_ptr(), _ptr(idx)
     d.skip_div, d.beta, d.threshold = skip_div, beta, threshold
-    d.debug = _ptr(debug)  # tests: bf16 [8][M][256], every layer's input
+    d.debug = _ptr(debug)  # tests: [8][M][256] (bf16; fp32 in the bf16x6 mode), every layer's input
     if _timer is not None:
         e0 = _timer.start()
         _lib.check(_lib.load().cn_sdf_mlp(d, _stream()), "cn_sdf_mlp")
         M = u0b.shape[0]
-        ka = [W.shape[1] for W in Ws]
+        ka = [16 * W.shape[0] if x6 else W.shape[1] for W in Ws]
         fl = sum(2.0 * M * 256 * k for k in ka)
-        _timer.symbols[("sdf_mlp",)] = "cn::sdf_mlp_kernel(cn::SdfMlpArgs)"
-        _timer.stop(("sdf_mlp",), e0, fl, 2.0 * M * (64 + tail.shape[1]) + 4.0 * M)
+        key = ("sdf_mlp",) + (("x6",) if x6 else ())
+        _timer.symbols[key] = ("void cn::sdf_mlp_x6_kernel<false>(cn::SdfMlpX6Args)" if x6 else
+                               "cn::sdf_mlp_kernel(cn::SdfMlpArgs)")
+        _timer.stop(key, e0, fl, u0b.element_size() * M * (64 + tail.shape[1]) + 4.0 * M)
     else:
         _lib.check(_lib.load().cn_sdf_mlp(d, _stream()), "cn_sdf_mlp")
     return sdf

@@ -93,7 +93,8 @@ int net_shape(const cn_sdf_net* n, NetShape* s) {
                                     (s->bf && N <= 256 && n->w_rows[L8 - 1] >= 256));
     }
     // cn_sdf_mlp's shape (fields._fused_query_ok)
-    bool f = !(n->flags & CN_SDF_LAYERED) && s->img && n->n_lin == 9 && s->HL == 256 && s->KE == 64 &&
+    // (bf16 images, or the bf16x6 mode's fp32 inputs and term images: sdf_mlp_x6_kernel, ABI v15)
+    bool f = !(n->flags & CN_SDF_LAYERED) && (s->img || s->x6) && n->n_lin == 9 && s->HL == 256 && s->KE == 64 &&
              s->sk >= 2 && s->sk <= 7;
     if (f) f = s->E + n->out_dim[s->sk - 1] == 256 && n->in_dim[8] == 256;
     for (int l = 0; f && l < 8; ++l)
@@ -106,11 +107,13 @@ int sdf_query_plan(const cn_sdf_net* n, const NetShape& s, int M, const float* x
                    const int32_t* idx, Plan& ws, hipStream_t st, bool run) {
     const float kSqrt2 = (float)std::sqrt(2.0);
     if (s.fused) {
-        // cn_sdf_embed's bf16 images (lin0's input; the skip concat's tail / sqrt 2), then one cn_sdf_mlp
-        void* u0b = ws.take((size_t)M * 64 * 2);
-        void* tail = ws.take((size_t)M * 64 * 2);
+        // cn_sdf_embed's bf16 images (lin0's input; the skip concat's tail / sqrt 2) -- fp32 rows in the bf16x6
+        // mode -- then one cn_sdf_mlp
+        const size_t esz = s.x6 ? 4 : 2;
+        void* u0b = ws.take((size_t)M * 64 * esz);
+        void* tail = ws.take((size_t)M * 64 * esz);
         if (!run) return CN_OK;
-        int rc = cn_sdf_embed(M, x, ldx, n->multires, n->scale, 64, u0b, 64, tail, 64, kSqrt2, 3, st);
+        int rc = cn_sdf_embed(M, x, ldx, n->multires, n->scale, 64, u0b, 64, tail, 64, kSqrt2, s.x6 ? 0 : 3, st);
         if (rc) return rc;
         cn_sdf_mlp_desc d{};
         d.u0 = u0b;
@@ -125,9 +128,10 @@ int sdf_query_plan(const cn_sdf_net* n, const NetShape& s, int M, const float* x
         d.skip_layer = s.sk - 1;
         for (int l = 0; l < 8; ++l) {
             d.W[l] = n->W[l];
-            d.ldw[l] = n->w_cols[l];
+            d.ldw[l] = s.x6 ? n->w_rows[l] : n->w_cols[l];  // (a term image's leading dimension: its rows)
             d.bias[l] = n->bias[l];
         }
+        d.format = s.x6 ? CN_MFMA_F32_BF16X6 : 0;
         d.head_w = n->head_w;
         d.head_b = n->head_b;
         d.sdf = sdf;

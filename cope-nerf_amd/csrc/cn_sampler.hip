@@ -357,12 +357,377 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_kernel(SdfMlpArgs p) {
 }
 
 
+// ---------------------------------------------------------------------------------------------------------
+// The same query in the fp32-class bf16x6 mode (config C2's GEMMs: every fp32 operand three RNE bf16 terms,
+// the six products with i + j <= 2, fp32 accumulate; cn_gemm.hip MODE 2).  One persistent workgroup of
+// four waves per CU takes 128 samples at a time (wave w: samples 32 w + (lane & 31)) through lin0 .. lin7
+// and the sdf row:
+//
+//  * the activations stay in registers as fp32 in the B-operand order (lane half h: features 16 ks + 8 h
+//    .. + 7 of k-step ks; 128 VGPRs for 32 samples x 256 features) and are split into their three terms per
+//    k-step, beside the MFMAs (the layer path splits them while staging: the same split3, the same bits);
+//    after a layer's epilogue (bias, softplus) four v_permlane32_swap per 8 values reorder the accumulator
+//    layout into the next layer's operand order;
+//  * the weights stream through an LDS-DMA ring of one 16-deep k-step per slot: that k-step's chunk of the
+//    layer's chunk-major term image ([256 rows][3 terms][16], 24 KB, contiguous in HBM / L2), 6 slots,
+//    5 in flight across layer and block boundaries; four waves share every byte fetched;
+//  * products are issued per output block in the layer path's order (k-steps ascending; per k-step the
+//    term pairs (act, weight) = (0,0) (1,0) (0,1) (2,0) (1,1) (0,2)), operands swapped (outᵀ = W · actᵀ),
+//    so every activation is bitwise the layer path's (cn_linear on the 128x128 tile for lin0, the
+//    256x256 tiles after, SOFTPLUS_HEAD's row-dot order for the sdf).
+// Per sample: the embedding's fp32 rows in (lin0's input, 256 B; the skip tail, 4 E B), the sdf out.
+constexpr int kX6NS = 6;            // ring slots
+constexpr int kX6Chunk = 24576;     // bytes per slot: 256 rows x 3 terms x 16 k bf16
+constexpr int kX6StepsPerBlock = 4 + 7 * 16;  // k-steps of lin0 (K = 64) and lin1 .. lin7 (K = 256)
+
+struct SdfMlpX6Args {
+    const float* u0;                  // [M][ld_u0] fp32: the embedding, 64 columns (lin0's input)
+    const float* tail;                // [M][ld_t] fp32: the embedding / u4div (the skip layer's tail)
+    int ld_u0, ld_t, M, nblocks;
+    const bf16_t* W[kMlpLayers];      // chunk-major term images [K/16][256 rows][48]
+    const float* bias[kMlpLayers];
+    int nout[kMlpLayers];
+    float inv_odiv[kMlpLayers];
+    const float* head_w;              // [256] sdf row of lin8 / scale
+    const float* head_b;
+    float* sdf;
+    const int* idx;
+    int skip_layer;
+    float beta, threshold;
+    float* dbg;                       // (DBG) every layer's input, fp32 [8][M][256]
+};
+
+template <bool DBG>
+__global__ void __launch_bounds__(256, 1) sdf_mlp_x6_kernel(SdfMlpX6Args p) {
+    __shared__ __attribute__((aligned(16))) char smem[kX6NS * kX6Chunk + kMlpLayers * 256 * 4 + 256 * 4];
+    float* sBias = reinterpret_cast<float*>(smem + kX6NS * kX6Chunk);
+    float* sHead = sBias + kMlpLayers * 256;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int h = lane >> 5;
+    const int l31 = lane & 31;
+
+    for (int i = tid; i < kMlpLayers * 256; i += 256) {
+        const int l = i >> 8, n = i & 255;
+        sBias[i] = n < p.nout[l] ? p.bias[l][n] : 0.0f;
+    }
+    sHead[tid] = p.head_w[tid];
+    __syncthreads();
+
+    const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem);
+    const uint32_t ldsBias = lds0 + kX6NS * kX6Chunk;
+    const uint32_t ldsHead = ldsBias + kMlpLayers * 256 * 4;
+
+    // k-step g of the workgroup's stream: step g % 116 of a sample block -> (layer, chunk)
+    auto step_of = [](int sb, int& l, int& c) __attribute__((always_inline)) {
+        if (sb < 4) {
+            l = 0;
+            c = sb;
+        } else {
+            l = 1 + ((sb - 4) >> 4);
+            c = (sb - 4) & 15;
+        }
+    };
+    // wave w copies bytes 6 KB w .. + 6 KB of the slot: six 1 KB pieces, lane l -> 16 bytes at 16 l (the LDS
+    // image is the chunk as it lies in the term image: row r at 96 r, term t at + 32 t, k half h at + 16 h)
+    auto issue = [&](int g) __attribute__((always_inline)) {
+        int l, c;
+        step_of(g % kX6StepsPerBlock, l, c);
+        const rsrc_t v = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.W[l]) + (int64_t)c * 256 * 48, 0,
+                                                           kX6Chunk, 0x00020000);
+        char* dst = smem + (g % kX6NS) * kX6Chunk + wave * 6144;
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(v, (__attribute__((address_space(3))) void*)(dst + j * 1024), 16,
+                                                     lane * 16, wave * 6144 + j * 1024, 0, 0);
+    };
+    // weight (A operand) reads: lane l -> row (l & 31) of 32-row block ib, term t, k half h
+    const uint32_t aoff = l31 * 96 + 16 * h;
+
+    const float c_exp = p.beta * 1.44269504088896341f;
+    const float c_thr = p.threshold * 1.44269504088896341f;
+    const float c_log = 0.693147180559945309f / p.beta;
+
+    const rsrc_t vu = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.u0), 0, p.M * p.ld_u0 * 4, 0x00020000);
+    const rsrc_t vt = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.tail), 0, p.M * p.ld_t * 4, 0x00020000);
+    const rsrc_t vi = __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(p.idx), 0, p.idx ? p.M * 4 : 0, 0x00020000);
+    int isd = 0;
+
+    int blk = blockIdx.x;
+    if (blk >= p.nblocks) return;
+    int g = 0;
+#pragma unroll
+    for (int d = 0; d < kX6NS - 1; ++d) issue(d);
+
+    floatx4 act[16][2];  // the current layer's input: k-step ks, lane half h: features 16 ks + 8 h + 4 e + (0..3)
+    floatx16 acc[8];
+    auto dump = [&](int l, int nks) __attribute__((always_inline)) {
+        if constexpr (DBG) {
+            const int m = blk * 128 + wave * 32 + l31;
+            if (m < p.M)
+#pragma unroll
+                for (int ks = 0; ks < 16; ++ks)
+                    if (ks < nks)
+#pragma unroll
+                        for (int e = 0; e < 2; ++e)
+                            *reinterpret_cast<floatx4*>(p.dbg + ((int64_t)l * p.M + m) * 256 + 16 * ks + 8 * h + 4 * e) =
+                                act[ks][e];
+        }
+    };
+    // one 16-deep k-step (stream position g) of the layer: the activations' terms, then per output block
+    // the six products in the layer path's order
+    auto kstep = [&](auto ks_c) __attribute__((always_inline)) {
+        constexpr int ks = decltype(ks_c)::value;
+        wait_vmcnt<6 * (kX6NS - 2)>();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        issue(g + kX6NS - 1);
+        const uint32_t sb = lds0 + (g % kX6NS) * kX6Chunk + aoff;
+        // weight terms 0 and 1 of the eight blocks (the first five products), term 2 after them
+        bf16x8 w0[8], w1[8], w2[8];
+#pragma unroll
+        for (int ib = 0; ib < 8; ++ib) w0[ib] = __builtin_bit_cast(bf16x8, lds_read_b128<0>(sb + ib * 32 * 96));
+#pragma unroll
+        for (int ib = 0; ib < 8; ++ib) w1[ib] = __builtin_bit_cast(bf16x8, lds_read_b128<32>(sb + ib * 32 * 96));
+        bf16x4 a0[2], a1[2], a2[2];
+        split3(act[ks][0], a0[0], a1[0], a2[0]);
+        split3(act[ks][1], a0[1], a1[1], a2[1]);
+        const bf16x8 b0 = __builtin_shufflevector(a0[0], a0[1], 0, 1, 2, 3, 4, 5, 6, 7);
+        const bf16x8 b1 = __builtin_shufflevector(a1[0], a1[1], 0, 1, 2, 3, 4, 5, 6, 7);
+        const bf16x8 b2 = __builtin_shufflevector(a2[0], a2[1], 0, 1, 2, 3, 4, 5, 6, 7);
+        asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(w0[0]), "+v"(w0[1]), "+v"(w0[2]), "+v"(w0[3]), "+v"(w0[4]),
+                     "+v"(w0[5]), "+v"(w0[6]), "+v"(w0[7]));
+        // (act term, weight term) = (0,0), (1,0) on every block
+#pragma unroll
+        for (int ib = 0; ib < 8; ++ib) acc[ib] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0[ib], b0, acc[ib], 0, 0, 0);
+#pragma unroll
+        for (int ib = 0; ib < 8; ++ib) acc[ib] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0[ib], b1, acc[ib], 0, 0, 0);
+#pragma unroll
+        for (int ib = 0; ib < 8; ++ib) w2[ib] = __builtin_bit_cast(bf16x8, lds_read_b128<64>(sb + ib * 32 * 96));
+        asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(w1[0]), "+v"(w1[1]), "+v"(w1[2]), "+v"(w1[3]), "+v"(w1[4]),
+                     "+v"(w1[5]), "+v"(w1[6]), "+v"(w1[7]));
+        // (0,1), (2,0), (1,1)
+#pragma unroll
+        for (int ib = 0; ib < 8; ++ib) acc[ib] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1[ib], b0, acc[ib], 0, 0, 0);
+#pragma unroll
+        for (int ib = 0; ib < 8; ++ib) acc[ib] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0[ib], b2, acc[ib], 0, 0, 0);
+#pragma unroll
+        for (int ib = 0; ib < 8; ++ib) acc[ib] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1[ib], b1, acc[ib], 0, 0, 0);
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w2[0]), "+v"(w2[1]), "+v"(w2[2]), "+v"(w2[3]), "+v"(w2[4]),
+                     "+v"(w2[5]), "+v"(w2[6]), "+v"(w2[7]));
+        // (0,2)
+#pragma unroll
+        for (int ib = 0; ib < 8; ++ib) acc[ib] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2[ib], b0, acc[ib], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        ++g;
+    };
+    auto zero_acc = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int ib = 0; ib < 8; ++ib)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[ib][r] = 0.0f;
+    };
+    auto read4 = [&](uint32_t base, auto ib_c, floatx4* v) __attribute__((always_inline)) {
+        constexpr int ib = decltype(ib_c)::value;
+        const uint32_t a = base + 16 * h;
+        v[0] = __builtin_bit_cast(floatx4, lds_read_b128<(32 * ib + 0) * 4>(a));
+        v[1] = __builtin_bit_cast(floatx4, lds_read_b128<(32 * ib + 8) * 4>(a));
+        v[2] = __builtin_bit_cast(floatx4, lds_read_b128<(32 * ib + 16) * 4>(a));
+        v[3] = __builtin_bit_cast(floatx4, lds_read_b128<(32 * ib + 24) * 4>(a));
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+    };
+    // feature n = 32 ib + 8 (r >> 2) + 4 h + (r & 3): softplus(acc + bias) / odiv, as cn_linear's epilogue
+    auto values = [&](auto ib_c, int l, const floatx4* bb, float* o) __attribute__((always_inline)) {
+        constexpr int ib = decltype(ib_c)::value;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[r] = softplus_hw(acc[ib][r] + bb[r >> 2][r & 3], c_exp, c_thr, c_log);
+        if (l == p.skip_layer) {
+            const float inv_odiv = p.inv_odiv[l];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[r] *= inv_odiv;
+        }
+    };
+    // a hidden layer's activations in the next layer's operand order: k-steps 2 ib (r < 8) and 2 ib + 1;
+    // lane half 0 keeps its rows r .. r + 3 and takes the other half's, half 1 the reverse with r + 4 .. r + 7
+    auto epi_act = [&](int l) __attribute__((always_inline)) {
+        static_for<8>([&](auto ib_c) {
+            constexpr int ib = decltype(ib_c)::value;
+            floatx4 bb[4];
+            read4(ldsBias + l * 1024, ib_c, bb);
+            float o[16];
+            values(ib_c, l, bb, o);
+#pragma unroll
+            for (int hs = 0; hs < 2; ++hs) {
+                float lo[4], hi[4];
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const auto sw = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, o[8 * hs + d]),
+                                                                     __builtin_bit_cast(unsigned, o[8 * hs + 4 + d]),
+                                                                     false, false);
+                    lo[d] = __builtin_bit_cast(float, (unsigned)sw[0]);
+                    hi[d] = __builtin_bit_cast(float, (unsigned)sw[1]);
+                }
+                act[2 * ib + hs][0] = floatx4{lo[0], lo[1], lo[2], lo[3]};
+                act[2 * ib + hs][1] = floatx4{hi[0], hi[1], hi[2], hi[3]};
+            }
+        });
+    };
+    // the skip layer: features n >= nout are the tail's fp32 values (emb / skip_div as cn_sdf_embed writes
+    // them), k-steps 12 .. 15 (nout >= 192)
+    auto fix_tail = [&](int l) __attribute__((always_inline)) {
+        const int nout = p.nout[l];
+        const int m = blk * 128 + wave * 32 + l31;
+        float t[4][8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int c = 16 * (12 + k) + 8 * h + j - nout;
+                t[k][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vt, (m * p.ld_t + max(c, 0)) * 4, 0, 0));
+            }
+        wait_vmcnt<0>();  // (a drain, once per block: the ring's chunks in flight land too)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                floatx4 v = act[12 + k][e];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = 16 * (12 + k) + 8 * h + 4 * e + q >= nout ? t[k][4 * e + q] : v[q];
+                act[12 + k][e] = v;
+            }
+    };
+    // the head: cn_linear SOFTPLUS_HEAD's row-dot order on the 64x128 wave tiles (cn_sdf_mlp's epi_head)
+    auto epi_head = [&]() __attribute__((always_inline)) {
+        constexpr int l = kMlpLayers - 1;
+        const float hb = p.head_b[0];
+        float part[2][16];
+        static_for<8>([&](auto ib_c) {
+            constexpr int ib = decltype(ib_c)::value;
+            floatx4 bb[4], hw[4];
+            read4(ldsBias + l * 1024, ib_c, bb);
+            read4(ldsHead, ib_c, hw);
+            float o[16];
+            values(ib_c, l, bb, o);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float x = o[r] * hw[r >> 2][r & 3];
+                part[ib >> 2][r] = (ib & 3) == 0 ? 0.0f + x : part[ib >> 2][r] + x;
+            }
+        });
+        float sw2[2];
+#pragma unroll
+        for (int wn = 0; wn < 2; ++wn) {
+            float t1[8], t2[4], t3[4];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) t1[r] = part[wn][r] + part[wn][r ^ 8];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) t2[r] = t1[r] + t1[r ^ 4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const unsigned u = __builtin_bit_cast(unsigned, t2[r]);
+                const auto sw = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+                t3[r] = __builtin_bit_cast(float, (unsigned)sw[0]) + __builtin_bit_cast(float, (unsigned)sw[1]);
+            }
+            const float t4a = t3[0] + t3[2], t4b = t3[1] + t3[3];
+            sw2[wn] = t4a + t4b;
+        }
+        const int row = blk * 128 + wave * 32 + l31;
+        if (h == 0 && row < p.M) p.sdf[p.idx ? isd : row] = (sw2[0] + sw2[1]) + hb;
+    };
+
+    for (; blk < p.nblocks; blk += gridDim.x) {
+        {
+            const int m = blk * 128 + wave * 32 + l31;
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+                for (int e = 0; e < 2; ++e)
+                    act[ks][e] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                 vu, (m * p.ld_u0 + 16 * ks + 8 * h + 4 * e) * 4, 0, 0));
+            isd = __builtin_amdgcn_raw_buffer_load_b32(vi, m * 4, 0, 0);
+        }
+        wait_vmcnt<0>();
+        dump(0, 4);
+        zero_acc();
+        static_for<4>(kstep);
+        epi_act(0);
+        dump(1, 16);
+        for (int l = 1; l < kMlpLayers - 1; ++l) {
+            zero_acc();
+            static_for<16>(kstep);
+            epi_act(l);
+            if (l == p.skip_layer) fix_tail(l);
+            dump(l + 1, 16);
+        }
+        zero_acc();
+        static_for<16>(kstep);
+        epi_head();
+    }
+    wait_vmcnt<0>();
+}
+
+
 }  // namespace cn
 
 using namespace cn;
 
+static int sdf_mlp_x6(const cn_sdf_mlp_desc* d, cn_stream_t stream) {
+    const int E = 4 * (1 + 2 * d->multires);
+    CN_REQUIRE(d->ld_u0 >= 64 && d->ld_u0 % 4 == 0 && al16(d->u0) && d->ld_t >= E && ((uintptr_t)d->tail & 3) == 0,
+               CN_ERR_ALIGN, "cn_sdf_mlp (bf16x6): u0 fp32 [M][64] (ld %% 4, 16-byte aligned) / tail fp32 [M][E]");
+    CN_REQUIRE((int64_t)d->M * (d->ld_u0 > d->ld_t ? d->ld_u0 : d->ld_t) * 4 < ((int64_t)1 << 31), CN_ERR_SHAPE,
+               "cn_sdf_mlp: M = %d too large for one launch", d->M);
+    SdfMlpX6Args a{};
+    for (int l = 0; l < kMlpLayers; ++l) {
+        CN_REQUIRE(d->W[l] && d->bias[l] && d->ldw[l] == 256 && al16(d->W[l]), CN_ERR_ARG,
+                   "cn_sdf_mlp (bf16x6): layer %d needs a chunk-major term image of 256 rows (ldw %lld)", l,
+                   (long long)d->ldw[l]);
+        a.W[l] = static_cast<const bf16_t*>(d->W[l]);
+        a.bias[l] = d->bias[l];
+        a.nout[l] = l == d->skip_layer ? 256 - E : 256;
+        a.inv_odiv[l] = l == d->skip_layer ? 1.0f / d->skip_div : 1.0f;
+    }
+    a.u0 = static_cast<const float*>(d->u0);
+    a.tail = static_cast<const float*>(d->tail);
+    a.ld_u0 = (int)d->ld_u0;
+    a.ld_t = (int)d->ld_t;
+    a.M = d->M;
+    a.nblocks = (d->M + 127) / 128;
+    a.head_w = d->head_w;
+    a.head_b = d->head_b;
+    a.sdf = d->sdf;
+    a.idx = d->idx;
+    a.skip_layer = d->skip_layer;
+    a.beta = d->beta;
+    a.threshold = d->threshold;
+    if (d->M == 0) return CN_OK;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    const int grid = a.nblocks < cus ? a.nblocks : cus;
+    a.dbg = static_cast<float*>(d->debug);
+    if (a.dbg)
+        sdf_mlp_x6_kernel<true><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+    else
+        sdf_mlp_x6_kernel<false><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+    return check_launch("cn_sdf_mlp");
+}
+
 extern "C" int cn_sdf_mlp(const cn_sdf_mlp_desc* d, cn_stream_t stream) {
     CN_REQUIRE(d && d->u0 && d->tail && d->sdf && d->head_w && d->head_b, CN_ERR_ARG, "cn_sdf_mlp: null pointer");
+    CN_REQUIRE(d->format == 0 || d->format == CN_MFMA_F32_BF16X6, CN_ERR_UNSUPPORTED,
+               "cn_sdf_mlp: format %d (0: bf16 images, CN_MFMA_F32_BF16X6: fp32 inputs and term images)", d->format);
+    if (d->format == CN_MFMA_F32_BF16X6) {
+        CN_REQUIRE(d->n_layers == kMlpLayers && d->hidden == 256 && d->kpad0 == 64, CN_ERR_UNSUPPORTED,
+                   "cn_sdf_mlp: %d layers of width %d (first K %d); the fused query takes 8 x 256 (K0 = 64)",
+                   d->n_layers, d->hidden, d->kpad0);
+        CN_REQUIRE(d->multires >= 0 && 4 * (1 + 2 * d->multires) <= 64 && d->skip_layer >= 1 &&
+                       d->skip_layer < kMlpLayers - 1 && 256 - 4 * (1 + 2 * d->multires) >= 192,
+                   CN_ERR_UNSUPPORTED, "cn_sdf_mlp: multires %d / skip layer %d", d->multires, d->skip_layer);
+        CN_REQUIRE(d->M >= 0, CN_ERR_SHAPE, "cn_sdf_mlp: M = %d", d->M);
+        return sdf_mlp_x6(d, stream);
+    }
     CN_REQUIRE(d->n_layers == kMlpLayers && d->hidden == 256 && d->kpad0 == 64, CN_ERR_UNSUPPORTED,
                "cn_sdf_mlp: %d layers of width %d (first K %d); the fused query takes 8 x 256 (K0 = 64)",
                d->n_layers, d->hidden, d->kpad0);

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define CN_ABI_VERSION 14
+#define CN_ABI_VERSION 15
 
 typedef void* cn_stream_t; /* hipStream_t */
 
@@ -535,7 +535,10 @@ typedef struct cn_sdf_mlp_desc {
     float* sdf;
     const int32_t* idx;
     float skip_div, beta, threshold;
-    void* debug; /* NULL, or bf16 [8][M][256]: every layer's input as the kernel holds it (tests) */
+    void* debug; /* NULL, or [8][M][256] (bf16; fp32 in the bf16x6 format): every layer's input as the kernel holds it (tests) */
+    int32_t format; /* 0: the bf16 mode (u0 / tail bf16 images, W bf16 [256][K]); CN_MFMA_F32_BF16X6 (ABI v15): the
+                       fp32-class mode -- u0 / tail fp32, W the chunk-major term images [K/16][256][48] of
+                       cn_pack_weights (ldw = 256, their rows), bitwise the layer-by-layer bf16x6 query */
 } cn_sdf_mlp_desc;
 int cn_sdf_mlp(const cn_sdf_mlp_desc* d, cn_stream_t stream);
 
