@@ -954,7 +954,9 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 vsj[j] = (lrow * p.ld_split + lcol + 32 * j) * 4;
                 keep[j] = live[j] && !spl[j] ? ~0u : 0u;
             }
-            constexpr int RG = kAux1 ? 2 : 4;          // accumulator rows r per group (even: bf16 pairs)
+            // accumulator rows r per group (even: bf16 pairs; one row for the three aux streams of the bf16x6
+            // BWD_SOFTPLUS, whose registers the next tile's staging sets share)
+            constexpr int RG = kAux1 ? (MODE == 1 ? 2 : 1) : 4;
             constexpr int NGD = TM * 16 / RG;          // groups per tile
             constexpr int ASTEP = AUX0B ? 64 : 128;    // bytes per 32-column block of aux0
             constexpr int XSTEP = AUX12B ? 64 : 128;   // ... of aux1 / aux2

@@ -457,7 +457,7 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_x6_kernel(SdfMlpX6Args p) {
     if (blk >= p.nblocks) return;
     int g = 0;
 #pragma unroll
-    for (int d = 0; d < kX6NS - 1; ++d) issue(d);
+    for (int d = 0; d < kX6NS - 2; ++d) issue(d);
 
     floatx4 act[16][2];  // the current layer's input: k-step ks, lane half h: features 16 ks + 8 h + 4 e + (0..3)
     floatx16 acc[8];
@@ -476,20 +476,35 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_x6_kernel(SdfMlpX6Args p) {
     };
     // one 16-deep k-step (stream position g) of the layer: the activations' terms, then per output block
     // the six products in the layer path's order
-    auto kstep = [&](auto ks_c) __attribute__((always_inline)) {
-        constexpr int ks = decltype(ks_c)::value;
-        wait_vmcnt<6 * (kX6NS - 2)>();
+    // weight terms 0 and 1 of the current k-step's eight blocks: read at the end of the previous k-step (its
+    // last products then run beside those reads), term 2 mid-step
+    bf16x8 w0[8], w1[8];
+    auto read_w = [&](int gg, auto t_c) __attribute__((always_inline)) {
+        constexpr int t = decltype(t_c)::value;
+        const uint32_t sb = lds0 + (gg % kX6NS) * kX6Chunk + aoff;
+#pragma unroll
+        for (int ib = 0; ib < 8; ++ib) {
+            const bf16x8 v = __builtin_bit_cast(bf16x8, lds_read_b128<32 * t>(sb + ib * 32 * 96));
+            if constexpr (t == 0) w0[ib] = v;
+            else w1[ib] = v;
+        }
+    };
+    // k-step g's chunk certified landed by every wave (this wave's pieces: the NS - 3 later chunks may fly;
+    // the barrier: every wave's, and every wave done reading chunk g - 2's slot, which the DMA issued here
+    // refills with chunk g + NS - 2)
+    auto land = [&](int gg) __attribute__((always_inline)) {
+        wait_vmcnt<6 * (kX6NS - 3)>();
         asm volatile("" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        issue(g + kX6NS - 1);
+        issue(gg + kX6NS - 2);
+    };
+    // one 16-deep k-step (stream position g) of the layer: the activations' terms, then per output block the
+    // six products in the layer path's order; chunk g + 1 is certified and its terms 0, 1 read before the
+    // sixth product
+    auto kstep = [&](auto ks_c) __attribute__((always_inline)) {
+        constexpr int ks = decltype(ks_c)::value;
         const uint32_t sb = lds0 + (g % kX6NS) * kX6Chunk + aoff;
-        // weight terms 0 and 1 of the eight blocks (the first five products), term 2 after them
-        bf16x8 w0[8], w1[8], w2[8];
-#pragma unroll
-        for (int ib = 0; ib < 8; ++ib) w0[ib] = __builtin_bit_cast(bf16x8, lds_read_b128<0>(sb + ib * 32 * 96));
-#pragma unroll
-        for (int ib = 0; ib < 8; ++ib) w1[ib] = __builtin_bit_cast(bf16x8, lds_read_b128<32>(sb + ib * 32 * 96));
         bf16x4 a0[2], a1[2], a2[2];
         split3(act[ks][0], a0[0], a1[0], a2[0]);
         split3(act[ks][1], a0[1], a1[1], a2[1]);
@@ -503,6 +518,7 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_x6_kernel(SdfMlpX6Args p) {
         for (int ib = 0; ib < 8; ++ib) acc[ib] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0[ib], b0, acc[ib], 0, 0, 0);
 #pragma unroll
         for (int ib = 0; ib < 8; ++ib) acc[ib] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0[ib], b1, acc[ib], 0, 0, 0);
+        bf16x8 w2[8];
 #pragma unroll
         for (int ib = 0; ib < 8; ++ib) w2[ib] = __builtin_bit_cast(bf16x8, lds_read_b128<64>(sb + ib * 32 * 96));
         asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(w1[0]), "+v"(w1[1]), "+v"(w1[2]), "+v"(w1[3]), "+v"(w1[4]),
@@ -514,11 +530,15 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_x6_kernel(SdfMlpX6Args p) {
         for (int ib = 0; ib < 8; ++ib) acc[ib] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0[ib], b2, acc[ib], 0, 0, 0);
 #pragma unroll
         for (int ib = 0; ib < 8; ++ib) acc[ib] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1[ib], b1, acc[ib], 0, 0, 0);
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w2[0]), "+v"(w2[1]), "+v"(w2[2]), "+v"(w2[3]), "+v"(w2[4]),
+        __builtin_amdgcn_sched_barrier(0);
+        land(g + 1);
+        read_w(g + 1, std::integral_constant<int, 0>{});
+        asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(w2[0]), "+v"(w2[1]), "+v"(w2[2]), "+v"(w2[3]), "+v"(w2[4]),
                      "+v"(w2[5]), "+v"(w2[6]), "+v"(w2[7]));
-        // (0,2)
+        // (0,2), beside the next chunk's term-1 reads
 #pragma unroll
         for (int ib = 0; ib < 8; ++ib) acc[ib] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2[ib], b0, acc[ib], 0, 0, 0);
+        read_w(g + 1, std::integral_constant<int, 1>{});
         __builtin_amdgcn_sched_barrier(0);
         ++g;
     };
@@ -636,6 +656,9 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_x6_kernel(SdfMlpX6Args p) {
         if (h == 0 && row < p.M) p.sdf[p.idx ? isd : row] = (sw2[0] + sw2[1]) + hb;
     };
 
+    land(0);
+    read_w(0, std::integral_constant<int, 0>{});
+    read_w(0, std::integral_constant<int, 1>{});
     for (; blk < p.nblocks; blk += gridDim.x) {
         {
             const int m = blk * 128 + wave * 32 + l31;
