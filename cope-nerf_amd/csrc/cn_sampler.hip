@@ -656,9 +656,19 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_x6_kernel(SdfMlpX6Args p) {
         if (h == 0 && row < p.M) p.sdf[p.idx ? isd : row] = (sw2[0] + sw2[1]) + hb;
     };
 
+    // the prefetched fragments complete (and become values the compiler may move) before any control-flow
+    // merge: a layer's end, the layer and block loops' back edges (a register copy the compiler inserts there
+    // would copy a read still in flight)
+    auto settle_w = [&]() __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w0[0]), "+v"(w0[1]), "+v"(w0[2]), "+v"(w0[3]), "+v"(w0[4]),
+                     "+v"(w0[5]), "+v"(w0[6]), "+v"(w0[7]));
+        asm volatile("" : "+v"(w1[0]), "+v"(w1[1]), "+v"(w1[2]), "+v"(w1[3]), "+v"(w1[4]), "+v"(w1[5]), "+v"(w1[6]),
+                     "+v"(w1[7]));
+    };
     land(0);
     read_w(0, std::integral_constant<int, 0>{});
     read_w(0, std::integral_constant<int, 1>{});
+    settle_w();
     for (; blk < p.nblocks; blk += gridDim.x) {
         {
             const int m = blk * 128 + wave * 32 + l31;
@@ -674,17 +684,20 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_x6_kernel(SdfMlpX6Args p) {
         dump(0, 4);
         zero_acc();
         static_for<4>(kstep);
+        settle_w();
         epi_act(0);
         dump(1, 16);
         for (int l = 1; l < kMlpLayers - 1; ++l) {
             zero_acc();
             static_for<16>(kstep);
+            settle_w();
             epi_act(l);
             if (l == p.skip_layer) fix_tail(l);
             dump(l + 1, 16);
         }
         zero_acc();
         static_for<16>(kstep);
+        settle_w();
         epi_head();
     }
     wait_vmcnt<0>();
