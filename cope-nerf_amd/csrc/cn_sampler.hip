@@ -376,6 +376,9 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_kernel(SdfMlpArgs p) {
 //    so every activation is bitwise the layer path's (cn_linear on the 128x128 tile for lin0, the
 //    256x256 tiles after, SOFTPLUS_HEAD's row-dot order for the sdf).
 // Per sample: the embedding's fp32 rows in (lin0's input, 256 B; the skip tail, 4 E B), the sdf out.
+#ifndef CN_X6Q_SPLIT_AHEAD
+#define CN_X6Q_SPLIT_AHEAD 1
+#endif
 constexpr int kX6NS = 6;            // ring slots
 constexpr int kX6Chunk = 24576;     // bytes per slot: 256 rows x 3 terms x 16 k bf16
 constexpr int kX6StepsPerBlock = 4 + 7 * 16;  // k-steps of lin0 (K = 64) and lin1 .. lin7 (K = 256)
@@ -418,6 +421,17 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_x6_kernel(SdfMlpX6Args p) {
     const uint32_t ldsBias = lds0 + kX6NS * kX6Chunk;
     const uint32_t ldsHead = ldsBias + kMlpLayers * 256 * 4;
 
+    // The slot's rows are 96 bytes (24 dwords): rows r and r + 8 would start on the same bank quad, a two-way
+    // conflict in every ds_read_b128 lane group.  So the six 16-byte pieces of a row with (r >> 3) odd are
+    // rotated by one place (its data starts 4 banks over): the fragment reads are conflict-free.  The DMA
+    // writes LDS linearly, so the rotation is in each lane's source offset: physical piece pp of the slot
+    // (= 384 w + 64 j + lane) holds logical piece (pp % 6 - rot(pp / 6)) mod 6 of row pp / 6.
+    int dvo[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const int pp = wave * 384 + j * 64 + lane, row = pp / 6;
+        dvo[j] = row * 96 + ((pp % 6 + 6 - ((row >> 3) & 1)) % 6) * 16;
+    }
     // k-step g of the workgroup's stream: step g % 116 of a sample block -> (layer, chunk)
     auto step_of = [](int sb, int& l, int& c) __attribute__((always_inline)) {
         if (sb < 4) {
@@ -439,10 +453,13 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_x6_kernel(SdfMlpX6Args p) {
 #pragma unroll
         for (int j = 0; j < 6; ++j)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(v, (__attribute__((address_space(3))) void*)(dst + j * 1024), 16,
-                                                     lane * 16, wave * 6144 + j * 1024, 0, 0);
+                                                     dvo[j], 0, 0, 0);
     };
-    // weight (A operand) reads: lane l -> row (l & 31) of 32-row block ib, term t, k half h
-    const uint32_t aoff = l31 * 96 + 16 * h;
+    // weight (A operand) reads: lane l -> row (l & 31) of 32-row block ib (32 rows keep the rotation), term t,
+    // k half h: logical piece 2 t + h
+    uint32_t aoff[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) aoff[t] = l31 * 96 + ((2 * t + h + ((l31 >> 3) & 1)) % 6) * 16;
 
     const float c_exp = p.beta * 1.44269504088896341f;
     const float c_thr = p.threshold * 1.44269504088896341f;
@@ -481,13 +498,13 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_x6_kernel(SdfMlpX6Args p) {
     bf16x8 w0[8], w1[8];
     auto read_w = [&](int gg, auto t_c) __attribute__((always_inline)) {
         constexpr int t = decltype(t_c)::value;
-        const uint32_t sb = lds0 + (gg % kX6NS) * kX6Chunk + aoff;
-#pragma unroll
-        for (int ib = 0; ib < 8; ++ib) {
-            const bf16x8 v = __builtin_bit_cast(bf16x8, lds_read_b128<32 * t>(sb + ib * 32 * 96));
+        const uint32_t sb = lds0 + (gg % kX6NS) * kX6Chunk + aoff[t];
+        static_for<8>([&](auto ib_c) {
+            constexpr int ib = decltype(ib_c)::value;
+            const bf16x8 v = __builtin_bit_cast(bf16x8, lds_read_b128<ib * 32 * 96>(sb));
             if constexpr (t == 0) w0[ib] = v;
             else w1[ib] = v;
-        }
+        });
     };
     // k-step g's chunk certified landed by every wave (this wave's pieces: the NS - 3 later chunks may fly;
     // the barrier: every wave's, and every wave done reading chunk g - 2's slot, which the DMA issued here
@@ -502,15 +519,27 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_x6_kernel(SdfMlpX6Args p) {
     // one 16-deep k-step (stream position g) of the layer: the activations' terms, then per output block the
     // six products in the layer path's order; chunk g + 1 is certified and its terms 0, 1 read before the
     // sixth product
-    auto kstep = [&](auto ks_c) __attribute__((always_inline)) {
-        constexpr int ks = decltype(ks_c)::value;
-        const uint32_t sb = lds0 + (g % kX6NS) * kX6Chunk + aoff;
+    // the three terms of k-step ks's activations (the layer path splits them while staging: the same split3)
+    auto split_act = [&](int ks, bf16x8& b0, bf16x8& b1, bf16x8& b2) __attribute__((always_inline)) {
         bf16x4 a0[2], a1[2], a2[2];
         split3(act[ks][0], a0[0], a1[0], a2[0]);
         split3(act[ks][1], a0[1], a1[1], a2[1]);
-        const bf16x8 b0 = __builtin_shufflevector(a0[0], a0[1], 0, 1, 2, 3, 4, 5, 6, 7);
-        const bf16x8 b1 = __builtin_shufflevector(a1[0], a1[1], 0, 1, 2, 3, 4, 5, 6, 7);
-        const bf16x8 b2 = __builtin_shufflevector(a2[0], a2[1], 0, 1, 2, 3, 4, 5, 6, 7);
+        b0 = __builtin_shufflevector(a0[0], a0[1], 0, 1, 2, 3, 4, 5, 6, 7);
+        b1 = __builtin_shufflevector(a1[0], a1[1], 0, 1, 2, 3, 4, 5, 6, 7);
+        b2 = __builtin_shufflevector(a2[0], a2[1], 0, 1, 2, 3, 4, 5, 6, 7);
+    };
+    bf16x8 nb0, nb1, nb2;  // (CN_X6Q_SPLIT_AHEAD) the next k-step's terms, split beside this step's products
+    auto kstep_n = [&](auto ks_c, auto nks_c) __attribute__((always_inline)) {
+        constexpr int ks = decltype(ks_c)::value, NKS = decltype(nks_c)::value;
+        const uint32_t sb = lds0 + (g % kX6NS) * kX6Chunk + aoff[2];
+        bf16x8 b0, b1, b2;
+        if (CN_X6Q_SPLIT_AHEAD && ks > 0) {
+            b0 = nb0;
+            b1 = nb1;
+            b2 = nb2;
+        } else {
+            split_act(ks, b0, b1, b2);
+        }
         asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(w0[0]), "+v"(w0[1]), "+v"(w0[2]), "+v"(w0[3]), "+v"(w0[4]),
                      "+v"(w0[5]), "+v"(w0[6]), "+v"(w0[7]));
         // (act term, weight term) = (0,0), (1,0) on every block
@@ -518,9 +547,12 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_x6_kernel(SdfMlpX6Args p) {
         for (int ib = 0; ib < 8; ++ib) acc[ib] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0[ib], b0, acc[ib], 0, 0, 0);
 #pragma unroll
         for (int ib = 0; ib < 8; ++ib) acc[ib] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0[ib], b1, acc[ib], 0, 0, 0);
+        if constexpr (CN_X6Q_SPLIT_AHEAD && ks + 1 < NKS) split_act(ks + 1, nb0, nb1, nb2);
         bf16x8 w2[8];
-#pragma unroll
-        for (int ib = 0; ib < 8; ++ib) w2[ib] = __builtin_bit_cast(bf16x8, lds_read_b128<64>(sb + ib * 32 * 96));
+        static_for<8>([&](auto ib_c) {
+            constexpr int ib = decltype(ib_c)::value;
+            w2[ib] = __builtin_bit_cast(bf16x8, lds_read_b128<ib * 32 * 96>(sb));
+        });
         asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(w1[0]), "+v"(w1[1]), "+v"(w1[2]), "+v"(w1[3]), "+v"(w1[4]),
                      "+v"(w1[5]), "+v"(w1[6]), "+v"(w1[7]));
         // (0,1), (2,0), (1,1)
@@ -542,6 +574,8 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_x6_kernel(SdfMlpX6Args p) {
         __builtin_amdgcn_sched_barrier(0);
         ++g;
     };
+    auto kstep4 = [&](auto ks_c) __attribute__((always_inline)) { kstep_n(ks_c, std::integral_constant<int, 4>{}); };
+    auto kstep = [&](auto ks_c) __attribute__((always_inline)) { kstep_n(ks_c, std::integral_constant<int, 16>{}); };
     auto zero_acc = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int ib = 0; ib < 8; ++ib)
@@ -683,7 +717,7 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_x6_kernel(SdfMlpX6Args p) {
         wait_vmcnt<0>();
         dump(0, 4);
         zero_acc();
-        static_for<4>(kstep);
+        static_for<4>(kstep4);
         settle_w();
         epi_act(0);
         dump(1, 16);
