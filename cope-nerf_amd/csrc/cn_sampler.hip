@@ -376,10 +376,16 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_kernel(SdfMlpArgs p) {
 //    so every activation is bitwise the layer path's (cn_linear on the 128x128 tile for lin0, the
 //    256x256 tiles after, SOFTPLUS_HEAD's row-dot order for the sdf).
 // Per sample: the embedding's fp32 rows in (lin0's input, 256 B; the skip tail, 4 E B), the sdf out.
+#ifndef CN_X6Q_EXP
+#define CN_X6Q_EXP 0  // measurement builds: 1 no weight stream, 2 no softplus in the epilogue
+#endif
 #ifndef CN_X6Q_SPLIT_AHEAD
 #define CN_X6Q_SPLIT_AHEAD 1
 #endif
-constexpr int kX6NS = 6;            // ring slots
+#ifndef CN_X6Q_DMA
+#define CN_X6Q_DMA 0  // 1: the weight chunks by LDS-DMA (measured slower: each 1 KB piece costs ~125 issue cycles)
+#endif
+constexpr int kX6NS = CN_X6Q_DMA ? 6 : 3;  // ring slots
 constexpr int kX6Chunk = 24576;     // bytes per slot: 256 rows x 3 terms x 16 k bf16
 constexpr int kX6StepsPerBlock = 4 + 7 * 16;  // k-steps of lin0 (K = 64) and lin1 .. lin7 (K = 256)
 
@@ -444,16 +450,36 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_x6_kernel(SdfMlpX6Args p) {
     };
     // wave w copies bytes 6 KB w .. + 6 KB of the slot: six 1 KB pieces, lane l -> 16 bytes at 16 l (the LDS
     // image is the chunk as it lies in the term image: row r at 96 r, term t at + 32 t, k half h at + 16 h)
-    auto issue = [&](int g) __attribute__((always_inline)) {
+    auto chunk_view = [&](int g) __attribute__((always_inline)) {
         int l, c;
         step_of(g % kX6StepsPerBlock, l, c);
-        const rsrc_t v = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.W[l]) + (int64_t)c * 256 * 48, 0,
-                                                           kX6Chunk, 0x00020000);
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.W[l]) + (int64_t)c * 256 * 48, 0, kX6Chunk,
+                                                 0x00020000);
+    };
+    auto issue = [&](int g) __attribute__((always_inline)) {
+        if (CN_X6Q_EXP == 1 || !CN_X6Q_DMA) return;  // (measurement build: no weight stream)
+        const rsrc_t v = chunk_view(g);
         char* dst = smem + (g % kX6NS) * kX6Chunk + wave * 6144;
 #pragma unroll
         for (int j = 0; j < 6; ++j)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(v, (__attribute__((address_space(3))) void*)(dst + j * 1024), 16,
                                                      dvo[j], 0, 0, 0);
+    };
+    // Register staging (CN_X6Q_DMA 0): a chunk's 6 pieces per lane are loaded one k-step ahead and written to their
+    // slot positions by ds_write_b128 -- about a sixth of an LDS-DMA piece's issue cycles each
+    floatx4 stg[6];
+    auto gload = [&](int g) __attribute__((always_inline)) {
+        if (CN_X6Q_EXP == 1 || CN_X6Q_DMA) return;
+        const rsrc_t v = chunk_view(g);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) stg[j] = bload4(v, dvo[j], 0);
+    };
+    auto swrite = [&](int g) __attribute__((always_inline)) {
+        if (CN_X6Q_EXP == 1 || CN_X6Q_DMA) return;
+        wait_vmcnt<0>();
+        char* dst = smem + (g % kX6NS) * kX6Chunk + wave * 6144 + lane * 16;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) *reinterpret_cast<floatx4*>(dst + j * 1024) = stg[j];
     };
     // weight (A operand) reads: lane l -> row (l & 31) of 32-row block ib (32 rows keep the rotation), term t,
     // k half h: logical piece 2 t + h
@@ -475,6 +501,13 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_x6_kernel(SdfMlpX6Args p) {
     int g = 0;
 #pragma unroll
     for (int d = 0; d < kX6NS - 2; ++d) issue(d);
+    if constexpr (!CN_X6Q_DMA) {  // chunks 0, 1 in their slots, chunk 2 in the staging registers
+        gload(0);
+        swrite(0);
+        gload(1);
+        swrite(1);
+        gload(2);
+    }
 
     floatx4 act[16][2];  // the current layer's input: k-step ks, lane half h: features 16 ks + 8 h + 4 e + (0..3)
     floatx16 acc[8];
@@ -509,8 +542,14 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_x6_kernel(SdfMlpX6Args p) {
     // k-step g's chunk certified landed by every wave (this wave's pieces: the NS - 3 later chunks may fly;
     // the barrier: every wave's, and every wave done reading chunk g - 2's slot, which the DMA issued here
     // refills with chunk g + NS - 2)
+    // (register staging: the barrier certifies chunk g written by every wave a step earlier -- each wave's
+    // writes retired by the lgkmcnt(0) -- and every wave done with chunk g - 2's slot)
     auto land = [&](int gg) __attribute__((always_inline)) {
-        wait_vmcnt<6 * (kX6NS - 3)>();
+        if constexpr (CN_X6Q_DMA) {
+            wait_vmcnt<6 * (kX6NS - 3)>();
+        } else {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
         asm volatile("" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
@@ -563,6 +602,8 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_x6_kernel(SdfMlpX6Args p) {
 #pragma unroll
         for (int ib = 0; ib < 8; ++ib) acc[ib] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1[ib], b1, acc[ib], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
+        swrite(g + 2);  // (register staging) chunk g + 2, loaded a step ago, into chunk g - 1's slot
+        gload(g + 3);
         land(g + 1);
         read_w(g + 1, std::integral_constant<int, 0>{});
         asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(w2[0]), "+v"(w2[1]), "+v"(w2[2]), "+v"(w2[3]), "+v"(w2[4]),
@@ -595,7 +636,9 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_x6_kernel(SdfMlpX6Args p) {
     auto values = [&](auto ib_c, int l, const floatx4* bb, float* o) __attribute__((always_inline)) {
         constexpr int ib = decltype(ib_c)::value;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) o[r] = softplus_hw(acc[ib][r] + bb[r >> 2][r & 3], c_exp, c_thr, c_log);
+        for (int r = 0; r < 16; ++r)
+            o[r] = CN_X6Q_EXP == 2 ? acc[ib][r] + bb[r >> 2][r & 3]  // (measurement build: no softplus)
+                                   : softplus_hw(acc[ib][r] + bb[r >> 2][r & 3], c_exp, c_thr, c_log);
         if (l == p.skip_layer) {
             const float inv_odiv = p.inv_odiv[l];
 #pragma unroll
