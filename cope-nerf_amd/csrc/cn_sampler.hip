@@ -383,7 +383,7 @@ __global__ void __launch_bounds__(256, 1) sdf_mlp_kernel(SdfMlpArgs p) {
 #define CN_X6Q_SPLIT_AHEAD 1
 #endif
 #ifndef CN_X6Q_DMA
-#define CN_X6Q_DMA 0  // 1: the weight chunks by LDS-DMA (measured slower: each 1 KB piece costs ~125 issue cycles)
+#define CN_X6Q_DMA 1  // 0: register staging of the weight chunks (measured 6 % slower, profiles/r6_ab.txt r6h)
 #endif
 constexpr int kX6NS = CN_X6Q_DMA ? 6 : 3;  // ring slots
 constexpr int kX6Chunk = 24576;     // bytes per slot: 256 rows x 3 terms x 16 k bf16
