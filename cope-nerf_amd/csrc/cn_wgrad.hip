@@ -501,6 +501,9 @@ __global__ void __launch_bounds__(128 * WM, 2) wgrad_x6_kernel(WgradArgs p) {
 // 767-772 vs 790-794 us per 2-pair C2-shape call on random data, 641-644 vs 666-676 with
 // L2-resident operands (the kernel is not HBM-bound); 16x16x32 MFMAs (higher clock, more
 // cycles) and a register-held split of the next 32-row chunk measured equal to the old kernel.
+#ifndef CN_WGRAD_TIED_LOADS
+#define CN_WGRAD_TIED_LOADS 1
+#endif
 template <int NRAW>
 __global__ void __launch_bounds__(512, 2) wgrad_x6r_kernel(WgradBatch batch) {
     constexpr int BNo = 256, MC = 16, PL = 8, LSB = 3 * PL + 4;  // 28 dwords per LDS row
@@ -547,7 +550,24 @@ __global__ void __launch_bounds__(512, 2) wgrad_x6r_kernel(WgradBatch batch) {
         const int col0 = sx ? k0 : n0;
         const rsrc_t v = make_view(src + (int64_t)mrow * ld + col0, (nrows * ld - col0) * 4);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) r4[r] = bload4(v, ((mq * 4 + r) * ld + cg * 4) * 4, 0);
+        for (int r = 0; r < 4; ++r) {
+#if CN_WGRAD_TIED_LOADS
+            // the load writes the set's own registers ("+v": the old value's), so the two register sets keep
+            // their places across the loop's back edge -- compiled loads got fresh destinations there, and the
+            // copies back (16 v_mov per two stages) waited for the loads one stage early (vmcnt(0) at the
+            // back edge).  The asm loads are not counted by the compiler: wait_set() waits for them.
+            const int off = ((mq * 4 + r) * ld + cg * 4) * 4;
+            asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "+v"(r4[r]) : "v"(off), "s"(v));
+#else
+            r4[r] = bload4(v, ((mq * 4 + r) * ld + cg * 4) * 4, 0);
+#endif
+        }
+    };
+    // (CN_WGRAD_TIED_LOADS) a set loaded a stage ago has landed: only the 4 loads issued since may fly
+    auto wait_set = [&](floatx4 (&r4)[4]) {
+#if CN_WGRAD_TIED_LOADS
+        asm volatile("s_waitcnt vmcnt(4)" : "+v"(r4[0]), "+v"(r4[1]), "+v"(r4[2]), "+v"(r4[3]));
+#endif
     };
     // split column e of the 4 x 4 block of a register set into the stage image of buffer `buf`
     auto split_col = [&](const floatx4 (&r4)[4], int e, int buf, bool bias) {
@@ -612,8 +632,10 @@ __global__ void __launch_bounds__(512, 2) wgrad_x6r_kernel(WgradBatch batch) {
     // the loop body stays one basic block
     const bool ybias = do_bias & !sx;
     auto bias_of = [&](int c) { return ybias & (c < nch); };
+    static_assert(!CN_WGRAD_TIED_LOADS || NRAW == 2, "wait_set counts one other set of 4 loads");
 #pragma unroll
     for (int s = 0; s < NRAW; ++s) gload(s, raw[s]);
+    wait_set(raw[0]);
     splitw(raw[0], 0, bias_of(0));
     __syncthreads();
     // stage c in set c % NRAW: the loop is unrolled NRAW-fold so the set indices are constants,
@@ -624,6 +646,7 @@ __global__ void __launch_bounds__(512, 2) wgrad_x6r_kernel(WgradBatch batch) {
             const int c = c0 + k;
             {
                 gload(c + NRAW, raw[k]);  // set k held stage c (split in the previous stage)
+                wait_set(raw[(k + 1) % NRAW]);
                 const bool bnext = bias_of(c + 1);
                 compute(c & 1, [&](int j) { split_col(raw[(k + 1) % NRAW], j, (c + 1) & 1, bnext); });
                 __syncthreads();  // stage c+1 written, stage c's buffer free
