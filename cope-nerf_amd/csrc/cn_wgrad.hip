@@ -570,12 +570,17 @@ __global__ void __launch_bounds__(512, 2) wgrad_x6r_kernel(WgradBatch batch) {
 #endif
     };
     // split column e of the 4 x 4 block of a register set into the stage image of buffer `buf`
-    auto split_col = [&](const floatx4 (&r4)[4], int e, int buf, bool bias) {
+    // (WB: the bias sums are taken at all -- only the Y waves of a job's first output tile; the other waves'
+    // stage loop carries no bias adds)
+    auto split_col = [&](auto wb_tag, const floatx4 (&r4)[4], int e, int buf, bool bias) {
+        constexpr bool WB = decltype(wb_tag)::value;
         float* img = smem + buf * IMG + (sx ? BNo * LSB : 0) + mq * 2;
         const floatx4 col = {r4[0][e], r4[1][e], r4[2][e], r4[3][e]};
-        // (scalar adds: a packed pair beside the MFMAs costs more issue cycles than two scalar ones)
-        const float s = add_f32(add_f32(col[0], col[1]), add_f32(col[2], col[3]));
-        bsum[e] = add_f32(bsum[e], bias ? s : 0.0f);
+        if constexpr (WB) {
+            // (scalar adds: a packed pair beside the MFMAs costs more issue cycles than two scalar ones)
+            const float s = add_f32(add_f32(col[0], col[1]), add_f32(col[2], col[3]));
+            bsum[e] = add_f32(bsum[e], bias ? s : 0.0f);
+        }
         bf16x4 t0, t1, t2;
         split3(col, t0, t1, t2);
         float* y = img + (cg * 4 + e) * LSB;
@@ -585,7 +590,7 @@ __global__ void __launch_bounds__(512, 2) wgrad_x6r_kernel(WgradBatch batch) {
     };
     auto splitw = [&](const floatx4 (&r4)[4], int buf, bool bias) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) split_col(r4, e, buf, bias);
+        for (int e = 0; e < 4; ++e) split_col(std::true_type{}, r4, e, buf, bias);
     };
 
     floatx16 acc[2][4];
@@ -640,19 +645,25 @@ __global__ void __launch_bounds__(512, 2) wgrad_x6r_kernel(WgradBatch batch) {
     __syncthreads();
     // stage c in set c % NRAW: the loop is unrolled NRAW-fold so the set indices are constants,
     // and runs whole NRAW-groups of stages (the stages past `total` read zeros: an empty view)
-    for (int c0 = 0; c0 < total; c0 += NRAW) {
+    auto stages = [&](auto wb_tag) {
+        for (int c0 = 0; c0 < total; c0 += NRAW) {
 #pragma unroll
-        for (int k = 0; k < NRAW; ++k) {
-            const int c = c0 + k;
-            {
-                gload(c + NRAW, raw[k]);  // set k held stage c (split in the previous stage)
-                wait_set(raw[(k + 1) % NRAW]);
-                const bool bnext = bias_of(c + 1);
-                compute(c & 1, [&](int j) { split_col(raw[(k + 1) % NRAW], j, (c + 1) & 1, bnext); });
-                __syncthreads();  // stage c+1 written, stage c's buffer free
+            for (int k = 0; k < NRAW; ++k) {
+                const int c = c0 + k;
+                {
+                    gload(c + NRAW, raw[k]);  // set k held stage c (split in the previous stage)
+                    wait_set(raw[(k + 1) % NRAW]);
+                    const bool bnext = bias_of(c + 1);
+                    compute(c & 1, [&](int j) { split_col(wb_tag, raw[(k + 1) % NRAW], j, (c + 1) & 1, bnext); });
+                    __syncthreads();  // stage c+1 written, stage c's buffer free
+                }
             }
         }
-    }
+    };
+    if (ybias)  // (wave-uniform)
+        stages(std::true_type{});
+    else
+        stages(std::false_type{});
     __syncthreads();  // LDS is reused for the bias partials
 
     const rsrc_t vP = make_view(p.part + (int64_t)slice * p.Npad * p.Kpad, p.Npad * p.Kpad * 4);
