@@ -1,11 +1,14 @@
 """Positional encoding (reference: model/neus_embedder.py:6-51).
 
 Only the dimension bookkeeping lives here: on the hot path the encoding is
-computed inside the HIP kernels (cn_sdf_embed / cn_color_extras), fused into
-the operand load of the first Linear.  `get_embedder` keeps the reference's
-call signature (multires, input_dims) -> (fn, out_dim) for API compatibility;
-its fn is a torch expression usable on any device, used by tests and by the
-out-of-scope NeRF branch only.
+computed by the HIP kernels cn_sdf_embed / cn_color_extras (csrc/cn_fields.hip),
+which write the first layers' operand rows (in bf16 mode the skip input's
+embedding tail straight into its operand image) for the first Linear to read;
+the round-3 fusion into that Linear's operand staging was measured no faster
+and removed in round 4.  `get_embedder` keeps the reference's call signature
+(multires, input_dims) -> (fn, out_dim) for API compatibility; its fn is a
+torch expression usable on any device, used by tests and by the out-of-scope
+NeRF branch only.
 """
 from __future__ import annotations
 

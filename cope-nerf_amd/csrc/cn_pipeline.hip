@@ -922,6 +922,9 @@ namespace {
 // Zero fill of n floats (the feature rows of lin8's gradient).  A kernel, not hipMemsetAsync: with
 // the memsets, replays of a captured training step left those rows differing from the eager step
 // from the second replay on (tests/test_gpu_configs.py::test_c5_graph_stage1_joint_pose_replays).
+// Isolated in ab/memset_graph.py (profiles/r6_ab.txt r6e): a captured ~1 KB hipMemsetAsync at a
+// 4-byte offset (db8 + 1) takes effect on the graph's first replay only (19 of 20 replays stale); the
+// 256 KB one beside it, and this kernel in its place, are right on every replay.
 __global__ void __launch_bounds__(256) zero_kernel(float* __restrict__ p, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = 0.0f;
 }
