@@ -292,3 +292,37 @@ def test_kernel_name_queries_follow_the_launch_choice():
     w.ldy0 = w.ldy1 = 128  # Y rows not 256-padded: the 128x64 tiles
     assert ops.kernel_name(_lib.load().cn_wgrad_kernel_name, w) == "void cn::wgrad_x6_kernel<2, 1>(cn::WgradArgs)"
     assert _lib.load().cn_linear_kernel_name(d, ctypes.create_string_buffer(8), 8) == -2  # CN_ERR_SHAPE
+
+
+def test_shape_key_sees_scalars_and_pointer_presence_only():
+    """ops._sized memoises the composed entry points' sizing on _lib.shape_key: pointer values must not
+    matter, their presence and every scalar (nested networks' too) must."""
+    from copenerf import _lib
+    n, c = _lib.SdfNet(), _lib.ColorNet()
+    d = _lib.RenderDesc()
+    d.sdf_net, d.color_net = ctypes.pointer(n), ctypes.pointer(c)
+    d.R, n.n_lin, n.beta = 4096, 9, 100.0
+    k0 = _lib.shape_key(d)
+    d.rays_o = 0x1000
+    k1 = _lib.shape_key(d)
+    assert k1 != k0
+    d.rays_o = 0x2000
+    n.W[2] = 0x3000
+    k2 = _lib.shape_key(d)
+    assert k2 != k1
+    n.W[2] = 0x4000
+    assert _lib.shape_key(d) == k2
+    for obj, field, val in ((d, "R", 2048), (n, "beta", 50.0), (c, "d_feature", 128), (n, "in_dim", None)):
+        if val is None:
+            getattr(obj, field)[3] += 1
+        else:
+            old = getattr(obj, field)
+            setattr(obj, field, val)
+            assert _lib.shape_key(d) != k2, field
+            setattr(obj, field, old)
+            continue
+        assert _lib.shape_key(d) != k2, field
+        getattr(obj, field)[3] -= 1
+    assert _lib.shape_key(d) == k2
+    d.color_net = None
+    assert _lib.shape_key(d) != k2
