@@ -96,7 +96,10 @@ def main():
                           ("relu", ops.EPI_RELU, dict(bias=bias)),
                           ("mul", ops.EPI_MUL, sg),
                           ("tangent", ops.EPI_TANGENT, sg),
-                          ("bwd_softplus", ops.EPI_BWD_SOFTPLUS, so)):
+                          ("bwd_softplus", ops.EPI_BWD_SOFTPLUS, so),
+                          # (stream-count probes: aux2 = aux1 -- two distinct aux streams; no aux1 / aux2 -- one)
+                          ("bwd_softplus_2str", ops.EPI_BWD_SOFTPLUS, dict(so, aux2=aux1)),
+                          ("bwd_softplus_1str", ops.EPI_BWD_SOFTPLUS, sg)):
         bench(res, "cn_linear x6 " + name, lambda: ops.linear(A, Bs, N, K, o0, epi, **kw))
     if os.environ.get("X6_AIMG"):  # (a -DCN_AB_X6_AIMG=1 library) A as a bf16x6 term image, no split while staging
         As = ops.split_bf16x3(A)  # [K/16, M, 48]: the layout of B's images
