@@ -61,6 +61,58 @@ def _worker(rank, world, port, batch, q, KW, R):
     dist.destroy_process_group()
 
 
+def _partition_oracle(KW, R, world, batch):
+    """The ranks' result restated in one process: each rank's share of the batch on its own trainer (same
+    seed), the stage-1 normalisers replaced by their global sums (the partial sums of a first pass, added in
+    rank order) and the loss terms scaled by the world size, as motion._allreduce_sum / _world do under a
+    process group; then the gradients summed in rank order and divided by the world size, as
+    train_step.flat_allreduce_mean does.  The same row partition per weight gradient as the ranks'."""
+    from copenerf import motion
+    from copenerf.train_step import SyntheticTrainer
+    from helpers import smooth_frames
+    n = R // world
+
+    def run(r, reduce_fn, world_fn):
+        saved = motion._allreduce_sum, motion._world
+        motion._allreduce_sum, motion._world = reduce_fn, world_fn
+        try:
+            tr = SyntheticTrainer("cuda:0", rays=n, **KW)
+            tr.images = smooth_frames(KW["n_images"], KW["H"], KW["W"], "cuda:0")
+            tr.begin_iteration()
+            part = {k: batch[k][r * n:(r + 1) * n] for k in ("pix", "pixn", "t_rand")}
+            tr.iteration(tr.batch_from_pixels(part["pix"], part["pixn"], part["t_rand"]))
+            return tr
+        finally:
+            motion._allreduce_sum, motion._world = saved
+
+    partial = []
+    for r in range(world):
+        sums = []
+        run(r, lambda x, group, _s=sums: (_s.append(x.detach().clone()), x)[1], lambda group: 1)
+        partial.append(sums)
+    assert len({len(s) for s in partial}) == 1
+    total = []
+    for i in range(len(partial[0])):
+        t = partial[0][i].clone()
+        for r in range(1, world):
+            t = t + partial[r][i]
+        total.append(t)
+    acc = None
+    for r in range(world):
+        calls = iter(total)
+        tr = run(r, lambda x, group: next(calls), lambda group: world)
+        flat = torch.cat([p.grad.reshape(-1) for p in tr.all_params if p.grad is not None])
+        acc = flat.clone() if acc is None else acc + flat
+        shapes = [(i, p.grad.shape) for i, p in enumerate(tr.all_params) if p.grad is not None]
+    acc = (acc / world).cpu().numpy()
+    out, o = {}, 0
+    for i, shp in shapes:
+        k = int(np.prod(shp))
+        out["p%d" % i] = acc[o:o + k].reshape(shp)
+        o += k
+    return out
+
+
 @pytest.mark.parametrize("world,workload", [(2, "joint_pose_stage1"), (4, "skateboard_c4"), (2, "skateboard_c4_8192")])
 def test_hip_data_parallel_equals_full_batch(world, workload):
     from copenerf.train_step import SyntheticTrainer
@@ -116,9 +168,31 @@ def test_hip_data_parallel_equals_full_batch(world, workload):
             d = (res[r][name] - g).astype(np.float64)
             rows.append((np.linalg.norm(d) / gn, np.abs(d).max() / scale, s_rel, s_el, name, r))
     rows.sort(key=lambda x: -x[0])
-    print(f"{workload}: worst (relative L2, element / scale, self spread L2, self element, param, rank):",
-          [(f"{a:.2e}", f"{b:.2e}", f"{c:.2e}", f"{d:.2e}", n, r, gref[n].shape) for a, b, c, d, n, r in rows[:24:world]])
+    print(f"{workload}: vs the full batch, worst (relative L2, element / scale, self spread L2, self element, param, "
+          "rank):", [(f"{a:.2e}", f"{b:.2e}", f"{c:.2e}", f"{d:.2e}", n, r, gref[n].shape)
+                     for a, b, c, d, n, r in rows[:24:world]])
     for rel, el, s_rel, s_el, name, r in rows:
         wide = R > 256 and gref[name].ndim == 2
         assert rel <= max(1e-4 if wide else 1e-5, 2 * s_rel), (name, r, rel, s_rel)
         assert el <= max(2e-4 if wide else 3e-5, 2 * s_el), (name, r, el, s_el)
+    # the excess over the reordering spread is the ranks' row partition.  Against the partition
+    # oracle (the ranks' shares computed here, summed in rank order) every parameter of every workload is
+    # held to the plain bar, 1e-5 relative L2 and 3e-5 of the largest element
+    gpart = _partition_oracle(KW, R, world, {k: batch[k] for k in ("pix", "pixn", "t_rand")})
+    assert set(gpart) == set(gref)
+    prow = []
+    for name, g in gpart.items():
+        scale = np.abs(g).max() + 1e-20
+        gn = np.linalg.norm(g.astype(np.float64)) + 1e-30
+        for r in range(world):
+            d = (res[r][name] - g).astype(np.float64)
+            prow.append((np.linalg.norm(d) / gn, np.abs(d).max() / scale, name, r))
+    prow.sort(key=lambda x: -x[0])
+    print(f"{workload}: vs the partition oracle, worst (relative L2, element / scale, param, rank):",
+          [(f"{a:.2e}", f"{b:.2e}", n, r) for a, b, n, r in prow[:12]])
+    # (measured: 2 ranks bitwise equal -- a + b in either order is one fp32 sum; 4 ranks within 8.7e-7, gloo's
+    # order of the four-term sums; profiles/r6p_dist_tests.txt)
+    for rel, el, name, r in prow:
+        if world == 2:
+            assert rel == 0.0 and el == 0.0, (name, r, rel, el)
+        assert rel <= 1e-5 and el <= 3e-5, (name, r, rel, el)
