@@ -717,9 +717,9 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                 const int lrow = part * PROWS + (g * GROUP + q) * RPP;  // wave-uniform slab row of the pass
                 // unconditional: the views make reads past a row (columns >= N) or
                 // past the last row harmless, and only region-0 lanes use the values
-                if (kAux0) x0[slot][q] = AUX0B ? bload_b16x4(view_at(tX0, lrow), voX0b, 0) : bload4(view_at(tX0, lrow), voX0, 0);
-                if (kAux1) x1[slot][q] = AUX12B ? bload_b16x4(view_at(tX1, lrow), voX1, 0) : bload4(view_at(tX1, lrow), voX1, 0);
-                if (kAux1) x2[slot][q] = AUX12B ? bload_b16x4(view_at(tX2, lrow), voX2, 0) : bload4(view_at(tX2, lrow), voX2, 0);
+                if (kAux0) x0[slot][q] = AUX0B ? bload_b16x4(view_at(tX0, lrow), voX0b, 0) : eload4(view_at(tX0, lrow), voX0, 0);
+                if (kAux1) x1[slot][q] = AUX12B ? bload_b16x4(view_at(tX1, lrow), voX1, 0) : eload4(view_at(tX1, lrow), voX1, 0);
+                if (kAux1) x2[slot][q] = AUX12B ? bload_b16x4(view_at(tX2, lrow), voX2, 0) : eload4(view_at(tX2, lrow), voX2, 0);
                 if (ROWV) rv[slot][q] = bload1(view_at(tR, lrow), rr * 4, 0);
                 if (kHead) hidx[slot][q] = __builtin_bit_cast(int, bload1(view_at(tI, lrow), rr * 4, 0));
             }
@@ -819,7 +819,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                             float part = 0.0f;
                             if (MAIN || region == 0) {
                                 main_vals(v, slot, q, o0);
-                                bstore4(view_at(tO0, lrow), voO0, 0, o0);  // (out0 NULL: empty view)
+                                estore4(view_at(tO0, lrow), voO0, 0, o0);  // (out0 NULL: empty view)
                                 sb0(o0);
                                 floatx4 s1;
 #pragma unroll
@@ -827,11 +827,11 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                                     part += o0[e] * hw[e];
                                     s1[e] = colv[e] * sigma_from_act(o0[e], p.aux_c);
                                 }
-                                bstore4(view_at(tO1, lrow), voO1, 0, s1);  // (out1 NULL: empty view)
+                                estore4(view_at(tO1, lrow), voO1, 0, s1);  // (out1 NULL: empty view)
                                 sb1(s1);
                             } else if (region == 2) {
-                                bstore4(view_at(tO0, lrow), voO0, 0, zero4);
-                                bstore4(view_at(tO1, lrow), voO1, 0, zero4);
+                                estore4(view_at(tO0, lrow), voO0, 0, zero4);
+                                estore4(view_at(tO1, lrow), voO1, 0, zero4);
                                 sb0(zero4);
                                 sb1(zero4);
                             }
@@ -847,22 +847,22 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         }
                         if constexpr (MAIN) {
                             main_vals(v, slot, q, o0);
-                            bstore4(view_at(tO0, lrow), voO0, 0, o0);
+                            estore4(view_at(tO0, lrow), voO0, 0, o0);
                             sb0(o0);
                         } else if (region == 0) {
                             main_vals(v, slot, q, o0);
-                            bstore4(view_at(tO0, lrow), voO0, 0, o0);
+                            estore4(view_at(tO0, lrow), voO0, 0, o0);
                             sb0(o0);
                         } else if (region == 1) {  // EPI_MUL split columns: raw (A·Bᵀ)/adiv
 #pragma unroll
                             for (int e = 0; e < 4; ++e) o0[e] = v[e] * p.inv_adiv;
-                            bstore4(view_at(tS, lrow), voS, 0, o0);
+                            estore4(view_at(tS, lrow), voS, 0, o0);
                             if (col < cNzero) {
-                                bstore4(view_at(tO0, lrow), voO0, 0, zero4);
+                                estore4(view_at(tO0, lrow), voO0, 0, zero4);
                                 sb0(zero4);
                             }
                         } else if (region == 2) {  // zero fill (region 3: past nzero, untouched)
-                            bstore4(view_at(tO0, lrow), voO0, 0, zero4);
+                            estore4(view_at(tO0, lrow), voO0, 0, zero4);
                             sb0(zero4);
                         }
                     }
@@ -922,7 +922,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         auto bimg_pair = [&](const TileView& t, int rowi, int vb, float o_r, float o_r1, unsigned sel) {
             const unsigned own = pack_b16x2(o_r, o_r1);
             const unsigned recv = __builtin_amdgcn_mov_dpp(own, 0xB1, 0xF, 0xF, true);  // lane ^ 1
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(recv, own, sel), view_at(t, rowi), vb, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(recv, own, sel), view_at(t, rowi), vb, 0, CN_EPI_AUX);
         };
         // The direct epilogues take the wave-uniform choices (fp32 out0 stored, bf16 image of it, MUL's
         // split output) as template flags: as branches inside the element loops they left the
@@ -972,12 +972,12 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                     const int r = r0 + q, row = i * 32 + (r & 3) + 8 * (r >> 2);
 #pragma unroll
                     for (int j = 0; j < TN; ++j) {
-                        xa[sl][q][j] = AUX0B ? bload_u16(view_at(tX0, row), v0, ASTEP * j)
-                                            : __builtin_bit_cast(unsigned, bload1(view_at(tX0, row), v0, ASTEP * j));
-                        if (kAux1) xb[sl][q][j] = AUX12B ? bload_u16(view_at(tX1, row), v1, XSTEP * j)
-                                                         : __builtin_bit_cast(unsigned, bload1(view_at(tX1, row), v1, XSTEP * j));
-                        if (kAux1) xc[sl][q][j] = AUX12B ? bload_u16(view_at(tX2, row), v2, XSTEP * j)
-                                                         : __builtin_bit_cast(unsigned, bload1(view_at(tX2, row), v2, XSTEP * j));
+                        xa[sl][q][j] = AUX0B ? eload_u16(view_at(tX0, row), v0, ASTEP * j)
+                                            : __builtin_bit_cast(unsigned, eload1(view_at(tX0, row), v0, ASTEP * j));
+                        if (kAux1) xb[sl][q][j] = AUX12B ? eload_u16(view_at(tX1, row), v1, XSTEP * j)
+                                                         : __builtin_bit_cast(unsigned, eload1(view_at(tX1, row), v1, XSTEP * j));
+                        if (kAux1) xc[sl][q][j] = AUX12B ? eload_u16(view_at(tX2, row), v2, XSTEP * j)
+                                                         : __builtin_bit_cast(unsigned, eload1(view_at(tX2, row), v2, XSTEP * j));
                     }
                 }
             };
@@ -1004,7 +1004,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         // fall past the view), out0 zero-filled there below.  No per-lane branch: the
                         // compiler would sink the aux load into it and drain vmcnt(0) there, the next
                         // tile's staging loads included
-                        if constexpr (EPI == CN_EPI_MUL && SPL) bstore1(view_at(tS, rowi), spl[j] ? vsj[j] : (1 << 30), 0, u);
+                        if constexpr (EPI == CN_EPI_MUL && SPL) estore1(view_at(tS, rowi), spl[j] ? vsj[j] : (1 << 30), 0, u);
                         const float sg = EPI == CN_EPI_BWD_RELU ? 0.0f : sigma_from_act(w0(xa[sl][q][j]), p.aux_c);
                         float o;
                         if constexpr (EPI == CN_EPI_BWD_RELU) {
@@ -1019,7 +1019,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         }
                         // (a bit mask, not a select: the compiler made the select a branch per element)
                         ov[j] = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, o) & keep[j]);
-                        if constexpr (O0) bstore1(vw, voj[j], 0, ov[j]);
+                        if constexpr (O0) estore1(vw, voj[j], 0, ov[j]);
                     }
                     if constexpr (B0) {
                         if (r & 1) {
@@ -1073,7 +1073,7 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         else if constexpr (EPI == CN_EPI_RELU) o = z > 0.0f ? z : 0.0f;
                         else o = z;
                         ov[j] = kSel ? o : live[j] ? o : 0.0f;
-                        if constexpr (O0) bstore1(vw, voj[j], 0, ov[j]);
+                        if constexpr (O0) estore1(vw, voj[j], 0, ov[j]);
                     }
                     if constexpr (B0) {
                         if (r & 1) {
@@ -1121,8 +1121,8 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
                         const float o = live[j] ? a : 0.0f;
                         ov0[j] = o;
                         ov1[j] = live[j] ? cj[j] * sigma_from_act(a, p.aux_c) : 0.0f;
-                        if (has_o0) bstore1(vw, voj[j], 0, o);
-                        if (has_o1) bstore1(vw1, vo1[j], 0, ov1[j]);
+                        if (has_o0) estore1(vw, voj[j], 0, o);
+                        if (has_o1) estore1(vw1, vo1[j], 0, ov1[j]);
                         part += o * hj[j];
                     }
                     if (has_b0 || has_b1) {
@@ -1298,20 +1298,35 @@ __global__ void __launch_bounds__(256) scale_cols_kernel(int M, int N4, const fl
 // 4 values at element offset i of an fp32 output, or of its bf16 operand image (ob)
 // four consecutive values of a row: fp32, or (B) a bf16 operand image widened
 template <bool B>
+#ifndef CN_STREAM_NT
+#define CN_STREAM_NT 0  // 1: the elementwise adjoint's rows read / written non-temporally (measurement switch)
+#endif
 __device__ __forceinline__ floatx4 load_row4(const void* p, int64_t i) {
     if constexpr (B) {
-        const u32x2_t w = *reinterpret_cast<const u32x2_t*>(static_cast<const bf16_t*>(p) + i);
+        const u32x2_t* a = reinterpret_cast<const u32x2_t*>(static_cast<const bf16_t*>(p) + i);
+        const u32x2_t w = CN_STREAM_NT ? __builtin_nontemporal_load(a) : *a;
         return floatx4{__builtin_bit_cast(float, w[0] << 16), __builtin_bit_cast(float, w[0] & 0xffff0000u),
                        __builtin_bit_cast(float, w[1] << 16), __builtin_bit_cast(float, w[1] & 0xffff0000u)};
     } else {
-        return *reinterpret_cast<const floatx4*>(static_cast<const float*>(p) + i);
+        const floatx4* a = reinterpret_cast<const floatx4*>(static_cast<const float*>(p) + i);
+        return CN_STREAM_NT ? __builtin_nontemporal_load(a) : *a;
     }
 }
 __device__ __forceinline__ void store_row4(void* out, bool ob, int64_t i, floatx4 v) {
-    if (ob)
-        *reinterpret_cast<bf16x4*>(static_cast<bf16_t*>(out) + i) = __builtin_convertvector(v, bf16x4);
-    else
-        *reinterpret_cast<floatx4*>(static_cast<float*>(out) + i) = v;
+    if (ob) {
+        bf16x4* a = reinterpret_cast<bf16x4*>(static_cast<bf16_t*>(out) + i);
+        const bf16x4 b = __builtin_convertvector(v, bf16x4);
+        if (CN_STREAM_NT)
+            __builtin_nontemporal_store(b, a);
+        else
+            *a = b;
+    } else {
+        floatx4* a = reinterpret_cast<floatx4*>(static_cast<float*>(out) + i);
+        if (CN_STREAM_NT)
+            __builtin_nontemporal_store(v, a);
+        else
+            *a = v;
+    }
 }
 
 // Adjoint of a softplus layer without a GEMM, when the upstream gradient of its output

@@ -52,6 +52,29 @@ __device__ __forceinline__ void bstore4(rsrc_t r, int voff, int soff, floatx4 v)
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, soff, 0);
 }
 
+// The epilogues' streams (aux rows read once, outputs written once) with a cache policy of their own:
+// CN_EPI_AUX (measurement switch; 2 = nt on gfx950).
+#ifndef CN_EPI_AUX
+#define CN_EPI_AUX 2  // nt: measured faster (profiles/r6_ab.txt r6v)
+#endif
+__device__ __forceinline__ floatx4 eload4(rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, CN_EPI_AUX));
+}
+__device__ __forceinline__ float eload1(rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, CN_EPI_AUX));
+}
+// (bf16 aux rows keep the default policy: a 32-column block is half a 128-byte line, and nt loads do not
+// allocate it in L2 for the neighbouring block's load -- measured slower, profiles/r6_ab.txt r6v)
+__device__ __forceinline__ unsigned eload_u16(rsrc_t r, int voff, int soff) {
+    return __builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, 0);
+}
+__device__ __forceinline__ void estore1(rsrc_t r, int voff, int soff, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, soff, CN_EPI_AUX);
+}
+__device__ __forceinline__ void estore4(rsrc_t r, int voff, int soff, floatx4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, soff, CN_EPI_AUX);
+}
+
 // bf16 operand images (ABI v10): a tile's rows of a bf16 tensor (ld in bf16 elements, a
 // multiple of 8) as the float-typed TileView over the same bytes (rows ld / 2 floats apart), so
 // view_at works unchanged; voffsets into it are byte offsets, as for fp32 views.

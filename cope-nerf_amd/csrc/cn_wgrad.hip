@@ -501,6 +501,9 @@ __global__ void __launch_bounds__(128 * WM, 2) wgrad_x6_kernel(WgradArgs p) {
 // 767-772 vs 790-794 us per 2-pair C2-shape call on random data, 641-644 vs 666-676 with
 // L2-resident operands (the kernel is not HBM-bound); 16x16x32 MFMAs (higher clock, more
 // cycles) and a register-held split of the next 32-row chunk measured equal to the old kernel.
+#ifndef CN_WGRAD_NT
+#define CN_WGRAD_NT 0  // 1: wgrad_x6r_kernel's raw rows loaded non-temporally (measurement switch)
+#endif
 #ifndef CN_WGRAD_TIED_LOADS
 #define CN_WGRAD_TIED_LOADS 0  // 1: measured slower (profiles/r6_ab.txt r6i)
 #endif
@@ -559,7 +562,7 @@ __global__ void __launch_bounds__(512, 2) wgrad_x6r_kernel(WgradBatch batch) {
             const int off = ((mq * 4 + r) * ld + cg * 4) * 4;
             asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "+v"(r4[r]) : "v"(off), "s"(v));
 #else
-            r4[r] = bload4(v, ((mq * 4 + r) * ld + cg * 4) * 4, 0);
+            r4[r] = CN_WGRAD_NT ? eload4(v, ((mq * 4 + r) * ld + cg * 4) * 4, 0) : bload4(v, ((mq * 4 + r) * ld + cg * 4) * 4, 0);
 #endif
         }
     };
