@@ -1299,7 +1299,7 @@ __global__ void __launch_bounds__(256) scale_cols_kernel(int M, int N4, const fl
 // four consecutive values of a row: fp32, or (B) a bf16 operand image widened
 template <bool B>
 #ifndef CN_STREAM_NT
-#define CN_STREAM_NT 0  // 1: the elementwise adjoint's rows read / written non-temporally (measurement switch)
+#define CN_STREAM_NT 1  // the elementwise adjoint's rows read / written non-temporally (profiles/r6_ab.txt r6w)
 #endif
 __device__ __forceinline__ floatx4 load_row4(const void* p, int64_t i) {
     if constexpr (B) {

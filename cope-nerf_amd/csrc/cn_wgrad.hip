@@ -502,7 +502,7 @@ __global__ void __launch_bounds__(128 * WM, 2) wgrad_x6_kernel(WgradArgs p) {
 // L2-resident operands (the kernel is not HBM-bound); 16x16x32 MFMAs (higher clock, more
 // cycles) and a register-held split of the next 32-row chunk measured equal to the old kernel.
 #ifndef CN_WGRAD_NT
-#define CN_WGRAD_NT 0  // 1: wgrad_x6r_kernel's raw rows loaded non-temporally (measurement switch)
+#define CN_WGRAD_NT 1  // wgrad_x6r_kernel's raw rows loaded non-temporally (profiles/r6_ab.txt r6w)
 #endif
 #ifndef CN_WGRAD_TIED_LOADS
 #define CN_WGRAD_TIED_LOADS 0  // 1: measured slower (profiles/r6_ab.txt r6i)
