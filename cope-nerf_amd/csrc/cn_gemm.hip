@@ -83,6 +83,9 @@ struct LinearArgs {
 //         and aux2 are bf16 images.
 constexpr int kTblCols = 512;  // widest N with a bias / colv (the LDS column table)
 
+#ifndef CN_DMA_A_NT
+#define CN_DMA_A_NT 0  // 1: the LDS-DMA ring's A chunks loaded non-temporally (measured slower: a 32-deep chunk is half a 128-byte line; profiles/r6_ab.txt r6x)
+#endif
 template <int WM, int WN, int TM, int TN, int BK, int OCC, int DEPTH, int EPI, bool ROWV, int MODE_>
 __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel(LinearArgs p) {
     constexpr int MODE = MODE_ & 3;         // the GEMM mode (0 fp32, 1 bf16, 2 bf16x6)
@@ -366,10 +369,18 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) linear_kernel
         const rsrc_t v = __builtin_amdgcn_make_buffer_rsrc(ufirst(base), 0, __builtin_amdgcn_readfirstlane(bytes),
                                                            0x00020000);
         char* dst = reinterpret_cast<char*>(smem) + slot * DSTAGE + (dsb ? DSIDEA : 0) + (dwave & 3) * 64 * DROWB;
+        // (A, read once per tile, non-temporally with CN_DMA_A_NT; the weights stay cached: every workgroup reads them)
+        if (CN_DMA_A_NT && !dsb) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(v, (__attribute__((address_space(3))) void*)(dst + j * 1024), 16,
-                                                     (drow + 16 * j) * ld * 2 + (kk + dch * 8) * 2, 0, 0, 0);
+            for (int j = 0; j < 4; ++j)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(v, (__attribute__((address_space(3))) void*)(dst + j * 1024), 16,
+                                                         (drow + 16 * j) * ld * 2 + (kk + dch * 8) * 2, 0, 0, 2);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(v, (__attribute__((address_space(3))) void*)(dst + j * 1024), 16,
+                                                         (drow + 16 * j) * ld * 2 + (kk + dch * 8) * 2, 0, 0, 0);
+        }
     };
     // MFMA operand reads: lane l's row (l & 31) of each 32-row block, 16-byte chunk 2 ks + (l >> 5)
     // at its swizzled place ((row >> 2) & 3 = ((l & 31) >> 2) & 3: the blocks start at multiples of 32)

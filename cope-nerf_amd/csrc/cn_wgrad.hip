@@ -501,6 +501,9 @@ __global__ void __launch_bounds__(128 * WM, 2) wgrad_x6_kernel(WgradArgs p) {
 // 767-772 vs 790-794 us per 2-pair C2-shape call on random data, 641-644 vs 666-676 with
 // L2-resident operands (the kernel is not HBM-bound); 16x16x32 MFMAs (higher clock, more
 // cycles) and a register-held split of the next 32-row chunk measured equal to the old kernel.
+#ifndef CN_WGRAD_DMA_NT
+#define CN_WGRAD_DMA_NT 1  // wgrad_b16d_kernel's image rows loaded non-temporally (profiles/r6_ab.txt r6x)
+#endif
 #ifndef CN_WGRAD_NT
 #define CN_WGRAD_NT 1  // wgrad_x6r_kernel's raw rows loaded non-temporally (profiles/r6_ab.txt r6w)
 #endif
@@ -967,7 +970,7 @@ __global__ void __launch_bounds__(512, 2) wgrad_b16d_kernel(WgradBatch batch) {
             const int row = wq * 8 + 2 * j + drow;
             const int ch = dch ^ ((row & 3) << 2);
             __builtin_amdgcn_raw_ptr_buffer_load_lds(v, (lds_void*)(dst + j * 1024), 16, row * ld * 2 + ch * 16,
-                                                     0, 0, 0);
+                                                     0, 0, CN_WGRAD_DMA_NT ? 2 : 0);
         }
     };
 
